@@ -1,0 +1,86 @@
+# dmlc-core for MI355X — native build.
+#
+#   make            -> dmlc_core_amd/lib/libdmlc.so (CPU runtime + HIP kernels for gfx950)
+#                      dmlc_core_amd/_dmlc*.so      (pybind11 module)
+#   make test-bin   -> build/dmlc_unittest           (C++ unit tests, no GPU needed)
+#   make tools      -> build/dmlc_gen, build/dmlc_bench_cpu
+#
+# Host code: g++ -std=c++17 -O3 -fopenmp -ffp-contract=off (bit-exact parsing).
+# Device code: hipcc --offload-arch=gfx950 (CDNA4 only; no other targets).
+
+ROCM ?= /opt/rocm
+HIPCC ?= $(ROCM)/bin/hipcc
+CXX ?= g++
+PYTHON ?= python3
+GPU_ARCH ?= gfx950
+BUILD ?= build
+LIBDIR := dmlc_core_amd/lib
+
+PY_INC := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_paths()['include'])")
+PYBIND_INC := $(shell $(PYTHON) -c "import pybind11;print(pybind11.get_include())")
+PY_EXT := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_config_var('EXT_SUFFIX'))")
+
+WARN := -Wall -Wno-unknown-pragmas -Wno-sign-compare
+CXXFLAGS_BASE := -std=c++17 -O3 -fPIC -fopenmp -ffp-contract=off -g1 $(WARN) -Iinclude -Isrc \
+  -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
+HIPFLAGS := -std=c++17 -O3 -fPIC --offload-arch=$(GPU_ARCH) -ffp-contract=off -Iinclude -Isrc \
+  -Wno-unused-result -munsafe-fp-atomics
+LDFLAGS_LIB := -shared -fopenmp -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64 -lrccl -ldl -lpthread
+
+CPU_SRCS := src/logging.cc src/io.cc src/recordio.cc src/data.cc src/config.cc src/synthetic.cc \
+  src/io/local_filesys.cc src/io/input_split_base.cc src/io/line_split.cc \
+  src/io/recordio_split.cc src/io/remote_filesys.cc \
+  src/io/shard_reader.cc \
+  src/gpu/runtime.cc src/gpu/device_parser.cc
+HIP_SRCS := $(wildcard src/gpu/*.hip)
+
+CPU_OBJS := $(patsubst src/%.cc,$(BUILD)/obj/%.o,$(CPU_SRCS))
+HIP_OBJS := $(patsubst src/%.hip,$(BUILD)/obj/%.hip.o,$(HIP_SRCS))
+HEADERS := $(wildcard include/dmlc/*.h include/dmlc/gpu/*.h include/dmlc/dist/*.h src/*/*.h)
+
+LIB := $(LIBDIR)/libdmlc.so
+PYMOD := dmlc_core_amd/_dmlc$(PY_EXT)
+
+all: $(LIB) $(PYMOD)
+
+$(BUILD)/obj/%.o: src/%.cc $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS_BASE) -c $< -o $@
+
+$(BUILD)/obj/%.hip.o: src/%.hip $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(CPU_OBJS) $(HIP_OBJS)
+	@mkdir -p $(LIBDIR)
+	$(CXX) -o $@ $^ $(LDFLAGS_LIB)
+
+$(PYMOD): src/python/module.cc $(LIB) $(HEADERS)
+	$(CXX) $(CXXFLAGS_BASE) -fvisibility=hidden -I$(PY_INC) -I$(PYBIND_INC) -shared \
+	  src/python/module.cc -o $@ -L$(LIBDIR) -ldmlc -Wl,-rpath,'$$ORIGIN/lib' \
+	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64
+
+TEST_SRCS := $(wildcard tests/cpp/*.cc)
+$(BUILD)/dmlc_unittest: $(TEST_SRCS) $(LIB) $(HEADERS)
+	@mkdir -p $(BUILD)
+	$(CXX) $(CXXFLAGS_BASE) $(TEST_SRCS) -o $@ -L$(LIBDIR) -ldmlc \
+	  -Wl,-rpath,$(abspath $(LIBDIR)) -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64 -lpthread
+
+test-bin: $(BUILD)/dmlc_unittest
+
+$(BUILD)/dmlc_gen: tools/dmlc_gen.cc $(LIB) $(HEADERS)
+	@mkdir -p $(BUILD)
+	$(CXX) $(CXXFLAGS_BASE) $< -o $@ -L$(LIBDIR) -ldmlc -Wl,-rpath,$(abspath $(LIBDIR)) \
+	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64
+
+$(BUILD)/dmlc_bench_cpu: tools/dmlc_bench_cpu.cc $(LIB) $(HEADERS)
+	@mkdir -p $(BUILD)
+	$(CXX) $(CXXFLAGS_BASE) $< -o $@ -L$(LIBDIR) -ldmlc -Wl,-rpath,$(abspath $(LIBDIR)) \
+	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64
+
+tools: $(BUILD)/dmlc_gen $(BUILD)/dmlc_bench_cpu
+
+clean:
+	rm -rf $(BUILD) $(LIB) $(PYMOD)
+
+.PHONY: all clean test-bin tools

@@ -1,0 +1,37 @@
+"""dmlc-core for MI355X.
+
+A brand-new, MI355X-native distributed-ML data runtime with the capabilities
+of dmlc-core: URI streams and filesystems, sharded InputSplits, RecordIO,
+LibSVM/LibFM/CSV parsers producing CSR RowBlocks, Parameter/Registry/JSON,
+ThreadedIter prefetch, and the dmlc-submit tracker -- plus a GPU ingestion
+path (pinned-host ring -> HIP/CDNA4 kernels -> CSR in HBM) and RCCL-based
+multi-GPU sharding.
+
+The native runtime lives in ``dmlc_core_amd/lib/libdmlc.so`` (C++17 + HIP for
+gfx950) and is exposed through ``dmlc_core_amd._dmlc`` (pybind11).  Build it
+with ``make -j8`` (or ``python -c "import __graft_entry__ as g; g.build()"``).
+"""
+from __future__ import annotations
+
+import os
+
+__version__ = "0.1.0"
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _load_native():
+    try:
+        from . import _dmlc  # noqa: F401
+    except ImportError as err:  # pragma: no cover - exercised only when unbuilt
+        raise ImportError(
+            "dmlc_core_amd native extension is not built; run `make -j8` in the repo root "
+            f"({err})") from err
+    return _dmlc
+
+
+_native = _load_native()
+
+from . import utils, io, data, ops, parallel, models  # noqa: E402,F401
+
+__all__ = ["utils", "io", "data", "ops", "parallel", "models", "__version__"]

@@ -1,0 +1,108 @@
+"""HIP (gfx950) kernels exposed as PyTorch operations on device CSR data.
+
+Every op launches a hand-written CDNA4 kernel from ``libdmlc.so`` on the
+current torch stream (src/gpu/feature_kernels.hip).  There is no PyTorch
+fallback: on a machine without the extension or a GPU these functions raise.
+
+CSR arguments are the dict returned by :func:`dmlc_core_amd.data.csr_to_torch`
+(``offset`` int64/uint64 [rows+1], ``index`` int32/uint32 or 64-bit [nnz],
+optional ``value`` float32 [nnz], optional ``field``).
+"""
+from __future__ import annotations
+
+from typing import Dict
+
+import torch
+
+from .. import _dmlc
+
+__all__ = ["spmv", "spmv_t", "hashed_dense", "SpMVFunction", "csr_spmv"]
+
+
+def _ptr(t) -> int:
+    return 0 if t is None else int(t.data_ptr())
+
+
+def _index64(csr: Dict) -> bool:
+    return csr["index"].element_size() == 8
+
+
+def _check(csr: Dict):
+    for k in ("offset", "index"):
+        t = csr[k]
+        if not t.is_cuda or not t.is_contiguous():
+            raise ValueError(f"csr[{k!r}] must be a contiguous device tensor")
+    if csr.get("value") is not None and csr["value"].dtype != torch.float32:
+        raise ValueError("csr['value'] must be float32")
+
+
+def _stream() -> int:
+    return int(torch.cuda.current_stream().cuda_stream)
+
+
+def spmv(csr: Dict, w: torch.Tensor, bias: float = 0.0) -> torch.Tensor:
+    """y[r] = sum_j value[j] * w[index[j]] + bias  (K11, 16 lanes per row)."""
+    _check(csr)
+    assert w.dtype == torch.float32 and w.is_cuda and w.is_contiguous()
+    nrows = csr["offset"].numel() - 1
+    y = torch.empty(nrows, dtype=torch.float32, device=w.device)
+    _dmlc.spmv(_ptr(csr["offset"]), _ptr(csr["index"]), _ptr(csr.get("value")), nrows, _ptr(w),
+               float(bias), _ptr(y), _stream(), _index64(csr))
+    return y
+
+
+def spmv_t(csr: Dict, d: torch.Tensor, num_features: int) -> torch.Tensor:
+    """g[index[j]] += value[j] * d[row(j)]  (transposed K11, f32 atomics)."""
+    _check(csr)
+    assert d.dtype == torch.float32 and d.is_cuda and d.is_contiguous()
+    g = torch.zeros(num_features, dtype=torch.float32, device=d.device)
+    nrows = csr["offset"].numel() - 1
+    _dmlc.spmv_t(_ptr(csr["offset"]), _ptr(csr["index"]), _ptr(csr.get("value")), nrows, _ptr(d),
+                 _ptr(g), _stream(), _index64(csr))
+    return g
+
+
+def hashed_dense(csr: Dict, dim: int, seed: int = 0, fp8: bool = True,
+                 scale: float = 1.0) -> torch.Tensor:
+    """K9: signed feature hashing of every row into ``dim`` buckets.
+
+    Returns float8_e4m3fn [rows, dim] (gfx950 OCP fp8, hardware conversion)
+    when ``fp8`` else float32.  LibFM fields are folded into the hash key.
+    """
+    _check(csr)
+    nrows = csr["offset"].numel() - 1
+    dev = csr["index"].device
+    if fp8:
+        out = torch.empty((nrows, dim), dtype=torch.uint8, device=dev)
+    else:
+        out = torch.empty((nrows, dim), dtype=torch.float32, device=dev)
+    _dmlc.hashed_dense(_ptr(csr["offset"]), _ptr(csr["index"]), _ptr(csr.get("value")),
+                       _ptr(csr.get("field")), nrows, int(dim), float(scale), int(seed) & 0xFFFFFFFF,
+                       _ptr(out), bool(fp8), _stream(), _index64(csr))
+    if fp8:
+        return out.view(torch.float8_e4m3fn)
+    return out
+
+
+class SpMVFunction(torch.autograd.Function):
+    """Autograd wrapper: forward = spmv, backward d/dw = spmv_t."""
+
+    @staticmethod
+    def forward(ctx, w, bias, csr_tuple):
+        offset, index, value = csr_tuple
+        csr = {"offset": offset, "index": index, "value": value}
+        ctx.csr = csr
+        ctx.num_features = w.numel()
+        return spmv(csr, w, 0.0) + bias
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        grad_out = grad_out.contiguous().float()
+        gw = spmv_t(ctx.csr, grad_out, ctx.num_features)
+        gb = grad_out.sum().reshape(1)
+        return gw, gb, None
+
+
+def csr_spmv(csr: Dict, w: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+    """Differentiable y = X w + b for a device CSR batch."""
+    return SpMVFunction.apply(w, bias, (csr["offset"], csr["index"], csr.get("value")))

@@ -1,0 +1,101 @@
+/*!
+ * \file dmlc/gpu/device_parser.h
+ * \brief GPU ingestion: text shard -> pinned ring -> HBM -> CSR, on MI355X.
+ *
+ * Pipeline:
+ *
+ *   reader thread ── parallel pread ──> pinned slot ring (P slots, ThreadedIter)
+ *        │                                     │ hipMemcpyAsync (copy stream)
+ *        ▼                                     ▼
+ *   InputSplit partition            device text ring (D slots, hipEvents)
+ *                                              │ K1 line index, K2 count, K3 scan,
+ *                                              │ K4 fill + K8 max (compute stream)
+ *                                              ▼
+ *                                   DeviceRowBlock / DeviceCSR in HBM
+ *
+ * The reference equivalent is Parser<I>::Create + ThreadedParser +
+ * ThreadedInputSplit (`src/data.cc:21-34`, `src/data/parser.h:71-126`,
+ * `src/io/threaded_input_split.h`), with OpenMP parsing replaced by the HIP
+ * kernels and the prefetch queues replaced by the pinned/device rings.
+ */
+#ifndef DMLC_GPU_DEVICE_PARSER_H_
+#define DMLC_GPU_DEVICE_PARSER_H_
+
+#include <map>
+#include <memory>
+#include <string>
+
+#include "./device_row_block.h"
+
+namespace dmlc {
+namespace gpu {
+
+/*! \brief knobs of the GPU ingestion pipeline (also settable as `?k=v` URI args) */
+struct DeviceParserConfig {
+  /*! \brief libsvm | libfm | csv */
+  std::string format{"libsvm"};
+  /*! \brief bytes per pinned / device text slot */
+  size_t chunk_bytes{64UL << 20};
+  /*! \brief pinned host slots queued ahead of the GPU */
+  int pinned_slots{3};
+  /*! \brief device text slots (H2D of chunk k+1 overlaps parsing of chunk k) */
+  int device_slots{2};
+  /*! \brief parallel pread threads of the reader */
+  int read_threads{8};
+  /*! \brief HIP device (-1 = current) */
+  int device{-1};
+  /*! \brief CSV: label column (-1 none), weight column, delimiter */
+  int label_column{-1};
+  int weight_column{-1};
+  char delimiter{','};
+  /*! \brief apply `?k=v` overrides (chunk_mb, pinned_slots, device_slots,
+   *  read_threads, device, format, label_column, weight_column, delimiter) */
+  void Update(const std::map<std::string, std::string>& args);
+};
+
+/*! \brief cumulative pipeline counters */
+struct DeviceParserStats {
+  size_t bytes{0};
+  size_t chunks{0};
+  size_t rows{0};
+  size_t nnz{0};
+  /*! \brief seconds the host waited for the reader (pinned ring empty) */
+  double wait_reader_sec{0};
+  /*! \brief seconds the host waited for GPU results */
+  double wait_gpu_sec{0};
+};
+
+/*!
+ * \brief GPU parser for one partition of a text dataset.
+ *
+ *  Streaming:   while (p->Next()) use(p->Value());   // one block per chunk
+ *  Resident:    DeviceCSR<uint32_t> csr; p->ParseAll(&csr);  // whole shard in HBM
+ */
+template <typename IndexType>
+class DeviceParser {
+ public:
+  /*!
+   * \param uri data uri (`?k=v` args override cfg)
+   * \param part_index / num_parts sharding as in InputSplit::Create
+   */
+  static DeviceParser* Create(const std::string& uri, unsigned part_index, unsigned num_parts,
+                              const DeviceParserConfig& cfg = DeviceParserConfig());
+  virtual ~DeviceParser() = default;
+  /*! \brief rewind to the first chunk */
+  virtual void BeforeFirst() = 0;
+  /*! \brief parse the next chunk; the block is ready on return */
+  virtual bool Next() = 0;
+  /*! \brief block of the last Next() (valid until the next call) */
+  virtual const DeviceRowBlock<IndexType>& Value() const = 0;
+  /*! \brief parse the rest of the partition, appending to `out` */
+  virtual void ParseAll(DeviceCSR<IndexType>* out) = 0;
+  /*! \brief total bytes of this partition */
+  virtual size_t PartitionBytes() const = 0;
+  virtual const DeviceParserStats& Stats() const = 0;
+  /*! \brief stream on which blocks are produced */
+  virtual hipStream_t stream() const = 0;
+};
+
+}  // namespace gpu
+}  // namespace dmlc
+#endif  // DMLC_GPU_DEVICE_PARSER_H_

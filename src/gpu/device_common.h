@@ -1,0 +1,119 @@
+/*!
+ * \file src/gpu/device_common.h
+ * \brief Wave64 / workgroup primitives shared by the gfx950 kernels.
+ *
+ * CDNA4 rules applied (cdna_hip_programming.md §1, §6): waves are 64 lanes,
+ * ballots are 64-bit, all block sizes are multiples of 64, cross-lane data
+ * moves through DPP/permute (__shfl*) rather than LDS where possible.
+ */
+#ifndef DMLC_GPU_DEVICE_COMMON_H_
+#define DMLC_GPU_DEVICE_COMMON_H_
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace dmlc {
+namespace gpu {
+namespace dev {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+/*! \brief make LDS writes of this wave visible to the other lanes of the wave */
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, kWave);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    T o = __shfl_xor(v, d, kWave);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+/*! \brief exclusive prefix sum across the wave; *total = wave sum */
+template <typename T>
+__device__ __forceinline__ T wave_excl_scan(T v, T* total) {
+  const int lane = lane_id();
+  T x = v;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    T y = __shfl_up(x, d, kWave);
+    if (lane >= d) x += y;
+  }
+  *total = __shfl(x, kWave - 1, kWave);
+  return x - v;
+}
+
+/*!
+ * \brief exclusive prefix across a 256-thread block (4 waves); *total = sum.
+ *  `smem` needs 4 elements; contains a __syncthreads.
+ */
+template <typename T>
+__device__ __forceinline__ T block_excl_scan_256(T v, T* smem, T* total) {
+  T wtotal;
+  T x = wave_excl_scan(v, &wtotal);
+  const int wid = threadIdx.x / kWave;
+  if (lane_id() == 0) smem[wid] = wtotal;
+  __syncthreads();
+  T base = 0, sum = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    T t = smem[w];
+    if (w < wid) base += t;
+    sum += t;
+  }
+  *total = sum;
+  return base + x;
+}
+
+template <typename T>
+__device__ __forceinline__ T block_sum_256(T v, T* smem) {
+  T t;
+  (void)block_excl_scan_256(v, smem, &t);
+  return t;
+}
+
+/*!
+ * \brief 16-bit mask of the bytes of a 16-byte vector equal to `c`
+ *  (exact SWAR zero-byte test per 32-bit word).
+ */
+__device__ __forceinline__ uint32_t byte_eq_mask(uint4 v, uint32_t c) {
+  const uint32_t pat = c * 0x01010101u;
+  uint32_t m = 0;
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t x = w[i] ^ pat;
+    // high bit of each byte set iff that byte of x is zero
+    const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+    // gather the 4 high bits into bits 0..3
+    const uint32_t g = ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+    m |= g << (4 * i);
+  }
+  return m;
+}
+
+__device__ __forceinline__ uint8_t vec_byte(uint4 v, int j) {
+  const uint32_t w = j < 4 ? v.x : (j < 8 ? v.y : (j < 12 ? v.z : v.w));
+  return static_cast<uint8_t>(w >> (8 * (j & 3)));
+}
+
+}  // namespace dev
+}  // namespace gpu
+}  // namespace dmlc
+#endif  // DMLC_GPU_DEVICE_COMMON_H_

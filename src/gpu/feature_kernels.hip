@@ -1,0 +1,203 @@
+/*!
+ * \file src/gpu/feature_kernels.hip
+ * \brief K9 hashed dense batches (f32 / OCP fp8 e4m3), K10 offset rebase,
+ *  K11 CSR SpMV and transposed SpMV, fills.
+ *
+ * K11 maps one row to a 16-lane group (4 rows per wave64): the survey's rows
+ * carry 20-60 non-zeros, so a whole wave per row would idle half of it; the
+ * group reduces with __shfl_xor at width 16.  The transposed product
+ * scatters with hardware f32 atomics (global_atomic_add_f32, built with
+ * -munsafe-fp-atomics), the right tool at this FLOP/byte ratio
+ * (cdna_hip_programming.md Guideline 12).
+ * K9 accumulates one row per wave in LDS (ds_add_f32) and converts pairs of
+ * f32 to fp8 with the gfx950 v_cvt_pk_fp8_f32 instruction.
+ */
+#include <hip/hip_runtime.h>
+
+#include "./device_common.h"
+#include "./kernels.h"
+
+namespace dmlc {
+namespace gpu {
+
+namespace {
+constexpr int kThreads = 256;
+constexpr int kGroup = 16;
+
+__global__ void k_fill(float* __restrict__ p, size_t n, float v) {
+  for (size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<size_t>(gridDim.x) * blockDim.x) {
+    p[i] = v;
+  }
+}
+
+__global__ void k_rebase(const uint64_t* __restrict__ src, size_t n, uint64_t src_base,
+                         uint64_t dst_base, uint64_t* __restrict__ dst) {
+  for (size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<size_t>(gridDim.x) * blockDim.x) {
+    dst[i] = src[i] - src_base + dst_base;
+  }
+}
+
+template <typename IndexType>
+__global__ __launch_bounds__(kThreads) void k_spmv(const uint64_t* __restrict__ offset,
+                                                   const IndexType* __restrict__ index,
+                                                   const float* __restrict__ value, size_t nrows,
+                                                   const float* __restrict__ w, float bias,
+                                                   float* __restrict__ y) {
+  const size_t ngroups = static_cast<size_t>(gridDim.x) * (kThreads / kGroup);
+  const int g = threadIdx.x % kGroup;
+  for (size_t r = blockIdx.x * static_cast<size_t>(kThreads / kGroup) + threadIdx.x / kGroup;
+       r < nrows; r += ngroups) {
+    const uint64_t b = offset[r], e = offset[r + 1];
+    float acc = 0.0f;
+    for (uint64_t j = b + g; j < e; j += kGroup) {
+      const float v = value != nullptr ? value[j] : 1.0f;
+      acc += v * w[index[j]];
+    }
+#pragma unroll
+    for (int d = kGroup / 2; d >= 1; d >>= 1) acc += __shfl_xor(acc, d, kGroup);
+    if (g == 0) y[r] = acc + bias;
+  }
+}
+
+template <typename IndexType>
+__global__ __launch_bounds__(kThreads) void k_spmvt(const uint64_t* __restrict__ offset,
+                                                    const IndexType* __restrict__ index,
+                                                    const float* __restrict__ value, size_t nrows,
+                                                    const float* __restrict__ d,
+                                                    float* __restrict__ grad) {
+  const size_t ngroups = static_cast<size_t>(gridDim.x) * (kThreads / kGroup);
+  const int g = threadIdx.x % kGroup;
+  for (size_t r = blockIdx.x * static_cast<size_t>(kThreads / kGroup) + threadIdx.x / kGroup;
+       r < nrows; r += ngroups) {
+    const uint64_t b = offset[r], e = offset[r + 1];
+    const float dr = d[r];
+    if (dr == 0.0f) continue;
+    for (uint64_t j = b + g; j < e; j += kGroup) {
+      const float v = value != nullptr ? value[j] : 1.0f;
+      atomicAdd(&grad[index[j]], v * dr);
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t hash_u64(uint64_t x, uint32_t seed) {
+  x ^= static_cast<uint64_t>(seed) * 0x9e3779b97f4a7c15ull;
+  x = (x ^ (x >> 33)) * 0xff51afd7ed558ccdull;
+  x = (x ^ (x >> 33)) * 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return static_cast<uint32_t>(x);
+}
+
+/*! \brief one row per wave; LDS row buffer of `dim` floats per wave */
+template <typename IndexType, bool kFP8>
+__global__ __launch_bounds__(kThreads) void k_hashed_dense(
+    const uint64_t* __restrict__ offset, const IndexType* __restrict__ index,
+    const float* __restrict__ value, const IndexType* __restrict__ field, size_t nrows, int dim,
+    float scale, uint32_t seed, void* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int wid = threadIdx.x / dev::kWave;
+  const int lane = dev::lane_id();
+  float* row = smem + static_cast<size_t>(wid) * dim;
+  const size_t nwaves = static_cast<size_t>(gridDim.x) * (kThreads / dev::kWave);
+  for (size_t r = blockIdx.x * static_cast<size_t>(kThreads / dev::kWave) + wid; r < nrows;
+       r += nwaves) {
+    for (int c = lane; c < dim; c += dev::kWave) row[c] = 0.0f;
+    dev::wave_sync();
+    const uint64_t b = offset[r], e = offset[r + 1];
+    for (uint64_t j = b + lane; j < e; j += dev::kWave) {
+      uint64_t key = static_cast<uint64_t>(index[j]);
+      if (field != nullptr) key ^= static_cast<uint64_t>(field[j]) << 40;
+      const uint32_t h = hash_u64(key, seed);
+      const int bucket = static_cast<int>(h % static_cast<uint32_t>(dim));
+      const float sign = (h & 0x80000000u) ? -1.0f : 1.0f;
+      const float v = value != nullptr ? value[j] : 1.0f;
+      atomicAdd(&row[bucket], sign * v);
+    }
+    dev::wave_sync();
+    if constexpr (kFP8) {
+      // 4 columns per lane-iteration -> one 32-bit store of 4 fp8 (e4m3, OCP on gfx950)
+      uint32_t* o = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(out) + r * dim);
+      for (int c = lane * 4; c < dim; c += dev::kWave * 4) {
+        int packed = __builtin_amdgcn_cvt_pk_fp8_f32(row[c] * scale, row[c + 1] * scale, 0, false);
+        packed = __builtin_amdgcn_cvt_pk_fp8_f32(row[c + 2] * scale, row[c + 3] * scale, packed, true);
+        o[c / 4] = static_cast<uint32_t>(packed);
+      }
+    } else {
+      float* o = static_cast<float*>(out) + r * dim;
+      for (int c = lane; c < dim; c += dev::kWave) o[c] = row[c];
+    }
+    dev::wave_sync();
+  }
+}
+
+int GridFor(size_t work, size_t per_block) {
+  size_t blocks = (work + per_block - 1) / per_block;
+  if (blocks == 0) blocks = 1;
+  return static_cast<int>(blocks < 16384 ? blocks : 16384);
+}
+}  // namespace
+
+void LaunchFill(float* p, size_t n, float v, hipStream_t stream) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_fill, dim3(GridFor(n, kThreads)), dim3(kThreads), 0, stream, p, n, v);
+}
+
+void LaunchOffsetRebase(const uint64_t* src_offset, size_t nrows, uint64_t src_base,
+                        uint64_t dst_base, uint64_t* dst_offset, hipStream_t stream) {
+  hipLaunchKernelGGL(k_rebase, dim3(GridFor(nrows + 1, kThreads)), dim3(kThreads), 0, stream,
+                     src_offset, nrows + 1, src_base, dst_base, dst_offset);
+}
+
+template <typename IndexType>
+void LaunchCSRSpMV(const uint64_t* offset, const IndexType* index, const float* value,
+                   size_t nrows, const float* w, float bias, float* y, hipStream_t stream) {
+  if (nrows == 0) return;
+  hipLaunchKernelGGL(k_spmv<IndexType>, dim3(GridFor(nrows, kThreads / kGroup)), dim3(kThreads),
+                     0, stream, offset, index, value, nrows, w, bias, y);
+}
+
+template <typename IndexType>
+void LaunchCSRSpMVT(const uint64_t* offset, const IndexType* index, const float* value,
+                    size_t nrows, const float* d, float* g, hipStream_t stream) {
+  if (nrows == 0) return;
+  hipLaunchKernelGGL(k_spmvt<IndexType>, dim3(GridFor(nrows, kThreads / kGroup)), dim3(kThreads),
+                     0, stream, offset, index, value, nrows, d, g);
+}
+
+template <typename IndexType>
+void LaunchHashedDenseFP8(const uint64_t* offset, const IndexType* index, const float* value,
+                          const IndexType* field, size_t nrows, int dim, float scale,
+                          uint32_t seed, uint8_t* out, hipStream_t stream) {
+  if (nrows == 0) return;
+  const size_t lds = static_cast<size_t>(dim) * sizeof(float) * (kThreads / dev::kWave);
+  hipLaunchKernelGGL((k_hashed_dense<IndexType, true>), dim3(GridFor(nrows, kThreads / dev::kWave)),
+                     dim3(kThreads), lds, stream, offset, index, value, field, nrows, dim, scale,
+                     seed, static_cast<void*>(out));
+}
+
+template <typename IndexType>
+void LaunchHashedDenseF32(const uint64_t* offset, const IndexType* index, const float* value,
+                          const IndexType* field, size_t nrows, int dim, uint32_t seed,
+                          float* out, hipStream_t stream) {
+  if (nrows == 0) return;
+  const size_t lds = static_cast<size_t>(dim) * sizeof(float) * (kThreads / dev::kWave);
+  hipLaunchKernelGGL((k_hashed_dense<IndexType, false>),
+                     dim3(GridFor(nrows, kThreads / dev::kWave)), dim3(kThreads), lds, stream,
+                     offset, index, value, field, nrows, dim, 1.0f, seed, static_cast<void*>(out));
+}
+
+#define DMLC_INSTANTIATE_FEATURE(I)                                                           \
+  template void LaunchCSRSpMV<I>(const uint64_t*, const I*, const float*, size_t, const float*, \
+                                 float, float*, hipStream_t);                                 \
+  template void LaunchCSRSpMVT<I>(const uint64_t*, const I*, const float*, size_t,            \
+                                  const float*, float*, hipStream_t);                         \
+  template void LaunchHashedDenseFP8<I>(const uint64_t*, const I*, const float*, const I*,    \
+                                        size_t, int, float, uint32_t, uint8_t*, hipStream_t); \
+  template void LaunchHashedDenseF32<I>(const uint64_t*, const I*, const float*, const I*,    \
+                                        size_t, int, uint32_t, float*, hipStream_t);
+DMLC_INSTANTIATE_FEATURE(uint32_t)
+DMLC_INSTANTIATE_FEATURE(uint64_t)
+
+}  // namespace gpu
+}  // namespace dmlc

@@ -1,0 +1,172 @@
+/*!
+ * \file src/gpu/kernels.h
+ * \brief Host-callable launchers of the CDNA4 (gfx950) ingestion kernels.
+ *
+ * Kernel inventory:
+ *   K1 line index        LaunchLineIndex          (text_kernels.hip)
+ *   K2 per-line count    LaunchTextCount          (text_kernels.hip)
+ *   K3 offsets scan      LaunchScanU64            (scan_kernels.hip)
+ *   K4 per-line fill     LaunchTextFill           (text_kernels.hip)
+ *   K5 CSV / K6 LibFM    same launchers, TextFormat::kCSV / kLibFM
+ *   K7 recordio decode   LaunchRecordIOIndex / LaunchRecordIOGather (recordio_kernels.hip)
+ *   K8 max reduce        fused into K4 (wave max + one atomicMax per wave)
+ *   K9 fp8 pack / hash   LaunchHashedDenseFP8     (feature_kernels.hip)
+ *   K10 csr concat       LaunchCSRAppend          (feature_kernels.hip)
+ *   K11 spmv / sdot      LaunchCSRSpMV, LaunchCSRSpMVT (feature_kernels.hip)
+ * All launchers are asynchronous on `stream` and never allocate or
+ * synchronise (graph-capture safe, cdna_hip_programming.md Guideline 9).
+ */
+#ifndef DMLC_GPU_KERNELS_H_
+#define DMLC_GPU_KERNELS_H_
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace dmlc {
+namespace gpu {
+
+/*! \brief padding (bytes) every device text buffer must have past its end */
+constexpr size_t kTextPadBytes = 4096;
+/*! \brief bytes per workgroup tile of the line-index kernels (256 lanes x 16 B) */
+constexpr size_t kLineTileBytes = 4096;
+
+enum class TextFormat : int { kLibSVM = 0, kLibFM = 1, kCSV = 2 };
+
+/*! \brief per-format knobs passed by value to the kernels */
+struct TextParseConfig {
+  TextFormat format{TextFormat::kLibSVM};
+  int label_column{-1};   // CSV
+  int weight_column{-1};  // CSV
+  char delimiter{','};    // CSV
+};
+
+/*! \brief per-chunk results written by the device */
+struct ChunkMeta {
+  unsigned long long nlines;     // candidate lines (K1)
+  unsigned long long nrows;      // valid rows (K3 total >> 32)
+  unsigned long long nnz;        // entries (K3 total & 0xffffffff)
+  unsigned long long max_index;  // K8
+  unsigned long long max_field;  // K8 (LibFM)
+  unsigned int flags;            // kFlag* bits
+  unsigned int pad;
+};
+constexpr unsigned kFlagWeight = 1u;
+constexpr unsigned kFlagQid = 2u;
+constexpr unsigned kFlagValue = 4u;
+constexpr unsigned kFlagField = 8u;
+constexpr unsigned kFlagNegIndex = 256u;
+constexpr unsigned kFlagOverflow = 512u;
+
+/*! \brief destination arrays of the fill pass (device pointers) */
+template <typename IndexType>
+struct FillTarget {
+  uint64_t* offset;  // row pointer (global)
+  float* label;
+  float* weight;
+  uint64_t* qid;
+  IndexType* field;  // may be null unless LibFM
+  IndexType* index;
+  float* value;
+  uint64_t row_base;  // first row written by this chunk
+  uint64_t nnz_base;  // first entry written by this chunk
+};
+
+/*! \brief scratch sizes for a chunk of `nbytes` */
+size_t LineIndexTiles(size_t nbytes);
+size_t ScanPartials(size_t n);
+
+/*!
+ * \brief K1a: count line starts per 4 KiB tile and scan the tile counts.
+ * \param tile_scratch >= LineIndexTiles(nbytes) u64
+ * \param meta meta->nlines receives the number of lines
+ */
+void LaunchLineCount(const char* text, size_t nbytes, uint64_t* tile_scratch, ChunkMeta* meta,
+                     hipStream_t stream);
+/*!
+ * \brief K1b: write the line start offsets (needs LaunchLineCount's scanned
+ *  tile_scratch); line_starts needs meta->nlines entries.
+ */
+void LaunchLineEmit(const char* text, size_t nbytes, const uint64_t* tile_scratch,
+                    uint32_t* line_starts, hipStream_t stream);
+
+/*!
+ * \brief K2: per-line (row_valid << 32 | nnz) into line_info[nlines]; sets
+ *  weight/qid flags in meta.
+ */
+void LaunchTextCount(const char* text, size_t nbytes, const uint32_t* line_starts,
+                     size_t nlines, const TextParseConfig& cfg, uint64_t* line_info,
+                     ChunkMeta* meta, hipStream_t stream);
+
+/*!
+ * \brief K3: exclusive scan of n u64 values in place; *total receives the sum.
+ * \param partials >= ScanPartials(n) + 1 u64
+ */
+void LaunchScanU64(uint64_t* data, size_t n, uint64_t* partials, uint64_t* total,
+                   hipStream_t stream);
+
+/*! \brief split the scan total into meta->nrows / meta->nnz */
+void LaunchMetaFromTotal(const uint64_t* total, ChunkMeta* meta, hipStream_t stream);
+
+/*!
+ * \brief K4 (+K5/K6/K8): parse every line into the CSR target. line_info must
+ *  hold the exclusive scan produced by K3.  Also writes the closing offset.
+ */
+template <typename IndexType>
+void LaunchTextFill(const char* text, size_t nbytes, const uint32_t* line_starts,
+                    size_t nlines, const TextParseConfig& cfg, const uint64_t* line_info,
+                    const FillTarget<IndexType>& out, uint64_t nrows, uint64_t nnz,
+                    ChunkMeta* meta, hipStream_t stream);
+
+// ----------------------------- RecordIO (K7) -----------------------------
+/*!
+ * \brief K7a: flag record heads (aligned magic + cflag 0/1) in a chunk of
+ *  `nwords` u32 words; head_pos receives compacted word positions,
+ *  meta->nlines the number of records.
+ */
+void LaunchRecordIOIndex(const uint32_t* words, size_t nwords, uint64_t* tile_scratch,
+                         uint32_t* head_pos, ChunkMeta* meta, hipStream_t stream);
+/*! \brief K7b: payload length of every record (multi-part aware) -> rec_len */
+void LaunchRecordIOLengths(const uint32_t* words, size_t nwords, const uint32_t* head_pos,
+                           size_t nrec, uint64_t* rec_len, hipStream_t stream);
+/*!
+ * \brief K7c: gather payloads contiguously: out + rec_off[i] (exclusive scan of
+ *  rec_len), re-inserting escaped magic words of multi-part records.
+ */
+void LaunchRecordIOGather(const uint32_t* words, size_t nwords, const uint32_t* head_pos,
+                          size_t nrec, const uint64_t* rec_off, uint8_t* out,
+                          hipStream_t stream);
+
+// --------------------------- features (K9-K11) ---------------------------
+/*!
+ * \brief K9: hashed dense batch in OCP fp8 e4m3: out[r, h(index) % dim] +=
+ *  value * scale, accumulated in f32 in LDS and converted with gfx950
+ *  v_cvt_pk_fp8_f32.  rows = nrows, dim <= 8192.
+ */
+template <typename IndexType>
+void LaunchHashedDenseFP8(const uint64_t* offset, const IndexType* index, const float* value,
+                          const IndexType* field, size_t nrows, int dim, float scale,
+                          uint32_t seed, uint8_t* out, hipStream_t stream);
+/*! \brief same but f32 output (reference for the fp8 path / bf16 consumers) */
+template <typename IndexType>
+void LaunchHashedDenseF32(const uint64_t* offset, const IndexType* index, const float* value,
+                          const IndexType* field, size_t nrows, int dim, uint32_t seed,
+                          float* out, hipStream_t stream);
+/*! \brief K11: y[r] = sum_j value * w[index] (+ bias), row per wave */
+template <typename IndexType>
+void LaunchCSRSpMV(const uint64_t* offset, const IndexType* index, const float* value,
+                   size_t nrows, const float* w, float bias, float* y, hipStream_t stream);
+/*! \brief K11^T: g[index] += value * d[r] (f32 atomics) */
+template <typename IndexType>
+void LaunchCSRSpMVT(const uint64_t* offset, const IndexType* index, const float* value,
+                    size_t nrows, const float* d, float* g, hipStream_t stream);
+/*! \brief K10: dst_offset[i] = src_offset[i] - src_base + dst_base for i<=nrows */
+void LaunchOffsetRebase(const uint64_t* src_offset, size_t nrows, uint64_t src_base,
+                        uint64_t dst_base, uint64_t* dst_offset, hipStream_t stream);
+/*! \brief fill n floats with v */
+void LaunchFill(float* p, size_t n, float v, hipStream_t stream);
+
+}  // namespace gpu
+}  // namespace dmlc
+#endif  // DMLC_GPU_KERNELS_H_

@@ -1,0 +1,96 @@
+/*!
+ * \file src/io/shard_reader.h
+ * \brief High-throughput reader of one InputSplit partition into
+ *  caller-provided (pinned) buffers: many parallel preads per buffer, cut at
+ *  the last record boundary, the partial record carried to the next buffer.
+ *
+ * This is the host stage of the MI355X pinned ring: the
+ * reference's ThreadedInputSplit reads 8 MiB with one fread at a time
+ * (`src/io/threaded_input_split.h:33-41`) which caps a rank at a few GB/s;
+ * here a 64-256 MiB pinned slot is filled by `nthread` concurrent preads of
+ * page-cache / NVMe data so that PCIe (not the CPU) is the bottleneck.
+ * Record semantics are exactly those of InputSplitBase (same partition
+ * boundaries, same '\n' insertion between text files, same record cut).
+ * Remote filesystems fall back to sequential Stream reads.
+ */
+#ifndef DMLC_IO_SHARD_READER_H_
+#define DMLC_IO_SHARD_READER_H_
+
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "./input_split_base.h"
+
+namespace dmlc {
+namespace io {
+
+/*! \brief fixed pool of worker threads running batches of jobs */
+class ReadPool {
+ public:
+  explicit ReadPool(int nthread);
+  ~ReadPool();
+  /*! \brief run every job (possibly in parallel) and wait for all */
+  void Run(const std::vector<std::function<void()>>& jobs);
+  int size() const { return static_cast<int>(workers_.size()); }
+
+ private:
+  void Worker();
+  std::vector<std::thread> workers_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::vector<std::function<void()>>* jobs_{nullptr};
+  std::atomic<size_t> next_{0};
+  size_t finished_{0};
+  uint64_t generation_{0};
+  bool stop_{false};
+  std::exception_ptr err_{nullptr};
+};
+
+class ShardReader {
+ public:
+  /*!
+   * \param split partition description (not owned; must outlive the reader)
+   * \param nthread parallel reads per Fill
+   */
+  ShardReader(InputSplitBase* split, int nthread);
+  ~ShardReader();
+  /*!
+   * \brief fill buf (capacity `cap`, multiple of the split's alignment) with
+   *  whole records.
+   * \return bytes written; 0 at the end of the partition
+   */
+  size_t Fill(char* buf, size_t cap);
+  /*! \brief rewind to the start of the partition */
+  void Reset();
+  /*! \brief bytes of the partition (excluding inserted newlines) */
+  size_t PartitionBytes() const { return part_bytes_; }
+  /*! \brief bytes consumed so far */
+  size_t BytesRead() const { return bytes_read_; }
+
+ private:
+  struct Seg {
+    size_t file;
+    size_t begin, end;
+    bool newline_after;  // text: insert '\n' after this segment
+  };
+  InputSplitBase* split_;
+  std::unique_ptr<ReadPool> pool_;
+  std::vector<Seg> segs_;
+  std::vector<int> fds_;
+  size_t part_bytes_{0};
+  size_t seg_idx_{0}, seg_off_{0};
+  bool pending_newline_{false};
+  std::string carry_;
+  size_t bytes_read_{0};
+  int Fd(size_t file);
+};
+
+}  // namespace io
+}  // namespace dmlc
+#endif  // DMLC_IO_SHARD_READER_H_

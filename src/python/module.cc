@@ -1,0 +1,488 @@
+/*!
+ * \file src/python/module.cc
+ * \brief pybind11 bindings: `dmlc_core_amd._dmlc`.
+ *
+ * Exposes the native runtime to Python: CPU parsers / InputSplit / RecordIO /
+ * streams (host RowBlocks as numpy arrays), the GPU DeviceParser whose HBM
+ * CSR arrays are handed to PyTorch zero-copy through DLPack capsules, and the
+ * HIP feature kernels.  No Python fallback exists for any of these: if the
+ * extension cannot load, importing the ops fails loudly.
+ */
+#include <dmlc/data.h>
+#include <dmlc/gpu/device_parser.h>
+#include <dmlc/io.h>
+#include <dmlc/logging.h>
+#include <dmlc/recordio.h>
+#include <dmlc/synthetic.h>
+#include <dmlc/timer.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../gpu/kernels.h"
+#include "./dlpack.h"
+
+namespace py = pybind11;
+using namespace dmlc;  // NOLINT
+
+namespace {
+
+// ------------------------------------------------------------------ dlpack
+struct DLCtx {
+  std::shared_ptr<void> owner;
+  std::vector<int64_t> shape;
+};
+
+void DLDeleter(DLManagedTensor* t) {
+  delete static_cast<DLCtx*>(t->manager_ctx);
+  delete t;
+}
+
+void CapsuleDeleter(PyObject* cap) {
+  // only delete if the consumer did not take ownership (renamed capsule)
+  if (PyCapsule_IsValid(cap, "dltensor")) {
+    auto* t = static_cast<DLManagedTensor*>(PyCapsule_GetPointer(cap, "dltensor"));
+    if (t != nullptr && t->deleter != nullptr) t->deleter(t);
+  }
+}
+
+template <typename T>
+DLDataType DType() {
+  DLDataType d;
+  d.lanes = 1;
+  d.bits = sizeof(T) * 8;
+  d.code = std::is_floating_point<T>::value ? kDLFloat
+                                            : (std::is_signed<T>::value ? kDLInt : kDLUInt);
+  return d;
+}
+
+template <typename T>
+py::object ToCapsule(const T* ptr, int64_t n, int device, std::shared_ptr<void> owner) {
+  auto* ctx = new DLCtx();
+  ctx->owner = std::move(owner);
+  ctx->shape = {n};
+  auto* t = new DLManagedTensor();
+  t->dl_tensor.data = const_cast<T*>(ptr);
+  t->dl_tensor.device = DLDevice{kDLROCM, device};
+  t->dl_tensor.ndim = 1;
+  t->dl_tensor.dtype = DType<T>();
+  t->dl_tensor.shape = ctx->shape.data();
+  t->dl_tensor.strides = nullptr;
+  t->dl_tensor.byte_offset = 0;
+  t->manager_ctx = ctx;
+  t->deleter = DLDeleter;
+  return py::reinterpret_steal<py::object>(PyCapsule_New(t, "dltensor", CapsuleDeleter));
+}
+
+template <typename T>
+py::array_t<T> ToNumpy(const T* ptr, size_t n) {
+  py::array_t<T> a(n);
+  if (n != 0) std::memcpy(a.mutable_data(), ptr, n * sizeof(T));
+  return a;
+}
+
+// --------------------------------------------------------------- host data
+template <typename I>
+py::dict BlockToDict(const RowBlock<I>& b) {
+  py::dict d;
+  const size_t nnz = b.offset[b.size] - b.offset[0];
+  std::vector<uint64_t> off(b.size + 1);
+  for (size_t i = 0; i <= b.size; ++i) off[i] = b.offset[i] - b.offset[0];
+  d["offset"] = ToNumpy(off.data(), off.size());
+  d["label"] = ToNumpy(b.label, b.size);
+  d["weight"] = b.weight ? py::object(ToNumpy(b.weight, b.size)) : py::none();
+  d["qid"] = b.qid ? py::object(ToNumpy(b.qid, b.size)) : py::none();
+  d["field"] = b.field ? py::object(ToNumpy(b.field + b.offset[0], nnz)) : py::none();
+  d["index"] = ToNumpy(b.index + b.offset[0], nnz);
+  d["value"] = b.value ? py::object(ToNumpy(b.value + b.offset[0], nnz)) : py::none();
+  return d;
+}
+
+template <typename I>
+class PyParser {
+ public:
+  PyParser(const std::string& uri, unsigned part, unsigned nparts, const std::string& type)
+      : p_(Parser<I>::Create(uri.c_str(), part, nparts, type.c_str())) {}
+  bool Next() {
+    py::gil_scoped_release nogil;
+    return p_->Next();
+  }
+  py::dict Value() { return BlockToDict(p_->Value()); }
+  void BeforeFirst() { p_->BeforeFirst(); }
+  size_t BytesRead() const { return p_->BytesRead(); }
+  /*! \brief parse everything, return (rows, nnz, seconds) without copying */
+  py::tuple Drain() {
+    size_t rows = 0, nnz = 0;
+    double t0 = GetTime();
+    {
+      py::gil_scoped_release nogil;
+      while (p_->Next()) {
+        const auto& b = p_->Value();
+        rows += b.size;
+        nnz += b.offset[b.size] - b.offset[0];
+      }
+    }
+    return py::make_tuple(rows, nnz, GetTime() - t0);
+  }
+
+ private:
+  std::unique_ptr<Parser<I>> p_;
+};
+
+template <typename I>
+class PyRowBlockIter {
+ public:
+  PyRowBlockIter(const std::string& uri, unsigned part, unsigned nparts, const std::string& type)
+      : it_(RowBlockIter<I>::Create(uri.c_str(), part, nparts, type.c_str())) {}
+  bool Next() { return it_->Next(); }
+  py::dict Value() { return BlockToDict(it_->Value()); }
+  void BeforeFirst() { it_->BeforeFirst(); }
+  size_t NumCol() const { return it_->NumCol(); }
+
+ private:
+  std::unique_ptr<RowBlockIter<I>> it_;
+};
+
+class PyInputSplit {
+ public:
+  PyInputSplit(const std::string& uri, unsigned part, unsigned nparts, const std::string& type,
+               const std::string& index_uri, bool shuffle, int seed, size_t batch_size)
+      : s_(index_uri.empty()
+               ? InputSplit::Create(uri.c_str(), part, nparts, type.c_str())
+               : InputSplit::Create(uri.c_str(), index_uri.c_str(), part, nparts, type.c_str(),
+                                    shuffle, seed, batch_size)) {}
+  py::object NextRecord() {
+    InputSplit::Blob b;
+    if (!s_->NextRecord(&b)) return py::none();
+    return py::bytes(static_cast<const char*>(b.dptr), b.size);
+  }
+  py::object NextChunk() {
+    InputSplit::Blob b;
+    if (!s_->NextChunk(&b)) return py::none();
+    return py::bytes(static_cast<const char*>(b.dptr), b.size);
+  }
+  py::object NextBatch(size_t n) {
+    InputSplit::Blob b;
+    if (!s_->NextBatch(&b, n)) return py::none();
+    return py::bytes(static_cast<const char*>(b.dptr), b.size);
+  }
+  void BeforeFirst() { s_->BeforeFirst(); }
+  void ResetPartition(unsigned part, unsigned nparts) { s_->ResetPartition(part, nparts); }
+  size_t TotalSize() { return s_->GetTotalSize(); }
+  void HintChunkSize(size_t n) { s_->HintChunkSize(n); }
+
+ private:
+  std::unique_ptr<InputSplit> s_;
+};
+
+class PyStream {
+ public:
+  PyStream(const std::string& uri, const std::string& mode)
+      : s_(Stream::Create(uri.c_str(), mode.c_str())) {}
+  py::bytes Read(size_t n) {
+    std::string buf(n, '\0');
+    size_t got = s_->Read(&buf[0], n);
+    buf.resize(got);
+    return py::bytes(buf);
+  }
+  void Write(const std::string& data) { s_->Write(data.data(), data.size()); }
+  void Close() { s_.reset(); }
+
+ private:
+  std::unique_ptr<Stream> s_;
+};
+
+class PyRecordIOWriter {
+ public:
+  explicit PyRecordIOWriter(const std::string& uri)
+      : s_(Stream::Create(uri.c_str(), "w")), w_(new RecordIOWriter(s_.get())) {}
+  void Write(const std::string& rec) { w_->WriteRecord(rec.data(), rec.size()); }
+  size_t Tell() const { return w_->Tell(); }
+  size_t ExceptCounter() const { return w_->except_counter(); }
+  void Close() {
+    w_.reset();
+    s_.reset();
+  }
+
+ private:
+  std::unique_ptr<Stream> s_;
+  std::unique_ptr<RecordIOWriter> w_;
+};
+
+class PyRecordIOReader {
+ public:
+  explicit PyRecordIOReader(const std::string& uri)
+      : s_(Stream::Create(uri.c_str(), "r")), r_(new RecordIOReader(s_.get())) {}
+  py::object Next() {
+    std::string rec;
+    if (!r_->NextRecord(&rec)) return py::none();
+    return py::bytes(rec);
+  }
+
+ private:
+  std::unique_ptr<Stream> s_;
+  std::unique_ptr<RecordIOReader> r_;
+};
+
+// ----------------------------------------------------------------- device
+template <typename I>
+class PyDeviceCSR {
+ public:
+  PyDeviceCSR() : csr_(std::make_shared<gpu::DeviceCSR<I>>()) {}
+  std::shared_ptr<gpu::DeviceCSR<I>> csr_;
+  size_t rows() const { return csr_->rows_; }
+  size_t nnz() const { return csr_->nnz_; }
+  uint64_t max_index() const { return csr_->max_index_; }
+  uint64_t max_field() const { return csr_->max_field_; }
+  size_t allocated_bytes() const { return csr_->AllocatedBytes(); }
+  py::dict Capsules() {
+    auto v = csr_->View();
+    std::shared_ptr<void> owner = csr_;
+    py::dict d;
+    d["offset"] = ToCapsule(v.offset, static_cast<int64_t>(v.size + 1), v.device, owner);
+    d["label"] = ToCapsule(v.label, static_cast<int64_t>(v.size), v.device, owner);
+    d["index"] = ToCapsule(v.index, static_cast<int64_t>(v.nnz), v.device, owner);
+    d["value"] = v.value ? ToCapsule(v.value, static_cast<int64_t>(v.nnz), v.device, owner)
+                         : py::none();
+    d["weight"] = v.weight ? ToCapsule(v.weight, static_cast<int64_t>(v.size), v.device, owner)
+                           : py::none();
+    d["qid"] = v.qid ? ToCapsule(v.qid, static_cast<int64_t>(v.size), v.device, owner)
+                     : py::none();
+    d["field"] = v.field ? ToCapsule(v.field, static_cast<int64_t>(v.nnz), v.device, owner)
+                         : py::none();
+    return d;
+  }
+  py::dict ToHost() {
+    auto h = gpu::CopyToHost(csr_->View());
+    return BlockToDict(h.GetBlock());
+  }
+  void Clear() { csr_->Clear(); }
+};
+
+template <typename I>
+class PyDeviceParser {
+ public:
+  PyDeviceParser(const std::string& uri, unsigned part, unsigned nparts, py::dict cfg_dict) {
+    gpu::DeviceParserConfig cfg;
+    std::map<std::string, std::string> args;
+    for (auto kv : cfg_dict) args[py::str(kv.first)] = py::str(kv.second);
+    cfg.Update(args);
+    p_.reset(gpu::DeviceParser<I>::Create(uri, part, nparts, cfg));
+  }
+  void ParseAll(PyDeviceCSR<I>& out) {  // NOLINT
+    py::gil_scoped_release nogil;
+    p_->ParseAll(out.csr_.get());
+  }
+  bool Next() {
+    py::gil_scoped_release nogil;
+    return p_->Next();
+  }
+  py::dict ValueToHost() {
+    auto h = gpu::CopyToHost(p_->Value());
+    return BlockToDict(h.GetBlock());
+  }
+  py::tuple ValueShape() const {
+    const auto& v = p_->Value();
+    return py::make_tuple(v.size, v.nnz, v.max_index);
+  }
+  void BeforeFirst() {
+    py::gil_scoped_release nogil;
+    p_->BeforeFirst();
+  }
+  size_t PartitionBytes() const { return p_->PartitionBytes(); }
+  py::dict Stats() const {
+    const auto& s = p_->Stats();
+    py::dict d;
+    d["bytes"] = s.bytes;
+    d["chunks"] = s.chunks;
+    d["rows"] = s.rows;
+    d["nnz"] = s.nnz;
+    d["wait_reader_sec"] = s.wait_reader_sec;
+    d["wait_gpu_sec"] = s.wait_gpu_sec;
+    return d;
+  }
+  uintptr_t Stream() const { return reinterpret_cast<uintptr_t>(p_->stream()); }
+
+ private:
+  std::unique_ptr<gpu::DeviceParser<I>> p_;
+};
+
+template <typename I>
+void BindIndexType(py::module_& m, const std::string& suffix) {
+  py::class_<PyParser<I>>(m, ("Parser" + suffix).c_str())
+      .def(py::init<const std::string&, unsigned, unsigned, const std::string&>(),
+           py::arg("uri"), py::arg("part") = 0, py::arg("nparts") = 1, py::arg("type") = "auto")
+      .def("next", &PyParser<I>::Next)
+      .def("value", &PyParser<I>::Value)
+      .def("before_first", &PyParser<I>::BeforeFirst)
+      .def("bytes_read", &PyParser<I>::BytesRead)
+      .def("drain", &PyParser<I>::Drain);
+  py::class_<PyRowBlockIter<I>>(m, ("RowBlockIter" + suffix).c_str())
+      .def(py::init<const std::string&, unsigned, unsigned, const std::string&>(),
+           py::arg("uri"), py::arg("part") = 0, py::arg("nparts") = 1, py::arg("type") = "auto")
+      .def("next", &PyRowBlockIter<I>::Next)
+      .def("value", &PyRowBlockIter<I>::Value)
+      .def("before_first", &PyRowBlockIter<I>::BeforeFirst)
+      .def("num_col", &PyRowBlockIter<I>::NumCol);
+  py::class_<PyDeviceCSR<I>>(m, ("DeviceCSR" + suffix).c_str())
+      .def(py::init<>())
+      .def_property_readonly("rows", &PyDeviceCSR<I>::rows)
+      .def_property_readonly("nnz", &PyDeviceCSR<I>::nnz)
+      .def_property_readonly("max_index", &PyDeviceCSR<I>::max_index)
+      .def_property_readonly("max_field", &PyDeviceCSR<I>::max_field)
+      .def_property_readonly("allocated_bytes", &PyDeviceCSR<I>::allocated_bytes)
+      .def("capsules", &PyDeviceCSR<I>::Capsules)
+      .def("to_host", &PyDeviceCSR<I>::ToHost)
+      .def("clear", &PyDeviceCSR<I>::Clear);
+  py::class_<PyDeviceParser<I>>(m, ("DeviceParser" + suffix).c_str())
+      .def(py::init<const std::string&, unsigned, unsigned, py::dict>(), py::arg("uri"),
+           py::arg("part") = 0, py::arg("nparts") = 1, py::arg("config") = py::dict())
+      .def("parse_all", &PyDeviceParser<I>::ParseAll)
+      .def("next", &PyDeviceParser<I>::Next)
+      .def("value_to_host", &PyDeviceParser<I>::ValueToHost)
+      .def("value_shape", &PyDeviceParser<I>::ValueShape)
+      .def("before_first", &PyDeviceParser<I>::BeforeFirst)
+      .def("partition_bytes", &PyDeviceParser<I>::PartitionBytes)
+      .def("stats", &PyDeviceParser<I>::Stats)
+      .def("stream", &PyDeviceParser<I>::Stream);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_dmlc, m) {
+  m.doc() = "dmlc-core for MI355X: native runtime bindings";
+  py::register_exception<dmlc::Error>(m, "DMLCError");
+  BindIndexType<uint32_t>(m, "");
+  BindIndexType<uint64_t>(m, "64");
+  py::class_<PyInputSplit>(m, "InputSplit")
+      .def(py::init<const std::string&, unsigned, unsigned, const std::string&,
+                    const std::string&, bool, int, size_t>(),
+           py::arg("uri"), py::arg("part") = 0, py::arg("nparts") = 1, py::arg("type") = "text",
+           py::arg("index_uri") = "", py::arg("shuffle") = false, py::arg("seed") = 0,
+           py::arg("batch_size") = 256)
+      .def("next_record", &PyInputSplit::NextRecord)
+      .def("next_chunk", &PyInputSplit::NextChunk)
+      .def("next_batch", &PyInputSplit::NextBatch)
+      .def("before_first", &PyInputSplit::BeforeFirst)
+      .def("reset_partition", &PyInputSplit::ResetPartition)
+      .def("total_size", &PyInputSplit::TotalSize)
+      .def("hint_chunk_size", &PyInputSplit::HintChunkSize);
+  py::class_<PyStream>(m, "Stream")
+      .def(py::init<const std::string&, const std::string&>(), py::arg("uri"),
+           py::arg("mode") = "r")
+      .def("read", &PyStream::Read)
+      .def("write", &PyStream::Write)
+      .def("close", &PyStream::Close);
+  py::class_<PyRecordIOWriter>(m, "RecordIOWriter")
+      .def(py::init<const std::string&>())
+      .def("write", &PyRecordIOWriter::Write)
+      .def("tell", &PyRecordIOWriter::Tell)
+      .def("except_counter", &PyRecordIOWriter::ExceptCounter)
+      .def("close", &PyRecordIOWriter::Close);
+  py::class_<PyRecordIOReader>(m, "RecordIOReader")
+      .def(py::init<const std::string&>())
+      .def("next", &PyRecordIOReader::Next);
+  m.def(
+      "write_synthetic",
+      [](const std::string& path, uint64_t row_begin, uint64_t row_end, const std::string& format,
+         uint64_t seed, uint32_t min_nnz, uint32_t max_nnz, uint64_t num_features,
+         uint32_t num_fields, uint32_t csv_columns, uint32_t record_bytes, uint32_t weight_every,
+         bool qid, int nthread) {
+        synthetic::Spec s;
+        s.format = format;
+        s.seed = seed;
+        s.min_nnz = min_nnz;
+        s.max_nnz = max_nnz;
+        s.num_features = num_features;
+        s.num_fields = num_fields;
+        s.csv_columns = csv_columns;
+        s.record_bytes = record_bytes;
+        s.weight_every = weight_every;
+        s.qid = qid;
+        py::gil_scoped_release nogil;
+        return synthetic::WriteRows(s, path, row_begin, row_end, nthread);
+      },
+      py::arg("path"), py::arg("row_begin"), py::arg("row_end"), py::arg("format") = "libsvm",
+      py::arg("seed") = 0, py::arg("min_nnz") = 20, py::arg("max_nnz") = 60,
+      py::arg("num_features") = 1000000, py::arg("num_fields") = 32, py::arg("csv_columns") = 29,
+      py::arg("record_bytes") = 512, py::arg("weight_every") = 0, py::arg("qid") = false,
+      py::arg("nthread") = 8);
+  // ---- HIP feature kernels on raw device pointers (torch tensors' data_ptr) ----
+  auto stream_of = [](uintptr_t s) { return reinterpret_cast<hipStream_t>(s); };
+  m.def(
+      "spmv",
+      [stream_of](uintptr_t offset, uintptr_t index, uintptr_t value, size_t nrows, uintptr_t w,
+                  float bias, uintptr_t y, uintptr_t stream, bool index64) {
+        auto* off = reinterpret_cast<const uint64_t*>(offset);
+        auto* val = reinterpret_cast<const float*>(value);
+        if (index64) {
+          gpu::LaunchCSRSpMV<uint64_t>(off, reinterpret_cast<const uint64_t*>(index), val, nrows,
+                                       reinterpret_cast<const float*>(w), bias,
+                                       reinterpret_cast<float*>(y), stream_of(stream));
+        } else {
+          gpu::LaunchCSRSpMV<uint32_t>(off, reinterpret_cast<const uint32_t*>(index), val, nrows,
+                                       reinterpret_cast<const float*>(w), bias,
+                                       reinterpret_cast<float*>(y), stream_of(stream));
+        }
+      },
+      py::arg("offset"), py::arg("index"), py::arg("value"), py::arg("nrows"), py::arg("w"),
+      py::arg("bias"), py::arg("y"), py::arg("stream"), py::arg("index64") = false);
+  m.def(
+      "spmv_t",
+      [stream_of](uintptr_t offset, uintptr_t index, uintptr_t value, size_t nrows, uintptr_t d,
+                  uintptr_t g, uintptr_t stream, bool index64) {
+        auto* off = reinterpret_cast<const uint64_t*>(offset);
+        auto* val = reinterpret_cast<const float*>(value);
+        if (index64) {
+          gpu::LaunchCSRSpMVT<uint64_t>(off, reinterpret_cast<const uint64_t*>(index), val, nrows,
+                                        reinterpret_cast<const float*>(d),
+                                        reinterpret_cast<float*>(g), stream_of(stream));
+        } else {
+          gpu::LaunchCSRSpMVT<uint32_t>(off, reinterpret_cast<const uint32_t*>(index), val, nrows,
+                                        reinterpret_cast<const float*>(d),
+                                        reinterpret_cast<float*>(g), stream_of(stream));
+        }
+      },
+      py::arg("offset"), py::arg("index"), py::arg("value"), py::arg("nrows"), py::arg("d"),
+      py::arg("g"), py::arg("stream"), py::arg("index64") = false);
+  m.def(
+      "hashed_dense",
+      [stream_of](uintptr_t offset, uintptr_t index, uintptr_t value, uintptr_t field,
+                  size_t nrows, int dim, float scale, uint32_t seed, uintptr_t out, bool fp8,
+                  uintptr_t stream, bool index64) {
+        CHECK(dim > 0 && dim <= 8192 && dim % 4 == 0) << "dim must be a multiple of 4 in (0, 8192]";
+        auto* off = reinterpret_cast<const uint64_t*>(offset);
+        auto* val = reinterpret_cast<const float*>(value);
+        if (index64) {
+          auto* idx = reinterpret_cast<const uint64_t*>(index);
+          auto* fld = reinterpret_cast<const uint64_t*>(field);
+          if (fp8) {
+            gpu::LaunchHashedDenseFP8<uint64_t>(off, idx, val, fld, nrows, dim, scale, seed,
+                                                reinterpret_cast<uint8_t*>(out), stream_of(stream));
+          } else {
+            gpu::LaunchHashedDenseF32<uint64_t>(off, idx, val, fld, nrows, dim, seed,
+                                                reinterpret_cast<float*>(out), stream_of(stream));
+          }
+        } else {
+          auto* idx = reinterpret_cast<const uint32_t*>(index);
+          auto* fld = reinterpret_cast<const uint32_t*>(field);
+          if (fp8) {
+            gpu::LaunchHashedDenseFP8<uint32_t>(off, idx, val, fld, nrows, dim, scale, seed,
+                                                reinterpret_cast<uint8_t*>(out), stream_of(stream));
+          } else {
+            gpu::LaunchHashedDenseF32<uint32_t>(off, idx, val, fld, nrows, dim, seed,
+                                                reinterpret_cast<float*>(out), stream_of(stream));
+          }
+        }
+      },
+      py::arg("offset"), py::arg("index"), py::arg("value"), py::arg("field"), py::arg("nrows"),
+      py::arg("dim"), py::arg("scale"), py::arg("seed"), py::arg("out"), py::arg("fp8"),
+      py::arg("stream"), py::arg("index64") = false);
+  m.def("gpu_device_count", &gpu::DeviceCount);
+  m.def("gpu_arch", &gpu::DeviceArchName);
+  m.def("get_time", &GetTime);
+}

@@ -1,0 +1,157 @@
+"""GPU ingestion (HIP kernels K1-K4/K8 + pinned ring) vs the CPU parsers:
+bit-identical CSR, compared row by row on concatenated blocks (block
+boundaries differ by design).  Chunk sizes are forced small so that records
+straddle chunk, file and shard boundaries."""
+import os
+
+import numpy as np
+import pytest
+
+from dmlc_core_amd import data
+import pyref
+
+pytestmark = pytest.mark.gpu
+
+
+def gpu_rows(uri, fmt, nparts=1, index64=False, **cfg):
+    parts = []
+    for r in range(nparts):
+        csr = data.GPUParser(uri, r, nparts, format=fmt, index64=index64, **cfg).parse_all()
+        h = csr.to_host()
+        parts.append(h)
+    return pyref.concat_blocks(parts)
+
+
+def cpu_rows(uri, fmt, nparts=1, index64=False):
+    blocks = []
+    for r in range(nparts):
+        blocks.extend(data.iter_blocks(uri, r, nparts, type=fmt, index64=index64))
+    return pyref.concat_blocks(blocks)
+
+
+def assert_same(a, b, field=False):
+    for k in ("label", "weight", "qid", "offset", "index", "value"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    if field:
+        np.testing.assert_array_equal(a["field"], b["field"])
+
+
+@pytest.mark.parametrize("chunk_kb", [4, 64, 4096])
+def test_libsvm_gpu_equals_cpu(tmp_path, chunk_kb):
+    p = str(tmp_path / "s.libsvm")
+    data.write_synthetic(p, 0, 4000, format="libsvm", seed=11, weight_every=5, qid=True)
+    g = gpu_rows(p, "libsvm", chunk_bytes=chunk_kb * 1024, read_threads=3)
+    c = cpu_rows(p, "libsvm")
+    assert_same(g, c)
+
+
+def test_libsvm_gpu_edge_cases(tmp_path):
+    from test_cpu_parsers import EDGE_LIBSVM
+    p = str(tmp_path / "e.libsvm")
+    with open(p, "w") as f:
+        f.write(EDGE_LIBSVM * 50)
+    assert_same(gpu_rows(p, "libsvm", chunk_bytes=4096), cpu_rows(p, "libsvm"))
+
+
+def test_long_lines_cross_lds_window(tmp_path):
+    # lines of ~20 KB (far beyond the 2 KiB per-wave LDS window) and long tokens
+    rng = np.random.default_rng(0)
+    lines = []
+    for r in range(40):
+        n = int(rng.integers(500, 1500))
+        idx = np.sort(rng.integers(0, 1 << 30, n))
+        toks = " ".join(f"{i}:{rng.random():.9f}" for i in idx)
+        lines.append(f"{r % 2} {toks} 7:{'1' * 300}.5")
+    p = str(tmp_path / "long.libsvm")
+    with open(p, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    assert_same(gpu_rows(p, "libsvm", chunk_bytes=128 * 1024), cpu_rows(p, "libsvm"))
+
+
+@pytest.mark.parametrize("nparts", [1, 2, 3, 8])
+def test_sharded_multifile_union(tmp_path, nparts):
+    d = tmp_path / "parts"
+    d.mkdir()
+    for i in range(4):
+        data.write_synthetic(str(d / f"part-{i}.libsvm"), i * 700, (i + 1) * 700, seed=4)
+    # a file without trailing newline: the split inserts one between files
+    with open(d / "part-9.libsvm", "w") as f:
+        f.write("1 1:1 2:2\n0 3:3")
+    g = gpu_rows(str(d), "libsvm", nparts=nparts, chunk_bytes=32 * 1024)
+    c = cpu_rows(str(d), "libsvm", nparts=nparts)
+    assert_same(g, c)
+    assert len(g["label"]) == 2802
+
+
+def test_libfm_gpu_equals_cpu(tmp_path):
+    p = str(tmp_path / "s.libfm")
+    data.write_synthetic(p, 0, 3000, format="libfm", seed=3)
+    with open(p, "a") as f:
+        f.write("1 1:2:0.5 3:4 5:6:7e1 junk 2\n0:2 7:8:9\n")
+    g = gpu_rows(p, "libfm", chunk_bytes=64 * 1024)
+    c = cpu_rows(p, "libfm")
+    assert_same(g, c, field=True)
+
+
+@pytest.mark.parametrize("label_column", [-1, 0, 3])
+def test_csv_gpu_equals_cpu(tmp_path, label_column):
+    p = str(tmp_path / "s.csv")
+    data.write_synthetic(p, 0, 3000, format="csv", seed=8)
+    with open(p, "a") as f:
+        f.write("1,,3\n  7 ,8,9,10\r\n")
+    uri = p + f"?label_column={label_column}"
+    g = gpu_rows(uri, "csv", chunk_bytes=64 * 1024, label_column=label_column)
+    c = cpu_rows(uri, "csv")
+    np.testing.assert_array_equal(g["label"], c["label"])
+    np.testing.assert_array_equal(g["offset"], c["offset"])
+    np.testing.assert_array_equal(g["index"], c["index"])
+    np.testing.assert_array_equal(g["value"], c["value"])
+
+
+def test_index64_gpu(tmp_path):
+    p = str(tmp_path / "b.libsvm")
+    with open(p, "w") as f:
+        f.write("1 4294967300:1 5:2\n0 18446744073709551615:3\n")
+    g = gpu_rows(p, "libsvm", index64=True)
+    c = cpu_rows(p, "libsvm", index64=True)
+    assert_same(g, c)
+
+
+def test_streaming_next_blocks(tmp_path):
+    p = str(tmp_path / "s.libsvm")
+    data.write_synthetic(p, 0, 5000, seed=2)
+    gp = data.GPUParser(p, chunk_bytes=256 * 1024)
+    for _epoch in range(2):
+        blocks = []
+        while gp.next():
+            blocks.append(gp.value_to_host())
+        assert len(blocks) > 3
+        assert_same(pyref.concat_blocks(blocks), cpu_rows(p, "libsvm"))
+        gp.before_first()
+
+
+def test_resident_parse_repeat_and_torch(tmp_path):
+    import torch
+    p = str(tmp_path / "s.libsvm")
+    data.write_synthetic(p, 0, 3000, seed=9)
+    gp = data.GPUParser(p, chunk_bytes=100 * 1024)
+    csr = data.DeviceCSR()
+    for _ in range(3):
+        gp.before_first()
+        csr.clear()
+        gp.parse_all(csr)
+        assert csr.rows == 3000
+    t = data.csr_to_torch(csr)
+    assert t["index"].device.type == "cuda"
+    c = cpu_rows(p, "libsvm")
+    np.testing.assert_array_equal(t["label"].cpu().numpy(), c["label"])
+    off = t["offset"].cpu().view(torch.int64).numpy() if t["offset"].dtype != torch.int64 else t["offset"].cpu().numpy()
+    np.testing.assert_array_equal(off.astype(np.uint64), c["offset"])
+
+
+def test_negative_index_raises_on_gpu(tmp_path):
+    p = str(tmp_path / "n.libsvm")
+    with open(p, "w") as f:
+        f.write("1 -3:1\n")
+    with pytest.raises(Exception):
+        data.GPUParser(p).parse_all()
