@@ -41,7 +41,7 @@ def parse_args():
     ap.add_argument("--chunk-mb", type=int, default=64)
     ap.add_argument("--read-threads", type=int, default=0, help="0: auto")
     ap.add_argument("--pinned-slots", type=int, default=4)
-    ap.add_argument("--device-slots", type=int, default=2)
+    ap.add_argument("--device-slots", type=int, default=3)
     ap.add_argument("--device", choices=["auto", "gpu", "cpu"], default="auto")
     return ap.parse_args()
 

@@ -21,6 +21,14 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def _load_native():
+    # One HIP runtime per process: PyTorch-ROCm bundles libamdhip64.so.7 (same
+    # SONAME as /opt/rocm's).  Loading torch first makes libdmlc.so bind to
+    # torch's copy, so device pointers, streams and events are shared; loading
+    # /opt/rocm's first would leave torch with "No HIP GPUs are available".
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # pragma: no cover - torch is optional for the C++-only path
+        pass
     try:
         from . import _dmlc  # noqa: F401
     except ImportError as err:  # pragma: no cover - exercised only when unbuilt

@@ -39,7 +39,7 @@ struct DeviceParserConfig {
   /*! \brief pinned host slots queued ahead of the GPU */
   int pinned_slots{3};
   /*! \brief device text slots (H2D of chunk k+1 overlaps parsing of chunk k) */
-  int device_slots{2};
+  int device_slots{3};
   /*! \brief parallel pread threads of the reader */
   int read_threads{8};
   /*! \brief HIP device (-1 = current) */

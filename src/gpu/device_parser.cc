@@ -111,10 +111,13 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   }
 
   ~DeviceParserImpl() override {
+    // make sure no transfer still reads a pinned slot we are about to free;
+    // destructors never throw, so errors are ignored here
+    if (copy_) (void)hipStreamSynchronize(copy_->get());
+    if (compute_) (void)hipStreamSynchronize(compute_->get());
+    for (auto& f : inflight_) iter_.Recycle(&f.slot);
+    inflight_.clear();
     iter_.Destroy();
-    // make sure no transfer still reads a pinned slot we are about to free
-    if (copy_) copy_->Synchronize();
-    if (compute_) compute_->Synchronize();
   }
 
   void BeforeFirst() override {
@@ -168,9 +171,13 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
         [reader]() { reader->Reset(); });
   }
 
-  /*! \brief queue H2D transfers until device_slots chunks are in flight */
+  /*!
+   * \brief queue H2D transfers until every device slot is in use.  The chunk
+   *  being parsed (busy_) still owns its slot: its parsed_ event has not been
+   *  recorded yet, so a copy queued into that slot would not wait for it.
+   */
   void FillPipeline() {
-    while (static_cast<int>(inflight_.size()) < cfg_.device_slots && !reader_done_) {
+    while (static_cast<int>(inflight_.size()) + busy_ < cfg_.device_slots && !reader_done_) {
       HostSlot* slot = nullptr;
       const double t0 = GetTime();
       if (!iter_.Next(&slot)) {
@@ -219,6 +226,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     if (inflight_.empty()) return false;
     Inflight cur = inflight_.front();
     inflight_.pop_front();
+    busy_ = 1;
     const size_t nbytes = cur.slot->size;
     const char* text = dtext_[cur.d]->template get<char>();
     hipStream_t s = compute_->get();
@@ -276,9 +284,12 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     tgt.value = out->value();
     tgt.row_base = row_base;
     tgt.nnz_base = nnz_base;
+    tgt.row_limit = row_base + hm.nrows;
+    tgt.nnz_limit = nnz_base + hm.nnz;
     LaunchTextFill<IndexType>(text, nbytes, lines_.get<uint32_t>(), nlines, tcfg_,
                               info_.get<uint64_t>(), tgt, hm.nrows, hm.nnz, accum, s);
     parsed_[cur.d]->Record(s);
+    busy_ = 0;
     out->rows_ = row_base + hm.nrows;
     out->nnz_ = nnz_base + hm.nnz;
     if (csv) out->has_value_ = out->nnz_ != 0;
@@ -294,6 +305,8 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   void FinishEpochMeta(DeviceCSR<IndexType>* out) {
     const ChunkMeta& acc = ReadMeta(1);
     CHECK(!(acc.flags & kFlagNegIndex)) << "negative feature index in " << cfg_.format << " input";
+    CHECK(!(acc.flags & kFlagOverflow))
+        << "internal error: GPU fill pass disagreed with the count pass (writes were dropped)";
     out->max_index_ = std::max<uint64_t>(out->max_index_, acc.max_index);
     out->max_field_ = std::max<uint64_t>(out->max_field_, acc.max_field);
     if (acc.flags & kFlagValue) out->has_value_ = true;
@@ -318,6 +331,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   ThreadedIter<HostSlot> iter_;
   std::deque<Inflight> inflight_;
   int next_dslot_{0};
+  int busy_{0};
   bool reader_done_{false};
   DeviceCSR<IndexType> block_;
   DeviceRowBlock<IndexType> view_;

@@ -69,8 +69,10 @@ struct FillTarget {
   IndexType* field;  // may be null unless LibFM
   IndexType* index;
   float* value;
-  uint64_t row_base;  // first row written by this chunk
-  uint64_t nnz_base;  // first entry written by this chunk
+  uint64_t row_base;   // first row written by this chunk
+  uint64_t nnz_base;   // first entry written by this chunk
+  uint64_t row_limit;  // rows [row_base, row_limit) may be written
+  uint64_t nnz_limit;  // entries [nnz_base, nnz_limit) may be written
 };
 
 /*! \brief scratch sizes for a chunk of `nbytes` */

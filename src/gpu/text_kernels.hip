@@ -251,8 +251,9 @@ struct LineVisitor {
   float* value{nullptr};
   IndexType* field{nullptr};
   uint64_t nnz_pos{0};
+  uint64_t nnz_limit{~0ull};
   uint64_t max_index{0}, max_field{0};
-  bool any_value{false}, neg{false};
+  bool any_value{false}, neg{false}, overflow{false};
 
   __device__ uint32_t classify(const char* tp, uint32_t len, uint32_t ord) {
     if constexpr (F == TextFormat::kCSV) {
@@ -324,6 +325,11 @@ struct LineVisitor {
   __device__ bool emit_enabled() const { return row_state == 1; }
   __device__ void emit(const char* tp, uint32_t len, uint32_t ord, uint32_t rank) {
     const uint64_t pos = nnz_pos + rank;
+    // defensive bound: a count/fill disagreement must never write out of bounds
+    if (pos >= nnz_limit) {
+      overflow = true;
+      return;
+    }
     bool bad = false;
     if constexpr (F == TextFormat::kCSV) {
       uint32_t i = 0;
@@ -415,7 +421,7 @@ __global__ __launch_bounds__(kThreads) void k_text_fill(const uint8_t* __restric
   uint8_t* win = reinterpret_cast<uint8_t*>(lds[wid]);
   const size_t nwaves = static_cast<size_t>(gridDim.x) * kWavesPerBlock;
   uint64_t wmax_index = 0, wmax_field = 0;
-  bool wany_value = false, wneg = false;
+  bool wany_value = false, wneg = false, woverflow = false;
   for (size_t line = static_cast<size_t>(blockIdx.x) * kWavesPerBlock + wid; line < nlines;
        line += nwaves) {
     const uint32_t b = line_starts[line];
@@ -429,12 +435,15 @@ __global__ __launch_bounds__(kThreads) void k_text_fill(const uint8_t* __restric
     vis.value = out.value;
     vis.field = out.field;
     vis.nnz_pos = out.nnz_base + (info & 0xffffffffull);
+    vis.nnz_limit = out.nnz_limit;
     walk_line<F, true>(text, b, e, win, cfg.delimiter, vis);
     wmax_index = vis.max_index > wmax_index ? vis.max_index : wmax_index;
     wmax_field = vis.max_field > wmax_field ? vis.max_field : wmax_field;
     wany_value |= vis.any_value;
     wneg |= vis.neg;
-    if (vis.row_state == 1) {
+    woverflow |= vis.overflow;
+    if (vis.row_state == 1 && row >= out.row_limit) woverflow = true;
+    if (vis.row_state == 1 && row < out.row_limit) {
       // broadcast the label-token results to lane 0 and write the row arrays
       const uint64_t lmask = __ballot(vis.is_label_lane);
       const int ll = lmask ? __ffsll(static_cast<long long>(lmask)) - 1 : 0;
@@ -458,12 +467,14 @@ __global__ __launch_bounds__(kThreads) void k_text_fill(const uint8_t* __restric
   const uint64_t mf = dev::wave_max(wmax_field);
   const bool av = __ballot(wany_value) != 0;
   const bool ng = __ballot(wneg) != 0;
+  const bool ov = __ballot(woverflow) != 0;
   if (lane == 0) {
     if (mi != 0) atomicMax(&meta->max_index, static_cast<unsigned long long>(mi));
     if (mf != 0) atomicMax(&meta->max_field, static_cast<unsigned long long>(mf));
     unsigned fl = 0;
     if (av) fl |= kFlagValue;
     if (ng) fl |= kFlagNegIndex;
+    if (ov) fl |= kFlagOverflow;
     if (F == TextFormat::kLibFM) fl |= kFlagField;
     if (fl != 0) atomicOr(&meta->flags, fl);
   }
