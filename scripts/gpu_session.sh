@@ -16,6 +16,9 @@ if [[ $STAGES == *test* ]]; then
   rc=$?; echo "pytest gpu rc=$rc"; tail -25 $OUT/pytest_gpu.log
   ok $rc || exit $rc
 fi
+if [[ $STAGES == *h2d* ]]; then
+  timeout -k 10 300 python scripts/h2d_bw.py > $OUT/h2d.json 2>&1; echo "h2d rc=$?"; cat $OUT/h2d.json
+fi
 if [[ $STAGES == *bench* ]]; then
   timeout -k 10 900 python bench.py $BENCH_ARGS > $OUT/bench.json 2> $OUT/bench.err
   rc=$?; echo "bench rc=$rc"; cat $OUT/bench.json; tail -5 $OUT/bench.err

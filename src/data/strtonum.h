@@ -42,11 +42,18 @@ DMLC_XINLINE bool isdigitchars(char c) {
   return (c >= '0' && c <= '9') || c == '+' || c == '-' || c == '.' || c == 'e' || c == 'E';
 }
 
+/*! \brief keeps a parameter out of template argument deduction */
+template <typename T>
+struct NonDeduced {
+  typedef T type;
+};
+
 /*!
  * \brief parse a float from [p, end) with the reference arithmetic
  * \param endptr receives the first unconsumed position
  */
-DMLC_XINLINE float StrToFloat(const char* p, const char* end, const char** endptr) {
+template <typename It>
+DMLC_XINLINE float StrToFloatT(It p, It end, typename NonDeduced<It>::type* endptr) {
 #if defined(__clang__)
 #pragma clang fp contract(off)
 #endif
@@ -99,14 +106,17 @@ DMLC_XINLINE float StrToFloat(const char* p, const char* end, const char** endpt
   if (endptr != nullptr) *endptr = p;
   return sign ? value : -value;
 }
+DMLC_XINLINE float StrToFloat(const char* p, const char* end, const char** endptr) {
+  return StrToFloatT<const char*>(p, end, endptr);
+}
 
 /*!
  * \brief parse an unsigned integer of type V from [p, end).
  *  A leading '-' sets *neg (the caller reports the error); '+' is accepted.
  *  Accumulation uses AccT, wrapping like the reference's 32-bit int.
  */
-template <typename V, typename AccT>
-DMLC_XINLINE V StrToUInt(const char* p, const char* end, const char** endptr, bool* neg) {
+template <typename V, typename AccT, typename It = const char*>
+DMLC_XINLINE V StrToUInt(It p, It end, typename NonDeduced<It>::type* endptr, bool* neg) {
   *neg = false;
   if (p != end && *p == '-') {
     *neg = true;
@@ -123,8 +133,8 @@ DMLC_XINLINE V StrToUInt(const char* p, const char* end, const char** endptr, bo
 }
 
 /*! \brief signed integer from [p, end) (two's-complement wrap on overflow) */
-template <typename V>
-DMLC_XINLINE V StrToInt(const char* p, const char* end, const char** endptr) {
+template <typename V, typename It = const char*>
+DMLC_XINLINE V StrToInt(It p, It end, typename NonDeduced<It>::type* endptr) {
   bool sign = true;
   if (p != end && *p == '-') {
     sign = false;
@@ -143,36 +153,41 @@ template <typename T>
 struct Str2T;
 template <>
 struct Str2T<float> {
-  DMLC_XINLINE static float get(const char* b, const char* e, bool* bad) {
+  template <typename It>
+  DMLC_XINLINE static float get(It b, It e, bool* bad) {
     *bad = false;
-    return StrToFloat(b, e, nullptr);
+    return StrToFloatT<It>(b, e, nullptr);
   }
 };
 template <>
 struct Str2T<uint32_t> {
   // reference: strtouint<int> -> 32-bit accumulation
-  DMLC_XINLINE static uint32_t get(const char* b, const char* e, bool* bad) {
-    return StrToUInt<uint32_t, uint32_t>(b, e, nullptr, bad);
+  template <typename It>
+  DMLC_XINLINE static uint32_t get(It b, It e, bool* bad) {
+    return StrToUInt<uint32_t, uint32_t, It>(b, e, nullptr, bad);
   }
 };
 template <>
 struct Str2T<uint64_t> {
-  DMLC_XINLINE static uint64_t get(const char* b, const char* e, bool* bad) {
-    return StrToUInt<uint64_t, uint64_t>(b, e, nullptr, bad);
+  template <typename It>
+  DMLC_XINLINE static uint64_t get(It b, It e, bool* bad) {
+    return StrToUInt<uint64_t, uint64_t, It>(b, e, nullptr, bad);
   }
 };
 template <>
 struct Str2T<int32_t> {
-  DMLC_XINLINE static int32_t get(const char* b, const char* e, bool* bad) {
+  template <typename It>
+  DMLC_XINLINE static int32_t get(It b, It e, bool* bad) {
     *bad = false;
-    return StrToInt<int32_t>(b, e, nullptr);
+    return StrToInt<int32_t, It>(b, e, nullptr);
   }
 };
 template <>
 struct Str2T<int64_t> {
-  DMLC_XINLINE static int64_t get(const char* b, const char* e, bool* bad) {
+  template <typename It>
+  DMLC_XINLINE static int64_t get(It b, It e, bool* bad) {
     *bad = false;
-    return StrToInt<int64_t>(b, e, nullptr);
+    return StrToInt<int64_t, It>(b, e, nullptr);
   }
 };
 
@@ -181,13 +196,13 @@ struct Str2T<int64_t> {
  * \return number of values parsed (0 when the token has no digitchar);
  *  *bad is set when an unsigned field had a minus sign
  */
-template <typename T1, typename T2>
-DMLC_XINLINE int ParsePair(const char* begin, const char* end, T1* v1, T2* v2, bool* bad) {
+template <typename T1, typename T2, typename It = const char*>
+DMLC_XINLINE int ParsePair(It begin, It end, T1* v1, T2* v2, bool* bad) {
   *bad = false;
-  const char* p = begin;
+  It p = begin;
   while (p != end && !isdigitchars(*p)) ++p;
   if (p == end) return 0;
-  const char* q = p;
+  It q = p;
   while (q != end && isdigitchars(*q)) ++q;
   bool b1 = false;
   *v1 = Str2T<T1>::get(p, q, &b1);
@@ -208,14 +223,13 @@ DMLC_XINLINE int ParsePair(const char* begin, const char* end, T1* v1, T2* v2, b
 }
 
 /*! \brief parse `v1:v2[:v3]` inside [begin, end) (one LibFM token) */
-template <typename T1, typename T2, typename T3>
-DMLC_XINLINE int ParseTriple(const char* begin, const char* end, T1* v1, T2* v2, T3* v3,
-                             bool* bad) {
+template <typename T1, typename T2, typename T3, typename It = const char*>
+DMLC_XINLINE int ParseTriple(It begin, It end, T1* v1, T2* v2, T3* v3, bool* bad) {
   *bad = false;
-  const char* p = begin;
+  It p = begin;
   while (p != end && !isdigitchars(*p)) ++p;
   if (p == end) return 0;
-  const char* q = p;
+  It q = p;
   while (q != end && isdigitchars(*q)) ++q;
   bool b1 = false, b2 = false, b3 = false;
   *v1 = Str2T<T1>::get(p, q, &b1);

@@ -8,14 +8,17 @@
  *    16-byte vector (global_load_dwordx4), classifies EOL bytes with a SWAR
  *    compare, and line starts are compacted with a workgroup scan.
  *  - K2/K4 run ONE WAVE64 PER LINE.  The wave streams its line through a
- *    2 KiB LDS window (two 1 KiB pieces, 16 B per lane, ds_write_b128): token
- *    starts are found from the registers just loaded (blank/delimiter SWAR
- *    masks + a shuffle for the previous byte), token ordinals come from a wave
- *    prefix sum, and every lane parses the tokens that start in its 16 bytes
- *    straight out of LDS (tokens that run past the window fall back to global
- *    memory).  K4 writes index/value at offset + rank, where rank is a second
- *    wave prefix sum over valid feature tokens, and reduces max(index) with one
- *    atomicMax per wave (K8).
+ *    2 KiB LDS window (two 1 KiB pieces, 16 B per lane, ds_write_b128).  Per
+ *    lane, SWAR compares of the 16 bytes just loaded give separator / digit /
+ *    delimiter bit masks; token starts, token ends (next separator: own mask,
+ *    else the first higher lane from a ballot + one shuffle, else the next
+ *    piece) and "token has a digit" are pure bit arithmetic, token ordinals
+ *    come from a wave prefix sum.  The owning lane then pulls the token's
+ *    bytes out of LDS with 3 x ds_read_b128 and a funnel shift into 8 VGPRs
+ *    and runs the shared parser on a register iterator (no dependent load per
+ *    byte); tokens > 32 B use the LDS/HBM pointer path.  K4 writes index/value
+ *    at offset + rank (a wave prefix sum over valid feature tokens) and
+ *    reduces max(index) with one atomicMax per wave (K8).
  *  - Number parsing is the shared host/device code of src/data/strtonum.h,
  *    so the device CSR is bit-identical to the CPU parsers' output.
  */
@@ -91,19 +94,83 @@ __global__ __launch_bounds__(kThreads) void k_line_emit(const uint8_t* __restric
 }
 
 // --------------------------------------------------------------- lines
-struct LineWindow {
-  uint8_t* win;    // this wave's LDS window (kWindow bytes)
-  uint32_t wbase;  // text position of win[0]
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+/*!
+ * \brief up to 32 bytes of a token held in 8 VGPRs; operator++ funnel-shifts
+ *  the window (v_alignbyte_b32), so the shared strtonum.h parsers run on
+ *  registers without a dependent memory load per byte.
+ */
+struct RegIter {
+  uint32_t w[8];
+  uint32_t pos;
+  __device__ __forceinline__ char operator*() const { return static_cast<char>(w[0] & 0xffu); }
+  __device__ __forceinline__ RegIter& operator++() {
+#pragma unroll
+    for (int i = 0; i < 7; ++i) w[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], 1);
+    w[7] >>= 8;
+    ++pos;
+    return *this;
+  }
+  __device__ __forceinline__ bool operator!=(const RegIter& o) const { return pos != o.pos; }
+  __device__ __forceinline__ bool operator==(const RegIter& o) const { return pos == o.pos; }
 };
 
-__device__ __forceinline__ uint8_t byte_at(const uint8_t* __restrict__ text, const LineWindow& w,
-                                           uint32_t q) {
-  const uint32_t off = q - w.wbase;
-  return off < kWindow ? w.win[off] : text[q];
-}
+/*! \brief one token of the current line: [p, q) in chunk coordinates */
+struct TokenRef {
+  const uint8_t* text;
+  const uint8_t* win;  // LDS window (2 KiB), win[0] = text[wbase]
+  uint32_t wbase;
+  uint32_t p, q;
+  bool has_digit;
+
+  __device__ __forceinline__ uint32_t len() const { return q - p; }
+  /*! \brief tokens of <= 32 bytes are parsed from registers */
+  __device__ __forceinline__ bool fast() const { return q - p <= 32; }
+  __device__ __forceinline__ RegIter reg() const {
+    // 3 x ds_read_b128 from the 16-byte aligned LDS offset, then a byte funnel
+    // shift by (offset & 15): bytes [p, p+32) land in w[0..7]
+    const uint32_t o = p - wbase;
+    const uint4* src = reinterpret_cast<const uint4*>(win + (o & ~15u));
+    const uint4 a = src[0], b = src[1], c = src[2];
+    uint32_t d[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+    const uint32_t s = o & 15u;
+    if (s & 8u) {
+#pragma unroll
+      for (int i = 0; i < 10; ++i) d[i] = d[i + 2];
+    }
+    if (s & 4u) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) d[i] = d[i + 1];
+    }
+    RegIter it;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) it.w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], s & 3u);
+    it.pos = 0;
+    return it;
+  }
+  /*! \brief generic pointer to the token (LDS if inside the window, else HBM) */
+  __device__ __forceinline__ const char* ptr() const {
+    return (q - wbase <= kWindow) ? reinterpret_cast<const char*>(win + (p - wbase))
+                                  : reinterpret_cast<const char*>(text + p);
+  }
+  /*! \brief call fn(begin, end) with register iterators (fast) or pointers */
+  template <class Fn>
+  __device__ __forceinline__ void with_bytes(Fn fn) const {
+    if (fast()) {
+      RegIter b = reg();
+      RegIter e = b;
+      e.pos = q - p;
+      fn(b, e);
+    } else {
+      const char* b = ptr();
+      fn(b, b + (q - p));
+    }
+  }
+};
 
 template <TextFormat F>
-__device__ __forceinline__ bool is_sep(uint8_t c, char delim) {
+__device__ __forceinline__ bool is_sep_byte(uint8_t c, char delim) {
   if constexpr (F == TextFormat::kCSV) {
     return c == static_cast<uint8_t>(delim) || c == '\n' || c == '\r';
   } else {
@@ -111,71 +178,170 @@ __device__ __forceinline__ bool is_sep(uint8_t c, char delim) {
   }
 }
 
-/*! \brief token-start bits of the 16 bytes at `pos` (within line [b, e)) */
+/*! \brief exact per-byte flags (bit j) of '0' <= byte <= '9' */
+__device__ __forceinline__ uint32_t digit_mask(uint4 v) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t x = w[i];
+    const uint32_t lo7 = x & 0x7F7F7F7Fu;
+    // hasbetween(x, '0'-1, '9'+1): high bit of each byte with 0x2F < c < 0x3A
+    const uint32_t t =
+        ((0x7F7F7F7Fu + 0x3A3A3A3Au) - lo7) & ~x & (lo7 + (0x7F7F7F7Fu - 0x2F2F2F2Fu)) & 0x80808080u;
+    const uint32_t g = ((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u);
+    m |= g << (4 * i);
+  }
+  return m;
+}
+
+__device__ __forceinline__ uint32_t digitchar_mask(uint4 v) {
+  return digit_mask(v) | dev::byte_eq_mask(v, '+') | dev::byte_eq_mask(v, '-') |
+         dev::byte_eq_mask(v, '.') | dev::byte_eq_mask(v, 'e') | dev::byte_eq_mask(v, 'E');
+}
+
+/*! \brief per-lane masks of one 16-byte vector of a line [b, e) */
+struct LaneMasks {
+  uint32_t sep;    // separator bytes, plus every byte outside [b, e)
+  uint32_t dig;    // digit characters inside [b, e)
+  uint32_t delim;  // CSV delimiter bytes inside [b, e)
+  uint32_t eol;    // EOL bytes
+};
+
 template <TextFormat F>
-__device__ __forceinline__ uint32_t token_start_mask(uint4 v, uint8_t prevb, uint32_t pos,
-                                                     uint32_t b, uint32_t e, char delim) {
+__device__ __forceinline__ LaneMasks lane_masks(uint4 v, uint32_t pos, uint32_t b, uint32_t e,
+                                                char delim) {
   uint32_t valid = 0xFFFFu;
   if (pos + 16 > e) valid = pos >= e ? 0u : ((1u << (e - pos)) - 1u);
-  if (pos < b) valid &= ~((1u << (b - pos)) - 1u);
-  const uint32_t eol = eol_mask(v);
+  if (pos < b) valid &= b - pos >= 16 ? 0u : ~((1u << (b - pos)) - 1u);
+  LaneMasks m;
+  m.eol = eol_mask(v);
   if constexpr (F == TextFormat::kCSV) {
-    const uint32_t dl = dev::byte_eq_mask(v, static_cast<uint8_t>(delim));
-    const uint32_t prev_dl = prevb == static_cast<uint8_t>(delim) ? 1u : 0u;
-    uint32_t starts = ~eol & ((dl << 1) | prev_dl);
-    if (b >= pos && b < pos + 16) starts |= 1u << (b - pos);  // the line start is a field
-    return starts & valid;
+    m.delim = dev::byte_eq_mask(v, static_cast<uint8_t>(delim)) & valid;
+    m.sep = (m.eol | m.delim | ~valid) & 0xFFFFu;
   } else {
-    const uint32_t sep = eol | dev::byte_eq_mask(v, ' ') | dev::byte_eq_mask(v, '\t');
-    const uint32_t prev_sep = (prevb == ' ' || prevb == '\t' || prevb == '\n' || prevb == '\r') ? 1u : 0u;
-    return ~sep & ((sep << 1) | prev_sep) & valid;
+    m.delim = 0;
+    m.sep = (m.eol | dev::byte_eq_mask(v, ' ') | dev::byte_eq_mask(v, '\t') | ~valid) & 0xFFFFu;
   }
+  m.dig = digitchar_mask(v) & valid;
+  return m;
 }
 
 /*!
- * \brief stream line [b, e) through the wave's LDS window and call
- *  `vis.classify(...)` for every token (phase 1); when `kEmit`, tokens whose
- *  classify returned 1 are passed to `vis.emit(..., rank)` (phase 2) where rank
- *  counts the earlier such tokens of the line.
+ * \brief first set bit at or after each lane's 16-byte range, searched over
+ *  the lanes above it and then the next piece: returns the chunk position or
+ *  kNone.  Must be called by the whole (converged) wave.
+ */
+__device__ __forceinline__ uint32_t next_after_lane(uint32_t mask, uint32_t pstart,
+                                                    uint32_t next_piece_first) {
+  const int lane = dev::lane_id();
+  const uint64_t bal = __ballot(mask != 0);
+  const uint64_t higher = lane == 63 ? 0ull : (bal & (~0ull << (lane + 1)));
+  const int nl = higher ? __ffsll(static_cast<long long>(higher)) - 1 : lane;
+  const uint32_t m2 = __shfl(mask, nl, dev::kWave);
+  if (higher == 0) return next_piece_first;
+  return pstart + 16u * nl + static_cast<uint32_t>(__ffs(m2) - 1);
+}
+
+/*! \brief first set bit of a whole piece (wave-uniform), or kNone */
+__device__ __forceinline__ uint32_t first_in_piece(uint32_t mask, uint32_t pstart) {
+  const uint64_t bal = __ballot(mask != 0);
+  if (bal == 0) return kNone;
+  const int fl = __ffsll(static_cast<long long>(bal)) - 1;
+  const uint32_t m2 = __shfl(mask, fl, dev::kWave);
+  return pstart + 16u * fl + static_cast<uint32_t>(__ffs(m2) - 1);
+}
+
+/*!
+ * \brief stream line [b, e) through the wave's LDS window and visit its
+ *  tokens.  Token boundaries and "contains a digit" come from per-lane byte
+ *  masks + ballots (no byte loops); numbers are parsed from registers.
+ *  Phase 1 calls vis.classify(tok, ord) for every token; with kEmit, tokens
+ *  for which vis.selected(tok, ord) holds are passed to vis.emit(tok, ord,
+ *  rank), rank = number of earlier selected tokens of the line.
  */
 template <TextFormat F, bool kEmit, class Visitor>
-__device__ void walk_line(const uint8_t* __restrict__ text, uint32_t b, uint32_t e,
-                          uint8_t* win, char delim, Visitor& vis) {
+__device__ void walk_line(const uint8_t* __restrict__ text, uint32_t b, uint32_t e, uint8_t* win,
+                          char delim, Visitor& vis) {
   const int lane = dev::lane_id();
-  LineWindow w{win, b & ~15u};
+  uint32_t wbase = b & ~15u;
   uint4* win4 = reinterpret_cast<uint4*>(win);
   auto load = [&](uint32_t addr) -> uint4 {
     return addr < e ? *reinterpret_cast<const uint4*>(text + addr) : make_uint4(0, 0, 0, 0);
   };
-  uint4 vcur = load(w.wbase + 16 * lane);
-  uint4 vnext = load(w.wbase + kPiece + 16 * lane);
+  uint4 vcur = load(wbase + 16 * lane);
+  uint4 vnext = load(wbase + kPiece + 16 * lane);
   win4[lane] = vcur;
   win4[64 + lane] = vnext;
+  LaneMasks mcur = lane_masks<F>(vcur, wbase + 16 * lane, b, e, delim);
+  LaneMasks mnext = lane_masks<F>(vnext, wbase + kPiece + 16 * lane, b, e, delim);
   dev::wave_sync();
-  uint32_t tok_base = 0;   // tokens in earlier pieces (wave-uniform)
-  uint32_t rank_base = 0;  // emitted tokens in earlier pieces (wave-uniform)
-  uint8_t prev_last = '\n';
-  for (uint32_t pstart = w.wbase; pstart < e; pstart += kPiece) {
+  uint32_t tok_base = 0, rank_base = 0;
+  bool prev_sep = true;     // byte before the line start behaves as a separator
+  bool prev_delim = false;  // CSV: previous byte was the delimiter
+  for (uint32_t pstart = wbase; pstart < e; pstart += kPiece) {
     const uint32_t pos = pstart + 16 * lane;
-    uint8_t prevb = static_cast<uint8_t>(__shfl_up(vcur.w >> 24, 1, dev::kWave));
-    if (lane == 0) prevb = prev_last;
-    const uint32_t smask = token_start_mask<F>(vcur, prevb, pos, b, e, delim);
+    // token starts of this lane's 16 bytes
+    uint32_t starts;
+    {
+      const uint32_t up_sep = __shfl_up(mcur.sep, 1, dev::kWave);
+      const uint32_t up_delim = __shfl_up(mcur.delim, 1, dev::kWave);
+      if constexpr (F == TextFormat::kCSV) {
+        const uint32_t pd = lane == 0 ? (prev_delim ? 1u : 0u) : ((up_delim >> 15) & 1u);
+        starts = ~mcur.eol & ~(mcur.sep & ~mcur.delim) & ((mcur.delim << 1) | pd);
+        if (b >= pos && b < pos + 16) starts |= 1u << (b - pos);
+        starts &= 0xFFFFu;
+      } else {
+        const uint32_t ps = lane == 0 ? (prev_sep ? 1u : 0u) : ((up_sep >> 15) & 1u);
+        starts = ~mcur.sep & ((mcur.sep << 1) | ps) & 0xFFFFu;
+      }
+    }
+    const uint32_t next_sep_piece = first_in_piece(mnext.sep, pstart + kPiece);
+    const uint32_t next_dig_piece = first_in_piece(mnext.dig, pstart + kPiece);
+    const uint32_t nsep = next_after_lane(mcur.sep, pstart, next_sep_piece);
+    const uint32_t ndig = next_after_lane(mcur.dig, pstart, next_dig_piece);
     uint32_t ntok_total;
-    const uint32_t tok_excl = dev::wave_excl_scan<uint32_t>(__popc(smask), &ntok_total);
+    const uint32_t tok_excl = dev::wave_excl_scan<uint32_t>(__popc(starts), &ntok_total);
+
+    auto make_token = [&](int j) -> TokenRef {
+      TokenRef t;
+      t.text = text;
+      t.win = win;
+      t.wbase = pstart;
+      t.p = pos + j;
+      const uint32_t own = mcur.sep & ~((1u << j) - 1u);
+      uint32_t q = own ? pos + (__ffs(own) - 1) : nsep;
+      bool scanned = false;
+      if (q == kNone) {
+        // token runs past the next piece: scan HBM (rare: > 1 KiB tokens)
+        q = pstart + 2 * kPiece;
+        while (q < e && !is_sep_byte<F>(text[q], delim)) ++q;
+        scanned = true;
+      }
+      if (q > e) q = e;
+      t.q = q;
+      const uint32_t ownd = mcur.dig & ~((1u << j) - 1u);
+      const uint32_t fd = ownd ? pos + (__ffs(ownd) - 1) : ndig;
+      if (fd != kNone) {
+        t.has_digit = fd < q;
+      } else if (scanned) {
+        bool hd = false;
+        for (uint32_t r = pstart + 2 * kPiece; r < q; ++r) hd |= data::isdigitchars(text[r]);
+        t.has_digit = hd;
+      } else {
+        t.has_digit = false;
+      }
+      return t;
+    };
+
     // phase 1: classify
-    uint32_t m = smask;
+    uint32_t m = starts;
     uint32_t ord = tok_base + tok_excl;
     uint32_t nsel = 0;
     while (m != 0) {
       const int j = __ffs(m) - 1;
       m &= m - 1;
-      const uint32_t p = pos + j;
-      uint32_t q = p;
-      while (q < e && !is_sep<F>(byte_at(text, w, q), delim)) ++q;
-      const char* tp = (q - w.wbase <= kWindow)
-                           ? reinterpret_cast<const char*>(w.win + (p - w.wbase))
-                           : reinterpret_cast<const char*>(text + p);
-      nsel += vis.classify(tp, q - p, ord);
+      nsel += vis.classify(make_token(j), ord);
       ++ord;
     }
     vis.after_classify(tok_base, ntok_total);
@@ -183,52 +349,54 @@ __device__ void walk_line(const uint8_t* __restrict__ text, uint32_t b, uint32_t
       uint32_t nsel_total;
       uint32_t rank = rank_base + dev::wave_excl_scan<uint32_t>(nsel, &nsel_total);
       if (vis.emit_enabled()) {
-        m = smask;
+        m = starts;
         ord = tok_base + tok_excl;
         while (m != 0) {
           const int j = __ffs(m) - 1;
           m &= m - 1;
-          const uint32_t p = pos + j;
-          uint32_t q = p;
-          while (q < e && !is_sep<F>(byte_at(text, w, q), delim)) ++q;
-          const char* tp = (q - w.wbase <= kWindow)
-                               ? reinterpret_cast<const char*>(w.win + (p - w.wbase))
-                               : reinterpret_cast<const char*>(text + p);
-          if (vis.selected(tp, q - p, ord)) vis.emit(tp, q - p, ord, rank++);
+          const TokenRef t = make_token(j);
+          if (vis.selected(t, ord)) vis.emit(t, ord, rank++);
           ++ord;
         }
       }
       rank_base += nsel_total;
     }
     tok_base += ntok_total;
-    prev_last = static_cast<uint8_t>(__shfl(vcur.w >> 24, 63, dev::kWave));
+    prev_sep = (__shfl(mcur.sep, 63, dev::kWave) >> 15) & 1u;
+    prev_delim = (__shfl(mcur.delim, 63, dev::kWave) >> 15) & 1u;
     // slide the window by one piece
     dev::wave_sync();
     vcur = vnext;
+    mcur = mnext;
     vnext = load(pstart + 2 * kPiece + 16 * lane);
+    mnext = lane_masks<F>(vnext, pstart + 2 * kPiece + 16 * lane, b, e, delim);
     win4[lane] = vcur;
     win4[64 + lane] = vnext;
-    w.wbase += kPiece;
     dev::wave_sync();
   }
 }
 
-__device__ __forceinline__ bool has_digitchar(const char* tp, uint32_t len) {
-  for (uint32_t i = 0; i < len; ++i) {
-    if (data::isdigitchars(tp[i])) return true;
+/*! \brief "qid:" prefix test on a token */
+__device__ __forceinline__ bool tok_is_qid(const TokenRef& t) {
+  if (t.len() < 4) return false;
+  if (t.fast()) {
+    const RegIter r = t.reg();
+    return (r.w[0] & 0xFFFFFFFFu) == 0x3A646971u;  // "qid:" little-endian
   }
-  return false;
+  const char* c = t.ptr();
+  return c[0] == 'q' && c[1] == 'i' && c[2] == 'd' && c[3] == ':';
 }
-__device__ __forceinline__ bool is_qid(const char* tp, uint32_t len) {
-  return len >= 4 && tp[0] == 'q' && tp[1] == 'i' && tp[2] == 'd' && tp[3] == ':';
-}
-/*! \brief `a[:b[:c]]` has at least two parts (LibFM feature rule) */
-__device__ __forceinline__ bool has_two_parts(const char* tp, uint32_t len) {
-  uint32_t i = 0;
-  while (i < len && !data::isdigitchars(tp[i])) ++i;
-  if (i == len) return false;
-  while (i < len && data::isdigitchars(tp[i])) ++i;
-  return i < len && tp[i] == ':';
+
+/*! \brief LibFM rule: the first digit-character run is followed by ':' */
+__device__ __forceinline__ bool tok_two_parts(const TokenRef& t) {
+  bool ok = false;
+  t.with_bytes([&](auto p, auto end) {
+    while (p != end && !data::isdigitchars(*p)) ++p;
+    if (p == end) return;
+    while (p != end && data::isdigitchars(*p)) ++p;
+    ok = p != end && *p == ':';
+  });
+  return ok;
 }
 
 /*!
@@ -237,15 +405,13 @@ __device__ __forceinline__ bool has_two_parts(const char* tp, uint32_t len) {
  */
 template <TextFormat F, typename IndexType>
 struct LineVisitor {
-  // configuration
   int label_col, weight_col;
   // label-token state (only the lane owning token 0 / the label column sets it)
   bool is_label_lane{false}, label_ok{false}, has_weight{false};
   float label{0.0f}, weight{1.0f};
   bool is_qid_lane{false};
   uint64_t qid{0};
-  // wave-uniform row validity
-  int row_state{0};  // 0 unknown, 1 ok, -1 invalid
+  int row_state{0};  // 0 unknown, 1 ok, -1 invalid (wave-uniform)
   // fill target (phase 2)
   IndexType* index{nullptr};
   float* value{nullptr};
@@ -255,21 +421,22 @@ struct LineVisitor {
   uint64_t max_index{0}, max_field{0};
   bool any_value{false}, neg{false}, overflow{false};
 
-  __device__ uint32_t classify(const char* tp, uint32_t len, uint32_t ord) {
+  __device__ uint32_t classify(const TokenRef& t, uint32_t ord) {
     if constexpr (F == TextFormat::kCSV) {
-      if (static_cast<int>(ord) == label_col) {
-        is_label_lane = true;
-        label_ok = true;
-        uint32_t i = 0;
-        while (i < len && data::isspace(tp[i])) ++i;
-        label = data::StrToFloat(tp + i, tp + len, nullptr);
-        return 0;
-      }
-      if (static_cast<int>(ord) == weight_col) {
-        has_weight = true;
-        uint32_t i = 0;
-        while (i < len && data::isspace(tp[i])) ++i;
-        weight = data::StrToFloat(tp + i, tp + len, nullptr);
+      if (static_cast<int>(ord) == label_col || static_cast<int>(ord) == weight_col) {
+        float v = 0.0f;
+        t.with_bytes([&](auto p, auto end) {
+          while (p != end && data::isspace(*p)) ++p;
+          v = data::StrToFloatT(p, end, static_cast<decltype(p)*>(nullptr));
+        });
+        if (static_cast<int>(ord) == label_col) {
+          is_label_lane = true;
+          label_ok = true;
+          label = v;
+        } else {
+          has_weight = true;
+          weight = v;
+        }
         return 0;
       }
       return 1;
@@ -277,8 +444,11 @@ struct LineVisitor {
       if (ord == 0) {
         is_label_lane = true;
         float l = 0.0f, wgt = 0.0f;
-        bool bad;
-        const int r = data::ParsePair<float, float>(tp, tp + len, &l, &wgt, &bad);
+        int r = 0;
+        if (t.has_digit) {
+          bool bad;
+          t.with_bytes([&](auto p, auto end) { r = data::ParsePair<float, float>(p, end, &l, &wgt, &bad); });
+        }
         label_ok = r >= 1;
         if (r >= 1) label = l;
         if (r == 2) {
@@ -288,28 +458,32 @@ struct LineVisitor {
         return 0;
       }
       if constexpr (F == TextFormat::kLibSVM) {
-        if (ord == 1 && is_qid(tp, len)) {
+        if (ord == 1 && tok_is_qid(t)) {
           is_qid_lane = true;
-          qid = static_cast<uint64_t>(data::StrToInt<int64_t>(tp + 4, tp + len, nullptr));
+          t.with_bytes([&](auto p, auto end) {
+            ++p; ++p; ++p; ++p;
+            qid = static_cast<uint64_t>(
+                data::StrToInt<int64_t>(p, end, static_cast<decltype(p)*>(nullptr)));
+          });
           return 0;
         }
-        return has_digitchar(tp, len) ? 1u : 0u;
+        return t.has_digit ? 1u : 0u;
       } else {
-        return has_two_parts(tp, len) ? 1u : 0u;
+        return (t.has_digit && tok_two_parts(t)) ? 1u : 0u;
       }
     }
   }
   /*! \brief same decision as classify, without side effects (phase 2) */
-  __device__ bool selected(const char* tp, uint32_t len, uint32_t ord) const {
+  __device__ bool selected(const TokenRef& t, uint32_t ord) const {
     if constexpr (F == TextFormat::kCSV) {
       return static_cast<int>(ord) != label_col && static_cast<int>(ord) != weight_col;
     } else {
       if (ord == 0) return false;
       if constexpr (F == TextFormat::kLibSVM) {
-        if (ord == 1 && is_qid(tp, len)) return false;
-        return has_digitchar(tp, len);
+        if (ord == 1 && tok_is_qid(t)) return false;
+        return t.has_digit;
       } else {
-        return has_two_parts(tp, len);
+        return t.has_digit && tok_two_parts(t);
       }
     }
   }
@@ -323,7 +497,7 @@ struct LineVisitor {
     }
   }
   __device__ bool emit_enabled() const { return row_state == 1; }
-  __device__ void emit(const char* tp, uint32_t len, uint32_t ord, uint32_t rank) {
+  __device__ void emit(const TokenRef& t, uint32_t ord, uint32_t rank) {
     const uint64_t pos = nnz_pos + rank;
     // defensive bound: a count/fill disagreement must never write out of bounds
     if (pos >= nnz_limit) {
@@ -332,16 +506,19 @@ struct LineVisitor {
     }
     bool bad = false;
     if constexpr (F == TextFormat::kCSV) {
-      uint32_t i = 0;
-      while (i < len && data::isspace(tp[i])) ++i;
-      const float v = data::StrToFloat(tp + i, tp + len, nullptr);
+      float v = 0.0f;
+      t.with_bytes([&](auto p, auto end) {
+        while (p != end && data::isspace(*p)) ++p;
+        v = data::StrToFloatT(p, end, static_cast<decltype(p)*>(nullptr));
+      });
       index[pos] = static_cast<IndexType>(rank);
       value[pos] = v;
       if (rank > max_index) max_index = rank;
     } else if constexpr (F == TextFormat::kLibSVM) {
       IndexType idx = 0;
       float v = 0.0f;
-      const int r = data::ParsePair<IndexType, float>(tp, tp + len, &idx, &v, &bad);
+      int r = 0;
+      t.with_bytes([&](auto p, auto end) { r = data::ParsePair<IndexType, float>(p, end, &idx, &v, &bad); });
       index[pos] = idx;
       value[pos] = r == 2 ? v : 1.0f;
       any_value |= (r == 2);
@@ -349,7 +526,10 @@ struct LineVisitor {
     } else {
       IndexType fid = 0, idx = 0;
       float v = 0.0f;
-      const int r = data::ParseTriple<IndexType, IndexType, float>(tp, tp + len, &fid, &idx, &v, &bad);
+      int r = 0;
+      t.with_bytes([&](auto p, auto end) {
+        r = data::ParseTriple<IndexType, IndexType, float>(p, end, &fid, &idx, &v, &bad);
+      });
       field[pos] = fid;
       index[pos] = idx;
       value[pos] = r == 3 ? v : 1.0f;
@@ -380,19 +560,18 @@ __global__ __launch_bounds__(kThreads) void k_text_count(const uint8_t* __restri
     LineVisitor<F, uint32_t> vis;
     vis.label_col = cfg.label_column;
     vis.weight_col = cfg.weight_column;
-    // count-only: classify returns 1 for feature tokens; sum them
     struct Counter {
       LineVisitor<F, uint32_t>* v;
       uint32_t nfeat{0};
-      __device__ uint32_t classify(const char* tp, uint32_t len, uint32_t ord) {
-        uint32_t s = v->classify(tp, len, ord);
+      __device__ uint32_t classify(const TokenRef& t, uint32_t ord) {
+        const uint32_t s = v->classify(t, ord);
         nfeat += s;
         return s;
       }
       __device__ void after_classify(uint32_t tb, uint32_t nt) { v->after_classify(tb, nt); }
       __device__ bool emit_enabled() const { return false; }
-      __device__ bool selected(const char*, uint32_t, uint32_t) const { return false; }
-      __device__ void emit(const char*, uint32_t, uint32_t, uint32_t) {}
+      __device__ bool selected(const TokenRef&, uint32_t) const { return false; }
+      __device__ void emit(const TokenRef&, uint32_t, uint32_t) {}
     } counter{&vis};
     walk_line<F, false>(text, b, e, win, cfg.delimiter, counter);
     const uint32_t nfeat = dev::wave_sum(counter.nfeat);
