@@ -48,6 +48,8 @@ struct DeviceParserConfig {
   int label_column{-1};
   int weight_column{-1};
   char delimiter{','};
+  /*! \brief LibSVM/LibFM: token-parallel kernels with exact per-line fallback */
+  bool fast_path{true};
   /*! \brief apply `?k=v` overrides (chunk_mb, pinned_slots, device_slots,
    *  read_threads, device, format, label_column, weight_column, delimiter) */
   void Update(const std::map<std::string, std::string>& args);
@@ -59,6 +61,8 @@ struct DeviceParserStats {
   size_t chunks{0};
   size_t rows{0};
   size_t nnz{0};
+  /*! \brief chunks the fast path handed to the exact per-line kernels */
+  size_t exact_chunks{0};
   /*! \brief seconds the host waited for the reader (pinned ring empty) */
   double wait_reader_sec{0};
   /*! \brief seconds the host waited for GPU results */

@@ -110,6 +110,8 @@ class DeviceCSR {
   IndexType* index() { return index_.get<IndexType>(); }
   float* value() { return value_.get<float>(); }
   size_t row_capacity() const { return row_cap_; }
+  /*! \brief rows the weight column can hold (0 when not allocated) */
+  size_t weight_capacity() const { return weight_.bytes() / sizeof(float); }
   size_t nnz_capacity() const { return nnz_cap_; }
   /*! \brief device bytes held */
   size_t AllocatedBytes() const {

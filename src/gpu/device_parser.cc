@@ -4,12 +4,18 @@
  *
  * Per chunk, in stream order:
  *   copy stream    : wait(parsed[d]) -> H2D(text[d]) -> record(copied[d])
- *   compute stream : wait(copied[d]) -> K1a line count + scan
- *                    [host reads nlines]  -> K1b emit, K2 count, K3 scan
- *                    [host reads nrows/nnz/flags, sizes the output]
- *                    -> K4 fill (+K8) -> record(parsed[d])
- * H2D of chunk k+1 is queued before chunk k is parsed, so PCIe transfers
- * overlap the kernels; the reader thread fills pinned slots further ahead.
+ *   compute stream : wait(copied[d]) -> parse -> record(parsed[d])
+ *
+ * LibSVM / LibFM chunks take the token-parallel fast path
+ * (token_kernels.hip: T1a count, T1b emit, T2 row info, K3 scan, T3 fill, one
+ * lane per token).  A chunk the fast path flags as irregular (qid tokens,
+ * digit-less tokens, label-less lines), and every CSV chunk, is parsed by the
+ * exact wave-per-line kernels (text_kernels.hip: K1 line index, K2 count, K3
+ * scan, K4 fill).  Both write bit-identical CSR for regular input.
+ * The host reads three tiny results per chunk (counts, sizes, flags); the
+ * H2D of the next chunks is queued before the current chunk is parsed, so
+ * PCIe transfers overlap the kernels and the reader thread fills pinned slots
+ * further ahead.
  */
 #include <dmlc/gpu/device_parser.h>
 #include <dmlc/logging.h>
@@ -17,6 +23,7 @@
 #include <dmlc/timer.h>
 
 #include <cstdlib>
+#include <cstring>
 #include <deque>
 #include <memory>
 #include <vector>
@@ -55,11 +62,13 @@ void DeviceParserConfig::Update(const std::map<std::string, std::string>& args) 
     } else if (k == "delimiter") {
       CHECK_EQ(v.size(), 1U) << "delimiter must be one character";
       delimiter = v[0];
+    } else if (k == "fast_path") {
+      fast_path = v != "0" && v != "false";
     }
   }
   chunk_bytes = (chunk_bytes + 4095) & ~size_t(4095);
   CHECK_GE(chunk_bytes, 4096U) << "chunk_bytes too small";
-  CHECK_LT(chunk_bytes, size_t(1) << 32) << "chunk_bytes must be < 4 GiB";
+  CHECK_LT(chunk_bytes, size_t(1) << 31) << "chunk_bytes must be < 2 GiB";
   CHECK_GE(pinned_slots, 1);
   CHECK_GE(device_slots, 1);
 }
@@ -70,6 +79,13 @@ namespace {
 struct HostSlot {
   PinnedBuffer buf;
   size_t size{0};
+};
+
+/*! \brief per-chunk sizes the host needs to place the output */
+struct ChunkPlan {
+  size_t nlines{0}, ntok{0};
+  uint64_t nrows{0}, nnz{0};
+  unsigned flags{0};
 };
 
 template <typename IndexType>
@@ -99,6 +115,8 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     copy_.reset(new Stream());
     for (int d = 0; d < cfg_.device_slots; ++d) {
       dtext_.emplace_back(new DeviceBuffer(cfg_.chunk_bytes + kTextPadBytes));
+      // the pad is read (never used) by 16-byte loads past the chunk end
+      DMLC_HIP_CHECK(hipMemset(dtext_.back()->get(), 0, cfg_.chunk_bytes + kTextPadBytes));
       copied_.emplace_back(new Event());
       parsed_.emplace_back(new Event());
       parsed_.back()->Record(compute_->get());
@@ -128,8 +146,9 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   bool Next() override {
     block_.Clear();
     block_.device_ = device_;
+    ResetEpoch();
     if (!ProcessOne(&block_, /*append=*/false)) return false;
-    FinishEpochMeta(&block_);
+    FinishEpoch(&block_);
     view_ = block_.View();
     return true;
   }
@@ -139,10 +158,10 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   void ParseAll(DeviceCSR<IndexType>* out) override {
     ScopedRange range("DeviceParser::ParseAll");
     out->device_ = device_;
-    ResetAccum();
+    ResetEpoch();
     while (ProcessOne(out, /*append=*/true)) {
     }
-    FinishEpochMeta(out);
+    FinishEpoch(out);
   }
 
   size_t PartitionBytes() const override { return reader_->PartitionBytes(); }
@@ -187,7 +206,6 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       stats_.wait_reader_sec += GetTime() - t0;
       const int d = next_dslot_;
       next_dslot_ = (next_dslot_ + 1) % cfg_.device_slots;
-      // the device slot is free once its previous chunk has been parsed
       DMLC_HIP_CHECK(hipStreamWaitEvent(copy_->get(), parsed_[d]->get(), 0));
       DMLC_HIP_CHECK(hipMemcpyAsync(dtext_[d]->get(), slot->buf.get(), slot->size,
                                     hipMemcpyHostToDevice, copy_->get()));
@@ -204,20 +222,148 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       inflight_.pop_front();
     }
     reader_done_ = false;
+    busy_ = 0;
   }
 
-  void ResetAccum() {
-    DMLC_HIP_CHECK(hipMemsetAsync(meta_.get<ChunkMeta>() + 1, 0, sizeof(ChunkMeta), compute_->get()));
+  void ResetEpoch() {
+    acc_max_index_ = acc_max_field_ = 0;
+    acc_flags_ = 0;
   }
 
-  /*! \brief copy device meta[which] to host (synchronising the compute stream) */
-  const ChunkMeta& ReadMeta(int which) {
+  /*! \brief device -> host copy of `bytes` at `src` (synchronises the compute stream) */
+  template <typename T>
+  T ReadBack(const void* src) {
     const double t0 = GetTime();
-    DMLC_HIP_CHECK(hipMemcpyAsync(hmeta_.get<ChunkMeta>() + which, meta_.get<ChunkMeta>() + which,
-                                  sizeof(ChunkMeta), hipMemcpyDeviceToHost, compute_->get()));
+    DMLC_HIP_CHECK(hipMemcpyAsync(hmeta_.get(), src, sizeof(T), hipMemcpyDeviceToHost,
+                                  compute_->get()));
     compute_->Synchronize();
     stats_.wait_gpu_sec += GetTime() - t0;
-    return hmeta_.get<ChunkMeta>()[which];
+    T v;
+    std::memcpy(&v, hmeta_.get(), sizeof(T));
+    return v;
+  }
+
+  void EnsureLineBuffers(size_t nlines, size_t ntok) {
+    lines_.Reserve((nlines + 1) * sizeof(uint32_t));
+    first_tok_.Reserve((nlines + 1) * sizeof(uint32_t));
+    info_.Reserve((nlines + 1) * sizeof(uint64_t));
+    partials_.Reserve((ScanPartials(nlines) + 2) * sizeof(uint64_t));
+    if (ntok != 0) {
+      tok_pos_.Reserve(ntok * sizeof(uint32_t));
+      tok_line_.Reserve(ntok * sizeof(uint32_t));
+    }
+  }
+
+  /*! \brief grow the output for this chunk and build the fill target */
+  FillTarget<IndexType> PrepareOutput(DeviceCSR<IndexType>* out, size_t row_base, size_t nnz_base,
+                                      const ChunkPlan& plan, bool need_weight, size_t nbytes) {
+    hipStream_t s = compute_->get();
+    const bool libfm = tcfg_.format == TextFormat::kLibFM;
+    if (row_base == 0) {
+      // first chunk: reserve for the whole partition from this chunk's density
+      const double scale = static_cast<double>(reader_->PartitionBytes()) /
+                           std::max<size_t>(nbytes, 1) * 1.05;
+      out->Reserve(static_cast<size_t>(plan.nrows * scale) + 1,
+                   static_cast<size_t>(plan.nnz * scale) + 1, libfm, s, 0, 0);
+    }
+    out->Reserve(row_base + plan.nrows, nnz_base + plan.nnz, libfm, s, row_base, nnz_base);
+    if (need_weight) out->EnableWeight(s);
+    if (plan.flags & kFlagQid) {
+      out->EnableQid(s);
+      out->has_qid_ = true;
+    }
+    FillTarget<IndexType> tgt;
+    tgt.offset = out->offset();
+    tgt.label = out->label();
+    tgt.weight = out->weight_capacity() >= out->row_capacity() ? out->weight() : nullptr;
+    tgt.qid = out->has_qid_ ? out->qid() : nullptr;
+    tgt.field = libfm ? out->field() : nullptr;
+    tgt.index = out->index();
+    tgt.value = out->value();
+    tgt.row_base = row_base;
+    tgt.nnz_base = nnz_base;
+    tgt.row_limit = row_base + plan.nrows;
+    tgt.nnz_limit = nnz_base + plan.nnz;
+    return tgt;
+  }
+
+  /*! \brief token-parallel parse; false when the chunk must take the exact path */
+  bool FastParse(const char* text, size_t nbytes, DeviceCSR<IndexType>* out, size_t row_base,
+                 size_t nnz_base, ChunkPlan* plan) {
+    hipStream_t s = compute_->get();
+    ChunkMeta* dmeta = meta_.get<ChunkMeta>();
+    uint64_t* packed = reinterpret_cast<uint64_t*>(dmeta + 1);
+    LaunchTokenCount(text, nbytes, tiles_.get<uint64_t>(), packed, s);
+    const uint64_t counts = ReadBack<uint64_t>(packed);
+    plan->nlines = counts >> 32;
+    plan->ntok = counts & 0xffffffffull;
+    AfterFirstSync();
+    EnsureLineBuffers(plan->nlines, plan->ntok);
+    LaunchTokenEmit(text, nbytes, tiles_.get<uint64_t>(), lines_.get<uint32_t>(),
+                    first_tok_.get<uint32_t>(), tok_pos_.get<uint32_t>(),
+                    tok_line_.get<uint32_t>(), s);
+    LaunchRowInfo(first_tok_.get<uint32_t>(), plan->nlines, plan->ntok, info_.get<uint64_t>(), s);
+    uint64_t* total = partials_.get<uint64_t>() + ScanPartials(plan->nlines) + 1;
+    LaunchScanU64(info_.get<uint64_t>(), plan->nlines, partials_.get<uint64_t>(), total, s);
+    const uint64_t t = ReadBack<uint64_t>(total);
+    plan->nrows = t >> 32;
+    plan->nnz = t & 0xffffffffull;
+    FillTarget<IndexType> tgt = PrepareOutput(out, row_base, nnz_base, *plan, true, nbytes);
+    DMLC_HIP_CHECK(hipMemsetAsync(dmeta, 0, sizeof(ChunkMeta), s));
+    LaunchTokenFill<IndexType>(text, nbytes, tcfg_.format, tok_pos_.get<uint32_t>(),
+                               tok_line_.get<uint32_t>(), plan->ntok, first_tok_.get<uint32_t>(),
+                               info_.get<uint64_t>(), tgt, plan->nrows, plan->nnz, dmeta, s);
+    const ChunkMeta m = ReadBack<ChunkMeta>(dmeta);
+    if (m.flags & kFlagIrregular) return false;
+    Accumulate(m);
+    return true;
+  }
+
+  /*! \brief exact wave-per-line parse (any input) */
+  void ExactParse(const char* text, size_t nbytes, DeviceCSR<IndexType>* out, size_t row_base,
+                  size_t nnz_base, ChunkPlan* plan, bool first_sync_done) {
+    hipStream_t s = compute_->get();
+    ChunkMeta* dmeta = meta_.get<ChunkMeta>();
+    DMLC_HIP_CHECK(hipMemsetAsync(dmeta, 0, sizeof(ChunkMeta), s));
+    LaunchLineCount(text, nbytes, tiles_.get<uint64_t>(), dmeta, s);
+    plan->nlines = ReadBack<ChunkMeta>(dmeta).nlines;
+    if (!first_sync_done) AfterFirstSync();
+    EnsureLineBuffers(plan->nlines, 0);
+    LaunchLineEmit(text, nbytes, tiles_.get<uint64_t>(), lines_.get<uint32_t>(), s);
+    LaunchTextCount(text, nbytes, lines_.get<uint32_t>(), plan->nlines, tcfg_,
+                    info_.get<uint64_t>(), dmeta, s);
+    uint64_t* total = partials_.get<uint64_t>() + ScanPartials(plan->nlines) + 1;
+    LaunchScanU64(info_.get<uint64_t>(), plan->nlines, partials_.get<uint64_t>(), total, s);
+    LaunchMetaFromTotal(total, dmeta, s);
+    const ChunkMeta hm = ReadBack<ChunkMeta>(dmeta);
+    plan->nrows = hm.nrows;
+    plan->nnz = hm.nnz;
+    plan->flags = hm.flags;
+    const bool csv = tcfg_.format == TextFormat::kCSV;
+    const bool need_weight = (hm.flags & kFlagWeight) || (csv && tcfg_.weight_column >= 0);
+    FillTarget<IndexType> tgt = PrepareOutput(out, row_base, nnz_base, *plan, need_weight, nbytes);
+    DMLC_HIP_CHECK(hipMemsetAsync(dmeta, 0, sizeof(ChunkMeta), s));
+    LaunchTextFill<IndexType>(text, nbytes, lines_.get<uint32_t>(), plan->nlines, tcfg_,
+                              info_.get<uint64_t>(), tgt, plan->nrows, plan->nnz, dmeta, s);
+    ChunkMeta m = ReadBack<ChunkMeta>(dmeta);
+    m.flags |= plan->flags & (kFlagWeight | kFlagQid);
+    if (csv && tcfg_.weight_column >= 0) m.flags |= kFlagWeight;
+    Accumulate(m);
+  }
+
+  void Accumulate(const ChunkMeta& m) {
+    CHECK(!(m.flags & kFlagNegIndex)) << "negative feature index in " << cfg_.format << " input";
+    CHECK(!(m.flags & kFlagOverflow))
+        << "internal error: GPU fill pass disagreed with the count pass (writes were dropped)";
+    acc_max_index_ = std::max<uint64_t>(acc_max_index_, m.max_index);
+    acc_max_field_ = std::max<uint64_t>(acc_max_field_, m.max_field);
+    acc_flags_ |= m.flags;
+  }
+
+  /*! \brief the H2D of the current chunk is complete: recycle and keep PCIe busy */
+  void AfterFirstSync() {
+    if (cur_slot_ != nullptr) iter_.Recycle(&cur_slot_);
+    FillPipeline();
   }
 
   /*! \brief parse one chunk into out (append or replace); false at end */
@@ -227,95 +373,51 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     Inflight cur = inflight_.front();
     inflight_.pop_front();
     busy_ = 1;
+    cur_slot_ = cur.slot;
     const size_t nbytes = cur.slot->size;
     const char* text = dtext_[cur.d]->template get<char>();
     hipStream_t s = compute_->get();
-    ChunkMeta* dmeta = meta_.get<ChunkMeta>();
-    ChunkMeta* accum = dmeta + 1;
-    if (!append) ResetAccum();
     ScopedRange range("parse_chunk");
     DMLC_HIP_CHECK(hipStreamWaitEvent(s, copied_[cur.d]->get(), 0));
-    DMLC_HIP_CHECK(hipMemsetAsync(dmeta, 0, sizeof(ChunkMeta), s));
-    // K1a: count lines
-    LaunchLineCount(text, nbytes, tiles_.get<uint64_t>(), dmeta, s);
-    const size_t nlines = ReadMeta(0).nlines;
-    // the H2D of this chunk is complete (the compute stream waited for it)
-    iter_.Recycle(&cur.slot);
-    // keep PCIe busy while we parse
-    FillPipeline();
-    lines_.Reserve((nlines + 1) * sizeof(uint32_t));
-    info_.Reserve((nlines + 1) * sizeof(uint64_t));
-    partials_.Reserve((ScanPartials(nlines) + 2) * sizeof(uint64_t));
-    LaunchLineEmit(text, nbytes, tiles_.get<uint64_t>(), lines_.get<uint32_t>(), s);
-    LaunchTextCount(text, nbytes, lines_.get<uint32_t>(), nlines, tcfg_, info_.get<uint64_t>(),
-                    dmeta, s);
-    uint64_t* total = partials_.get<uint64_t>() + ScanPartials(nlines) + 1;
-    LaunchScanU64(info_.get<uint64_t>(), nlines, partials_.get<uint64_t>(), total, s);
-    LaunchMetaFromTotal(total, dmeta, s);
-    const ChunkMeta hm = ReadMeta(0);
-    // size the output
     const size_t row_base = append ? out->rows_ : 0;
     const size_t nnz_base = append ? out->nnz_ : 0;
-    const bool libfm = tcfg_.format == TextFormat::kLibFM;
-    if (append && out->rows_ == 0 && stats_.bytes == 0) {
-      // first chunk of a resident parse: reserve for the whole partition
-      const double scale = static_cast<double>(reader_->PartitionBytes()) /
-                           std::max<size_t>(nbytes, 1) * 1.05;
-      out->Reserve(static_cast<size_t>(hm.nrows * scale) + 1,
-                   static_cast<size_t>(hm.nnz * scale) + 1, libfm, s, 0, 0);
+    ChunkPlan plan;
+    const bool token_format = tcfg_.format != TextFormat::kCSV;
+    bool done = false;
+    if (token_format && cfg_.fast_path) {
+      done = FastParse(text, nbytes, out, row_base, nnz_base, &plan);
+      if (!done) stats_.exact_chunks += 1;
     }
-    out->Reserve(row_base + hm.nrows, nnz_base + hm.nnz, libfm, s, row_base, nnz_base);
-    const bool csv = tcfg_.format == TextFormat::kCSV;
-    if ((hm.flags & kFlagWeight) || (csv && tcfg_.weight_column >= 0)) {
-      out->EnableWeight(s);
-      out->has_weight_ = true;
+    if (!done) {
+      ExactParse(text, nbytes, out, row_base, nnz_base, &plan, token_format && cfg_.fast_path);
     }
-    if (hm.flags & kFlagQid) {
-      out->EnableQid(s);
-      out->has_qid_ = true;
-    }
-    FillTarget<IndexType> tgt;
-    tgt.offset = out->offset();
-    tgt.label = out->label();
-    tgt.weight = out->has_weight_ ? out->weight() : nullptr;
-    tgt.qid = out->has_qid_ ? out->qid() : nullptr;
-    tgt.field = libfm ? out->field() : nullptr;
-    tgt.index = out->index();
-    tgt.value = out->value();
-    tgt.row_base = row_base;
-    tgt.nnz_base = nnz_base;
-    tgt.row_limit = row_base + hm.nrows;
-    tgt.nnz_limit = nnz_base + hm.nnz;
-    LaunchTextFill<IndexType>(text, nbytes, lines_.get<uint32_t>(), nlines, tcfg_,
-                              info_.get<uint64_t>(), tgt, hm.nrows, hm.nnz, accum, s);
+    if (cur_slot_ != nullptr) iter_.Recycle(&cur_slot_);
     parsed_[cur.d]->Record(s);
     busy_ = 0;
-    out->rows_ = row_base + hm.nrows;
-    out->nnz_ = nnz_base + hm.nnz;
-    if (csv) out->has_value_ = out->nnz_ != 0;
-    if (libfm) out->has_field_ = true;
+    out->rows_ = row_base + plan.nrows;
+    out->nnz_ = nnz_base + plan.nnz;
+    if (acc_flags_ & kFlagWeight) out->has_weight_ = true;
+    if (tcfg_.format == TextFormat::kCSV) out->has_value_ = out->nnz_ != 0;
+    if (tcfg_.format == TextFormat::kLibFM) out->has_field_ = true;
     stats_.bytes += nbytes;
     stats_.chunks += 1;
-    stats_.rows += hm.nrows;
-    stats_.nnz += hm.nnz;
+    stats_.rows += plan.nrows;
+    stats_.nnz += plan.nnz;
     return true;
   }
 
-  /*! \brief read the accumulated max/flags after the last fill */
-  void FinishEpochMeta(DeviceCSR<IndexType>* out) {
-    const ChunkMeta& acc = ReadMeta(1);
-    CHECK(!(acc.flags & kFlagNegIndex)) << "negative feature index in " << cfg_.format << " input";
-    CHECK(!(acc.flags & kFlagOverflow))
-        << "internal error: GPU fill pass disagreed with the count pass (writes were dropped)";
-    out->max_index_ = std::max<uint64_t>(out->max_index_, acc.max_index);
-    out->max_field_ = std::max<uint64_t>(out->max_field_, acc.max_field);
-    if (acc.flags & kFlagValue) out->has_value_ = true;
+  /*! \brief publish the accumulated max / flags of this epoch */
+  void FinishEpoch(DeviceCSR<IndexType>* out) {
+    out->max_index_ = std::max<uint64_t>(out->max_index_, acc_max_index_);
+    out->max_field_ = std::max<uint64_t>(out->max_field_, acc_max_field_);
+    if (acc_flags_ & kFlagValue) out->has_value_ = true;
+    if (acc_flags_ & kFlagWeight) out->has_weight_ = true;
     if (out->rows_ == 0) {
       // keep a valid (zero) closing offset for empty partitions
       out->Reserve(1, 1, false, compute_->get());
       DMLC_HIP_CHECK(hipMemsetAsync(out->offset(), 0, sizeof(uint64_t), compute_->get()));
-      compute_->Synchronize();
     }
+    compute_->Synchronize();
   }
 
   DeviceParserConfig cfg_;
@@ -326,13 +428,16 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   std::unique_ptr<Stream> compute_, copy_;
   std::vector<std::unique_ptr<DeviceBuffer>> dtext_;
   std::vector<std::unique_ptr<Event>> copied_, parsed_;
-  DeviceBuffer tiles_, lines_, info_, partials_, meta_;
+  DeviceBuffer tiles_, lines_, first_tok_, tok_pos_, tok_line_, info_, partials_, meta_;
   PinnedBuffer hmeta_;
   ThreadedIter<HostSlot> iter_;
   std::deque<Inflight> inflight_;
+  HostSlot* cur_slot_{nullptr};
   int next_dslot_{0};
   int busy_{0};
   bool reader_done_{false};
+  uint64_t acc_max_index_{0}, acc_max_field_{0};
+  unsigned acc_flags_{0};
   DeviceCSR<IndexType> block_;
   DeviceRowBlock<IndexType> view_;
   DeviceParserStats stats_;

@@ -742,8 +742,11 @@ void LaunchTextFill(const char* text, size_t nbytes, const uint32_t* line_starts
         break;
     }
   }
-  hipLaunchKernelGGL(k_close_offsets, dim3(1), dim3(1), 0, stream, out.offset,
-                     out.row_base + nrows, out.nnz_base + nnz);
+  LaunchCloseOffsets(out.offset, out.row_base + nrows, out.nnz_base + nnz, stream);
+}
+
+void LaunchCloseOffsets(uint64_t* offset, uint64_t row_end, uint64_t nnz_end, hipStream_t stream) {
+  hipLaunchKernelGGL(k_close_offsets, dim3(1), dim3(1), 0, stream, offset, row_end, nnz_end);
 }
 
 template void LaunchTextFill<uint32_t>(const char*, size_t, const uint32_t*, size_t,

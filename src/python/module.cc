@@ -301,6 +301,7 @@ class PyDeviceParser {
     d["chunks"] = s.chunks;
     d["rows"] = s.rows;
     d["nnz"] = s.nnz;
+    d["exact_chunks"] = s.exact_chunks;
     d["wait_reader_sec"] = s.wait_reader_sec;
     d["wait_gpu_sec"] = s.wait_gpu_sec;
     return d;

@@ -45,6 +45,32 @@ def test_libsvm_gpu_equals_cpu(tmp_path, chunk_kb):
     assert_same(g, c)
 
 
+@pytest.mark.parametrize("fast", [0, 1])
+@pytest.mark.parametrize("weights", [0, 3])
+def test_fast_and_exact_paths_agree(tmp_path, fast, weights):
+    p = str(tmp_path / "s.libsvm")
+    data.write_synthetic(p, 0, 3000, format="libsvm", seed=21, weight_every=weights)
+    g = gpu_rows(p, "libsvm", chunk_bytes=64 * 1024, fast_path=fast)
+    assert_same(g, cpu_rows(p, "libsvm"))
+
+
+def test_irregular_chunks_fall_back(tmp_path):
+    # qid tokens and digit-less tokens are not handled by the token-parallel
+    # path: those chunks must be re-parsed exactly, the rest stay fast
+    p = str(tmp_path / "m.libsvm")
+    data.write_synthetic(p, 0, 2000, format="libsvm", seed=5)
+    with open(p, "a") as f:
+        f.write("1 qid:9 1:1 2:2\n0 junk 3:1\n")
+    data.write_synthetic(str(tmp_path / "tail.libsvm"), 2000, 4000, seed=5)
+    with open(p, "a") as f:
+        f.write(open(str(tmp_path / "tail.libsvm")).read())
+    gp = data.GPUParser(p, chunk_bytes=64 * 1024)
+    csr = gp.parse_all()
+    st = gp.stats()
+    assert 0 < st["exact_chunks"] < st["chunks"]
+    assert_same(pyref.concat_blocks([csr.to_host()]), cpu_rows(p, "libsvm"))
+
+
 def test_libsvm_gpu_edge_cases(tmp_path):
     from test_cpu_parsers import EDGE_LIBSVM
     p = str(tmp_path / "e.libsvm")
