@@ -88,6 +88,47 @@ __device__ __forceinline__ T block_sum_256(T v, T* smem) {
   return t;
 }
 
+template <typename T>
+__device__ __forceinline__ T wave_or(T v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v |= __shfl_xor(v, d, kWave);
+  return v;
+}
+
+/*!
+ * \brief reduce (max, max, or) over a 256-thread workgroup and store the
+ *  result in slot blockIdx.x — every thread of the block must call it.
+ */
+template <typename Partial>
+__device__ __forceinline__ void block_store_partial(unsigned long long mi, unsigned long long mf,
+                                                    unsigned fl, Partial* partials) {
+  __shared__ unsigned long long s_mi[4], s_mf[4];
+  __shared__ unsigned s_fl[4];
+  mi = wave_max(mi);
+  mf = wave_max(mf);
+  fl = wave_or(fl);
+  const int wid = threadIdx.x / kWave;
+  if (lane_id() == 0) {
+    s_mi[wid] = mi;
+    s_mf[wid] = mf;
+    s_fl[wid] = fl;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Partial p;
+    p.max_index = s_mi[0];
+    p.max_field = s_mf[0];
+    p.flags = s_fl[0];
+    p.pad = 0;
+    for (int w = 1; w < static_cast<int>(blockDim.x) / kWave; ++w) {
+      p.max_index = s_mi[w] > p.max_index ? s_mi[w] : p.max_index;
+      p.max_field = s_mf[w] > p.max_field ? s_mf[w] : p.max_field;
+      p.flags |= s_fl[w];
+    }
+    partials[blockIdx.x] = p;
+  }
+}
+
 /*!
  * \brief 16-bit mask of the bytes of a 16-byte vector equal to `c`
  *  (exact SWAR zero-byte test per 32-bit word).

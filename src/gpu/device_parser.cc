@@ -124,6 +124,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     tiles_.Reserve(LineIndexTiles(cfg_.chunk_bytes) * sizeof(uint64_t));
     meta_.Reserve(2 * sizeof(ChunkMeta));
     hmeta_.Reserve(2 * sizeof(ChunkMeta));
+    slots_.Reserve(kMaxPartialBlocks * sizeof(MetaPartial));
     iter_.set_max_capacity(static_cast<size_t>(cfg_.pinned_slots));
     StartReader();
   }
@@ -312,7 +313,8 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     DMLC_HIP_CHECK(hipMemsetAsync(dmeta, 0, sizeof(ChunkMeta), s));
     LaunchTokenFill<IndexType>(text, nbytes, tcfg_.format, tok_pos_.get<uint32_t>(),
                                tok_line_.get<uint32_t>(), plan->ntok, first_tok_.get<uint32_t>(),
-                               info_.get<uint64_t>(), tgt, plan->nrows, plan->nnz, dmeta, s);
+                               info_.get<uint64_t>(), tgt, plan->nrows, plan->nnz,
+                               slots_.get<MetaPartial>(), dmeta, s);
     const ChunkMeta m = ReadBack<ChunkMeta>(dmeta);
     if (m.flags & kFlagIrregular) return false;
     Accumulate(m);
@@ -331,7 +333,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     EnsureLineBuffers(plan->nlines, 0);
     LaunchLineEmit(text, nbytes, tiles_.get<uint64_t>(), lines_.get<uint32_t>(), s);
     LaunchTextCount(text, nbytes, lines_.get<uint32_t>(), plan->nlines, tcfg_,
-                    info_.get<uint64_t>(), dmeta, s);
+                    info_.get<uint64_t>(), slots_.get<MetaPartial>(), dmeta, s);
     uint64_t* total = partials_.get<uint64_t>() + ScanPartials(plan->nlines) + 1;
     LaunchScanU64(info_.get<uint64_t>(), plan->nlines, partials_.get<uint64_t>(), total, s);
     LaunchMetaFromTotal(total, dmeta, s);
@@ -344,7 +346,8 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     FillTarget<IndexType> tgt = PrepareOutput(out, row_base, nnz_base, *plan, need_weight, nbytes);
     DMLC_HIP_CHECK(hipMemsetAsync(dmeta, 0, sizeof(ChunkMeta), s));
     LaunchTextFill<IndexType>(text, nbytes, lines_.get<uint32_t>(), plan->nlines, tcfg_,
-                              info_.get<uint64_t>(), tgt, plan->nrows, plan->nnz, dmeta, s);
+                              info_.get<uint64_t>(), tgt, plan->nrows, plan->nnz,
+                              slots_.get<MetaPartial>(), dmeta, s);
     ChunkMeta m = ReadBack<ChunkMeta>(dmeta);
     m.flags |= plan->flags & (kFlagWeight | kFlagQid);
     if (csv && tcfg_.weight_column >= 0) m.flags |= kFlagWeight;
@@ -429,6 +432,8 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   std::vector<std::unique_ptr<DeviceBuffer>> dtext_;
   std::vector<std::unique_ptr<Event>> copied_, parsed_;
   DeviceBuffer tiles_, lines_, first_tok_, tok_pos_, tok_line_, info_, partials_, meta_;
+  /*! \brief per-workgroup reduction slots (MetaPartial) */
+  DeviceBuffer slots_;
   PinnedBuffer hmeta_;
   ThreadedIter<HostSlot> iter_;
   std::deque<Inflight> inflight_;

@@ -59,6 +59,25 @@ constexpr unsigned kFlagField = 8u;
 constexpr unsigned kFlagNegIndex = 256u;
 constexpr unsigned kFlagOverflow = 512u;
 
+/*!
+ * \brief per-workgroup reduction slot.  Kernels never hit one global word from
+ *  every wave (same-address atomics serialise at the memory side, ~10 ns each:
+ *  62k waves x 3 atomics cost 1.5 ms per chunk); each workgroup reduces in
+ *  LDS and writes its slot, then k_reduce_partials folds the slots into the
+ *  ChunkMeta with one workgroup.
+ */
+struct MetaPartial {
+  unsigned long long max_index;
+  unsigned long long max_field;
+  unsigned int flags;
+  unsigned int pad;
+};
+/*! \brief max workgroups of any kernel that writes MetaPartial slots */
+constexpr int kMaxPartialBlocks = 8192;
+/*! \brief fold nblocks MetaPartial slots into meta (max / or) with one workgroup */
+void LaunchReducePartials(const MetaPartial* partials, int nblocks, ChunkMeta* meta,
+                          hipStream_t stream);
+
 /*! \brief destination arrays of the fill pass (device pointers) */
 template <typename IndexType>
 struct FillTarget {
@@ -99,7 +118,7 @@ void LaunchLineEmit(const char* text, size_t nbytes, const uint64_t* tile_scratc
  */
 void LaunchTextCount(const char* text, size_t nbytes, const uint32_t* line_starts,
                      size_t nlines, const TextParseConfig& cfg, uint64_t* line_info,
-                     ChunkMeta* meta, hipStream_t stream);
+                     MetaPartial* partials, ChunkMeta* meta, hipStream_t stream);
 
 /*!
  * \brief K3: exclusive scan of n u64 values in place; *total receives the sum.
@@ -119,7 +138,7 @@ template <typename IndexType>
 void LaunchTextFill(const char* text, size_t nbytes, const uint32_t* line_starts,
                     size_t nlines, const TextParseConfig& cfg, const uint64_t* line_info,
                     const FillTarget<IndexType>& out, uint64_t nrows, uint64_t nnz,
-                    ChunkMeta* meta, hipStream_t stream);
+                    MetaPartial* partials, ChunkMeta* meta, hipStream_t stream);
 
 /*! \brief offset[row_end] = nnz_end (closing row pointer of a chunk) */
 void LaunchCloseOffsets(uint64_t* offset, uint64_t row_end, uint64_t nnz_end, hipStream_t stream);
@@ -149,7 +168,7 @@ template <typename IndexType>
 void LaunchTokenFill(const char* text, size_t nbytes, TextFormat format, const uint32_t* tok_pos,
                      const uint32_t* tok_line, size_t ntok, const uint32_t* line_first_tok,
                      const uint64_t* line_info, const FillTarget<IndexType>& out, uint64_t nrows,
-                     uint64_t nnz, ChunkMeta* meta, hipStream_t stream);
+                     uint64_t nnz, MetaPartial* partials, ChunkMeta* meta, hipStream_t stream);
 
 // ----------------------------- RecordIO (K7) -----------------------------
 /*!

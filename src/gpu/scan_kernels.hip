@@ -102,6 +102,41 @@ __global__ __launch_bounds__(kThreads) void k_scan_down(uint64_t* __restrict__ d
   }
 }
 
+__global__ __launch_bounds__(kThreads) void k_reduce_partials(const MetaPartial* __restrict__ p,
+                                                              int n, ChunkMeta* meta) {
+  unsigned long long mi = 0, mf = 0;
+  unsigned fl = 0;
+  for (int i = threadIdx.x; i < n; i += kThreads) {
+    const MetaPartial q = p[i];
+    mi = q.max_index > mi ? q.max_index : mi;
+    mf = q.max_field > mf ? q.max_field : mf;
+    fl |= q.flags;
+  }
+  __shared__ unsigned long long s_mi[4], s_mf[4];
+  __shared__ unsigned s_fl[4];
+  mi = dev::wave_max(mi);
+  mf = dev::wave_max(mf);
+  fl = dev::wave_or(fl);
+  const int wid = threadIdx.x / dev::kWave;
+  if (dev::lane_id() == 0) {
+    s_mi[wid] = mi;
+    s_mf[wid] = mf;
+    s_fl[wid] = fl;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w) {
+      s_mi[0] = s_mi[w] > s_mi[0] ? s_mi[w] : s_mi[0];
+      s_mf[0] = s_mf[w] > s_mf[0] ? s_mf[w] : s_mf[0];
+      s_fl[0] |= s_fl[w];
+    }
+    // single writer, stream ordered: merge into what earlier kernels stored
+    meta->max_index = s_mi[0] > meta->max_index ? s_mi[0] : meta->max_index;
+    meta->max_field = s_mf[0] > meta->max_field ? s_mf[0] : meta->max_field;
+    meta->flags |= s_fl[0];
+  }
+}
+
 __global__ void k_meta_from_total(const uint64_t* __restrict__ total, ChunkMeta* meta) {
   const uint64_t t = *total;
   meta->nrows = t >> 32;
@@ -121,6 +156,12 @@ void LaunchScanU64(uint64_t* data, size_t n, uint64_t* partials, uint64_t* total
   hipLaunchKernelGGL(k_scan_reduce, dim3(np), dim3(kThreads), 0, stream, data, n, partials);
   hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(kThreads), 0, stream, partials, np, total);
   hipLaunchKernelGGL(k_scan_down, dim3(np), dim3(kThreads), 0, stream, data, n, partials);
+}
+
+void LaunchReducePartials(const MetaPartial* partials, int nblocks, ChunkMeta* meta,
+                          hipStream_t stream) {
+  hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(kThreads), 0, stream, partials, nblocks,
+                     meta);
 }
 
 void LaunchMetaFromTotal(const uint64_t* total, ChunkMeta* meta, hipStream_t stream) {

@@ -547,12 +547,13 @@ __global__ __launch_bounds__(kThreads) void k_text_count(const uint8_t* __restri
                                                          const uint32_t* __restrict__ line_starts,
                                                          size_t nlines, TextParseConfig cfg,
                                                          uint64_t* __restrict__ line_info,
-                                                         ChunkMeta* __restrict__ meta) {
+                                                         MetaPartial* __restrict__ partials) {
   __shared__ uint4 lds[kWavesPerBlock][kWindow / 16];
   const int wid = threadIdx.x / dev::kWave;
   const int lane = dev::lane_id();
   uint8_t* win = reinterpret_cast<uint8_t*>(lds[wid]);
   const size_t nwaves = static_cast<size_t>(gridDim.x) * kWavesPerBlock;
+  unsigned wflags = 0;
   for (size_t line = static_cast<size_t>(blockIdx.x) * kWavesPerBlock + wid; line < nlines;
        line += nwaves) {
     const uint32_t b = line_starts[line];
@@ -578,12 +579,11 @@ __global__ __launch_bounds__(kThreads) void k_text_count(const uint8_t* __restri
     const bool row_ok = vis.row_state == 1;
     const bool w = __ballot(vis.has_weight) != 0;
     const bool qd = __ballot(vis.is_qid_lane) != 0;
-    if (lane == 0) {
-      line_info[line] = row_ok ? ((1ull << 32) | nfeat) : 0ull;
-      if (row_ok && w) atomicOr(&meta->flags, kFlagWeight);
-      if (row_ok && qd) atomicOr(&meta->flags, kFlagQid);
-    }
+    if (lane == 0) line_info[line] = row_ok ? ((1ull << 32) | nfeat) : 0ull;
+    if (row_ok && w) wflags |= kFlagWeight;
+    if (row_ok && qd) wflags |= kFlagQid;
   }
+  dev::block_store_partial(0ull, 0ull, wflags, partials);
 }
 
 // ------------------------------------------------------------------ K4
@@ -593,7 +593,7 @@ __global__ __launch_bounds__(kThreads) void k_text_fill(const uint8_t* __restric
                                                         size_t nlines, TextParseConfig cfg,
                                                         const uint64_t* __restrict__ line_info,
                                                         FillTarget<IndexType> out,
-                                                        ChunkMeta* __restrict__ meta) {
+                                                        MetaPartial* __restrict__ partials) {
   __shared__ uint4 lds[kWavesPerBlock][kWindow / 16];
   const int wid = threadIdx.x / dev::kWave;
   const int lane = dev::lane_id();
@@ -641,22 +641,14 @@ __global__ __launch_bounds__(kThreads) void k_text_fill(const uint8_t* __restric
       }
     }
   }
-  // K8: one atomic per wave
-  const uint64_t mi = dev::wave_max(wmax_index);
-  const uint64_t mf = dev::wave_max(wmax_field);
-  const bool av = __ballot(wany_value) != 0;
-  const bool ng = __ballot(wneg) != 0;
-  const bool ov = __ballot(woverflow) != 0;
-  if (lane == 0) {
-    if (mi != 0) atomicMax(&meta->max_index, static_cast<unsigned long long>(mi));
-    if (mf != 0) atomicMax(&meta->max_field, static_cast<unsigned long long>(mf));
-    unsigned fl = 0;
-    if (av) fl |= kFlagValue;
-    if (ng) fl |= kFlagNegIndex;
-    if (ov) fl |= kFlagOverflow;
-    if (F == TextFormat::kLibFM) fl |= kFlagField;
-    if (fl != 0) atomicOr(&meta->flags, fl);
-  }
+  // K8: workgroup reduction into this block's slot (no same-address atomics)
+  unsigned fl = 0;
+  if (wany_value) fl |= kFlagValue;
+  if (wneg) fl |= kFlagNegIndex;
+  if (woverflow) fl |= kFlagOverflow;
+  if (F == TextFormat::kLibFM) fl |= kFlagField;
+  dev::block_store_partial(static_cast<unsigned long long>(wmax_index),
+                           static_cast<unsigned long long>(wmax_field), fl, partials);
 }
 
 __global__ void k_close_offsets(uint64_t* offset, uint64_t row_end, uint64_t nnz_end) {
@@ -698,49 +690,51 @@ void LaunchLineEmit(const char* text, size_t nbytes, const uint64_t* tile_scratc
 }
 
 void LaunchTextCount(const char* text, size_t nbytes, const uint32_t* line_starts, size_t nlines,
-                     const TextParseConfig& cfg, uint64_t* line_info, ChunkMeta* meta,
-                     hipStream_t stream) {
+                     const TextParseConfig& cfg, uint64_t* line_info, MetaPartial* partials,
+                     ChunkMeta* meta, hipStream_t stream) {
   if (nlines == 0) return;
   const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
   const dim3 grid(LineGrid(nlines)), block(kThreads);
   switch (cfg.format) {
     case TextFormat::kLibSVM:
       hipLaunchKernelGGL(k_text_count<TextFormat::kLibSVM>, grid, block, 0, stream, t, nbytes,
-                         line_starts, nlines, cfg, line_info, meta);
+                         line_starts, nlines, cfg, line_info, partials);
       break;
     case TextFormat::kLibFM:
       hipLaunchKernelGGL(k_text_count<TextFormat::kLibFM>, grid, block, 0, stream, t, nbytes,
-                         line_starts, nlines, cfg, line_info, meta);
+                         line_starts, nlines, cfg, line_info, partials);
       break;
     case TextFormat::kCSV:
       hipLaunchKernelGGL(k_text_count<TextFormat::kCSV>, grid, block, 0, stream, t, nbytes,
-                         line_starts, nlines, cfg, line_info, meta);
+                         line_starts, nlines, cfg, line_info, partials);
       break;
   }
+  LaunchReducePartials(partials, static_cast<int>(grid.x), meta, stream);
 }
 
 template <typename IndexType>
 void LaunchTextFill(const char* text, size_t nbytes, const uint32_t* line_starts, size_t nlines,
                     const TextParseConfig& cfg, const uint64_t* line_info,
                     const FillTarget<IndexType>& out, uint64_t nrows, uint64_t nnz,
-                    ChunkMeta* meta, hipStream_t stream) {
+                    MetaPartial* partials, ChunkMeta* meta, hipStream_t stream) {
   if (nlines != 0) {
     const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
     const dim3 grid(LineGrid(nlines)), block(kThreads);
     switch (cfg.format) {
       case TextFormat::kLibSVM:
         hipLaunchKernelGGL((k_text_fill<TextFormat::kLibSVM, IndexType>), grid, block, 0, stream,
-                           t, nbytes, line_starts, nlines, cfg, line_info, out, meta);
+                           t, nbytes, line_starts, nlines, cfg, line_info, out, partials);
         break;
       case TextFormat::kLibFM:
         hipLaunchKernelGGL((k_text_fill<TextFormat::kLibFM, IndexType>), grid, block, 0, stream,
-                           t, nbytes, line_starts, nlines, cfg, line_info, out, meta);
+                           t, nbytes, line_starts, nlines, cfg, line_info, out, partials);
         break;
       case TextFormat::kCSV:
         hipLaunchKernelGGL((k_text_fill<TextFormat::kCSV, IndexType>), grid, block, 0, stream, t,
-                           nbytes, line_starts, nlines, cfg, line_info, out, meta);
+                           nbytes, line_starts, nlines, cfg, line_info, out, partials);
         break;
     }
+    LaunchReducePartials(partials, static_cast<int>(grid.x), meta, stream);
   }
   LaunchCloseOffsets(out.offset, out.row_base + nrows, out.nnz_base + nnz, stream);
 }
@@ -752,11 +746,11 @@ void LaunchCloseOffsets(uint64_t* offset, uint64_t row_end, uint64_t nnz_end, hi
 template void LaunchTextFill<uint32_t>(const char*, size_t, const uint32_t*, size_t,
                                        const TextParseConfig&, const uint64_t*,
                                        const FillTarget<uint32_t>&, uint64_t, uint64_t,
-                                       ChunkMeta*, hipStream_t);
+                                       MetaPartial*, ChunkMeta*, hipStream_t);
 template void LaunchTextFill<uint64_t>(const char*, size_t, const uint32_t*, size_t,
                                        const TextParseConfig&, const uint64_t*,
                                        const FillTarget<uint64_t>&, uint64_t, uint64_t,
-                                       ChunkMeta*, hipStream_t);
+                                       MetaPartial*, ChunkMeta*, hipStream_t);
 
 }  // namespace gpu
 }  // namespace dmlc

@@ -179,7 +179,8 @@ template <TextFormat F, typename IndexType>
 __global__ __launch_bounds__(kThreads) void k_tok_fill(
     const uint8_t* __restrict__ text, size_t n, const uint32_t* __restrict__ tok_pos,
     const uint32_t* __restrict__ tok_line, size_t ntok, const uint32_t* __restrict__ line_first_tok,
-    const uint64_t* __restrict__ line_info, FillTarget<IndexType> out, ChunkMeta* __restrict__ meta) {
+    const uint64_t* __restrict__ line_info, FillTarget<IndexType> out,
+    MetaPartial* __restrict__ partials) {
   uint64_t mx_index = 0, mx_field = 0;
   bool any_value = false, any_weight = false, irregular = false, neg = false;
   for (size_t k = blockIdx.x * static_cast<size_t>(kThreads) + threadIdx.x; k < ntok;
@@ -205,6 +206,7 @@ __global__ __launch_bounds__(kThreads) void k_tok_fill(
           out.label[row] = l;
           out.offset[row] = nnz0;
           if (out.weight != nullptr) out.weight[row] = r == 2 ? wgt : 1.0f;
+          if (out.qid != nullptr) out.qid[row] = 0;  // qid lines take the exact path
         }
         any_weight |= (r == 2);
         return;
@@ -265,23 +267,15 @@ __global__ __launch_bounds__(kThreads) void k_tok_fill(
     }
     neg |= bad;
   }
-  const uint64_t mi = dev::wave_max(mx_index);
-  const uint64_t mf = dev::wave_max(mx_field);
-  const bool av = __ballot(any_value) != 0;
-  const bool aw = __ballot(any_weight) != 0;
-  const bool ir = __ballot(irregular) != 0;
-  const bool ng = __ballot(neg) != 0;
-  if (dev::lane_id() == 0) {
-    if (mi != 0) atomicMax(&meta->max_index, static_cast<unsigned long long>(mi));
-    if (mf != 0) atomicMax(&meta->max_field, static_cast<unsigned long long>(mf));
-    unsigned fl = 0;
-    if (av) fl |= kFlagValue;
-    if (aw) fl |= kFlagWeight;
-    if (ir) fl |= kFlagIrregular;
-    if (ng) fl |= kFlagNegIndex;
-    if (F == TextFormat::kLibFM) fl |= kFlagField;
-    if (fl != 0) atomicOr(&meta->flags, fl);
-  }
+  // K8: workgroup reduction into this block's slot (no same-address atomics)
+  unsigned fl = 0;
+  if (any_value) fl |= kFlagValue;
+  if (any_weight) fl |= kFlagWeight;
+  if (irregular) fl |= kFlagIrregular;
+  if (neg) fl |= kFlagNegIndex;
+  if (F == TextFormat::kLibFM) fl |= kFlagField;
+  dev::block_store_partial(static_cast<unsigned long long>(mx_index),
+                           static_cast<unsigned long long>(mx_field), fl, partials);
 }
 
 int Grid(size_t work, size_t per_block, size_t cap) {
@@ -324,17 +318,20 @@ template <typename IndexType>
 void LaunchTokenFill(const char* text, size_t nbytes, TextFormat format, const uint32_t* tok_pos,
                      const uint32_t* tok_line, size_t ntok, const uint32_t* line_first_tok,
                      const uint64_t* line_info, const FillTarget<IndexType>& out, uint64_t nrows,
-                     uint64_t nnz, ChunkMeta* meta, hipStream_t stream) {
+                     uint64_t nnz, MetaPartial* partials, ChunkMeta* meta, hipStream_t stream) {
   if (ntok != 0) {
-    const dim3 grid(Grid(ntok, kThreads, 1 << 16)), block(kThreads);
+    // ~1000 workgroups x 4 tokens per lane: enough waves to fill 256 CUs,
+    // few enough partial slots for the single-workgroup reduction
+    const dim3 grid(Grid(ntok, kThreads * 4, 2048)), block(kThreads);
     const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
     if (format == TextFormat::kLibFM) {
       hipLaunchKernelGGL((k_tok_fill<TextFormat::kLibFM, IndexType>), grid, block, 0, stream, t,
-                         nbytes, tok_pos, tok_line, ntok, line_first_tok, line_info, out, meta);
+                         nbytes, tok_pos, tok_line, ntok, line_first_tok, line_info, out, partials);
     } else {
       hipLaunchKernelGGL((k_tok_fill<TextFormat::kLibSVM, IndexType>), grid, block, 0, stream, t,
-                         nbytes, tok_pos, tok_line, ntok, line_first_tok, line_info, out, meta);
+                         nbytes, tok_pos, tok_line, ntok, line_first_tok, line_info, out, partials);
     }
+    LaunchReducePartials(partials, static_cast<int>(grid.x), meta, stream);
   }
   LaunchCloseOffsets(out.offset, out.row_base + nrows, out.nnz_base + nnz, stream);
 }
@@ -342,11 +339,11 @@ void LaunchTokenFill(const char* text, size_t nbytes, TextFormat format, const u
 template void LaunchTokenFill<uint32_t>(const char*, size_t, TextFormat, const uint32_t*,
                                         const uint32_t*, size_t, const uint32_t*, const uint64_t*,
                                         const FillTarget<uint32_t>&, uint64_t, uint64_t,
-                                        ChunkMeta*, hipStream_t);
+                                        MetaPartial*, ChunkMeta*, hipStream_t);
 template void LaunchTokenFill<uint64_t>(const char*, size_t, TextFormat, const uint32_t*,
                                         const uint32_t*, size_t, const uint32_t*, const uint64_t*,
                                         const FillTarget<uint64_t>&, uint64_t, uint64_t,
-                                        ChunkMeta*, hipStream_t);
+                                        MetaPartial*, ChunkMeta*, hipStream_t);
 
 }  // namespace gpu
 }  // namespace dmlc
