@@ -43,6 +43,8 @@ def parse_args():
     ap.add_argument("--pinned-slots", type=int, default=4)
     ap.add_argument("--device-slots", type=int, default=3)
     ap.add_argument("--device", choices=["auto", "gpu", "cpu"], default="auto")
+    ap.add_argument("--zero-copy", default="auto", choices=["auto", "0", "1"],
+                    help="mmap + hipHostRegister the shard (DMA from page cache)")
     return ap.parse_args()
 
 
@@ -117,7 +119,8 @@ def main():
     if use_gpu:
         parser = data.GPUParser(ddir, rank, world, format="libsvm", chunk_mb=args.chunk_mb,
                                 read_threads=read_threads, pinned_slots=args.pinned_slots,
-                                device_slots=args.device_slots, device=local_rank)
+                                device_slots=args.device_slots, device=local_rank,
+                                zero_copy=args.zero_copy)
         csr = data.DeviceCSR()
 
         def step():
@@ -187,6 +190,8 @@ def main():
                 "chunk_mb": args.chunk_mb,
                 "read_threads": read_threads,
                 "device": "gpu" if use_gpu else "cpu",
+                "ingest": ("zero-copy mmap+hipHostRegister DMA" if use_gpu and parser.stats().get("zero_copy")
+                           else "parallel pread -> pinned ring -> hipMemcpyAsync"),
             },
             "per_gpu_rows_per_sec": round(value / max(1, world), 1),
             "input_GBps": round(nbytes * args.steps / elapsed / 1e9, 3),

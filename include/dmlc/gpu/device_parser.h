@@ -50,6 +50,12 @@ struct DeviceParserConfig {
   char delimiter{','};
   /*! \brief LibSVM/LibFM: token-parallel kernels with exact per-line fallback */
   bool fast_path{true};
+  /*!
+   * \brief zero-copy ingest: mmap the partition and hipHostRegister it so the
+   *  DMA engines read the page cache directly (-1 auto with fallback to the
+   *  pinned pread ring, 0 off, 1 required)
+   */
+  int zero_copy{-1};
   /*! \brief apply `?k=v` overrides (chunk_mb, pinned_slots, device_slots,
    *  read_threads, device, format, label_column, weight_column, delimiter) */
   void Update(const std::map<std::string, std::string>& args);
@@ -67,6 +73,9 @@ struct DeviceParserStats {
   double wait_reader_sec{0};
   /*! \brief seconds the host waited for GPU results */
   double wait_gpu_sec{0};
+  /*! \brief zero-copy mode active, and the one-time mmap + register cost */
+  bool zero_copy{false};
+  double register_sec{0};
 };
 
 /*!

@@ -23,6 +23,11 @@ if [[ $STAGES == *bench* ]]; then
   timeout -k 10 900 python bench.py $BENCH_ARGS > $OUT/bench.json 2> $OUT/bench.err
   rc=$?; echo "bench rc=$rc"; cat $OUT/bench.json; tail -5 $OUT/bench.err
   [ $rc -eq 0 ] || exit $rc
+  if [ -n "${BENCH2_ARGS:-}" ]; then
+    timeout -k 10 900 python bench.py $BENCH2_ARGS > $OUT/bench2.json 2> $OUT/bench2.err
+    rc=$?; echo "bench2 rc=$rc"; cat $OUT/bench2.json; tail -5 $OUT/bench2.err
+    [ $rc -eq 0 ] || exit $rc
+  fi
 fi
 if [[ $STAGES == *prof* ]]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \

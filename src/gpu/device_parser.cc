@@ -23,6 +23,10 @@
 #include <dmlc/timer.h>
 
 #include <cstdlib>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include <algorithm>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -64,6 +68,8 @@ void DeviceParserConfig::Update(const std::map<std::string, std::string>& args) 
       delimiter = v[0];
     } else if (k == "fast_path") {
       fast_path = v != "0" && v != "false";
+    } else if (k == "zero_copy") {
+      zero_copy = (v == "auto" || v == "-1") ? -1 : ((v == "0" || v == "false") ? 0 : 1);
     }
   }
   chunk_bytes = (chunk_bytes + 4095) & ~size_t(4095);
@@ -79,6 +85,104 @@ namespace {
 struct HostSlot {
   PinnedBuffer buf;
   size_t size{0};
+};
+
+/*!
+ * \brief zero-copy source: the partition's files are mmap'ed and registered
+ *  with hipHostRegister(ReadOnly), so every H2D DMA reads the page cache
+ *  directly (no CPU memcpy into pinned slots).  Chunks are cut at line
+ *  boundaries inside one file; a file boundary always ends a chunk, so no
+ *  record ever spans files and no '\n' has to be inserted.
+ */
+class ZeroCopySource {
+ public:
+  struct Piece {
+    const char* ptr;
+    size_t size;
+  };
+  /*! \brief map + register every segment; false (and unmapped) on failure */
+  bool Init(io::InputSplitBase* split, size_t chunk_bytes) {
+    chunk_bytes_ = chunk_bytes;
+    const long page = sysconf(_SC_PAGESIZE);
+    for (const auto& seg : split->ShardSegments()) {
+      const int fd = split->filesystem()->OpenRawFd(split->files()[seg.file_index].path);
+      if (fd < 0) return Fail();
+      const size_t map_off = seg.begin & ~static_cast<size_t>(page - 1);
+      const size_t map_len = seg.end - map_off;
+      void* p = mmap(nullptr, map_len, PROT_READ, MAP_SHARED | MAP_POPULATE, fd, map_off);
+      ::close(fd);
+      if (p == MAP_FAILED) return Fail();
+      Mapping m{p, map_len, false};
+      maps_.push_back(m);
+      hipError_t err = hipHostRegister(p, map_len, hipHostRegisterReadOnly);
+      if (err != hipSuccess) {
+        (void)hipGetLastError();
+        return Fail();
+      }
+      maps_.back().registered = true;
+      segs_.push_back(Seg{static_cast<const char*>(p) + (seg.begin - map_off), seg.end - seg.begin});
+    }
+    return true;
+  }
+  ~ZeroCopySource() { Release(); }
+  void Reset() {
+    seg_ = 0;
+    off_ = 0;
+  }
+  /*! \brief next chunk of whole lines; false at the end */
+  bool Next(Piece* out) {
+    while (seg_ < segs_.size() && off_ >= segs_[seg_].size) {
+      ++seg_;
+      off_ = 0;
+    }
+    if (seg_ >= segs_.size()) return false;
+    const Seg& s = segs_[seg_];
+    const char* b = s.ptr + off_;
+    size_t len = std::min(chunk_bytes_, s.size - off_);
+    if (off_ + len < s.size) {
+      // cut after the last EOL of the window
+      size_t cut = len;
+      while (cut > 0 && b[cut - 1] != '\n' && b[cut - 1] != '\r') --cut;
+      CHECK(cut != 0) << "a line is longer than chunk_bytes (" << chunk_bytes_ << ")";
+      len = cut;
+    }
+    out->ptr = b;
+    out->size = len;
+    off_ += len;
+    return true;
+  }
+  size_t PartitionBytes() const {
+    size_t n = 0;
+    for (const auto& s : segs_) n += s.size;
+    return n;
+  }
+
+ private:
+  struct Mapping {
+    void* ptr;
+    size_t len;
+    bool registered;
+  };
+  struct Seg {
+    const char* ptr;
+    size_t size;
+  };
+  bool Fail() {
+    Release();
+    return false;
+  }
+  void Release() {
+    for (auto& m : maps_) {
+      if (m.registered) (void)hipHostUnregister(m.ptr);
+      munmap(m.ptr, m.len);
+    }
+    maps_.clear();
+    segs_.clear();
+  }
+  size_t chunk_bytes_{0};
+  std::vector<Mapping> maps_;
+  std::vector<Seg> segs_;
+  size_t seg_{0}, off_{0};
 };
 
 /*! \brief per-chunk sizes the host needs to place the output */
@@ -126,7 +230,18 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     hmeta_.Reserve(2 * sizeof(ChunkMeta));
     slots_.Reserve(kMaxPartialBlocks * sizeof(MetaPartial));
     iter_.set_max_capacity(static_cast<size_t>(cfg_.pinned_slots));
-    StartReader();
+    if (cfg_.zero_copy != 0) {
+      zc_.reset(new ZeroCopySource());
+      const double t0 = GetTime();
+      if (!zc_->Init(split_.get(), cfg_.chunk_bytes)) {
+        CHECK(cfg_.zero_copy != 1) << "zero_copy=1 but the input cannot be mmap'ed + registered";
+        zc_.reset();
+      } else {
+        stats_.register_sec = GetTime() - t0;
+        stats_.zero_copy = true;
+      }
+    }
+    if (zc_ == nullptr) StartReader();
   }
 
   ~DeviceParserImpl() override {
@@ -134,14 +249,21 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     // destructors never throw, so errors are ignored here
     if (copy_) (void)hipStreamSynchronize(copy_->get());
     if (compute_) (void)hipStreamSynchronize(compute_->get());
-    for (auto& f : inflight_) iter_.Recycle(&f.slot);
+    for (auto& f : inflight_) {
+      if (f.slot != nullptr) iter_.Recycle(&f.slot);
+    }
     inflight_.clear();
     iter_.Destroy();
+    zc_.reset();
   }
 
   void BeforeFirst() override {
     DrainInflight();
-    iter_.BeforeFirst();
+    if (zc_ != nullptr) {
+      zc_->Reset();
+    } else {
+      iter_.BeforeFirst();
+    }
   }
 
   bool Next() override {
@@ -165,14 +287,17 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     FinishEpoch(out);
   }
 
-  size_t PartitionBytes() const override { return reader_->PartitionBytes(); }
+  size_t PartitionBytes() const override {
+    return zc_ != nullptr ? zc_->PartitionBytes() : reader_->PartitionBytes();
+  }
   const DeviceParserStats& Stats() const override { return stats_; }
   hipStream_t stream() const override { return compute_->get(); }
 
  private:
   struct Inflight {
-    HostSlot* slot;
+    HostSlot* slot;  // nullptr in zero-copy mode
     int d;
+    size_t size;
   };
 
   void StartReader() {
@@ -199,19 +324,33 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   void FillPipeline() {
     while (static_cast<int>(inflight_.size()) + busy_ < cfg_.device_slots && !reader_done_) {
       HostSlot* slot = nullptr;
-      const double t0 = GetTime();
-      if (!iter_.Next(&slot)) {
-        reader_done_ = true;
-        break;
+      const void* src = nullptr;
+      size_t size = 0;
+      if (zc_ != nullptr) {
+        ZeroCopySource::Piece piece;
+        if (!zc_->Next(&piece)) {
+          reader_done_ = true;
+          break;
+        }
+        src = piece.ptr;
+        size = piece.size;
+      } else {
+        const double t0 = GetTime();
+        if (!iter_.Next(&slot)) {
+          reader_done_ = true;
+          break;
+        }
+        stats_.wait_reader_sec += GetTime() - t0;
+        src = slot->buf.get();
+        size = slot->size;
       }
-      stats_.wait_reader_sec += GetTime() - t0;
       const int d = next_dslot_;
       next_dslot_ = (next_dslot_ + 1) % cfg_.device_slots;
       DMLC_HIP_CHECK(hipStreamWaitEvent(copy_->get(), parsed_[d]->get(), 0));
-      DMLC_HIP_CHECK(hipMemcpyAsync(dtext_[d]->get(), slot->buf.get(), slot->size,
-                                    hipMemcpyHostToDevice, copy_->get()));
+      DMLC_HIP_CHECK(
+          hipMemcpyAsync(dtext_[d]->get(), src, size, hipMemcpyHostToDevice, copy_->get()));
       copied_[d]->Record(copy_->get());
-      inflight_.push_back(Inflight{slot, d});
+      inflight_.push_back(Inflight{slot, d, size});
     }
   }
 
@@ -219,7 +358,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     copy_->Synchronize();
     compute_->Synchronize();
     while (!inflight_.empty()) {
-      iter_.Recycle(&inflight_.front().slot);
+      if (inflight_.front().slot != nullptr) iter_.Recycle(&inflight_.front().slot);
       inflight_.pop_front();
     }
     reader_done_ = false;
@@ -377,7 +516,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     inflight_.pop_front();
     busy_ = 1;
     cur_slot_ = cur.slot;
-    const size_t nbytes = cur.slot->size;
+    const size_t nbytes = cur.size;
     const char* text = dtext_[cur.d]->template get<char>();
     hipStream_t s = compute_->get();
     ScopedRange range("parse_chunk");
@@ -436,6 +575,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   DeviceBuffer slots_;
   PinnedBuffer hmeta_;
   ThreadedIter<HostSlot> iter_;
+  std::unique_ptr<ZeroCopySource> zc_;
   std::deque<Inflight> inflight_;
   HostSlot* cur_slot_{nullptr};
   int next_dslot_{0};

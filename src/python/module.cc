@@ -304,6 +304,8 @@ class PyDeviceParser {
     d["exact_chunks"] = s.exact_chunks;
     d["wait_reader_sec"] = s.wait_reader_sec;
     d["wait_gpu_sec"] = s.wait_gpu_sec;
+    d["zero_copy"] = s.zero_copy;
+    d["register_sec"] = s.register_sec;
     return d;
   }
   uintptr_t Stream() const { return reinterpret_cast<uintptr_t>(p_->stream()); }

@@ -54,6 +54,22 @@ def test_fast_and_exact_paths_agree(tmp_path, fast, weights):
     assert_same(g, cpu_rows(p, "libsvm"))
 
 
+@pytest.mark.parametrize("zero_copy", [0, 1])
+def test_zero_copy_and_pinned_ring_agree(tmp_path, zero_copy):
+    d = tmp_path / "zc"
+    d.mkdir()
+    for i in range(3):
+        data.write_synthetic(str(d / f"p{i}.libsvm"), i * 900, (i + 1) * 900, seed=13)
+    with open(d / "p9.libsvm", "w") as f:
+        f.write("1 1:1 2:2\n0 3:3")  # no trailing newline at a file boundary
+    for nparts in (1, 3):
+        g = gpu_rows(str(d), "libsvm", nparts=nparts, chunk_bytes=48 * 1024, zero_copy=zero_copy)
+        assert_same(g, cpu_rows(str(d), "libsvm", nparts=nparts))
+    gp = data.GPUParser(str(d), chunk_bytes=48 * 1024, zero_copy=zero_copy)
+    gp.parse_all()
+    assert gp.stats()["zero_copy"] == bool(zero_copy)
+
+
 def test_irregular_chunks_fall_back(tmp_path):
     # qid tokens and digit-less tokens are not handled by the token-parallel
     # path: those chunks must be re-parsed exactly, the rest stay fast
