@@ -68,6 +68,20 @@ $(BUILD)/dmlc_unittest: $(TEST_SRCS) $(LIB) $(HEADERS)
 
 test-bin: $(BUILD)/dmlc_unittest
 
+# Sanitizer builds of the CPU library + unit tests: no HIP code,
+# so they run anywhere.  `make tsan && build/dmlc_unittest_tsan`.
+SAN_SRCS := $(filter-out src/gpu/%,$(CPU_SRCS))
+SAN_FLAGS := -std=c++17 -O1 -g -fno-omit-frame-pointer -ffp-contract=off $(WARN) -Iinclude -Isrc \
+  -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -fopenmp
+$(BUILD)/dmlc_unittest_tsan: $(TEST_SRCS) $(SAN_SRCS) $(HEADERS)
+	@mkdir -p $(BUILD)
+	$(CXX) $(SAN_FLAGS) -fsanitize=thread $(TEST_SRCS) $(SAN_SRCS) -o $@ -ldl -lpthread
+$(BUILD)/dmlc_unittest_asan: $(TEST_SRCS) $(SAN_SRCS) $(HEADERS)
+	@mkdir -p $(BUILD)
+	$(CXX) $(SAN_FLAGS) -fsanitize=address,undefined $(TEST_SRCS) $(SAN_SRCS) -o $@ -ldl -lpthread
+tsan: $(BUILD)/dmlc_unittest_tsan
+asan: $(BUILD)/dmlc_unittest_asan
+
 $(BUILD)/dmlc_gen: tools/dmlc_gen.cc $(LIB) $(HEADERS)
 	@mkdir -p $(BUILD)
 	$(CXX) $(CXXFLAGS_BASE) $< -o $@ -L$(LIBDIR) -ldmlc -Wl,-rpath,$(abspath $(LIBDIR)) \
@@ -83,4 +97,4 @@ tools: $(BUILD)/dmlc_gen $(BUILD)/dmlc_bench_cpu
 clean:
 	rm -rf $(BUILD) $(LIB) $(PYMOD)
 
-.PHONY: all clean test-bin tools
+.PHONY: all clean test-bin tools tsan asan

@@ -23,6 +23,8 @@ class MemoryFixedSizeStream : public SeekStream {
   MemoryFixedSizeStream(void* p_buffer, size_t buffer_size)
       : p_buffer_(reinterpret_cast<char*>(p_buffer)),
         buffer_size_(buffer_size) {}
+  using SeekStream::Read;
+  using SeekStream::Write;
   size_t Read(void* ptr, size_t size) override {
     CHECK(curr_ptr_ <= buffer_size_) << "read position past end of fixed buffer";
     size_t nread = std::min(buffer_size_ - curr_ptr_, size);
@@ -51,6 +53,8 @@ class MemoryFixedSizeStream : public SeekStream {
 class MemoryStringStream : public SeekStream {
  public:
   explicit MemoryStringStream(std::string* p_buffer) : p_buffer_(p_buffer) {}
+  using SeekStream::Read;
+  using SeekStream::Write;
   size_t Read(void* ptr, size_t size) override {
     CHECK(curr_ptr_ <= p_buffer_->length());
     size_t nread = std::min(p_buffer_->length() - curr_ptr_, size);

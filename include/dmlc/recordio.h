@@ -29,7 +29,7 @@ namespace dmlc {
 class RecordIOWriter {
  public:
   /*! \brief magic word marking a record head */
-  static const uint32_t kMagic = 0xced7230a;
+  static constexpr uint32_t kMagic = 0xced7230a;
   /*! \brief pack (cflag, length) into the lrec word */
   inline static uint32_t EncodeLRec(uint32_t cflag, uint32_t length) {
     return (cflag << 29U) | length;

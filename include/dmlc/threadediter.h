@@ -229,7 +229,7 @@ inline void ThreadedIter<DType>::ProducerLoop(std::function<bool(DType**)> next,
     {
       std::lock_guard<std::mutex> lock(mutex_);
       if (err != nullptr) {
-        iter_exception_ = err;
+        iter_exception_ = std::move(err);  // the consumer holds the only reference
         produce_end_ = true;
         if (cell != nullptr) free_cells_.push_back(cell);
       } else if (has_next) {
