@@ -9,6 +9,8 @@
  * extension cannot load, importing the ops fails loudly.
  */
 #include <dmlc/data.h>
+#include <dmlc/dist/communicator.h>
+#include <dmlc/dist/tracker_client.h>
 #include <dmlc/gpu/device_parser.h>
 #include <dmlc/io.h>
 #include <dmlc/logging.h>
@@ -488,4 +490,108 @@ PYBIND11_MODULE(_dmlc, m) {
   m.def("gpu_device_count", &gpu::DeviceCount);
   m.def("gpu_arch", &gpu::DeviceArchName);
   m.def("get_time", &GetTime);
+
+  // ---------------------------------------------------------------- dist
+  using dist::TrackerClient;
+  py::class_<TrackerClient>(m, "TrackerClient")
+      .def(py::init<std::string, int, std::string, int, int, double>(), py::arg("uri") = "",
+           py::arg("port") = 0, py::arg("jobid") = "", py::arg("rank") = -1,
+           py::arg("world_size") = -1, py::arg("timeout") = 600.0)
+      .def("start",
+           [](TrackerClient& c, bool recover) {
+             dist::Topology t;
+             {
+               py::gil_scoped_release nogil;
+               t = c.Start(recover);
+             }
+             return py::make_tuple(t.rank, t.parent, t.world_size, t.tree, t.ring_prev,
+                                   t.ring_next);
+           },
+           py::arg("recover") = false)
+      .def("print", &TrackerClient::Print, py::call_guard<py::gil_scoped_release>())
+      .def("shutdown", &TrackerClient::Shutdown, py::call_guard<py::gil_scoped_release>())
+      .def("heartbeat", &TrackerClient::Heartbeat, py::call_guard<py::gil_scoped_release>())
+      .def("start_heartbeat", &TrackerClient::StartHeartbeat, py::arg("period") = 5.0)
+      .def("stop_heartbeat", &TrackerClient::StopHeartbeat,
+           py::call_guard<py::gil_scoped_release>())
+      .def("rccl_put",
+           [](TrackerClient& c, const std::string& key, py::bytes blob) {
+             std::string b = blob;
+             py::gil_scoped_release nogil;
+             c.RcclPut(key, b);
+           })
+      .def("rccl_get",
+           [](TrackerClient& c, const std::string& key) {
+             std::string b;
+             {
+               py::gil_scoped_release nogil;
+               b = c.RcclGet(key);
+             }
+             return py::bytes(b);
+           })
+      .def("barrier", &TrackerClient::Barrier, py::arg("key") = "default",
+           py::arg("count") = -1, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("rank", &TrackerClient::rank)
+      .def_property_readonly("world_size", &TrackerClient::world_size);
+
+  using dist::Communicator;
+  py::enum_<dist::DataType>(m, "DataType")
+      .value("int8", dist::DataType::kInt8).value("uint8", dist::DataType::kUInt8)
+      .value("int32", dist::DataType::kInt32).value("uint32", dist::DataType::kUInt32)
+      .value("int64", dist::DataType::kInt64).value("uint64", dist::DataType::kUInt64)
+      .value("float16", dist::DataType::kFloat16).value("float32", dist::DataType::kFloat32)
+      .value("float64", dist::DataType::kFloat64).value("bfloat16", dist::DataType::kBFloat16);
+  py::enum_<dist::ReduceOp>(m, "ReduceOp")
+      .value("sum", dist::ReduceOp::kSum).value("prod", dist::ReduceOp::kProd)
+      .value("max", dist::ReduceOp::kMax).value("min", dist::ReduceOp::kMin)
+      .value("avg", dist::ReduceOp::kAvg);
+  py::class_<Communicator>(m, "Communicator")
+      .def(py::init([](int rank, int world, int device, py::bytes uid) {
+             std::string id = uid;
+             py::gil_scoped_release nogil;
+             return new Communicator(rank, world, device, id);
+           }),
+           py::arg("rank"), py::arg("world_size"), py::arg("device"), py::arg("unique_id"))
+      .def_static("available", &Communicator::Available)
+      .def_static("library_path", &Communicator::LibraryPath)
+      .def_static("new_unique_id", []() { return py::bytes(Communicator::NewUniqueId()); })
+      .def_property_readonly("rank", &Communicator::rank)
+      .def_property_readonly("world_size", &Communicator::world_size)
+      .def_property_readonly("device", &Communicator::device)
+      .def("all_reduce",
+           [stream_of](Communicator& c, uintptr_t send, uintptr_t recv, size_t count,
+                       dist::DataType dt, dist::ReduceOp op, uintptr_t stream) {
+             c.AllReduce(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), count,
+                         dt, op, stream_of(stream));
+           })
+      .def("broadcast",
+           [stream_of](Communicator& c, uintptr_t send, uintptr_t recv, size_t count,
+                       dist::DataType dt, int root, uintptr_t stream) {
+             c.Broadcast(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), count,
+                         dt, root, stream_of(stream));
+           })
+      .def("all_gather",
+           [stream_of](Communicator& c, uintptr_t send, uintptr_t recv, size_t count,
+                       dist::DataType dt, uintptr_t stream) {
+             c.AllGather(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), count,
+                         dt, stream_of(stream));
+           })
+      .def("reduce_scatter",
+           [stream_of](Communicator& c, uintptr_t send, uintptr_t recv, size_t count,
+                       dist::DataType dt, dist::ReduceOp op, uintptr_t stream) {
+             c.ReduceScatter(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv),
+                             count, dt, op, stream_of(stream));
+           })
+      .def("all_to_all_v",
+           [stream_of](Communicator& c, uintptr_t send, std::vector<size_t> sc,
+                       std::vector<size_t> sd, uintptr_t recv, std::vector<size_t> rc,
+                       std::vector<size_t> rd, dist::DataType dt, uintptr_t stream) {
+             c.AllToAllV(reinterpret_cast<const void*>(send), sc, sd, reinterpret_cast<void*>(recv),
+                         rc, rd, dt, stream_of(stream));
+           })
+      .def("barrier", [stream_of](Communicator& c, uintptr_t stream) {
+        py::gil_scoped_release nogil;
+        c.Barrier(stream_of(stream));
+      })
+      .def("abort", &Communicator::Abort);
 }

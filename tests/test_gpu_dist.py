@@ -1,0 +1,60 @@
+"""Native RCCL communicator on one MI355X (world size 1: RCCL refuses two
+ranks on one device, and multi-GPU runs belong to the driver's 8-GPU node).
+Checks every collective against the trivially known result, and that the
+communicator reuses PyTorch's RCCL instead of loading a second copy."""
+import pytest
+import torch
+
+from dmlc_core_amd import _dmlc
+
+pytestmark = pytest.mark.gpu
+
+
+def _ptr(t):
+    return t.data_ptr()
+
+
+def test_rccl_collectives_world1():
+    assert _dmlc.Communicator.available()
+    # torch (imported first by dmlc_core_amd) already loaded its RCCL
+    assert "torch" in _dmlc.Communicator.library_path(), _dmlc.Communicator.library_path()
+    uid = _dmlc.Communicator.new_unique_id()
+    assert len(uid) == 128
+    comm = _dmlc.Communicator(0, 1, 0, uid)
+    s = torch.cuda.current_stream().cuda_stream
+    x = torch.arange(1000, dtype=torch.float32, device="cuda")
+    y = torch.empty_like(x)
+    comm.all_reduce(_ptr(x), _ptr(y), x.numel(), _dmlc.DataType.float32, _dmlc.ReduceOp.sum, s)
+    g = torch.empty_like(x)
+    comm.all_gather(_ptr(x), _ptr(g), x.numel(), _dmlc.DataType.float32, s)
+    b = torch.zeros_like(x)
+    comm.broadcast(_ptr(x), _ptr(b), x.numel(), _dmlc.DataType.float32, 0, s)
+    m = torch.tensor([5, 9], dtype=torch.int64, device="cuda")
+    mo = torch.empty_like(m)
+    comm.all_reduce(_ptr(m), _ptr(mo), 2, _dmlc.DataType.int64, _dmlc.ReduceOp.max, s)
+    a2a = torch.empty(300, dtype=torch.float32, device="cuda")
+    comm.all_to_all_v(_ptr(x), [300], [100], _ptr(a2a), [300], [0], _dmlc.DataType.float32, s)
+    comm.barrier(s)
+    torch.cuda.synchronize()
+    assert torch.equal(y, x) and torch.equal(g, x) and torch.equal(b, x)
+    assert mo.tolist() == [5, 9]
+    assert torch.equal(a2a, x[100:400])
+    del comm
+
+
+def test_torch_rccl_process_group_world1(tmp_path):
+    import torch.distributed as td
+    from dmlc_core_amd.parallel import dist
+    import os
+    os.environ.update({"RANK": "0", "WORLD_SIZE": "1", "MASTER_ADDR": "127.0.0.1",
+                       "MASTER_PORT": "29533"})
+    try:
+        info = dist.init("nccl")
+        assert info["world_size"] == 1
+        counts, mx = dist.global_stats([3.0, 4.0], 17)
+        assert counts == [3.0, 4.0] and mx == 17
+        assert td.get_backend() == "nccl"
+    finally:
+        dist.finalize()
+        for k in ("RANK", "WORLD_SIZE", "MASTER_PORT"):
+            os.environ.pop(k, None)

@@ -1,0 +1,315 @@
+"""Tracker / launcher tests with in-process fake workers:
+topology parity with the reference, rank assignment, recover, the new rccl /
+barrier / heartbeat commands, dmlc-submit --cluster local end to end, a
+gloo process group bootstrapped through the tracker, and the command lines
+of the cluster backends (dry run)."""
+import os
+import subprocess
+import sys
+import textwrap
+import threading
+import time
+
+import pytest
+
+from dmlc_core_amd.parallel import tracker as trk
+from dmlc_core_amd.parallel.client import TrackerClient
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _reference_link_map(n):
+    """The reference algorithm, written out with Python sets (test oracle)."""
+    def nbr(r):
+        r1 = r + 1
+        out = []
+        if r1 > 1:
+            out.append(r1 // 2 - 1)
+        if r1 * 2 - 1 < n:
+            out.append(r1 * 2 - 1)
+        if r1 * 2 < n:
+            out.append(r1 * 2)
+        return out
+    tree = {r: nbr(r) for r in range(n)}
+    parent = {r: (r + 1) // 2 - 1 for r in range(n)}
+
+    def share(r):
+        cset = set(tree[r]) - {parent[r]}
+        if not cset:
+            return [r]
+        lst, cnt = [r], 0
+        for v in cset:
+            sub = share(v)
+            cnt += 1
+            if cnt == len(cset):
+                sub.reverse()
+            lst += sub
+        return lst
+    order = share(0)
+    ring = {order[i]: (order[(i - 1) % n], order[(i + 1) % n]) for i in range(n)}
+    rmap, k = {0: 0}, 0
+    for i in range(n - 1):
+        k = ring[k][1]
+        rmap[k] = i + 1
+    return ({rmap[k]: [rmap[x] for x in v] for k, v in tree.items()},
+            {rmap[k]: (-1 if k == 0 else rmap[v]) for k, v in parent.items()},
+            {rmap[k]: (rmap[a], rmap[b]) for k, (a, b) in ring.items()})
+
+
+def test_topology_matches_reference_measurement():
+    tree, parent, ring = trk.link_map(8)
+    # SURVEY §2.11 [measured] 8-rank output of the reference tracker
+    expect = {0: [1, 7], 1: [0, 2, 4], 2: [1, 3], 3: [2], 4: [1], 5: [7], 6: [7], 7: [0, 5, 6]}
+    assert {k: sorted(v) for k, v in tree.items()} == expect
+    assert ring[0] == (7, 1)
+    assert all(ring[r] == ((r - 1) % 8, (r + 1) % 8) for r in range(8))
+
+
+@pytest.mark.parametrize("n", list(range(1, 40)) + [64, 100, 257])
+def test_topology_equals_reference_algorithm(n):
+    tree, parent, ring = trk.link_map(n)
+    rt, rp, rr = _reference_link_map(n)
+    assert {k: sorted(v) for k, v in tree.items()} == {k: sorted(v) for k, v in rt.items()}
+    assert parent == rp
+    assert ring == rr
+
+
+def _start_tracker(n, **kw):
+    t = trk.RabitTracker("127.0.0.1", n, port=19091, port_end=19999, **kw)
+    t.start(n)
+    return t
+
+
+def test_fake_workers_rank_rccl_barrier_print_shutdown():
+    n = 6
+    t = _start_tracker(n, timeout=60)
+    results = {}
+    errors = []
+
+    def worker(i):
+        try:
+            c = TrackerClient("127.0.0.1", t.port, jobid=f"job{i}")
+            topo = c.start()
+            uid = c.exchange_unique_id(lambda: b"\x01" * 128, key="world")
+            c.barrier("b1")
+            c.print(f"hello from {topo.rank}")
+            c.barrier("b2")
+            results[i] = (topo, uid)
+            c.shutdown()
+        except Exception as e:  # pragma: no cover - surfaced below
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(n)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(60)
+    t.join(30)
+    assert not errors, errors
+    ranks = sorted(r[0].rank for r in results.values())
+    assert ranks == list(range(n))
+    assert all(r[1] == b"\x01" * 128 for r in results.values())
+    assert all(r[0].world_size == n for r in results.values())
+    tree, parent, ring = trk.link_map(n)
+    for topo, _ in results.values():
+        assert sorted(topo.tree) == sorted(tree[topo.rank])
+        assert topo.parent == parent[topo.rank]
+    assert len([m for m in t.messages if m.startswith("hello from")]) == n
+
+
+def test_recover_keeps_rank_by_jobid():
+    t = _start_tracker(2, timeout=60)
+    out = {}
+
+    def run(i):
+        c = TrackerClient("127.0.0.1", t.port, jobid=f"task{i}")
+        out[i] = c.start().rank
+        if i == 1:
+            # restart: a fresh client with the same jobid and its old rank
+            c2 = TrackerClient("127.0.0.1", t.port, jobid=f"task{i}", rank=out[i])
+            out["re"] = c2.start(recover=True).rank
+        c.shutdown()
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(60)
+    t.join(30)
+    assert out["re"] == out[1]
+
+
+def test_heartbeat_timeout_fails_the_job():
+    t = _start_tracker(2, heartbeat_timeout=1.0, timeout=60)
+    c0 = TrackerClient("127.0.0.1", t.port)
+    c1 = TrackerClient("127.0.0.1", t.port)
+    th = [threading.Thread(target=c.start) for c in (c0, c1)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(30)
+    c0.heartbeat()
+    c1.heartbeat()
+    c1.shutdown()
+    # c0 "dies": no more heartbeats and no shutdown
+    with pytest.raises(trk.TrackerError, match="missed heartbeats"):
+        t.join(30)
+
+
+def test_job_timeout():
+    t = _start_tracker(3, timeout=1.0)
+    with pytest.raises(trk.TrackerError, match="did not finish"):
+        t.join(30)
+
+
+WORKER = textwrap.dedent("""
+    import os, sys
+    sys.path.insert(0, {root!r})
+    from dmlc_core_amd.parallel.client import TrackerClient
+    c = TrackerClient()
+    topo = c.start()
+    uid = c.exchange_unique_id(lambda: os.urandom(128))
+    c.barrier("x")
+    c.print("rank=%d task=%s local=%s uid=%s" % (topo.rank, os.environ["DMLC_TASK_ID"],
+            os.environ.get("DMLC_LOCAL_RANK"), uid[:4].hex()))
+    c.shutdown()
+""")
+
+
+def _submit(args, timeout=240):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    return subprocess.run([sys.executable, "-m", "dmlc_core_amd.parallel.launch.submit", *args],
+                          capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
+
+
+def test_submit_local_end_to_end(tmp_path):
+    script = tmp_path / "w.py"
+    script.write_text(WORKER.format(root=ROOT))
+    p = _submit(["--cluster", "local", "--num-workers", "4", "--gpus-per-node", "2",
+                 "--host-ip", "127.0.0.1", "--timeout", "200", sys.executable, str(script)])
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stderr.splitlines() if "rank=" in l]
+    assert len(lines) == 4
+    uids = {l.split("uid=")[1] for l in lines}
+    assert len(uids) == 1  # everyone got rank 0's id
+    assert sorted(l.split("local=")[1].split()[0] for l in lines) == ["0", "0", "1", "1"]
+
+
+TORCH_WORKER = textwrap.dedent("""
+    import os, sys
+    sys.path.insert(0, {root!r})
+    import torch
+    from dmlc_core_amd.parallel import dist
+    info = dist.init("gloo")
+    counts, mx = dist.global_stats([1.0, float(info["rank"])], max_index=10 * info["rank"])
+    g = dist.all_gather_counts(info["rank"] + 1, 2 * info["rank"])
+    model = torch.nn.Linear(4, 1)
+    torch.manual_seed(info["rank"])
+    red = dist.GradAllReducer(model.parameters(), bucket_mb=0.00001)
+    loss = model(torch.randn(8, 4)).sum()
+    loss.backward()
+    red.synchronize()
+    ref = torch.tensor([model.weight.grad.sum().item()])
+    import torch.distributed as td
+    allg = [torch.zeros(1) for _ in range(info["world_size"])]
+    td.all_gather(allg, ref)
+    assert all(torch.allclose(a, ref) for a in allg), "grads differ across ranks"
+    assert counts[0] == info["world_size"], counts
+    assert mx == 10 * (info["world_size"] - 1)
+    assert [x[0] for x in g] == list(range(1, info["world_size"] + 1))
+    print("OK", info["rank"], flush=True)
+    dist.finalize()
+""")
+
+
+def test_gloo_process_group_via_tracker(tmp_path):
+    script = tmp_path / "t.py"
+    script.write_text(TORCH_WORKER.format(root=ROOT))
+    p = _submit(["--cluster", "local", "--num-workers", "3", "--host-ip", "127.0.0.1",
+                 "--timeout", "200", sys.executable, str(script)])
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    assert p.stdout.count("OK") == 3
+
+
+def test_gloo_process_group_via_torch_env(tmp_path):
+    script = tmp_path / "t.py"
+    script.write_text(TORCH_WORKER.format(root=ROOT).replace(
+        'info = dist.init("gloo")',
+        'os.environ.pop("DMLC_TRACKER_URI"); info = dist.init("gloo")\n'
+        'c = __import__("dmlc_core_amd.parallel.client", fromlist=["x"]).TrackerClient()\n'
+        'c.rank = info["rank"]'))
+    # the tracker still needs a shutdown per rank: send it from the worker
+    script.write_text(script.read_text().replace(
+        "dist.finalize()", "dist.finalize(); c.shutdown()"))
+    p = _submit(["--cluster", "local", "--num-workers", "2", "--torch-env", "1",
+                 "--host-ip", "127.0.0.1", "--timeout", "200", sys.executable, str(script)])
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    assert p.stdout.count("OK") == 2
+
+
+@pytest.mark.parametrize("cluster,needle", [
+    ("mpi", "mpirun -n 4"),
+    ("slurm", "srun --share --exclusive=user"),
+    ("sge", "qsub -cwd -t 1-4"),
+    ("mesos", "mesos-execute"),
+    ("kubernetes", "amd.com/gpu"),
+    ("yarn", "org.apache.hadoop.yarn.dmlc.Client"),
+    ("local", "DMLC_LOCAL_RANK=1"),
+])
+def test_backend_dry_run(cluster, needle, tmp_path):
+    args = ["--cluster", cluster, "--num-workers", "4", "--gpus-per-node", "8", "--dry-run",
+            "--env", "FOO=bar", "echo", "hi"]
+    if cluster == "mesos":
+        args = ["--mesos-master", "m:5050"] + args
+    p = _submit(args, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert needle in p.stdout
+    assert "FOO" in p.stdout
+
+
+def test_ssh_dry_run(tmp_path):
+    hf = tmp_path / "hosts"
+    hf.write_text("10.0.0.1\n10.0.0.2:2222\n")
+    p = _submit(["--cluster", "ssh", "--num-workers", "4", "--host-file", str(hf), "--dry-run",
+                 "--gpus-per-node", "8", "echo", "hi"], timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("ssh")]
+    assert len(lines) == 4
+    assert sum("10.0.0.2" in l and "-p 2222" in l for l in lines) == 2
+
+
+def test_native_cpp_client_against_python_tracker():
+    from dmlc_core_amd import _dmlc
+    n = 4
+    t = _start_tracker(n, timeout=60)
+    out, errors = {}, []
+
+    def worker(i):
+        try:
+            c = _dmlc.TrackerClient("127.0.0.1", t.port, f"cpp{i}", -1, -1, 30.0)
+            rank, parent, world, tree, prev, nxt = c.start()
+            if rank == 0:
+                c.rccl_put("world", b"\x07" * 128)
+                uid = b"\x07" * 128
+            else:
+                uid = c.rccl_get("world")
+            c.barrier("cpp")
+            c.print(f"cpp rank {rank}")
+            out[i] = (rank, parent, world, sorted(tree), prev, nxt, uid)
+            c.shutdown()
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(n)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(60)
+    t.join(30)
+    assert not errors, errors
+    tree, parent, ring = trk.link_map(n)
+    assert sorted(v[0] for v in out.values()) == list(range(n))
+    for rank, par, world, tr, prev, nxt, uid in out.values():
+        assert world == n and par == parent[rank] and tr == sorted(tree[rank])
+        assert (prev, nxt) == ring[rank]
+        assert uid == b"\x07" * 128
