@@ -71,7 +71,7 @@ test-bin: $(BUILD)/dmlc_unittest
 
 # Sanitizer builds of the CPU library + unit tests: no HIP code,
 # so they run anywhere.  `make tsan && build/dmlc_unittest_tsan`.
-SAN_SRCS := $(filter-out src/gpu/%,$(CPU_SRCS))
+SAN_SRCS := $(filter-out src/gpu/% src/dist/communicator.cc,$(CPU_SRCS))
 SAN_FLAGS := -std=c++17 -O1 -g -fno-omit-frame-pointer -ffp-contract=off $(WARN) -Iinclude -Isrc \
   -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -fopenmp
 $(BUILD)/dmlc_unittest_tsan: $(TEST_SRCS) $(SAN_SRCS) $(HEADERS)
