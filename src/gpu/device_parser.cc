@@ -37,6 +37,7 @@
 #include "../io/shard_reader.h"
 #include "../io/uri_spec.h"
 #include "./kernels.h"
+#include "./zero_copy_source.h"
 
 namespace dmlc {
 namespace gpu {
@@ -85,104 +86,6 @@ namespace {
 struct HostSlot {
   PinnedBuffer buf;
   size_t size{0};
-};
-
-/*!
- * \brief zero-copy source: the partition's files are mmap'ed and registered
- *  with hipHostRegister(ReadOnly), so every H2D DMA reads the page cache
- *  directly (no CPU memcpy into pinned slots).  Chunks are cut at line
- *  boundaries inside one file; a file boundary always ends a chunk, so no
- *  record ever spans files and no '\n' has to be inserted.
- */
-class ZeroCopySource {
- public:
-  struct Piece {
-    const char* ptr;
-    size_t size;
-  };
-  /*! \brief map + register every segment; false (and unmapped) on failure */
-  bool Init(io::InputSplitBase* split, size_t chunk_bytes) {
-    chunk_bytes_ = chunk_bytes;
-    const long page = sysconf(_SC_PAGESIZE);
-    for (const auto& seg : split->ShardSegments()) {
-      const int fd = split->filesystem()->OpenRawFd(split->files()[seg.file_index].path);
-      if (fd < 0) return Fail();
-      const size_t map_off = seg.begin & ~static_cast<size_t>(page - 1);
-      const size_t map_len = seg.end - map_off;
-      void* p = mmap(nullptr, map_len, PROT_READ, MAP_SHARED | MAP_POPULATE, fd, map_off);
-      ::close(fd);
-      if (p == MAP_FAILED) return Fail();
-      Mapping m{p, map_len, false};
-      maps_.push_back(m);
-      hipError_t err = hipHostRegister(p, map_len, hipHostRegisterReadOnly);
-      if (err != hipSuccess) {
-        (void)hipGetLastError();
-        return Fail();
-      }
-      maps_.back().registered = true;
-      segs_.push_back(Seg{static_cast<const char*>(p) + (seg.begin - map_off), seg.end - seg.begin});
-    }
-    return true;
-  }
-  ~ZeroCopySource() { Release(); }
-  void Reset() {
-    seg_ = 0;
-    off_ = 0;
-  }
-  /*! \brief next chunk of whole lines; false at the end */
-  bool Next(Piece* out) {
-    while (seg_ < segs_.size() && off_ >= segs_[seg_].size) {
-      ++seg_;
-      off_ = 0;
-    }
-    if (seg_ >= segs_.size()) return false;
-    const Seg& s = segs_[seg_];
-    const char* b = s.ptr + off_;
-    size_t len = std::min(chunk_bytes_, s.size - off_);
-    if (off_ + len < s.size) {
-      // cut after the last EOL of the window
-      size_t cut = len;
-      while (cut > 0 && b[cut - 1] != '\n' && b[cut - 1] != '\r') --cut;
-      CHECK(cut != 0) << "a line is longer than chunk_bytes (" << chunk_bytes_ << ")";
-      len = cut;
-    }
-    out->ptr = b;
-    out->size = len;
-    off_ += len;
-    return true;
-  }
-  size_t PartitionBytes() const {
-    size_t n = 0;
-    for (const auto& s : segs_) n += s.size;
-    return n;
-  }
-
- private:
-  struct Mapping {
-    void* ptr;
-    size_t len;
-    bool registered;
-  };
-  struct Seg {
-    const char* ptr;
-    size_t size;
-  };
-  bool Fail() {
-    Release();
-    return false;
-  }
-  void Release() {
-    for (auto& m : maps_) {
-      if (m.registered) (void)hipHostUnregister(m.ptr);
-      munmap(m.ptr, m.len);
-    }
-    maps_.clear();
-    segs_.clear();
-  }
-  size_t chunk_bytes_{0};
-  std::vector<Mapping> maps_;
-  std::vector<Seg> segs_;
-  size_t seg_{0}, off_{0};
 };
 
 /*! \brief per-chunk sizes the host needs to place the output */

@@ -171,19 +171,31 @@ void LaunchTokenFill(const char* text, size_t nbytes, TextFormat format, const u
                      uint64_t nnz, MetaPartial* partials, ChunkMeta* meta, hipStream_t stream);
 
 // ----------------------------- RecordIO (K7) -----------------------------
+/*! \brief error bits reported by the RecordIO kernels */
+constexpr uint32_t kRecErrTruncated = 1;   // a part runs past the chunk end
+constexpr uint32_t kRecErrBadPart = 2;     // continuation part without its head
+/*! \brief u64 tile counters needed for `nwords` words */
+size_t RecordIOTiles(size_t nwords);
 /*!
- * \brief K7a: flag record heads (aligned magic + cflag 0/1) in a chunk of
- *  `nwords` u32 words; head_pos receives compacted word positions,
- *  meta->nlines the number of records.
+ * \brief K7a: count record heads (aligned magic whose lrec has cflag 0/1) per
+ *  4096-word tile and exclusive-scan the tile counts in place;
+ *  *nrec receives the number of records.  partials >= ScanPartials(tiles)+1.
  */
-void LaunchRecordIOIndex(const uint32_t* words, size_t nwords, uint64_t* tile_scratch,
-                         uint32_t* head_pos, ChunkMeta* meta, hipStream_t stream);
-/*! \brief K7b: payload length of every record (multi-part aware) -> rec_len */
-void LaunchRecordIOLengths(const uint32_t* words, size_t nwords, const uint32_t* head_pos,
-                           size_t nrec, uint64_t* rec_len, hipStream_t stream);
+void LaunchRecordIOCount(const uint32_t* words, size_t nwords, uint64_t* tile_counts,
+                         uint64_t* partials, uint64_t* nrec, hipStream_t stream);
+/*! \brief K7b: compacted, ordered word positions of the record heads */
+void LaunchRecordIOEmit(const uint32_t* words, size_t nwords, const uint64_t* tile_counts,
+                        uint32_t* head_pos, hipStream_t stream);
 /*!
- * \brief K7c: gather payloads contiguously: out + rec_off[i] (exclusive scan of
- *  rec_len), re-inserting escaped magic words of multi-part records.
+ * \brief K7c: payload bytes of every record, following multi-part chains
+ *  (continuation parts add their length plus the re-inserted 4-byte magic);
+ *  error bits are OR-ed into *err.
+ */
+void LaunchRecordIOLengths(const uint32_t* words, size_t nwords, const uint32_t* head_pos,
+                           size_t nrec, uint64_t* rec_len, uint32_t* err, hipStream_t stream);
+/*!
+ * \brief K7d: gather payloads contiguously to out + rec_off[i] (exclusive
+ *  scan of rec_len), re-inserting the escaped magic between parts.
  */
 void LaunchRecordIOGather(const uint32_t* words, size_t nwords, const uint32_t* head_pos,
                           size_t nrec, const uint64_t* rec_off, uint8_t* out,

@@ -12,6 +12,8 @@
 #include <dmlc/dist/communicator.h>
 #include <dmlc/dist/tracker_client.h>
 #include <dmlc/gpu/device_parser.h>
+#include <dmlc/gpu/device_recordio.h>
+#include <dmlc/gpu/hip_utils.h>
 #include <dmlc/io.h>
 #include <dmlc/logging.h>
 #include <dmlc/recordio.h>
@@ -356,6 +358,88 @@ void BindIndexType(py::module_& m, const std::string& suffix) {
       .def("stream", &PyDeviceParser<I>::Stream);
 }
 
+// --------------------------------------------------------------- device recordio
+class PyDeviceRecordIO {
+ public:
+  PyDeviceRecordIO(const std::string& uri, unsigned part, unsigned nparts, py::dict kwargs) {
+    gpu::DeviceRecordIOConfig cfg;
+    std::map<std::string, std::string> args;
+    for (auto kv : kwargs) args[py::str(kv.first)] = py::str(kv.second);
+    cfg.Update(args);
+    reader_.reset(gpu::DeviceRecordIOReader::Create(uri, part, nparts, cfg));
+    DMLC_HIP_CHECK(hipGetDevice(&device_));
+  }
+  bool Next() {
+    py::gil_scoped_release nogil;
+    return reader_->Next();
+  }
+  py::dict ValueCapsules() { return Batch(reader_->Value()); }
+  /*! \brief (offsets numpy, payload bytes) of the last Next() */
+  py::tuple ValueToHost() { return ToHost(reader_->Value()); }
+  py::tuple ResidentToHost() { return ToHost(Resident()); }
+  void BeforeFirst() { reader_->BeforeFirst(); }
+  size_t PartitionBytes() const { return reader_->PartitionBytes(); }
+  py::dict Stats() const {
+    const auto& s = reader_->Stats();
+    py::dict d;
+    d["bytes"] = s.bytes;
+    d["chunks"] = s.chunks;
+    d["records"] = s.records;
+    d["zero_copy"] = s.zero_copy;
+    d["wait_gpu_sec"] = s.wait_gpu_sec;
+    return d;
+  }
+  uintptr_t Stream() const { return reinterpret_cast<uintptr_t>(reader_->stream()); }
+
+ private:
+  const gpu::DeviceRecordBatch& Resident() { return resident_view_; }
+  py::dict Batch(const gpu::DeviceRecordBatch& b) {
+    py::dict d;
+    d["size"] = b.size;
+    d["bytes"] = b.bytes;
+    d["offset"] = ToCapsule(b.offset, static_cast<int64_t>(b.size + 1), device_, reader_);
+    d["data"] = ToCapsule(b.data, static_cast<int64_t>(b.bytes), device_, reader_);
+    return d;
+  }
+  py::tuple ToHost(const gpu::DeviceRecordBatch& b) {
+    std::vector<uint64_t> off(b.size + 1, 0);
+    std::string data(b.bytes, '\0');
+    DMLC_HIP_CHECK(hipStreamSynchronize(reader_->stream()));
+    if (b.size > 0) {
+      DMLC_HIP_CHECK(hipMemcpy(off.data(), b.offset, off.size() * 8, hipMemcpyDeviceToHost));
+    }
+    if (b.bytes > 0) DMLC_HIP_CHECK(hipMemcpy(&data[0], b.data, b.bytes, hipMemcpyDeviceToHost));
+    return py::make_tuple(ToNumpy(off.data(), off.size()), py::bytes(data));
+  }
+  std::shared_ptr<gpu::DeviceRecordIOReader> reader_;
+  gpu::DeviceRecordBatch resident_view_;
+  int device_{0};
+
+  friend void BindRecordIO(py::module_& m);
+};
+
+void BindRecordIO(py::module_& m) {
+  py::class_<PyDeviceRecordIO>(m, "DeviceRecordIO")
+      .def(py::init<const std::string&, unsigned, unsigned, py::dict>(), py::arg("uri"),
+           py::arg("part") = 0, py::arg("nparts") = 1, py::arg("config") = py::dict())
+      .def("next", &PyDeviceRecordIO::Next)
+      .def("read_all",
+           [](PyDeviceRecordIO& self) {
+             {
+               py::gil_scoped_release nogil;
+               self.resident_view_ = self.reader_->ReadAll();
+             }
+             return self.Batch(self.resident_view_);
+           })
+      .def("value", &PyDeviceRecordIO::ValueCapsules)
+      .def("value_to_host", &PyDeviceRecordIO::ValueToHost)
+      .def("resident_to_host", &PyDeviceRecordIO::ResidentToHost)
+      .def("before_first", &PyDeviceRecordIO::BeforeFirst)
+      .def("partition_bytes", &PyDeviceRecordIO::PartitionBytes)
+      .def("stats", &PyDeviceRecordIO::Stats)
+      .def("stream", &PyDeviceRecordIO::Stream);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_dmlc, m) {
@@ -363,6 +447,7 @@ PYBIND11_MODULE(_dmlc, m) {
   py::register_exception<dmlc::Error>(m, "DMLCError");
   BindIndexType<uint32_t>(m, "");
   BindIndexType<uint64_t>(m, "64");
+  BindRecordIO(m);
   py::class_<PyInputSplit>(m, "InputSplit")
       .def(py::init<const std::string&, unsigned, unsigned, const std::string&,
                     const std::string&, bool, int, size_t>(),
