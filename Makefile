@@ -30,7 +30,8 @@ LDFLAGS_LIB := -shared -fopenmp -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64 
 CPU_SRCS := src/logging.cc src/io.cc src/recordio.cc src/data.cc src/config.cc src/synthetic.cc \
   src/io/local_filesys.cc src/io/input_split_base.cc src/io/line_split.cc \
   src/io/recordio_split.cc src/io/remote_filesys.cc \
-  src/io/shard_reader.cc \
+  src/io/shard_reader.cc src/io/http.cc src/io/s3_filesys.cc src/io/azure_filesys.cc \
+  src/io/hdfs_filesys.cc \
   src/gpu/runtime.cc src/gpu/device_parser.cc src/gpu/device_recordio.cc \
   src/dist/tracker_client.cc src/dist/communicator.cc
 HIP_SRCS := $(wildcard src/gpu/*.hip)

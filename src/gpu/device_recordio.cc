@@ -158,7 +158,14 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
           exhausted_ = true;
           break;
         }
-        CHECK_LE(blob.size, cfg_.chunk_bytes + 16) << "RecordIO chunk larger than chunk_bytes";
+        if (blob.size + 16 > s.text.bytes() || blob.size + 16 > s.staging.bytes()) {
+          // the split's chunks can exceed the hint: grow this slot once both
+          // streams no longer touch it
+          DMLC_HIP_CHECK(hipStreamSynchronize(copy_.get()));
+          DMLC_HIP_CHECK(hipStreamSynchronize(compute_.get()));
+          s.text.Reserve(blob.size + 16);
+          s.staging.Reserve(blob.size + 16);
+        }
         if (s.used) s.copied.Synchronize();  // staging[d] free again
         std::memcpy(s.staging.get<char>(), blob.dptr, blob.size);
         src = s.staging.get<char>();

@@ -109,8 +109,14 @@ py::dict BlockToDict(const RowBlock<I>& b) {
 template <typename I>
 class PyParser {
  public:
-  PyParser(const std::string& uri, unsigned part, unsigned nparts, const std::string& type)
-      : p_(Parser<I>::Create(uri.c_str(), part, nparts, type.c_str())) {}
+  PyParser(const std::string& uri, unsigned part, unsigned nparts, const std::string& type) {
+    py::gil_scoped_release nogil;
+    p_.reset(Parser<I>::Create(uri.c_str(), part, nparts, type.c_str()));
+  }
+  ~PyParser() {
+    py::gil_scoped_release nogil;
+    p_.reset();
+  }
   bool Next() {
     py::gil_scoped_release nogil;
     return p_->Next();
@@ -140,9 +146,14 @@ class PyParser {
 template <typename I>
 class PyRowBlockIter {
  public:
-  PyRowBlockIter(const std::string& uri, unsigned part, unsigned nparts, const std::string& type)
-      : it_(RowBlockIter<I>::Create(uri.c_str(), part, nparts, type.c_str())) {}
-  bool Next() { return it_->Next(); }
+  PyRowBlockIter(const std::string& uri, unsigned part, unsigned nparts, const std::string& type) {
+    py::gil_scoped_release nogil;
+    it_.reset(RowBlockIter<I>::Create(uri.c_str(), part, nparts, type.c_str()));
+  }
+  bool Next() {
+    py::gil_scoped_release nogil;
+    return it_->Next();
+  }
   py::dict Value() { return BlockToDict(it_->Value()); }
   void BeforeFirst() { it_->BeforeFirst(); }
   size_t NumCol() const { return it_->NumCol(); }
@@ -154,27 +165,51 @@ class PyRowBlockIter {
 class PyInputSplit {
  public:
   PyInputSplit(const std::string& uri, unsigned part, unsigned nparts, const std::string& type,
-               const std::string& index_uri, bool shuffle, int seed, size_t batch_size)
-      : s_(index_uri.empty()
-               ? InputSplit::Create(uri.c_str(), part, nparts, type.c_str())
-               : InputSplit::Create(uri.c_str(), index_uri.c_str(), part, nparts, type.c_str(),
-                                    shuffle, seed, batch_size)) {}
+               const std::string& index_uri, bool shuffle, int seed, size_t batch_size) {
+    py::gil_scoped_release nogil;
+    s_.reset(index_uri.empty()
+                 ? InputSplit::Create(uri.c_str(), part, nparts, type.c_str())
+                 : InputSplit::Create(uri.c_str(), index_uri.c_str(), part, nparts, type.c_str(),
+                                      shuffle, seed, batch_size));
+  }
+  ~PyInputSplit() {
+    py::gil_scoped_release nogil;
+    s_.reset();
+  }
   py::object NextRecord() {
     InputSplit::Blob b;
-    if (!s_->NextRecord(&b)) return py::none();
+    bool ok;
+    {
+      py::gil_scoped_release nogil;
+      ok = s_->NextRecord(&b);
+    }
+    if (!ok) return py::none();
     return py::bytes(static_cast<const char*>(b.dptr), b.size);
   }
   py::object NextChunk() {
     InputSplit::Blob b;
-    if (!s_->NextChunk(&b)) return py::none();
+    bool ok;
+    {
+      py::gil_scoped_release nogil;
+      ok = s_->NextChunk(&b);
+    }
+    if (!ok) return py::none();
     return py::bytes(static_cast<const char*>(b.dptr), b.size);
   }
   py::object NextBatch(size_t n) {
     InputSplit::Blob b;
-    if (!s_->NextBatch(&b, n)) return py::none();
+    bool ok;
+    {
+      py::gil_scoped_release nogil;
+      ok = s_->NextBatch(&b, n);
+    }
+    if (!ok) return py::none();
     return py::bytes(static_cast<const char*>(b.dptr), b.size);
   }
-  void BeforeFirst() { s_->BeforeFirst(); }
+  void BeforeFirst() {
+    py::gil_scoped_release nogil;
+    s_->BeforeFirst();
+  }
   void ResetPartition(unsigned part, unsigned nparts) { s_->ResetPartition(part, nparts); }
   size_t TotalSize() { return s_->GetTotalSize(); }
   void HintChunkSize(size_t n) { s_->HintChunkSize(n); }
@@ -185,16 +220,32 @@ class PyInputSplit {
 
 class PyStream {
  public:
-  PyStream(const std::string& uri, const std::string& mode)
-      : s_(Stream::Create(uri.c_str(), mode.c_str())) {}
+  // every call may block on I/O (remote filesystems): release the GIL
+  PyStream(const std::string& uri, const std::string& mode) {
+    py::gil_scoped_release nogil;
+    s_.reset(Stream::Create(uri.c_str(), mode.c_str()));
+  }
+  ~PyStream() {
+    py::gil_scoped_release nogil;
+    s_.reset();
+  }
   py::bytes Read(size_t n) {
     std::string buf(n, '\0');
-    size_t got = s_->Read(&buf[0], n);
-    buf.resize(got);
+    {
+      py::gil_scoped_release nogil;
+      size_t got = s_->Read(&buf[0], n);
+      buf.resize(got);
+    }
     return py::bytes(buf);
   }
-  void Write(const std::string& data) { s_->Write(data.data(), data.size()); }
-  void Close() { s_.reset(); }
+  void Write(const std::string& data) {
+    py::gil_scoped_release nogil;
+    s_->Write(data.data(), data.size());
+  }
+  void Close() {
+    py::gil_scoped_release nogil;
+    s_.reset();
+  }
 
  private:
   std::unique_ptr<Stream> s_;

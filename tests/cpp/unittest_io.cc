@@ -16,7 +16,31 @@
 #include <vector>
 
 #include "../../src/data/strtonum.h"
+#include "../../src/io/crypto.h"
 #include "./testing.h"
+
+TEST(Crypto, Sha256HmacBase64Vectors) {
+  namespace c = dmlc::io::crypto;
+  EXPECT_EQ(c::Hex(c::Sha256Digest("abc")),
+            "ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad");
+  EXPECT_EQ(c::Hex(c::Sha256Digest("")),
+            "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855");
+  std::string million(1000000, 'a');
+  EXPECT_EQ(c::Hex(c::Sha256Digest(million)),
+            "cdc76e5c9914fb9281a1c7e284d73e67f1809a48a497200e046d39ccc7112cd0");
+  // RFC 4231 test case 2
+  EXPECT_EQ(c::Hex(c::HmacSha256("Jefe", "what do ya want for nothing?")),
+            "5bdcc146bf60754e6a042426089575c75a003f089d2739839dec58b964ec3843");
+  // RFC 4231 test case 6 (key longer than the block)
+  EXPECT_EQ(c::Hex(c::HmacSha256(std::string(131, '\xaa'),
+                                 "Test Using Larger Than Block-Size Key - Hash Key First")),
+            "60e431591ee0b67f0d8a26aacbf5b77f8e0bc6213728c5140546040f0ee37f54");
+  EXPECT_EQ(c::Base64Encode("foobar"), "Zm9vYmFy");
+  EXPECT_EQ(c::Base64Encode("fooba"), "Zm9vYmE=");
+  EXPECT_EQ(c::Base64Decode("Zm9vYg=="), "foob");
+  EXPECT_EQ(c::UriEncode("a b/c~"), "a%20b%2Fc~");
+  EXPECT_EQ(c::UriEncode("a b/c", false), "a%20b/c");
+}
 
 namespace {
 

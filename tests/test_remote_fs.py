@@ -1,0 +1,135 @@
+"""s3:// (SigV4), azure:// (SharedKey) and http:// backends against in-process
+mock servers that verify request signatures: streams, ranged reads larger and
+smaller than the read-ahead block, multipart / block-list uploads, paginated
+listings, and sharded InputSplit + parser over remote files."""
+import os
+
+import numpy as np
+import pytest
+
+import mock_remote
+from dmlc_core_amd import _dmlc, data, io
+
+pytestmark = pytest.mark.skipif(not os.path.exists("/usr/lib/x86_64-linux-gnu/libcurl.so.4"),
+                                reason="libcurl not installed")
+
+
+@pytest.fixture(scope="module")
+def s3():
+    srv = mock_remote.serve(mock_remote.S3Handler)
+    os.environ.update({"S3_ENDPOINT": f"http://127.0.0.1:{srv.server_address[1]}",
+                       "S3_ACCESS_KEY_ID": "AKIDTEST", "S3_SECRET_ACCESS_KEY": "secret",
+                       "S3_REGION": "us-east-1", "DMLC_S3_WRITE_BUFFER_MB": "5"})
+    yield mock_remote.S3Handler
+    srv.shutdown()
+
+
+@pytest.fixture(scope="module")
+def azure():
+    srv = mock_remote.serve(mock_remote.AzureHandler)
+    os.environ.update({"AZURE_STORAGE_ENDPOINT": f"http://127.0.0.1:{srv.server_address[1]}",
+                       "AZURE_STORAGE_ACCOUNT": mock_remote.AzureHandler.account,
+                       "AZURE_STORAGE_ACCESS_KEY": mock_remote.AzureHandler.key})
+    yield mock_remote.AzureHandler
+    srv.shutdown()
+
+
+def _blob(n, seed=0):
+    return np.random.default_rng(seed).integers(0, 256, n, dtype=np.uint8).tobytes()
+
+
+def _read_all(uri, chunk=1 << 20):
+    s = io.Stream(uri, "r")
+    out = bytearray()
+    while True:
+        b = s.read(chunk)
+        if not b:
+            return bytes(out)
+        out += b
+
+
+def test_s3_write_read_roundtrip_multipart(s3):
+    payload = _blob(12 * (1 << 20) + 12345)  # > 2 parts of 5 MiB
+    w = io.Stream("s3://bk1/dir/obj.bin", "w")
+    for i in range(0, len(payload), 3 << 20):
+        w.write(payload[i:i + (3 << 20)])
+    w.close()
+    assert s3.store["bk1/dir/obj.bin"] == payload
+    assert _read_all("s3://bk1/dir/obj.bin", chunk=64 << 20) == payload  # direct-to-buffer path
+    assert _read_all("s3://bk1/dir/obj.bin", chunk=4096) == payload      # read-ahead path
+
+
+def test_s3_small_put_and_listing_pagination(s3):
+    for i in range(5):
+        w = io.Stream(f"s3://bk2/data/part-{i}.txt", "w")
+        w.write(f"{i} 1:{i}\n".encode() * (i + 1))
+        w.close()
+    w = io.Stream("s3://bk2/data/sub/x.txt", "w")
+    w.write(b"0 1:1\n")
+    w.close()
+    # a text InputSplit over the "directory" lists every object (pages of 2)
+    split_recs = []
+    for part in range(3):
+        split_recs += [r.rstrip(b"\x00\n") for r in io.iter_records("s3://bk2/data", part, 3, "text")]
+    expect = [f"{i} 1:{i}".encode() for i in range(5) for _ in range(i + 1)]
+    assert split_recs == expect  # sub/ is a directory and is not descended into
+
+
+def test_s3_parser_matches_local(s3, tmp_path):
+    local = tmp_path / "s.libsvm"
+    data.write_synthetic(str(local), 0, 3000, seed=3)
+    raw = local.read_bytes()
+    w = io.Stream("s3://bk3/train.libsvm", "w")
+    w.write(raw)
+    w.close()
+    for nparts in (1, 2):
+        for part in range(nparts):
+            a = list(data.iter_blocks("s3://bk3/train.libsvm", part, nparts, type="libsvm"))
+            b = list(data.iter_blocks(str(local), part, nparts, type="libsvm"))
+            import pyref
+            ca, cb = pyref.concat_blocks(a), pyref.concat_blocks(b)
+            np.testing.assert_array_equal(ca["index"], cb["index"])
+            np.testing.assert_array_equal(ca["value"], cb["value"])
+
+
+def test_s3_bad_signature_rejected(s3):
+    os.environ["S3_SECRET_ACCESS_KEY"] = "wrong"
+    try:
+        with pytest.raises(Exception):
+            io.Stream("s3://bk-wrong/x", "r")
+    finally:
+        os.environ["S3_SECRET_ACCESS_KEY"] = "secret"
+
+
+def test_azure_roundtrip_blocks_and_listing(azure):
+    big = _blob((64 << 20) + 1000, seed=1)  # > one 64 MiB block -> Put Block List
+    w = io.Stream("azure://cont/big/blob.bin", "w")
+    w.write(big)
+    w.close()
+    assert azure.store["cont/big/blob.bin"] == big
+    assert _read_all("azure://cont/big/blob.bin", chunk=16 << 20) == big
+    for i in range(4):
+        w = io.Stream(f"azure://cont/txt/p{i}", "w")
+        w.write(f"line{i}\n".encode())
+        w.close()
+    recs = [r.rstrip(b"\x00\n") for p in range(2) for r in io.iter_records("azure://cont/txt", p, 2, "text")]
+    assert recs == [f"line{i}".encode() for i in range(4)]
+
+
+def test_http_ranged_reads():
+    srv = mock_remote.serve(mock_remote.PlainHandler)
+    try:
+        payload = _blob(3 << 20, seed=2)
+        mock_remote.PlainHandler.store["/files/a.bin"] = payload
+        url = f"http://127.0.0.1:{srv.server_address[1]}/files/a.bin"
+        assert _read_all(url, chunk=1000) == payload
+        mock_remote.PlainHandler.store["/files/t.txt"] = b"a\nbb\nccc\n"
+        url = f"http://127.0.0.1:{srv.server_address[1]}/files/t.txt"
+        assert [r.rstrip(b"\x00\n") for r in io.iter_records(url, 0, 1, "text")] == [b"a", b"bb", b"ccc"]
+    finally:
+        srv.shutdown()
+
+
+def test_hdfs_fails_loudly_without_libhdfs():
+    with pytest.raises(_dmlc.DMLCError, match="libhdfs"):
+        io.Stream("hdfs://namenode:8020/x", "r")
