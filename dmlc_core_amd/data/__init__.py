@@ -14,7 +14,7 @@ from typing import Dict, Iterator, Optional
 from .. import _dmlc
 
 __all__ = ["Parser", "RowBlockIter", "GPUParser", "DeviceCSR", "csr_to_torch", "iter_blocks",
-           "write_synthetic"]
+           "write_synthetic", "to_sparse_csr", "GPUBlockDataset"]
 
 write_synthetic = _dmlc.write_synthetic
 
@@ -79,6 +79,16 @@ class GPUParser:
     def value_to_host(self) -> Dict:
         return self._p.value_to_host()
 
+    def value_torch(self) -> Dict:
+        """Zero-copy torch views of the last next() block (valid until next())."""
+        import torch.utils.dlpack as tdl
+
+        return {k: None if c is None else tdl.from_dlpack(c)
+                for k, c in self._p.value_capsules().items()}
+
+    def stream(self) -> int:
+        return self._p.stream()
+
     def stats(self) -> Dict:
         return self._p.stats()
 
@@ -95,3 +105,52 @@ def csr_to_torch(csr) -> Dict[str, Optional["object"]]:
     for k, cap in csr.capsules().items():
         out[k] = None if cap is None else tdl.from_dlpack(cap)
     return out
+
+
+def to_sparse_csr(t: Dict, num_cols: Optional[int] = None):
+    """torch.sparse_csr_tensor view of a device CSR dict (``csr_to_torch`` /
+    ``GPUParser.value_torch`` output).  Index arrays are widened to int64
+    (torch's sparse CSR layout); values default to 1 for binary rows."""
+    import torch
+
+    offset = t["offset"]
+    crow = (offset.view(torch.int64) if offset.dtype == torch.uint64 else offset).to(torch.int64)
+    crow = crow - crow[0]
+    idx = t["index"]
+    if idx.dtype == torch.uint32:
+        col = idx.view(torch.int32).to(torch.int64)  # indices < 2^31 in practice
+    elif idx.dtype == torch.uint64:
+        col = idx.view(torch.int64)
+    else:
+        col = idx.to(torch.int64)
+    base = int(offset[0].item()) if offset.numel() else 0
+    nnz = int(crow[-1].item()) if crow.numel() else 0
+    col = col[base:base + nnz]
+    val = t.get("value")
+    val = torch.ones(nnz, dtype=torch.float32, device=col.device) if val is None else val[base:base + nnz]
+    ncols = int(num_cols) if num_cols is not None else (int(col.max().item()) + 1 if nnz else 0)
+    return torch.sparse_csr_tensor(crow, col, val, size=(crow.numel() - 1, ncols))
+
+
+class GPUBlockDataset:
+    """torch.utils.data-style iterable over GPU-parsed blocks of one shard.
+
+    Each item is a dict of device tensors for one parsed chunk (offset,
+    label, index, value, ...).  The tensors are views of the parser's buffers:
+    consume (or clone) them before requesting the next item.  Use with
+    ``DataLoader(ds, batch_size=None)`` or iterate directly.
+    """
+
+    def __init__(self, uri: str, part: int = 0, nparts: int = 1, format: str = "libsvm",  # noqa: A002
+                 epochs: int = 1, **config):
+        self.args = (uri, part, nparts, format, config)
+        self.epochs = epochs
+
+    def __iter__(self):
+        uri, part, nparts, fmt, config = self.args
+        p = GPUParser(uri, part, nparts, format=fmt, **config)
+        for epoch in range(self.epochs):
+            if epoch:
+                p.before_first()
+            while p.next():
+                yield p.value_torch()

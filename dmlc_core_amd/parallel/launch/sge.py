@@ -38,11 +38,12 @@ def submit(args):
     def launch(nworker, nserver, envs):
         envs = dict(envs)
         envs.update(user_envs(args))
-        script = write_runscript(os.path.join(os.getcwd(), "rundmlc.sh"), cmd)
+        script = os.path.join(os.getcwd(), "rundmlc.sh")
         c = build_command(args, envs, nworker + nserver, script)
         if args.dry_run:
             print(" ".join(c))
             return
+        write_runscript(script, cmd)
         os.makedirs(args.sge_log_dir or os.path.join(os.getcwd(), "sge-log"), exist_ok=True)
         subprocess.check_call(c)
 

@@ -364,9 +364,26 @@ class PyDeviceParser {
     return d;
   }
   uintptr_t Stream() const { return reinterpret_cast<uintptr_t>(p_->stream()); }
+  /*! \brief DLPack capsules of the last Next() block (valid until the next call) */
+  py::dict ValueCapsules() {
+    const auto& v = p_->Value();
+    std::shared_ptr<void> owner = p_;
+    py::dict d;
+    d["offset"] = ToCapsule(v.offset, static_cast<int64_t>(v.size + 1), v.device, owner);
+    d["label"] = ToCapsule(v.label, static_cast<int64_t>(v.size), v.device, owner);
+    d["index"] = ToCapsule(v.index, static_cast<int64_t>(v.nnz), v.device, owner);
+    d["value"] = v.value ? ToCapsule(v.value, static_cast<int64_t>(v.nnz), v.device, owner)
+                         : py::none();
+    d["weight"] = v.weight ? ToCapsule(v.weight, static_cast<int64_t>(v.size), v.device, owner)
+                           : py::none();
+    d["qid"] = v.qid ? ToCapsule(v.qid, static_cast<int64_t>(v.size), v.device, owner) : py::none();
+    d["field"] = v.field ? ToCapsule(v.field, static_cast<int64_t>(v.nnz), v.device, owner)
+                         : py::none();
+    return d;
+  }
 
  private:
-  std::unique_ptr<gpu::DeviceParser<I>> p_;
+  std::shared_ptr<gpu::DeviceParser<I>> p_;
 };
 
 template <typename I>
@@ -403,6 +420,7 @@ void BindIndexType(py::module_& m, const std::string& suffix) {
       .def("next", &PyDeviceParser<I>::Next)
       .def("value_to_host", &PyDeviceParser<I>::ValueToHost)
       .def("value_shape", &PyDeviceParser<I>::ValueShape)
+      .def("value_capsules", &PyDeviceParser<I>::ValueCapsules)
       .def("before_first", &PyDeviceParser<I>::BeforeFirst)
       .def("partition_bytes", &PyDeviceParser<I>::PartitionBytes)
       .def("stats", &PyDeviceParser<I>::Stats)
