@@ -48,19 +48,34 @@ def parse_args():
     return ap.parse_args()
 
 
-def dataset_dir(args) -> str:
-    return os.path.join(args.data_dir, f"libsvm_{args.rows}r_{NUM_PARTS}p_seed0")
+def dataset_dir(args, world: int) -> str:
+    # one copy per world size: the page cache of a part lives on the NUMA node
+    # of the rank that wrote it, which must be the rank that reads it
+    return os.path.join(args.data_dir, f"libsvm_{args.rows}r_{NUM_PARTS}p_seed0_w{world}")
 
 
 def ensure_dataset(args, rank: int, world: int, barrier) -> str:
-    """Rank r writes parts r, r+world, ...; a .done marker per part."""
+    """Rank r writes the parts its byte-range shard covers (parts
+    [16r/N, 16(r+1)/N) for N | 16), so their page-cache pages are first-touched
+    on its GPU's NUMA node; a .done marker per part.  The content depends only
+    on --rows (deterministic row ranges), never on N."""
+    import shutil
+
     from dmlc_core_amd.data import write_synthetic
 
-    d = dataset_dir(args)
+    d = dataset_dir(args, world)
+    if rank == 0 and os.path.isdir(args.data_dir):
+        prefix = f"libsvm_{args.rows}r_{NUM_PARTS}p_seed0"
+        for name in os.listdir(args.data_dir):
+            if name.startswith(prefix) and os.path.join(args.data_dir, name) != d:
+                shutil.rmtree(os.path.join(args.data_dir, name), ignore_errors=True)
+    barrier()
     os.makedirs(d, exist_ok=True)
     per = (args.rows + NUM_PARTS - 1) // NUM_PARTS
-    nthread = max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
-    for p in range(rank, NUM_PARTS, world):
+    nthread = max(1, min(16, len(os.sched_getaffinity(0))))
+    for p in range(NUM_PARTS):
+        if p * world // NUM_PARTS != rank:
+            continue
         path = os.path.join(d, f"part-{p:05d}.libsvm")
         done = path + ".done"
         if os.path.exists(done):
@@ -99,6 +114,11 @@ def main():
         torch.cuda.set_device(local_rank)
 
     dev = torch.device("cuda", local_rank) if use_gpu else torch.device("cpu")
+    numa = {"numa_node": -1}
+    if use_gpu:
+        from dmlc_core_amd.parallel.affinity import bind_to_gpu
+
+        numa = bind_to_gpu(local_rank)
 
     def barrier():
         if dist is not None:
@@ -114,7 +134,7 @@ def main():
     from dmlc_core_amd import data
 
     ddir = ensure_dataset(args, rank, world, barrier)
-    read_threads = args.read_threads or max(4, min(16, (os.cpu_count() or 8) // max(1, world)))
+    read_threads = args.read_threads or max(4, min(16, len(os.sched_getaffinity(0))))
 
     if use_gpu:
         parser = data.GPUParser(ddir, rank, world, format="libsvm", chunk_mb=args.chunk_mb,
@@ -190,6 +210,7 @@ def main():
                 "chunk_mb": args.chunk_mb,
                 "read_threads": read_threads,
                 "device": "gpu" if use_gpu else "cpu",
+                "numa_node_rank0": numa.get("numa_node", -1),
                 "ingest": ("zero-copy mmap+hipHostRegister DMA" if use_gpu and parser.stats().get("zero_copy")
                            else "parallel pread -> pinned ring -> hipMemcpyAsync"),
             },

@@ -225,6 +225,10 @@ class AzureFileSystem : public FileSystem {
       Fail("Azure open " + blob, head);
     }
     const size_t size = std::strtoull(head.headers["content-length"].c_str(), nullptr, 10);
+    return OpenForReadSized(path, size);
+  }
+  SeekStream* OpenForReadSized(const URI& path, size_t size) override {
+    const std::string blob = BlobOf(path);
     auto c = c_;
     return new RangedReadStream(size, [c, blob](size_t off, size_t len, char* dst) -> size_t {
       auto req = c->Make("GET", blob, {},

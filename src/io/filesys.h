@@ -74,6 +74,14 @@ class FileSystem {
    *  (local files only); -1 when the backend has none.
    */
   virtual int OpenRawFd(const URI& /*path*/) { return -1; }
+  /*!
+   * \brief open for reading when the size is already known (from a listing):
+   *  remote backends skip their HEAD request, so a reader can issue many
+   *  parallel ranged GETs on one object cheaply.  Default: OpenForRead.
+   */
+  virtual SeekStream* OpenForReadSized(const URI& path, size_t /*size*/) {
+    return OpenForRead(path, false);
+  }
 };
 
 }  // namespace io

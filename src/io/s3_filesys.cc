@@ -272,6 +272,11 @@ class S3FileSystem : public FileSystem {
       Fail("S3 open s3://" + c_->bucket() + "/" + key, head);
     }
     const size_t size = std::strtoull(head.headers["content-length"].c_str(), nullptr, 10);
+    return OpenForReadSized(path, size);
+  }
+
+  SeekStream* OpenForReadSized(const URI& path, size_t size) override {
+    const std::string key = KeyOf(path);
     auto c = c_;
     return new RangedReadStream(size, [c, key](size_t off, size_t len, char* dst) -> size_t {
       auto req = c->Make("GET", key, {},
@@ -364,6 +369,9 @@ class HttpFileSystem : public FileSystem {
       Fail("HTTP open " + path.str(), r);
     }
     const size_t size = std::strtoull(r.headers["content-length"].c_str(), nullptr, 10);
+    return OpenForReadSized(path, size);
+  }
+  SeekStream* OpenForReadSized(const URI& path, size_t size) override {
     const std::string url = path.str();
     return new RangedReadStream(size, [url](size_t off, size_t len, char* dst) -> size_t {
       HttpRequest req;

@@ -88,6 +88,8 @@ void ReadPool::Run(const std::vector<std::function<void()>>& jobs) {
 
 // --------------------------------------------------------------- reader
 namespace {
+constexpr size_t kRemotePiece = 8UL << 20;
+
 void PreadFull(int fd, char* dst, size_t len, size_t off) {
   while (len != 0) {
     const ssize_t n = ::pread(fd, dst, len, static_cast<off_t>(off));
@@ -117,8 +119,8 @@ ShardReader::ShardReader(InputSplitBase* split, int nthread)
       if (fd >= 0) {
         PreadFull(fd, &last, 1, s.end - 1);
       } else {
-        std::unique_ptr<SeekStream> st(
-            split->filesystem()->OpenForRead(split->files()[s.file].path));
+        std::unique_ptr<SeekStream> st(split->filesystem()->OpenForReadSized(
+            split->files()[s.file].path, split->files()[s.file].size));
         st->Seek(s.end - 1);
         CHECK_EQ(st->Read(&last, 1), 1U);
       }
@@ -177,20 +179,28 @@ size_t ShardReader::Fill(char* buf, size_t cap) {
         jobs.emplace_back([fd, dst, len, off]() { PreadFull(fd, dst, len, off); });
       }
     } else {
-      // remote filesystem: one sequential ranged read
+      // remote filesystem: parallel ranged GETs, one stream per piece (size
+      // known from the listing, so no HEAD per piece).  Pieces of >= 8 MiB
+      // amortise request latency; the pool size bounds connections in flight.
       FileSystem* fs = split_->filesystem();
       const URI path = split_->files()[s.file].path;
-      char* dst = buf + pos;
-      jobs.emplace_back([fs, path, dst, n, file_off]() {
-        std::unique_ptr<SeekStream> st(fs->OpenForRead(path));
-        st->Seek(file_off);
-        size_t got = 0;
-        while (got < n) {
-          const size_t r = st->Read(dst + got, n - got);
-          CHECK(r != 0) << "unexpected end of " << path.str();
-          got += r;
-        }
-      });
+      const size_t fsize = split_->files()[s.file].size;
+      const size_t piece = std::max(kRemotePiece, (n + pool_->size() - 1) / std::max(1, pool_->size()));
+      for (size_t o = 0; o < n; o += piece) {
+        const size_t len = std::min(piece, n - o);
+        char* dst = buf + pos + o;
+        const size_t off = file_off + o;
+        jobs.emplace_back([fs, path, fsize, dst, len, off]() {
+          std::unique_ptr<SeekStream> st(fs->OpenForReadSized(path, fsize));
+          st->Seek(off);
+          size_t got = 0;
+          while (got < len) {
+            const size_t r = st->Read(dst + got, len - got);
+            CHECK(r != 0) << "unexpected end of " << path.str();
+            got += r;
+          }
+        });
+      }
     }
     pos += n;
     seg_off_ += n;

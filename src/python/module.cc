@@ -28,6 +28,9 @@
 #include <vector>
 
 #include "../gpu/kernels.h"
+#include "../io/line_split.h"
+#include "../io/recordio_split.h"
+#include "../io/shard_reader.h"
 #include "./dlpack.h"
 
 namespace py = pybind11;
@@ -326,6 +329,7 @@ class PyDeviceParser {
     std::map<std::string, std::string> args;
     for (auto kv : cfg_dict) args[py::str(kv.first)] = py::str(kv.second);
     cfg.Update(args);
+    py::gil_scoped_release nogil;  // opening a remote split lists / HEADs over HTTP
     p_.reset(gpu::DeviceParser<I>::Create(uri, part, nparts, cfg));
   }
   void ParseAll(PyDeviceCSR<I>& out) {  // NOLINT
@@ -435,7 +439,10 @@ class PyDeviceRecordIO {
     std::map<std::string, std::string> args;
     for (auto kv : kwargs) args[py::str(kv.first)] = py::str(kv.second);
     cfg.Update(args);
-    reader_.reset(gpu::DeviceRecordIOReader::Create(uri, part, nparts, cfg));
+    {
+      py::gil_scoped_release nogil;
+      reader_.reset(gpu::DeviceRecordIOReader::Create(uri, part, nparts, cfg));
+    }
     DMLC_HIP_CHECK(hipGetDevice(&device_));
   }
   bool Next() {
@@ -641,6 +648,39 @@ PYBIND11_MODULE(_dmlc, m) {
       py::arg("offset"), py::arg("index"), py::arg("value"), py::arg("field"), py::arg("nrows"),
       py::arg("dim"), py::arg("scale"), py::arg("seed"), py::arg("out"), py::arg("fp8"),
       py::arg("stream"), py::arg("index64") = false);
+  m.def(
+      "read_partition",
+      [](const std::string& uri, unsigned part, unsigned nparts, const std::string& type,
+         int nthread, size_t chunk_bytes) {
+        // the host stage of the GPU ring (parallel pread / parallel ranged
+        // GETs) as a plain API: whole-record chunks of one partition
+        CHECK(type == "text" || type == "recordio")
+            << "read_partition: type must be text or recordio, got " << type;
+        std::vector<std::string> chunks;
+        {
+          py::gil_scoped_release nogil;  // listing + reads may hit a (Python) server
+          io::URI path(uri.c_str());
+          io::FileSystem* fs = io::FileSystem::GetInstance(path);
+          std::unique_ptr<io::InputSplitBase> split;
+          if (type == "text") {
+            split.reset(new io::LineSplitter(fs, uri.c_str(), part, nparts));
+          } else {
+            split.reset(new io::RecordIOSplitter(fs, uri.c_str(), part, nparts));
+          }
+          io::ShardReader reader(split.get(), nthread);
+          std::string buf(chunk_bytes, '\0');
+          for (;;) {
+            const size_t n = reader.Fill(&buf[0], buf.size());
+            if (n == 0) break;
+            chunks.emplace_back(buf.data(), n);
+          }
+        }
+        py::list out;
+        for (auto& c : chunks) out.append(py::bytes(c));
+        return out;
+      },
+      py::arg("uri"), py::arg("part") = 0, py::arg("nparts") = 1, py::arg("type") = "text",
+      py::arg("nthread") = 8, py::arg("chunk_bytes") = 64UL << 20);
   m.def("gpu_device_count", &gpu::DeviceCount);
   m.def("gpu_arch", &gpu::DeviceArchName);
   m.def("get_time", &GetTime);

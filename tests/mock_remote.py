@@ -63,6 +63,7 @@ class S3Handler(_Base):
     region = "us-east-1"
     page = 2
     requests = 0
+    heads = 0
 
     def _verify(self) -> bool:
         auth = self.headers.get("Authorization")
@@ -99,6 +100,7 @@ class S3Handler(_Base):
         return bucket, key, dict(urllib.parse.parse_qsl(u.query, keep_blank_values=True))
 
     def do_HEAD(self):
+        type(self).heads += 1
         r = self._route()
         if r is None:
             return
