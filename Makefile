@@ -3,7 +3,7 @@
 #   make            -> dmlc_core_amd/lib/libdmlc.so (CPU runtime + HIP kernels for gfx950)
 #                      dmlc_core_amd/_dmlc*.so      (pybind11 module)
 #   make test-bin   -> build/dmlc_unittest           (C++ unit tests, no GPU needed)
-#   make tools      -> build/dmlc_gen, build/dmlc_bench_cpu
+#   make tools      -> build/dmlc_gen, build/dmlc_bench_cpu, build/dmlc_recordio_dist
 #
 # Host code: g++ -std=c++17 -O3 -fopenmp -ffp-contract=off (bit-exact parsing).
 # Device code: hipcc --offload-arch=gfx950 (CDNA4 only; no other targets).
@@ -94,7 +94,12 @@ $(BUILD)/dmlc_bench_cpu: tools/dmlc_bench_cpu.cc $(LIB) $(HEADERS)
 	$(CXX) $(CXXFLAGS_BASE) $< -o $@ -L$(LIBDIR) -ldmlc -Wl,-rpath,$(abspath $(LIBDIR)) \
 	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64
 
-tools: $(BUILD)/dmlc_gen $(BUILD)/dmlc_bench_cpu
+$(BUILD)/dmlc_recordio_dist: tools/dmlc_recordio_dist.cc $(LIB) $(HEADERS)
+	@mkdir -p $(BUILD)
+	$(CXX) $(CXXFLAGS_BASE) $< -o $@ -L$(LIBDIR) -ldmlc -Wl,-rpath,$(abspath $(LIBDIR)) \
+	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64
+
+tools: $(BUILD)/dmlc_gen $(BUILD)/dmlc_bench_cpu $(BUILD)/dmlc_recordio_dist
 
 clean:
 	rm -rf $(BUILD) $(LIB) $(PYMOD)

@@ -58,3 +58,32 @@ def test_torch_rccl_process_group_world1(tmp_path):
         dist.finalize()
         for k in ("RANK", "WORLD_SIZE", "MASTER_PORT"):
             os.environ.pop(k, None)
+
+
+def test_native_recordio_worker_via_dmlc_submit(tmp_path):
+    """BASELINE config 3 end to end, no Python in the worker: dmlc-submit ->
+    tracker -> C++ TrackerClient -> rccl id exchange -> RCCL communicator ->
+    sharded K7 RecordIO decode -> RCCL all-reduce of the counts."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from dmlc_core_amd import data
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "build", "dmlc_recordio_dist")
+    assert os.path.exists(exe), "build with `make tools` (done by __graft_entry__.build)"
+    rec = str(tmp_path / "d.rec")
+    data.write_synthetic(rec, 0, 50000, format="recordio", seed=2, record_bytes=200)
+    env = dict(os.environ, PYTHONPATH=root)
+    p = subprocess.run([sys.executable, "-m", "dmlc_core_amd.parallel.launch.submit",
+                        "--cluster", "local", "--num-workers", "1", "--gpus-per-node", "1",
+                        "--host-ip", "127.0.0.1", "--timeout", "100", exe, rec, "3", "1", "1"],
+                       capture_output=True, text=True, timeout=110, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["records"] == 50000 and out["n_gpus"] == 1
+    assert out["payload_bytes"] == 50000 * 200
+    assert out["value"] > 0
