@@ -3,7 +3,8 @@
 #   make            -> dmlc_core_amd/lib/libdmlc.so (CPU runtime + HIP kernels for gfx950)
 #                      dmlc_core_amd/_dmlc*.so      (pybind11 module)
 #   make test-bin   -> build/dmlc_unittest           (C++ unit tests, no GPU needed)
-#   make tools      -> build/dmlc_gen, build/dmlc_bench_cpu, build/dmlc_recordio_dist
+#   make tools      -> build/dmlc_gen, build/dmlc_bench_cpu, build/dmlc_recordio_dist,
+#                      build/dmlc_fs, build/dmlc_recordio
 #
 # Host code: g++ -std=c++17 -O3 -fopenmp -ffp-contract=off (bit-exact parsing).
 # Device code: hipcc --offload-arch=gfx950 (CDNA4 only; no other targets).
@@ -99,7 +100,23 @@ $(BUILD)/dmlc_recordio_dist: tools/dmlc_recordio_dist.cc $(LIB) $(HEADERS)
 	$(CXX) $(CXXFLAGS_BASE) $< -o $@ -L$(LIBDIR) -ldmlc -Wl,-rpath,$(abspath $(LIBDIR)) \
 	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64
 
-tools: $(BUILD)/dmlc_gen $(BUILD)/dmlc_bench_cpu $(BUILD)/dmlc_recordio_dist
+$(BUILD)/dmlc_fs: tools/dmlc_fs.cc $(LIB) $(HEADERS)
+	@mkdir -p $(BUILD)
+	$(CXX) $(CXXFLAGS_BASE) $< -o $@ -L$(LIBDIR) -ldmlc -Wl,-rpath,$(abspath $(LIBDIR)) \
+	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64
+
+$(BUILD)/dmlc_recordio: tools/dmlc_recordio.cc $(LIB) $(HEADERS)
+	@mkdir -p $(BUILD)
+	$(CXX) $(CXXFLAGS_BASE) $< -o $@ -L$(LIBDIR) -ldmlc -Wl,-rpath,$(abspath $(LIBDIR)) \
+	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64
+
+$(BUILD)/dmlc_parameter_example: examples/parameter.cc $(LIB) $(HEADERS)
+	@mkdir -p $(BUILD)
+	$(CXX) $(CXXFLAGS_BASE) $< -o $@ -L$(LIBDIR) -ldmlc -Wl,-rpath,$(abspath $(LIBDIR)) \
+	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64
+
+tools: $(BUILD)/dmlc_parameter_example $(BUILD)/dmlc_gen $(BUILD)/dmlc_bench_cpu $(BUILD)/dmlc_recordio_dist $(BUILD)/dmlc_fs \
+  $(BUILD)/dmlc_recordio
 
 clean:
 	rm -rf $(BUILD) $(LIB) $(PYMOD)
