@@ -187,7 +187,8 @@ def test_resident_parse_repeat_and_torch(tmp_path):
     assert t["index"].device.type == "cuda"
     c = cpu_rows(p, "libsvm")
     np.testing.assert_array_equal(t["label"].cpu().numpy(), c["label"])
-    off = t["offset"].cpu().view(torch.int64).numpy() if t["offset"].dtype != torch.int64 else t["offset"].cpu().numpy()
+    off = t["offset"].cpu()
+    off = (off.view(torch.int64) if off.dtype != torch.int64 else off).numpy()
     np.testing.assert_array_equal(off.astype(np.uint64), c["offset"])
 
 
