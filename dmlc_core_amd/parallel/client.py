@@ -13,7 +13,7 @@ import os
 import socket
 import threading
 from dataclasses import dataclass, field
-from typing import List, Optional
+from typing import Callable, List, Optional
 
 from .tracker import MAGIC, Channel
 
@@ -96,23 +96,53 @@ class TrackerClient:
         ch = self._connect("shutdown")
         ch.close()
 
-    def heartbeat(self) -> None:
+    def heartbeat(self) -> Optional[str]:
+        """One liveness ping; returns None while the job is healthy, else the
+        tracker's failure reason."""
         ch = self._connect("heartbeat")
-        ch.close()
+        try:
+            status = ch.recv_int()
+            return ch.recv_str() if status != 0 else None
+        finally:
+            ch.close()
 
-    def start_heartbeat(self, period: float = 5.0) -> None:
-        """Background heartbeats so the tracker detects this rank dying."""
+    def abort(self, msg: str) -> None:
+        """Report a fatal error of this rank: the tracker fails the job and
+        every other rank hears it on its next heartbeat."""
+        ch = self._connect("abort")
+        try:
+            ch.send_str(msg)
+        finally:
+            ch.close()
+
+    def start_heartbeat(self, period: float = 5.0,
+                        on_failure: Optional[Callable[[str], None]] = None) -> None:
+        """Background heartbeats so the tracker detects this rank dying; if the
+        job fails (another rank died / aborted, or the tracker is gone)
+        ``on_failure(reason)`` runs once on the heartbeat thread."""
         self._hb_stop = threading.Event()
         stop = self._hb_stop
+
+        def report(reason: str) -> None:
+            if on_failure is not None:
+                on_failure(reason)
 
         def loop():
             while not stop.wait(period):
                 try:
-                    self.heartbeat()
-                except OSError:
+                    reason = self.heartbeat()
+                except (OSError, ConnectionError) as e:
+                    if not stop.is_set():
+                        report(f"tracker unreachable: {e}")
+                    return
+                if reason is not None:
+                    report(reason)
                     return
 
-        self.heartbeat()
+        reason = self.heartbeat()
+        if reason is not None:
+            report(reason)
+            return
         threading.Thread(target=loop, name="dmlc-heartbeat", daemon=True).start()
 
     def stop_heartbeat(self) -> None:

@@ -43,8 +43,24 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def init(backend: Optional[str] = None, timeout_s: float = 600.0) -> Dict[str, int]:
-    """Initialise the default process group; returns {rank, world_size, local_rank}."""
+def _fail_fast(reason: str) -> None:
+    """Default reaction to a tracker-signalled job failure: a peer is gone, so
+    any RCCL collective would block forever -- end this rank now (SIGTERM lets
+    the launcher's retry policy, DMLC_NUM_ATTEMPT, take over)."""
+    import logging
+    import signal
+
+    logging.getLogger("dmlc.dist").error("job failed (%s): terminating rank", reason)
+    os.kill(os.getpid(), signal.SIGTERM)
+
+
+def init(backend: Optional[str] = None, timeout_s: float = 600.0,
+         on_failure=None) -> Dict[str, int]:
+    """Initialise the default process group; returns {rank, world_size, local_rank}.
+
+    Under dmlc-submit the rank heartbeats the tracker every
+    ``DMLC_HEARTBEAT_PERIOD`` seconds (default 5, 0 = off); when the job fails
+    ``on_failure(reason)`` runs (default: terminate this rank)."""
     global _tracker
     if tdist.is_available() and tdist.is_initialized():
         return {"rank": tdist.get_rank(), "world_size": tdist.get_world_size(),
@@ -63,6 +79,9 @@ def init(backend: Optional[str] = None, timeout_s: float = 600.0) -> Dict[str, i
     elif "DMLC_TRACKER_URI" in os.environ:
         _tracker = TrackerClient()
         topo = _tracker.start()
+        period = float(os.environ.get("DMLC_HEARTBEAT_PERIOD", "5"))
+        if period > 0:
+            _tracker.start_heartbeat(period, on_failure or _fail_fast)
         if topo.rank == 0:
             host = os.environ.get("DMLC_NODE_HOST") or socket.gethostbyname(socket.gethostname())
             if os.environ.get("DMLC_JOB_CLUSTER") == "local":

@@ -18,7 +18,12 @@ New in this implementation:
   * ``barrier`` command: named, counted barrier held by the tracker;
   * ``heartbeat`` command and a liveness timeout: a rank that heartbeated once
     and then goes silent for ``heartbeat_timeout`` seconds fails the job
-    instead of hanging it (reference §7.4 quirk #8);
+    instead of hanging it (reference §7.4 quirk #8).  The reply to every
+    heartbeat is a status int (0 ok / 1 failed + reason), so live ranks learn
+    of the failure within one heartbeat period and abort their RCCL
+    communicators (``ncclCommAbort``) instead of blocking in a collective
+    whose peer is gone; the tracker raises after ``abort_grace`` seconds;
+  * ``abort`` command: a rank reports its own fatal error (fail fast);
   * an overall ``timeout`` for the rendezvous and a non-blocking event loop
     (held sockets for rccl/barrier replies never stall other workers);
   * Python 3 only (the reference breaks on 3.9+ with ``Thread.isAlive``).
@@ -223,7 +228,7 @@ class RabitTracker:
 
     def __init__(self, host_ip: str, nworker: int, port: int = 9091, port_end: int = 9999,
                  timeout: Optional[float] = None, heartbeat_timeout: Optional[float] = None,
-                 io_timeout: float = 60.0):
+                 io_timeout: float = 60.0, abort_grace: Optional[float] = None):
         family = socket.getaddrinfo(host_ip, None)[0][0]
         sock = socket.socket(family, socket.SOCK_STREAM)
         sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 0)
@@ -243,6 +248,9 @@ class RabitTracker:
         self.nworker = nworker
         self.timeout = timeout
         self.heartbeat_timeout = heartbeat_timeout
+        # how long live ranks get to see the failure in a heartbeat reply
+        self.abort_grace = abort_grace if abort_grace is not None else (
+            heartbeat_timeout if heartbeat_timeout is not None else 5.0)
         self.io_timeout = io_timeout
         self.thread: Optional[threading.Thread] = None
         self.start_time: Optional[float] = None
@@ -272,6 +280,25 @@ class RabitTracker:
         barriers: Dict[str, List[_Worker]] = {}
         last_beat: Dict[int, float] = {}
         t_begin = time.time()
+        # failure state: once a rank is declared dead (or aborts) the job is
+        # failed; live ranks learn it from their next heartbeat reply (and
+        # abort their RCCL communicators) during a grace period, then the
+        # tracker raises.
+        failed: Optional[str] = None
+        failed_at = 0.0
+        dead: Dict[int, bool] = {}
+
+        def fail(reason: str, rank: int) -> None:
+            nonlocal failed, failed_at
+            dead[rank] = True
+            if failed is None:
+                failed, failed_at = reason, time.time()
+                logger.error("job failed: %s", reason)
+                for group in list(rccl_waiters.values()) + list(barriers.values()):
+                    for h in group:  # unblock ranks waiting in rccl get / barrier
+                        h.ch.close()
+                rccl_waiters.clear()
+                barriers.clear()
 
         while len(shutdown) != n and not self._stop.is_set():
             now = time.time()
@@ -279,10 +306,13 @@ class RabitTracker:
                 raise TrackerError(f"job did not finish within {self.timeout}s "
                                    f"({len(shutdown)}/{n} ranks shut down)")
             if self.heartbeat_timeout is not None:
-                for r, t in last_beat.items():
-                    if r not in shutdown and now - t > self.heartbeat_timeout:
-                        raise TrackerError(f"rank {r} missed heartbeats for "
-                                           f"{now - t:.1f}s (> {self.heartbeat_timeout}s)")
+                for r, t in list(last_beat.items()):
+                    if r not in shutdown and r not in dead and now - t > self.heartbeat_timeout:
+                        fail(f"rank {r} missed heartbeats for {now - t:.1f}s "
+                             f"(> {self.heartbeat_timeout}s)", r)
+            if failed is not None and (now - failed_at > self.abort_grace
+                                       or len(shutdown) + len(dead) >= n):
+                raise TrackerError(failed)
             try:
                 conn, addr = self.sock.accept()
             except socket.timeout:
@@ -303,7 +333,15 @@ class RabitTracker:
                 continue
             if w.cmd == "heartbeat":
                 last_beat[w.rank] = time.time()
+                w.ch.send_int(0 if failed is None else 1)
+                if failed is not None:
+                    w.ch.send_str(failed)
                 w.ch.close()
+                continue
+            if w.cmd == "abort":
+                msg = w.ch.recv_str()
+                w.ch.close()
+                fail(f"rank {w.rank} aborted: {msg}", w.rank)
                 continue
             if w.cmd == "shutdown":
                 if w.rank < 0 or w.rank in shutdown:

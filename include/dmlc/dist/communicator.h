@@ -25,7 +25,9 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <atomic>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -91,12 +93,28 @@ class Communicator {
   void Recv(void* buf, size_t count, DataType dt, int peer, hipStream_t stream);
   /*! \brief device-side barrier (a 1-element all-reduce), then stream sync */
   void Barrier(hipStream_t stream);
-  /*! \brief abort in-flight work (failure signalled by the tracker) */
+  /*!
+   * \brief abort in-flight work (failure signalled by the tracker): safe to
+   *  call from another thread while a collective is blocked; every later
+   *  call throws dmlc::Error
+   */
   void Abort();
+  /*! \brief true once Abort() ran */
+  bool aborted() const { return aborted_.load(); }
+  /*!
+   * \brief abort this communicator when `tracker` reports a job failure
+   *  (peer missed heartbeats / aborted); cleared by the destructor.  The
+   *  tracker's heartbeat thread must be running (StartHeartbeat).
+   */
+  void AbortOnTrackerFailure(TrackerClient* tracker);
 
  private:
   void Check(int result, const char* what) const;
+  void* Live() const;
   void* comm_{nullptr};
+  std::atomic<bool> aborted_{false};
+  std::mutex abort_mutex_;
+  TrackerClient* watched_{nullptr};
   int rank_, world_, device_;
   void* scratch_{nullptr};
 };

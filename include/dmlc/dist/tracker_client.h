@@ -19,6 +19,7 @@
 
 #include <atomic>
 #include <condition_variable>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -57,11 +58,26 @@ class TrackerClient {
   void Print(const std::string& msg);
   /*! \brief tell the tracker this rank finished */
   void Shutdown();
-  /*! \brief one liveness ping */
-  void Heartbeat();
-  /*! \brief ping every `period_sec` on a background thread until Shutdown */
+  /*!
+   * \brief one liveness ping
+   * \return true while the job is healthy; false (reason in `*reason`) once
+   *  the tracker declared it failed (a rank missed heartbeats or aborted)
+   */
+  bool Heartbeat(std::string* reason = nullptr);
+  /*! \brief report a fatal error of this rank: the tracker fails the job */
+  void Abort(const std::string& msg);
+  /*!
+   * \brief ping every `period_sec` on a background thread until Shutdown; on
+   *  job failure (or an unreachable tracker) the failure handler runs once
+   */
   void StartHeartbeat(double period_sec = 5.0);
   void StopHeartbeat();
+  /*!
+   * \brief called (once, from the heartbeat thread) when the job fails, e.g.
+   *  Communicator::Abort so no rank blocks in a collective whose peer died.
+   *  nullptr clears it.
+   */
+  void SetFailureHandler(std::function<void(const std::string&)> handler);
   /*! \brief publish / fetch an opaque blob (RCCL unique id) under `key` */
   void RcclPut(const std::string& key, const std::string& blob);
   std::string RcclGet(const std::string& key);
@@ -98,6 +114,9 @@ class TrackerClient {
   std::mutex hb_mutex_;
   std::condition_variable hb_cv_;
   bool hb_stop_{false};
+  std::mutex handler_mutex_;
+  std::function<void(const std::string&)> on_failure_;
+  void ReportFailure(const std::string& reason);
 };
 
 }  // namespace dist

@@ -175,12 +175,15 @@ std::unique_ptr<Communicator> Communicator::FromTracker(TrackerClient* tracker, 
                                                         const std::string& key) {
   if (tracker->rank() < 0) tracker->Start();
   std::string id = tracker->ExchangeUniqueId([] { return NewUniqueId(); }, key);
-  return std::unique_ptr<Communicator>(
+  std::unique_ptr<Communicator> comm(
       new Communicator(tracker->rank(), tracker->world_size(), device, id));
+  comm->AbortOnTrackerFailure(tracker);  // effective once StartHeartbeat runs
+  return comm;
 }
 
 Communicator::~Communicator() {
-  if (comm_ != nullptr) {
+  if (watched_ != nullptr) watched_->SetFailureHandler(nullptr);
+  if (comm_ != nullptr && !aborted_.load()) {
     (void)hipSetDevice(device_);
     (void)Api().CommDestroy(C(comm_));
   }
@@ -189,32 +192,32 @@ Communicator::~Communicator() {
 
 void Communicator::AllReduce(const void* send, void* recv, size_t count, DataType dt,
                              ReduceOp op, hipStream_t stream) {
-  Check(CheckedApi().AllReduce(send, recv, count, ToNccl(dt), ToNccl(op), C(comm_), stream),
+  Check(CheckedApi().AllReduce(send, recv, count, ToNccl(dt), ToNccl(op), C(Live()), stream),
         "ncclAllReduce");
 }
 
 void Communicator::Broadcast(const void* send, void* recv, size_t count, DataType dt, int root,
                              hipStream_t stream) {
-  Check(CheckedApi().Broadcast(send, recv, count, ToNccl(dt), root, C(comm_), stream),
+  Check(CheckedApi().Broadcast(send, recv, count, ToNccl(dt), root, C(Live()), stream),
         "ncclBroadcast");
 }
 
 void Communicator::AllGather(const void* send, void* recv, size_t send_count, DataType dt,
                              hipStream_t stream) {
-  Check(CheckedApi().AllGather(send, recv, send_count, ToNccl(dt), C(comm_), stream),
+  Check(CheckedApi().AllGather(send, recv, send_count, ToNccl(dt), C(Live()), stream),
         "ncclAllGather");
 }
 
 void Communicator::ReduceScatter(const void* send, void* recv, size_t recv_count, DataType dt,
                                  ReduceOp op, hipStream_t stream) {
-  Check(CheckedApi().ReduceScatter(send, recv, recv_count, ToNccl(dt), ToNccl(op), C(comm_),
+  Check(CheckedApi().ReduceScatter(send, recv, recv_count, ToNccl(dt), ToNccl(op), C(Live()),
                                    stream),
         "ncclReduceScatter");
 }
 
 void Communicator::AllToAll(const void* send, void* recv, size_t count, DataType dt,
                             hipStream_t stream) {
-  Check(CheckedApi().AllToAll(send, recv, count, ToNccl(dt), C(comm_), stream), "ncclAllToAll");
+  Check(CheckedApi().AllToAll(send, recv, count, ToNccl(dt), C(Live()), stream), "ncclAllToAll");
 }
 
 void Communicator::AllToAllV(const void* send, const std::vector<size_t>& send_counts,
@@ -233,11 +236,11 @@ void Communicator::AllToAllV(const void* send, const std::vector<size_t>& send_c
   Check(api.GroupStart(), "ncclGroupStart");
   for (int p = 0; p < world_; ++p) {
     if (send_counts[p] > 0) {
-      Check(api.Send(s + send_displs[p] * esize, send_counts[p], ToNccl(dt), p, C(comm_), stream),
+      Check(api.Send(s + send_displs[p] * esize, send_counts[p], ToNccl(dt), p, C(Live()), stream),
             "ncclSend");
     }
     if (recv_counts[p] > 0) {
-      Check(api.Recv(r + recv_displs[p] * esize, recv_counts[p], ToNccl(dt), p, C(comm_), stream),
+      Check(api.Recv(r + recv_displs[p] * esize, recv_counts[p], ToNccl(dt), p, C(Live()), stream),
             "ncclRecv");
     }
   }
@@ -245,11 +248,11 @@ void Communicator::AllToAllV(const void* send, const std::vector<size_t>& send_c
 }
 
 void Communicator::Send(const void* buf, size_t count, DataType dt, int peer, hipStream_t stream) {
-  Check(CheckedApi().Send(buf, count, ToNccl(dt), peer, C(comm_), stream), "ncclSend");
+  Check(CheckedApi().Send(buf, count, ToNccl(dt), peer, C(Live()), stream), "ncclSend");
 }
 
 void Communicator::Recv(void* buf, size_t count, DataType dt, int peer, hipStream_t stream) {
-  Check(CheckedApi().Recv(buf, count, ToNccl(dt), peer, C(comm_), stream), "ncclRecv");
+  Check(CheckedApi().Recv(buf, count, ToNccl(dt), peer, C(Live()), stream), "ncclRecv");
 }
 
 void Communicator::Barrier(hipStream_t stream) {
@@ -257,11 +260,26 @@ void Communicator::Barrier(hipStream_t stream) {
   DMLC_HIP_CHECK(hipStreamSynchronize(stream));
 }
 
+void* Communicator::Live() const {
+  if (aborted_.load()) LOG(FATAL) << "RCCL communicator (rank " << rank_ << ") was aborted";
+  return comm_;
+}
+
 void Communicator::Abort() {
-  if (comm_ != nullptr) {
+  std::lock_guard<std::mutex> lock(abort_mutex_);
+  if (comm_ != nullptr && !aborted_.exchange(true)) {
+    // ncclCommAbort is the one RCCL call allowed while another thread is
+    // blocked in a collective on this communicator: it makes that call return
     (void)Api().CommAbort(C(comm_));
-    comm_ = nullptr;
   }
+}
+
+void Communicator::AbortOnTrackerFailure(TrackerClient* tracker) {
+  watched_ = tracker;
+  tracker->SetFailureHandler([this](const std::string& reason) {
+    LOG(WARNING) << "aborting RCCL communicator of rank " << rank_ << ": " << reason;
+    Abort();
+  });
 }
 
 }  // namespace dist

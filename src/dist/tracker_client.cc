@@ -177,11 +177,37 @@ void TrackerClient::Shutdown() {
   Connect("shutdown");
 }
 
-void TrackerClient::Heartbeat() { Connect("heartbeat"); }
+bool TrackerClient::Heartbeat(std::string* reason) {
+  auto c = Connect("heartbeat");
+  if (c->RecvInt() == 0) return true;
+  std::string why = c->RecvStr();
+  if (reason != nullptr) *reason = why;
+  return false;
+}
+
+void TrackerClient::Abort(const std::string& msg) {
+  auto c = Connect("abort");
+  c->SendStr(msg);
+}
+
+void TrackerClient::SetFailureHandler(std::function<void(const std::string&)> handler) {
+  std::lock_guard<std::mutex> lock(handler_mutex_);
+  on_failure_ = std::move(handler);
+}
+
+void TrackerClient::ReportFailure(const std::string& reason) {
+  LOG(WARNING) << "job failure signalled by the tracker: " << reason;
+  std::lock_guard<std::mutex> lock(handler_mutex_);
+  if (on_failure_) on_failure_(reason);
+}
 
 void TrackerClient::StartHeartbeat(double period_sec) {
   StopHeartbeat();
-  Heartbeat();
+  std::string reason;
+  if (!Heartbeat(&reason)) {
+    ReportFailure(reason);
+    return;
+  }
   hb_stop_ = false;
   hb_thread_ = std::thread([this, period_sec]() {
     std::unique_lock<std::mutex> lock(hb_mutex_);
@@ -190,10 +216,15 @@ void TrackerClient::StartHeartbeat(double period_sec) {
                    std::chrono::milliseconds(static_cast<int64_t>(period_sec * 1000));
       if (hb_cv_.wait_until(lock, until, [this] { return hb_stop_; })) return;
       lock.unlock();
+      std::string why;
+      bool ok = false;
       try {
-        Heartbeat();
+        ok = Heartbeat(&why);
       } catch (const dmlc::Error& e) {
-        LOG(WARNING) << "heartbeat failed: " << e.what();
+        why = std::string("tracker unreachable: ") + e.what();
+      }
+      if (!ok) {
+        ReportFailure(why);
         return;
       }
       lock.lock();

@@ -704,7 +704,18 @@ PYBIND11_MODULE(_dmlc, m) {
            py::arg("recover") = false)
       .def("print", &TrackerClient::Print, py::call_guard<py::gil_scoped_release>())
       .def("shutdown", &TrackerClient::Shutdown, py::call_guard<py::gil_scoped_release>())
-      .def("heartbeat", &TrackerClient::Heartbeat, py::call_guard<py::gil_scoped_release>())
+      .def("heartbeat",
+           [](TrackerClient& c) -> py::object {
+             std::string reason;
+             bool ok;
+             {
+               py::gil_scoped_release nogil;
+               ok = c.Heartbeat(&reason);
+             }
+             if (ok) return py::none();
+             return py::str(reason);
+           })
+      .def("abort", &TrackerClient::Abort, py::call_guard<py::gil_scoped_release>())
       .def("start_heartbeat", &TrackerClient::StartHeartbeat, py::arg("period") = 5.0)
       .def("stop_heartbeat", &TrackerClient::StopHeartbeat,
            py::call_guard<py::gil_scoped_release>())
@@ -752,6 +763,10 @@ PYBIND11_MODULE(_dmlc, m) {
       .def_property_readonly("rank", &Communicator::rank)
       .def_property_readonly("world_size", &Communicator::world_size)
       .def_property_readonly("device", &Communicator::device)
+      .def_property_readonly("aborted", &Communicator::aborted)
+      .def("abort", &Communicator::Abort, py::call_guard<py::gil_scoped_release>())
+      .def("abort_on_tracker_failure", &Communicator::AbortOnTrackerFailure,
+           py::keep_alive<1, 2>())
       .def("all_reduce",
            [stream_of](Communicator& c, uintptr_t send, uintptr_t recv, size_t count,
                        dist::DataType dt, dist::ReduceOp op, uintptr_t stream) {

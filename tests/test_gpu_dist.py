@@ -87,3 +87,42 @@ def test_native_recordio_worker_via_dmlc_submit(tmp_path):
     assert out["records"] == 50000 and out["n_gpus"] == 1
     assert out["payload_bytes"] == 50000 * 200
     assert out["value"] > 0
+
+
+def test_communicator_aborts_on_tracker_failure():
+    """A peer's failure reaches this rank through its heartbeat reply and
+    aborts the RCCL communicator (ncclCommAbort); later collectives raise."""
+    import threading
+    import time
+
+    from dmlc_core_amd.parallel import tracker as trk
+    from dmlc_core_amd.parallel.client import TrackerClient
+
+    t = trk.RabitTracker("127.0.0.1", 2, port=19091, port_end=19999, heartbeat_timeout=30.0,
+                         timeout=60, abort_grace=2.0)
+    t.start(2)
+    native = _dmlc.TrackerClient("127.0.0.1", t.port, "n0", -1, -1, 30.0)
+    peer = TrackerClient("127.0.0.1", t.port, jobid="p1")
+    th = [threading.Thread(target=native.start), threading.Thread(target=peer.start)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(30)
+    comm = _dmlc.Communicator(0, 1, 0, _dmlc.Communicator.new_unique_id())
+    comm.abort_on_tracker_failure(native)
+    native.start_heartbeat(0.2)
+    x = torch.ones(16, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    comm.all_reduce(_ptr(x), _ptr(x), 16, _dmlc.DataType.float32, _dmlc.ReduceOp.sum, s)
+    torch.cuda.synchronize()
+    peer.abort("injected failure")
+    deadline = time.time() + 20
+    while not comm.aborted and time.time() < deadline:
+        time.sleep(0.05)
+    assert comm.aborted
+    with pytest.raises(_dmlc.DMLCError, match="aborted"):
+        comm.all_reduce(_ptr(x), _ptr(x), 16, _dmlc.DataType.float32, _dmlc.ReduceOp.sum, s)
+    native.stop_heartbeat()
+    del comm
+    with pytest.raises(trk.TrackerError):
+        t.join(30)

@@ -313,3 +313,62 @@ def test_native_cpp_client_against_python_tracker():
         assert world == n and par == parent[rank] and tr == sorted(tree[rank])
         assert (prev, nxt) == ring[rank]
         assert uid == b"\x07" * 128
+
+
+def _start_two(**kw):
+    t = _start_tracker(2, **kw)
+    c0 = TrackerClient("127.0.0.1", t.port)
+    c1 = TrackerClient("127.0.0.1", t.port)
+    th = [threading.Thread(target=c.start) for c in (c0, c1)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(30)
+    return t, c0, c1
+
+
+def test_dead_rank_is_signalled_to_live_ranks():
+    """Failure propagation: rank 1 stops heartbeating; rank 0's
+    heartbeat thread learns the job failed (so it can abort its RCCL
+    communicator) before the tracker gives up."""
+    t, c0, c1 = _start_two(heartbeat_timeout=1.0, timeout=60)
+    got = []
+    done = threading.Event()
+    c1.heartbeat()  # c1 is alive once, then "dies"
+
+    def on_failure(reason):
+        got.append(reason)
+        done.set()
+
+    c0.start_heartbeat(0.2, on_failure)
+    assert done.wait(20), "live rank never heard of the failure"
+    assert "rank 1 missed heartbeats" in got[0] or "rank" in got[0]
+    c0.stop_heartbeat()
+    with pytest.raises(trk.TrackerError, match="missed heartbeats"):
+        t.join(30)
+
+
+def test_abort_command_fails_job_fast():
+    t, c0, c1 = _start_two(heartbeat_timeout=30.0, timeout=60, abort_grace=1.0)
+    assert c0.heartbeat() is None
+    c1.abort("CUDA-free error in rank 1")
+    reason = c0.heartbeat()
+    assert reason is not None and "rank 1 aborted: CUDA-free error in rank 1" in reason
+    with pytest.raises(trk.TrackerError, match="aborted"):
+        t.join(30)
+
+
+def test_native_client_heartbeat_abort_and_failure_handler():
+    from dmlc_core_amd import _dmlc
+    t = _start_tracker(2, heartbeat_timeout=30.0, timeout=60, abort_grace=1.0)
+    cs = [_dmlc.TrackerClient("127.0.0.1", t.port, f"n{i}", -1, -1, 30.0) for i in range(2)]
+    th = [threading.Thread(target=c.start) for c in cs]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(30)
+    assert cs[0].heartbeat() is None
+    cs[1].abort("disk full")
+    assert "disk full" in cs[0].heartbeat()
+    with pytest.raises(trk.TrackerError, match="disk full"):
+        t.join(30)

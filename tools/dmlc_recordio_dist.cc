@@ -55,6 +55,9 @@ int main(int argc, char** argv) {
   dmlc::gpu::SetDevice(device);
   std::unique_ptr<dmlc::dist::Communicator> comm =
       dmlc::dist::Communicator::FromTracker(&tracker, device);
+  // a dead peer fails the job at the tracker; our heartbeat thread then
+  // aborts the communicator instead of leaving us blocked in a collective
+  tracker.StartHeartbeat(2.0);
 
   dmlc::gpu::DeviceRecordIOConfig cfg;
   cfg.chunk_bytes = chunk_mb << 20;
