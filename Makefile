@@ -28,7 +28,7 @@ HIPFLAGS := -std=c++17 -O3 -fPIC --offload-arch=$(GPU_ARCH) -ffp-contract=off -I
   -Wno-unused-result -munsafe-fp-atomics
 LDFLAGS_LIB := -shared -fopenmp -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64 -lrccl -ldl -lpthread
 
-CPU_SRCS := src/logging.cc src/io.cc src/recordio.cc src/data.cc src/config.cc src/synthetic.cc \
+CPU_SRCS := src/logging.cc src/fault.cc src/io.cc src/recordio.cc src/data.cc src/config.cc src/synthetic.cc \
   src/io/local_filesys.cc src/io/input_split_base.cc src/io/line_split.cc \
   src/io/recordio_split.cc src/io/remote_filesys.cc \
   src/io/shard_reader.cc src/io/http.cc src/io/s3_filesys.cc src/io/azure_filesys.cc \

@@ -5,6 +5,7 @@
  *  (which keeps the reference framing, `tracker/dmlc_tracker/tracker.py:24-135`).
  */
 #include <dmlc/dist/tracker_client.h>
+#include <dmlc/fault.h>
 #include <dmlc/logging.h>
 #include <netdb.h>
 #include <netinet/in.h>
@@ -127,6 +128,7 @@ TrackerClient::TrackerClient(std::string uri, int port, std::string jobid, int r
 TrackerClient::~TrackerClient() { StopHeartbeat(); }
 
 std::unique_ptr<TrackerClient::Conn> TrackerClient::Connect(const std::string& cmd) {
+  DMLC_FAULT_POINT("tracker");
   std::unique_ptr<Conn> c(new Conn(uri_, port_, timeout_sec_));
   c->SendInt(kMagic);
   int32_t magic = c->RecvInt();

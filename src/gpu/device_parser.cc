@@ -18,6 +18,7 @@
  * further ahead.
  */
 #include <dmlc/gpu/device_parser.h>
+#include <dmlc/fault.h>
 #include <dmlc/logging.h>
 #include <dmlc/threadediter.h>
 #include <dmlc/timer.h>
@@ -226,6 +227,9 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
    */
   void FillPipeline() {
     while (static_cast<int>(inflight_.size()) + busy_ < cfg_.device_slots && !reader_done_) {
+      // fault points sit before a slot is taken, so a failure leaks nothing
+      if (zc_ != nullptr) DMLC_FAULT_POINT("read");
+      DMLC_FAULT_POINT("h2d");
       HostSlot* slot = nullptr;
       const void* src = nullptr;
       size_t size = 0;
@@ -413,6 +417,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
 
   /*! \brief parse one chunk into out (append or replace); false at end */
   bool ProcessOne(DeviceCSR<IndexType>* out, bool append) {
+    DMLC_FAULT_POINT("parse");
     FillPipeline();
     if (inflight_.empty()) return false;
     Inflight cur = inflight_.front();

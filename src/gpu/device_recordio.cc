@@ -9,6 +9,7 @@
  *                    -> K7d gather -> record(parsed[d])
  * The H2D of the next chunks is queued before the current chunk is decoded.
  */
+#include <dmlc/fault.h>
 #include <dmlc/gpu/device_recordio.h>
 #include <dmlc/gpu/hip_utils.h>
 #include <dmlc/logging.h>
@@ -140,6 +141,7 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
   /*! \brief queue H2D copies of the next chunks into free device slots */
   void FillPipeline() {
     while (!exhausted_ && static_cast<int>(inflight_.size()) < kSlots) {
+      DMLC_FAULT_POINT("recordio");
       const int d = next_slot_;
       Slot& s = slots_[d];
       const char* src = nullptr;

@@ -5,6 +5,7 @@
 #include "./http.h"
 
 #include <dlfcn.h>
+#include <dmlc/fault.h>
 #include <dmlc/logging.h>
 
 #include <algorithm>
@@ -203,7 +204,8 @@ HttpResponse Http::PerformRetry(const HttpRequest& req, int retries, int pause_m
 size_t RangedReadStream::FetchRetry(size_t offset, size_t len, char* dst) {
   size_t done = 0;
   for (int attempt = 0; done < len; ++attempt) {
-    const size_t got = fetch_(offset + done, len - done, dst + done);
+    // an injected "http" fault is a transient failure: nothing arrives, retry
+    const size_t got = DMLC_FAULT_SOFT("http") ? 0 : fetch_(offset + done, len - done, dst + done);
     done += got;
     if (got == 0) {
       CHECK_LT(attempt, 50) << "ranged read at offset " << offset + done << " failed 50 times";

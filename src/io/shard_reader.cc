@@ -4,6 +4,7 @@
  */
 #include "./shard_reader.h"
 
+#include <dmlc/fault.h>
 #include <dmlc/logging.h>
 #include <errno.h>
 #include <unistd.h>
@@ -150,6 +151,7 @@ void ShardReader::Reset() {
 }
 
 size_t ShardReader::Fill(char* buf, size_t cap) {
+  DMLC_FAULT_POINT("read");
   CHECK(carry_.size() < cap) << "a single record (" << carry_.size()
                              << " bytes) does not fit the chunk size " << cap
                              << "; increase chunk_bytes";

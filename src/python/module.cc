@@ -9,6 +9,7 @@
  * extension cannot load, importing the ops fails loudly.
  */
 #include <dmlc/data.h>
+#include <dmlc/fault.h>
 #include <dmlc/dist/communicator.h>
 #include <dmlc/dist/tracker_client.h>
 #include <dmlc/gpu/device_parser.h>
@@ -681,6 +682,9 @@ PYBIND11_MODULE(_dmlc, m) {
       },
       py::arg("uri"), py::arg("part") = 0, py::arg("nparts") = 1, py::arg("type") = "text",
       py::arg("nthread") = 8, py::arg("chunk_bytes") = 64UL << 20);
+  m.def("fault_configure", &fault::Configure, py::arg("spec"),
+        "arm DMLC_FAULT_INJECT-style faults (\"\" disarms); resets pass counters");
+  m.def("fault_count", &fault::Count, py::arg("point"));
   m.def("gpu_device_count", &gpu::DeviceCount);
   m.def("gpu_arch", &gpu::DeviceArchName);
   m.def("get_time", &GetTime);
