@@ -60,6 +60,7 @@ class GPUParser:
         cfg = {"format": format}
         cfg.update({k: str(v) for k, v in config.items()})
         self.index64 = index64
+        self._where = {"uri": uri, "part": part, "nparts": nparts, "format": format}
         cls = _dmlc.DeviceParser64 if index64 else _dmlc.DeviceParser
         self._p = cls(uri, part, nparts, cfg)
 
@@ -72,6 +73,25 @@ class GPUParser:
 
     def before_first(self):
         self._p.before_first()
+
+    def tell(self) -> int:
+        """Mid-epoch resume cursor: partition byte offset of the first record
+        not yet delivered (a record boundary)."""
+        return self._p.tell()
+
+    def seek(self, cursor: int) -> None:
+        """Continue from a :meth:`tell` cursor."""
+        self._p.seek(int(cursor))
+
+    def state_dict(self) -> Dict:
+        """Checkpointable position (store it next to the model state)."""
+        return dict(self._where, cursor=self.tell())
+
+    def load_state_dict(self, state: Dict) -> None:
+        for k in ("uri", "part", "nparts", "format"):
+            if state[k] != self._where[k]:
+                raise ValueError(f"state is for {k}={state[k]!r}, parser has {self._where[k]!r}")
+        self.seek(state["cursor"])
 
     def next(self) -> bool:
         return self._p.next()

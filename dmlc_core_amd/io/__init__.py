@@ -4,10 +4,11 @@ from __future__ import annotations
 
 from typing import Dict, Iterator, List, Tuple
 
-from .._dmlc import DeviceRecordIO, InputSplit, RecordIOReader, RecordIOWriter, Stream  # noqa: F401
+from .._dmlc import (DeviceRecordIO, InputSplit, PartitionReader, RecordIOReader,  # noqa: F401
+                     RecordIOWriter, Stream, read_partition)
 
 __all__ = ["InputSplit", "RecordIOReader", "RecordIOWriter", "Stream", "iter_records",
-           "GPURecordIO", "split_records"]
+           "GPURecordIO", "split_records", "PartitionReader", "read_partition"]
 
 
 def iter_records(uri: str, part: int = 0, nparts: int = 1, type: str = "text"):  # noqa: A002

@@ -96,6 +96,16 @@ class DeviceParser {
   virtual ~DeviceParser() = default;
   /*! \brief rewind to the first chunk */
   virtual void BeforeFirst() = 0;
+  /*!
+   * \brief mid-epoch resume cursor: partition byte offset of the first record
+   *  not yet delivered by Next() / ParseAll().  Serialise it with
+   *  the model checkpoint; a new parser over the same (uri, part, nparts)
+   *  continues from it with Seek().  Zero-copy and pinned-ring modes share
+   *  the cursor space.
+   */
+  virtual size_t Tell() const = 0;
+  /*! \brief continue from a Tell() cursor (drains in-flight work first) */
+  virtual void Seek(size_t cursor) = 0;
   /*! \brief parse the next chunk; the block is ready on return */
   virtual bool Next() = 0;
   /*! \brief block of the last Next() (valid until the next call) */

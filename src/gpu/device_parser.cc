@@ -87,6 +87,8 @@ namespace {
 struct HostSlot {
   PinnedBuffer buf;
   size_t size{0};
+  /*! \brief partition cursor after this chunk (ShardReader::Tell) */
+  size_t end_pos{0};
 };
 
 /*! \brief per-chunk sizes the host needs to place the output */
@@ -161,13 +163,20 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     zc_.reset();
   }
 
-  void BeforeFirst() override {
+  void BeforeFirst() override { Seek(0); }
+
+  size_t Tell() const override { return cursor_; }
+
+  void Seek(size_t cursor) override {
+    CHECK_LE(cursor, PartitionBytes()) << "DeviceParser::Seek: cursor beyond the partition";
     DrainInflight();
     if (zc_ != nullptr) {
-      zc_->Reset();
+      zc_->Seek(cursor);
     } else {
+      seek_pos_ = cursor;
       iter_.BeforeFirst();
     }
+    cursor_ = cursor;
   }
 
   bool Next() override {
@@ -202,6 +211,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     HostSlot* slot;  // nullptr in zero-copy mode
     int d;
     size_t size;
+    size_t end_pos;  // resume cursor once this chunk is delivered
   };
 
   void StartReader() {
@@ -215,9 +225,12 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
           }
           ScopedRange r("pinned_fill");
           (*dptr)->size = reader->Fill((*dptr)->buf.template get<char>(), cap);
+          (*dptr)->end_pos = reader->Tell();
           return (*dptr)->size != 0;
         },
-        [reader]() { reader->Reset(); });
+        // BeforeFirst / Seek: the consumer sets seek_pos_ before the
+        // ThreadedIter handshake, which orders it before this call
+        [this, reader]() { reader->Seek(seek_pos_); });
   }
 
   /*!
@@ -232,7 +245,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       DMLC_FAULT_POINT("h2d");
       HostSlot* slot = nullptr;
       const void* src = nullptr;
-      size_t size = 0;
+      size_t size = 0, end_pos = 0;
       if (zc_ != nullptr) {
         ZeroCopySource::Piece piece;
         if (!zc_->Next(&piece)) {
@@ -241,6 +254,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
         }
         src = piece.ptr;
         size = piece.size;
+        end_pos = zc_->Tell();
       } else {
         const double t0 = GetTime();
         if (!iter_.Next(&slot)) {
@@ -250,6 +264,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
         stats_.wait_reader_sec += GetTime() - t0;
         src = slot->buf.get();
         size = slot->size;
+        end_pos = slot->end_pos;
       }
       const int d = next_dslot_;
       next_dslot_ = (next_dslot_ + 1) % cfg_.device_slots;
@@ -257,7 +272,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       DMLC_HIP_CHECK(
           hipMemcpyAsync(dtext_[d]->get(), src, size, hipMemcpyHostToDevice, copy_->get()));
       copied_[d]->Record(copy_->get());
-      inflight_.push_back(Inflight{slot, d, size});
+      inflight_.push_back(Inflight{slot, d, size, end_pos});
     }
   }
 
@@ -424,6 +439,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     inflight_.pop_front();
     busy_ = 1;
     cur_slot_ = cur.slot;
+    cursor_ = cur.end_pos;
     const size_t nbytes = cur.size;
     const char* text = dtext_[cur.d]->template get<char>();
     hipStream_t s = compute_->get();
@@ -486,6 +502,10 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   std::unique_ptr<ZeroCopySource> zc_;
   std::deque<Inflight> inflight_;
   HostSlot* cur_slot_{nullptr};
+  /*! \brief resume cursor (partition offset after the last delivered chunk) */
+  size_t cursor_{0};
+  /*! \brief where the reader restarts on the next BeforeFirst handshake */
+  size_t seek_pos_{0};
   int next_dslot_{0};
   int busy_{0};
   bool reader_done_{false};

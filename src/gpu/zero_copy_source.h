@@ -88,6 +88,25 @@ class ZeroCopySource {
     off_ += len;
     return true;
   }
+  /*!
+   * \brief partition byte offset of the next piece (same cursor space as
+   *  io::ShardReader::Tell: file bytes only, always a record boundary)
+   */
+  size_t Tell() const {
+    size_t n = 0;
+    for (size_t i = 0; i < seg_ && i < segs_.size(); ++i) n += segs_[i].size;
+    return n + off_;
+  }
+  /*! \brief continue from a Tell() cursor */
+  void Seek(size_t pos) {
+    seg_ = 0;
+    off_ = pos;
+    while (seg_ < segs_.size() && off_ >= segs_[seg_].size) {
+      off_ -= segs_[seg_].size;
+      ++seg_;
+    }
+    CHECK(seg_ < segs_.size() || off_ == 0) << "cursor beyond the partition";
+  }
   size_t PartitionBytes() const {
     size_t n = 0;
     for (const auto& s : segs_) n += s.size;

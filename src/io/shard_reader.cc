@@ -142,6 +142,25 @@ int ShardReader::Fd(size_t file) {
   return fds_[file];
 }
 
+void ShardReader::Seek(size_t pos) {
+  CHECK_LE(pos, part_bytes_) << "cursor beyond the partition";
+  Reset();
+  size_t base = 0;
+  seg_idx_ = segs_.size();
+  for (size_t i = 0; i < segs_.size(); ++i) {
+    const size_t len = segs_[i].end - segs_[i].begin;
+    if (pos < base + len) {
+      // a cursor on a segment boundary means "previous file fully consumed",
+      // so no separator newline is pending here
+      seg_idx_ = i;
+      seg_off_ = pos - base;
+      break;
+    }
+    base += len;
+  }
+  bytes_read_ = pos;
+}
+
 void ShardReader::Reset() {
   seg_idx_ = 0;
   seg_off_ = 0;

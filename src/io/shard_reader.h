@@ -72,6 +72,15 @@ class ShardReader {
   size_t PartitionBytes() const { return part_bytes_; }
   /*! \brief bytes consumed so far */
   size_t BytesRead() const { return bytes_read_; }
+  /*!
+   * \brief resume cursor: partition byte offset (file bytes only, inserted
+   *  newlines excluded) of the first record not yet returned by Fill.  Always
+   *  a record boundary, so Seek(Tell()) in a new reader over the same
+   *  partition continues exactly where this one stopped.
+   */
+  size_t Tell() const { return bytes_read_ - carry_.size(); }
+  /*! \brief continue from a cursor returned by Tell() */
+  void Seek(size_t pos);
 
  private:
   struct Seg {

@@ -166,6 +166,48 @@ class PyRowBlockIter {
   std::unique_ptr<RowBlockIter<I>> it_;
 };
 
+/*! \brief the GPU ring's host stage as a Python iterator with a resume cursor */
+class PyPartitionReader {
+ public:
+  PyPartitionReader(const std::string& uri, unsigned part, unsigned nparts,
+                    const std::string& type, int nthread, size_t chunk_bytes)
+      : buf_(chunk_bytes, '\0') {
+    CHECK(type == "text" || type == "recordio")
+        << "PartitionReader: type must be text or recordio, got " << type;
+    py::gil_scoped_release nogil;  // listing may hit an in-process (Python) server
+    io::URI path(uri.c_str());
+    io::FileSystem* fs = io::FileSystem::GetInstance(path);
+    if (type == "text") {
+      split_.reset(new io::LineSplitter(fs, uri.c_str(), part, nparts));
+    } else {
+      split_.reset(new io::RecordIOSplitter(fs, uri.c_str(), part, nparts));
+    }
+    reader_.reset(new io::ShardReader(split_.get(), nthread));
+  }
+  ~PyPartitionReader() {
+    py::gil_scoped_release nogil;
+    reader_.reset();
+    split_.reset();
+  }
+  py::object Next() {
+    size_t n;
+    {
+      py::gil_scoped_release nogil;
+      n = reader_->Fill(&buf_[0], buf_.size());
+    }
+    if (n == 0) return py::none();
+    return py::bytes(buf_.data(), n);
+  }
+  size_t Tell() const { return reader_->Tell(); }
+  void Seek(size_t pos) { reader_->Seek(pos); }
+  size_t PartitionBytes() const { return reader_->PartitionBytes(); }
+
+ private:
+  std::string buf_;
+  std::unique_ptr<io::InputSplitBase> split_;
+  std::unique_ptr<io::ShardReader> reader_;
+};
+
 class PyInputSplit {
  public:
   PyInputSplit(const std::string& uri, unsigned part, unsigned nparts, const std::string& type,
@@ -353,6 +395,11 @@ class PyDeviceParser {
     py::gil_scoped_release nogil;
     p_->BeforeFirst();
   }
+  size_t Tell() const { return p_->Tell(); }
+  void Seek(size_t cursor) {
+    py::gil_scoped_release nogil;
+    p_->Seek(cursor);
+  }
   size_t PartitionBytes() const { return p_->PartitionBytes(); }
   py::dict Stats() const {
     const auto& s = p_->Stats();
@@ -427,6 +474,8 @@ void BindIndexType(py::module_& m, const std::string& suffix) {
       .def("value_shape", &PyDeviceParser<I>::ValueShape)
       .def("value_capsules", &PyDeviceParser<I>::ValueCapsules)
       .def("before_first", &PyDeviceParser<I>::BeforeFirst)
+      .def("tell", &PyDeviceParser<I>::Tell)
+      .def("seek", &PyDeviceParser<I>::Seek)
       .def("partition_bytes", &PyDeviceParser<I>::PartitionBytes)
       .def("stats", &PyDeviceParser<I>::Stats)
       .def("stream", &PyDeviceParser<I>::Stream);
@@ -525,6 +574,14 @@ PYBIND11_MODULE(_dmlc, m) {
   BindIndexType<uint32_t>(m, "");
   BindIndexType<uint64_t>(m, "64");
   BindRecordIO(m);
+  py::class_<PyPartitionReader>(m, "PartitionReader")
+      .def(py::init<const std::string&, unsigned, unsigned, const std::string&, int, size_t>(),
+           py::arg("uri"), py::arg("part") = 0, py::arg("nparts") = 1, py::arg("type") = "text",
+           py::arg("nthread") = 8, py::arg("chunk_bytes") = 64UL << 20)
+      .def("next", &PyPartitionReader::Next)
+      .def("tell", &PyPartitionReader::Tell)
+      .def("seek", &PyPartitionReader::Seek)
+      .def("partition_bytes", &PyPartitionReader::PartitionBytes);
   py::class_<PyInputSplit>(m, "InputSplit")
       .def(py::init<const std::string&, unsigned, unsigned, const std::string&,
                     const std::string&, bool, int, size_t>(),
