@@ -12,7 +12,7 @@ echo "== host: $(nproc) cpus"; df -h /tmp | tail -1; free -g | head -2
 rocm-smi --showproductname 2>/dev/null | grep -E 'GPU|Card' | head -3 || true
 ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
 if [[ $STAGES == *test* ]]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
   rc=$?; echo "pytest gpu rc=$rc"; tail -25 $OUT/pytest_gpu.log
   ok $rc || exit $rc
 fi

@@ -10,8 +10,11 @@ C++ / HIP (include/, src/, tools/, tests/cpp/, examples/):
   * headers carry an include guard (#ifndef X_H_ / #define X_H_) or #pragma once
   * no CUDA compatibility layers: no `__HIP_PLATFORM_NVIDIA__` / `__CUDACC__`
     dual paths, no `cuda*` runtime calls, no hipify markers
-  * device code never writes through the scalar data cache (s_store_*,
-    s_buffer_store_*, s_scratch_store_*, s_dcache_wb, s_dcache_discard)
+  * device code never writes through the scalar data cache: no scalar-memory
+    instruction that stores or is atomic, and no scalar data-cache operation
+    other than the invalidate. Checked on the sources AND on the disassembly of
+    every built gfx950 code object under build/obj/gpu (llvm-objdump), so
+    compiler-emitted code is covered too.
   * `using namespace` only in .cc files
 Python (dmlc_core_amd/, tests/, scripts/, top level):
   * every file compiles; no tabs; line length <= 110
@@ -34,8 +37,12 @@ CPP_EXT = (".h", ".cc", ".hip", ".cpp")
 SKIP_DIRS = {"__pycache__", "build", ".git", "gpurun_out"}
 
 CUDA_COMPAT = re.compile(r"__HIP_PLATFORM_NVIDIA__|__CUDACC__|\bcuda[A-Z]\w*\(|HIPIFY|hipify")
-SCALAR_STORE = re.compile(r"\bs_(?:buffer_|scratch_)?store_dword|\bs_dcache_(?:wb|discard)\b|"
-                          r"\bs_atomic_|\bs_buffer_atomic_")
+# Structural rule: any scalar-prefixed mnemonic containing "store" or "atomic",
+# and any scalar cache operation that is not the invalidate.
+SCALAR_STORE = re.compile(r"\bs_\w*(?:store|atomic)\w*|\bs_\w*cache_(?!inv)\w+")
+OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+BUNDLER = "/opt/rocm/lib/llvm/bin/clang-offload-bundler"
+OBJCOPY = "/opt/rocm/lib/llvm/bin/llvm-objcopy"
 
 Finding = Tuple[str, int, str]
 
@@ -79,6 +86,40 @@ def lint_cpp(path: str) -> List[Finding]:
     return out
 
 
+def lint_code_objects() -> List[Finding]:
+    """Disassemble every built gfx950 code object and apply SCALAR_STORE to the
+    instruction stream (the sources may be clean while the compiler is not)."""
+    import glob
+    import subprocess
+    import tempfile
+    out: List[Finding] = []
+    objs = sorted(glob.glob(os.path.join(ROOT, "build", "obj", "gpu", "*.hip.o")))
+    if not objs or not all(os.path.exists(t) for t in (OBJDUMP, BUNDLER, OBJCOPY)):
+        return out
+    with tempfile.TemporaryDirectory() as tmp:
+        for obj in objs:
+            rel = os.path.relpath(obj, ROOT)
+            dev = os.path.join(tmp, os.path.basename(obj) + ".gfx950")
+            fatbin = os.path.join(tmp, os.path.basename(obj) + ".fatbin")
+            # hipcc -c embeds the offload bundle in the host object's .hip_fatbin section.
+            subprocess.run([OBJCOPY, "--dump-section", ".hip_fatbin=" + fatbin, obj,
+                            os.path.join(tmp, "host.o")], capture_output=True)
+            if not os.path.exists(fatbin):
+                out.append((rel, 1, "no .hip_fatbin section to disassemble"))
+                continue
+            r = subprocess.run([BUNDLER, "--type=o", "--input=" + fatbin, "--output=" + dev,
+                                "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--unbundle"],
+                               capture_output=True, text=True)
+            if r.returncode != 0 or not os.path.exists(dev):
+                out.append((rel, 1, "no gfx950 code object in the offload bundle"))
+                continue
+            d = subprocess.run([OBJDUMP, "-d", dev], capture_output=True, text=True)
+            for i, line in enumerate(d.stdout.split("\n"), 1):
+                if SCALAR_STORE.search(line):
+                    out.append((rel, i, "scalar-cache store / atomic in disassembly"))
+    return out
+
+
 def lint_py(path: str) -> List[Finding]:
     out: List[Finding] = []
     rel = os.path.relpath(path, ROOT)
@@ -114,6 +155,7 @@ def main(argv=None) -> int:
     for p in _walk(CPP_DIRS, CPP_EXT):
         ncpp += 1
         findings += lint_cpp(p)
+    findings += lint_code_objects()
     py_files = list(_walk(PY_DIRS, (".py",)))
     py_files += [os.path.join(ROOT, f) for f in os.listdir(ROOT) if f.endswith(".py")]
     for p in py_files:
