@@ -24,8 +24,9 @@ New in this implementation:
     communicators (``ncclCommAbort``) instead of blocking in a collective
     whose peer is gone; the tracker raises after ``abort_grace`` seconds;
   * ``abort`` command: a rank reports its own fatal error (fail fast);
-  * an overall ``timeout`` for the rendezvous and a non-blocking event loop
-    (held sockets for rccl/barrier replies never stall other workers);
+  * an overall ``timeout`` for the rendezvous; the accept loop hands every
+    connection to its own thread, so neither a slow ``start`` negotiation nor
+    held rccl/barrier sockets ever delay another rank's heartbeat;
   * Python 3 only (the reference breaks on 3.9+ with ``Thread.isAlive``).
 """
 from __future__ import annotations
@@ -223,6 +224,31 @@ class _Worker:
 
 
 # --------------------------------------------------------------------------- tracker
+class _JobState:
+    """Mutable rendezvous state shared by the tracker's connection threads."""
+
+    def __init__(self, n: int):
+        self.n = n
+        self.shutdown: Dict[int, bool] = {}
+        self.wait_conn: Dict[int, _Worker] = {}
+        self.job_map: Dict[str, int] = {}
+        self.pending: List[_Worker] = []
+        self.todo: List[int] = []
+        self.tree = self.parent = self.ring = None
+        self.rccl_ids: Dict[str, bytes] = {}
+        self.rccl_waiters: Dict[str, List[_Worker]] = {}
+        self.barriers: Dict[str, List[_Worker]] = {}
+        self.last_beat: Dict[int, float] = {}
+        # failure state: once a rank is declared dead (or aborts) the job is
+        # failed; live ranks learn it from their next heartbeat reply (and
+        # abort their RCCL communicators) during a grace period, then the
+        # tracker raises.
+        self.failed: Optional[str] = None
+        self.failed_at = 0.0
+        self.dead: Dict[int, bool] = {}
+        self.fatal: Optional[BaseException] = None
+
+
 class RabitTracker:
     """Rendezvous server for `nworker` processes."""
 
@@ -259,6 +285,9 @@ class RabitTracker:
         self.messages: List[str] = []
         self.assigned: Dict[int, str] = {}
         self._stop = threading.Event()
+        self._mu = threading.Lock()        # job state
+        self._start_mu = threading.Lock()  # rank assignment / link negotiation
+        self._state: Optional[_JobState] = None
         logger.info("tracker listening on %s:%d", host_ip, self.port)
 
     def worker_envs(self) -> Dict[str, object]:
@@ -268,164 +297,199 @@ class RabitTracker:
 
     # ---------------------------------------------------------------- main loop
     def _serve(self) -> None:
-        n = self.nworker
-        shutdown: Dict[int, bool] = {}
-        wait_conn: Dict[int, _Worker] = {}
-        job_map: Dict[str, int] = {}
-        pending: List[_Worker] = []
-        todo: List[int] = []
-        tree = parent = ring = None
-        rccl_ids: Dict[str, bytes] = {}
-        rccl_waiters: Dict[str, List[_Worker]] = {}
-        barriers: Dict[str, List[_Worker]] = {}
-        last_beat: Dict[int, float] = {}
+        """Accept loop. Every connection is handled on its own thread, so a
+        slow handshake or a long link negotiation (``start``) never delays
+        another rank's heartbeat; shared job state is guarded by ``_mu`` and
+        rank assignment is serialised by ``_start_mu`` (never held together
+        with blocking I/O under ``_mu``)."""
+        st = _JobState(self.nworker)
+        self._state = st
         t_begin = time.time()
-        # failure state: once a rank is declared dead (or aborts) the job is
-        # failed; live ranks learn it from their next heartbeat reply (and
-        # abort their RCCL communicators) during a grace period, then the
-        # tracker raises.
-        failed: Optional[str] = None
-        failed_at = 0.0
-        dead: Dict[int, bool] = {}
-
-        def fail(reason: str, rank: int) -> None:
-            nonlocal failed, failed_at
-            dead[rank] = True
-            if failed is None:
-                failed, failed_at = reason, time.time()
-                logger.error("job failed: %s", reason)
-                for group in list(rccl_waiters.values()) + list(barriers.values()):
-                    for h in group:  # unblock ranks waiting in rccl get / barrier
-                        h.ch.close()
-                rccl_waiters.clear()
-                barriers.clear()
-
-        while len(shutdown) != n and not self._stop.is_set():
-            now = time.time()
-            if self.timeout is not None and now - t_begin > self.timeout:
-                raise TrackerError(f"job did not finish within {self.timeout}s "
-                                   f"({len(shutdown)}/{n} ranks shut down)")
-            if self.heartbeat_timeout is not None:
-                for r, t in list(last_beat.items()):
-                    if r not in shutdown and r not in dead and now - t > self.heartbeat_timeout:
-                        fail(f"rank {r} missed heartbeats for {now - t:.1f}s "
-                             f"(> {self.heartbeat_timeout}s)", r)
-            if failed is not None and (now - failed_at > self.abort_grace
-                                       or len(shutdown) + len(dead) >= n):
-                raise TrackerError(failed)
+        while not self._stop.is_set():
+            with self._mu:
+                if len(st.shutdown) >= st.n:
+                    break
+                if st.fatal is not None:
+                    raise st.fatal
+                now = time.time()
+                if self.timeout is not None and now - t_begin > self.timeout:
+                    raise TrackerError(f"job did not finish within {self.timeout}s "
+                                       f"({len(st.shutdown)}/{st.n} ranks shut down)")
+                if self.heartbeat_timeout is not None:
+                    for r, t in list(st.last_beat.items()):
+                        if r not in st.shutdown and r not in st.dead and \
+                                now - t > self.heartbeat_timeout:
+                            self._fail(st, f"rank {r} missed heartbeats for {now - t:.1f}s "
+                                           f"(> {self.heartbeat_timeout}s)", r)
+                if st.failed is not None and (
+                        now - st.failed_at > self.abort_grace
+                        or len(set(st.shutdown) | set(st.dead)) >= st.n):
+                    raise TrackerError(st.failed)
             try:
                 conn, addr = self.sock.accept()
             except socket.timeout:
                 continue
             conn.settimeout(self.io_timeout)
-            try:
-                w = _Worker(conn, addr)
-            except (ConnectionError, OSError, UnicodeDecodeError) as e:
-                logger.warning("dropping connection from %s: %s", addr, e)
-                conn.close()
-                continue
-
-            if w.cmd == "print":
-                msg = w.ch.recv_str().rstrip()
-                self.messages.append(msg)
-                logger.info("%s", msg)
-                w.ch.close()
-                continue
-            if w.cmd == "heartbeat":
-                last_beat[w.rank] = time.time()
-                w.ch.send_int(0 if failed is None else 1)
-                if failed is not None:
-                    w.ch.send_str(failed)
-                w.ch.close()
-                continue
-            if w.cmd == "abort":
-                msg = w.ch.recv_str()
-                w.ch.close()
-                fail(f"rank {w.rank} aborted: {msg}", w.rank)
-                continue
-            if w.cmd == "shutdown":
-                if w.rank < 0 or w.rank in shutdown:
-                    raise TrackerError(f"bad shutdown from rank {w.rank}")
-                shutdown[w.rank] = True
-                last_beat.pop(w.rank, None)
-                logger.debug("shutdown from rank %d", w.rank)
-                w.ch.close()
-                continue
-            if w.cmd == "rccl":
-                op = w.ch.recv_int()
-                key = w.ch.recv_str()
-                if op == 0:  # put
-                    rccl_ids[key] = w.ch.recv_bytes()
-                    w.ch.send_int(0)
-                    w.ch.close()
-                    for h in rccl_waiters.pop(key, []):
-                        h.ch.send_bytes(rccl_ids[key])
-                        h.ch.close()
-                elif key in rccl_ids:
-                    w.ch.send_bytes(rccl_ids[key])
-                    w.ch.close()
-                else:
-                    rccl_waiters.setdefault(key, []).append(w)
-                continue
-            if w.cmd == "barrier":
-                key = w.ch.recv_str()
-                count = w.ch.recv_int()
-                group = barriers.setdefault(key, [])
-                group.append(w)
-                if len(group) >= count:
-                    for h in barriers.pop(key):
-                        h.ch.send_int(0)
-                        h.ch.close()
-                continue
-            if w.cmd not in ("start", "recover"):
-                logger.warning("unknown command %r from %s", w.cmd, w.host)
-                w.ch.close()
-                continue
-
-            if tree is None:
-                if w.cmd != "start":
-                    raise TrackerError("first worker must send start")
-                if w.world_size > 0:
-                    n = self.nworker = w.world_size
-                tree, parent, ring = link_map(n)
-                todo = list(range(n))
-            elif w.world_size not in (-1, n):
-                raise TrackerError(f"world size mismatch: {w.world_size} vs {n}")
-            if w.cmd == "recover" and w.rank < 0:
-                raise TrackerError("recover needs an explicit rank")
-
-            rank = w.decide_rank(job_map)
-            if rank == -1:
-                if not todo:
-                    raise TrackerError("more workers than the world size")
-                pending.append(w)
-                if len(pending) == len(todo):
-                    pending.sort(key=lambda x: x.host)
-                    for p in pending:
-                        r = todo.pop(0)
-                        if p.jobid != "NULL":
-                            job_map[p.jobid] = r
-                        p.assign_rank(r, wait_conn, tree, parent, ring)
-                        self.assigned[r] = p.host
-                        if p.wait_accept > 0:
-                            wait_conn[r] = p
-                    pending = []
-                if not todo and self.start_time is None:
-                    logger.info("all %d workers started", n)
-                    self.start_time = time.time()
-            else:
-                if rank in todo:
-                    todo.remove(rank)
-                w.assign_rank(rank, wait_conn, tree, parent, ring)
-                self.assigned[rank] = w.host
-                if w.wait_accept > 0:
-                    wait_conn[rank] = w
-                if not todo and self.start_time is None:
-                    self.start_time = time.time()
+            th = threading.Thread(target=self._handle, args=(st, conn, addr),
+                                  name="dmlc-tracker-conn", daemon=True)
+            th.start()
         self.end_time = time.time()
         if self.start_time is not None:
             logger.info("all workers finished; %.3f s between start and finish",
                         self.end_time - self.start_time)
+
+    def _fail(self, st: "_JobState", reason: str, rank: int) -> None:
+        """Mark the job failed (caller holds _mu). Live ranks learn it from
+        their next heartbeat reply during the abort grace period."""
+        st.dead[rank] = True
+        if st.failed is None:
+            st.failed, st.failed_at = reason, time.time()
+            logger.error("job failed: %s", reason)
+            for group in list(st.rccl_waiters.values()) + list(st.barriers.values()):
+                for h in group:  # unblock ranks waiting in rccl get / barrier
+                    h.ch.close()
+            st.rccl_waiters.clear()
+            st.barriers.clear()
+
+    def _handle(self, st: "_JobState", conn: socket.socket, addr) -> None:
+        try:
+            w = _Worker(conn, addr)
+        except (ConnectionError, OSError, UnicodeDecodeError) as e:
+            logger.warning("dropping connection from %s: %s", addr, e)
+            conn.close()
+            return
+        try:
+            self._dispatch(st, w)
+        except TrackerError as e:
+            with self._mu:
+                if st.fatal is None:
+                    st.fatal = e
+            w.ch.close()
+        except (ConnectionError, OSError, UnicodeDecodeError) as e:
+            logger.warning("command %r from %s failed: %s", w.cmd, w.host, e)
+            w.ch.close()
+
+    def _dispatch(self, st: "_JobState", w: _Worker) -> None:
+        if w.cmd == "print":
+            msg = w.ch.recv_str().rstrip()
+            with self._mu:
+                self.messages.append(msg)
+            logger.info("%s", msg)
+            w.ch.close()
+            return
+        if w.cmd == "heartbeat":
+            with self._mu:
+                st.last_beat[w.rank] = time.time()
+                failed = st.failed
+            w.ch.send_int(0 if failed is None else 1)
+            if failed is not None:
+                w.ch.send_str(failed)
+            w.ch.close()
+            return
+        if w.cmd == "abort":
+            msg = w.ch.recv_str()
+            w.ch.close()
+            with self._mu:
+                self._fail(st, f"rank {w.rank} aborted: {msg}", w.rank)
+            return
+        if w.cmd == "shutdown":
+            with self._mu:
+                if w.rank < 0 or w.rank in st.shutdown:
+                    raise TrackerError(f"bad shutdown from rank {w.rank}")
+                st.shutdown[w.rank] = True
+                st.last_beat.pop(w.rank, None)
+            logger.debug("shutdown from rank %d", w.rank)
+            w.ch.close()
+            return
+        if w.cmd == "rccl":
+            op = w.ch.recv_int()
+            key = w.ch.recv_str()
+            if op == 0:  # put
+                blob = w.ch.recv_bytes()
+                w.ch.send_int(0)
+                w.ch.close()
+                with self._mu:
+                    st.rccl_ids[key] = blob
+                    waiters = st.rccl_waiters.pop(key, [])
+                for h in waiters:
+                    self._reply_close(h, lambda c: c.send_bytes(blob))
+                return
+            with self._mu:
+                blob = st.rccl_ids.get(key)
+                if blob is None:
+                    st.rccl_waiters.setdefault(key, []).append(w)
+                    return
+            w.ch.send_bytes(blob)
+            w.ch.close()
+            return
+        if w.cmd == "barrier":
+            key = w.ch.recv_str()
+            count = w.ch.recv_int()
+            with self._mu:
+                group = st.barriers.setdefault(key, [])
+                group.append(w)
+                release = st.barriers.pop(key) if len(group) >= count else []
+            for h in release:
+                self._reply_close(h, lambda c: c.send_int(0))
+            return
+        if w.cmd not in ("start", "recover"):
+            logger.warning("unknown command %r from %s", w.cmd, w.host)
+            w.ch.close()
+            return
+        with self._start_mu:
+            self._start(st, w)
+
+    @staticmethod
+    def _reply_close(h: _Worker, fn) -> None:
+        try:
+            fn(h.ch)
+        except OSError as e:
+            logger.warning("reply to %s failed: %s", h.host, e)
+        h.ch.close()
+
+    def _start(self, st: "_JobState", w: _Worker) -> None:
+        """Rank assignment + link negotiation (serialised by _start_mu)."""
+        if st.tree is None:
+            if w.cmd != "start":
+                raise TrackerError("first worker must send start")
+            if w.world_size > 0:
+                with self._mu:
+                    st.n = self.nworker = w.world_size
+            st.tree, st.parent, st.ring = link_map(st.n)
+            st.todo = list(range(st.n))
+        elif w.world_size not in (-1, st.n):
+            raise TrackerError(f"world size mismatch: {w.world_size} vs {st.n}")
+        if w.cmd == "recover" and w.rank < 0:
+            raise TrackerError("recover needs an explicit rank")
+
+        rank = w.decide_rank(st.job_map)
+        if rank == -1:
+            if not st.todo:
+                raise TrackerError("more workers than the world size")
+            st.pending.append(w)
+            if len(st.pending) == len(st.todo):
+                st.pending.sort(key=lambda x: x.host)
+                for p in st.pending:
+                    r = st.todo.pop(0)
+                    if p.jobid != "NULL":
+                        st.job_map[p.jobid] = r
+                    p.assign_rank(r, st.wait_conn, st.tree, st.parent, st.ring)
+                    self.assigned[r] = p.host
+                    if p.wait_accept > 0:
+                        st.wait_conn[r] = p
+                st.pending = []
+            if not st.todo and self.start_time is None:
+                logger.info("all %d workers started", st.n)
+                self.start_time = time.time()
+        else:
+            if rank in st.todo:
+                st.todo.remove(rank)
+            w.assign_rank(rank, st.wait_conn, st.tree, st.parent, st.ring)
+            self.assigned[rank] = w.host
+            if w.wait_accept > 0:
+                st.wait_conn[rank] = w
+            if not st.todo and self.start_time is None:
+                self.start_time = time.time()
 
     def _run(self) -> None:
         try:

@@ -28,6 +28,7 @@
 #include <atomic>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <vector>
 
@@ -114,6 +115,9 @@ class Communicator {
   void* comm_{nullptr};
   std::atomic<bool> aborted_{false};
   std::mutex abort_mutex_;
+  // collectives hold it shared across their enqueue; Abort takes it exclusive
+  // (bounded wait) so ncclCommAbort never frees a comm mid-enqueue
+  mutable std::shared_timed_mutex use_mu_;
   TrackerClient* watched_{nullptr};
   int rank_, world_, device_;
   void* scratch_{nullptr};

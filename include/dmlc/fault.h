@@ -12,7 +12,8 @@
  *   DMLC_FAULT_INJECT="read:3,h2d:1"   # 3rd reader fill and 1st H2D copy fail
  *
  * Points: read (host reader fill / zero-copy piece), h2d (host->device copy),
- * parse (GPU parse of a chunk), recordio (GPU RecordIO chunk), http (one
+ * parse (GPU parse of a chunk, before it starts), parse_fill (after the
+ * chunk's kernels ran, before it is delivered), recordio (GPU RecordIO chunk), http (one
  * ranged GET returns nothing -> exercises the retry loop), tracker (tracker
  * connection).  A fault is a dmlc::Error thrown from that stage ("http" is
  * soft: a transient failure the caller retries).  Off (one relaxed atomic

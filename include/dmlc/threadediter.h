@@ -13,8 +13,8 @@
  * Implementation is new: one mutex + two condition variables, an explicit
  * state machine {kProduce, kBeforeFirst, kDestroy}, and any exception type
  * (not only dmlc::Error) is transported through std::exception_ptr.
- * The GPU ingestion path (dmlc/gpu/pinned_ring.h) generalises this pattern to
- * pinned-host + device cells whose recycling is gated on hipEvents.
+ * The GPU ingestion path (src/gpu/device_parser.cc) runs its pinned-host
+ * slots through this iterator and gates device-slot reuse on hipEvents.
  */
 #ifndef DMLC_THREADEDITER_H_
 #define DMLC_THREADEDITER_H_

@@ -60,8 +60,6 @@ class CSVParser : public TextParserBase<IndexType, DType> {
     IndexType idx = 0;
     real_t label = 0.0f, weight = 1.0f;
     bool has_weight = false;
-    const size_t row_begin = out->index.size();
-    out->index.reserve(row_begin + 32);
     while (true) {
       const char* fe = static_cast<const char*>(std::memchr(p, delim, le - p));
       if (fe == nullptr) fe = le;
@@ -93,6 +91,11 @@ class CSVParser : public TextParserBase<IndexType, DType> {
   void ParseBlock(const char* begin, const char* end,
                   RowBlockContainer<IndexType, DType>* out) override {
     out->Clear();
+    // one up-front reservation per block (a field is at least 2 bytes with its
+    // delimiter); push_back's geometric growth covers any underestimate
+    const size_t est = static_cast<size_t>(end - begin) / 4;
+    out->index.reserve(est);
+    out->value.reserve(est);
     const char delim = param_.delimiter[0];
     const int lc = param_.label_column, wc = param_.weight_column;
     Base::ForEachLine(begin, end, [&](const char* lb, const char* le) {

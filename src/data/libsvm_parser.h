@@ -33,6 +33,34 @@ class LibSVMParser : public TextParserBase<IndexType, DType> {
   using Base = TextParserBase<IndexType, DType>;
   LibSVMParser(InputSplit* source, int nthread) : Base(source, nthread) {}
 
+  /*!
+   * \brief single-pass parse of the common `digits[:number]` feature token.
+   *  Returns false (nothing consumed) when the token needs the general
+   *  ParsePair grammar. Equivalent to ParsePair on the tokens it accepts:
+   *  StrToUInt / StrToFloat only consume digitchars, so they stop at the same
+   *  byte whether bounded by the digitchars run or by the token end, and
+   *  ParsePair ignores whatever follows the value inside the token.
+   */
+  static inline bool FastFeature(const char* tb, const char* te, IndexType* idx, real_t* val,
+                                 RowBlockContainer<IndexType, DType>* out) {
+    const char* p = tb;
+    if (!isdigit(*p)) return false;
+    IndexType v = 0;
+    do {
+      v = static_cast<IndexType>(v * 10u + static_cast<IndexType>(*p - '0'));
+      ++p;
+    } while (p != te && isdigit(*p));
+    if (p == te) {
+      out->PushFeature(v, DType(1.0f), false);
+      return true;
+    }
+    if (*p != ':' || p + 1 == te || !isdigitchars(p[1])) return false;
+    *idx = v;
+    *val = StrToFloat(p + 1, te, nullptr);
+    out->PushFeature(v, static_cast<DType>(*val), true);
+    return true;
+  }
+
   /*! \brief parse one line into out (exposed for tests / the GPU oracle) */
   static inline void ParseLine(const char* lb, const char* le,
                                RowBlockContainer<IndexType, DType>* out) {
@@ -56,6 +84,7 @@ class LibSVMParser : public TextParserBase<IndexType, DType> {
       }
       IndexType idx = 0;
       real_t val = 0.0f;
+      if (FastFeature(tb, te, &idx, &val, out)) continue;
       const int rr = ParsePair<IndexType, real_t>(tb, te, &idx, &val, &bad);
       if (rr < 1) continue;
       CHECK(!bad) << "negative feature index in LibSVM token \""

@@ -8,7 +8,9 @@
 #include <dmlc/logging.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <mutex>
+#include <shared_mutex>
 
 #include <dmlc/gpu/hip_utils.h>
 
@@ -192,24 +194,28 @@ Communicator::~Communicator() {
 
 void Communicator::AllReduce(const void* send, void* recv, size_t count, DataType dt,
                              ReduceOp op, hipStream_t stream) {
+  std::shared_lock<std::shared_timed_mutex> use(use_mu_);
   Check(CheckedApi().AllReduce(send, recv, count, ToNccl(dt), ToNccl(op), C(Live()), stream),
         "ncclAllReduce");
 }
 
 void Communicator::Broadcast(const void* send, void* recv, size_t count, DataType dt, int root,
                              hipStream_t stream) {
+  std::shared_lock<std::shared_timed_mutex> use(use_mu_);
   Check(CheckedApi().Broadcast(send, recv, count, ToNccl(dt), root, C(Live()), stream),
         "ncclBroadcast");
 }
 
 void Communicator::AllGather(const void* send, void* recv, size_t send_count, DataType dt,
                              hipStream_t stream) {
+  std::shared_lock<std::shared_timed_mutex> use(use_mu_);
   Check(CheckedApi().AllGather(send, recv, send_count, ToNccl(dt), C(Live()), stream),
         "ncclAllGather");
 }
 
 void Communicator::ReduceScatter(const void* send, void* recv, size_t recv_count, DataType dt,
                                  ReduceOp op, hipStream_t stream) {
+  std::shared_lock<std::shared_timed_mutex> use(use_mu_);
   Check(CheckedApi().ReduceScatter(send, recv, recv_count, ToNccl(dt), ToNccl(op), C(Live()),
                                    stream),
         "ncclReduceScatter");
@@ -217,6 +223,7 @@ void Communicator::ReduceScatter(const void* send, void* recv, size_t recv_count
 
 void Communicator::AllToAll(const void* send, void* recv, size_t count, DataType dt,
                             hipStream_t stream) {
+  std::shared_lock<std::shared_timed_mutex> use(use_mu_);
   Check(CheckedApi().AllToAll(send, recv, count, ToNccl(dt), C(Live()), stream), "ncclAllToAll");
 }
 
@@ -230,6 +237,7 @@ void Communicator::AllToAllV(const void* send, const std::vector<size_t>& send_c
   CHECK_EQ(send_displs.size(), static_cast<size_t>(world_));
   CHECK_EQ(recv_displs.size(), static_cast<size_t>(world_));
   RcclApi& api = CheckedApi();
+  std::shared_lock<std::shared_timed_mutex> use(use_mu_);  // whole group
   const size_t esize = DataTypeSize(dt);
   const char* s = static_cast<const char*>(send);
   char* r = static_cast<char*>(recv);
@@ -248,10 +256,12 @@ void Communicator::AllToAllV(const void* send, const std::vector<size_t>& send_c
 }
 
 void Communicator::Send(const void* buf, size_t count, DataType dt, int peer, hipStream_t stream) {
+  std::shared_lock<std::shared_timed_mutex> use(use_mu_);
   Check(CheckedApi().Send(buf, count, ToNccl(dt), peer, C(Live()), stream), "ncclSend");
 }
 
 void Communicator::Recv(void* buf, size_t count, DataType dt, int peer, hipStream_t stream) {
+  std::shared_lock<std::shared_timed_mutex> use(use_mu_);
   Check(CheckedApi().Recv(buf, count, ToNccl(dt), peer, C(Live()), stream), "ncclRecv");
 }
 
@@ -267,11 +277,17 @@ void* Communicator::Live() const {
 
 void Communicator::Abort() {
   std::lock_guard<std::mutex> lock(abort_mutex_);
-  if (comm_ != nullptr && !aborted_.exchange(true)) {
-    // ncclCommAbort is the one RCCL call allowed while another thread is
-    // blocked in a collective on this communicator: it makes that call return
-    (void)Api().CommAbort(C(comm_));
+  if (comm_ == nullptr || aborted_.exchange(true)) return;
+  // aborted_ is set first, so no new collective starts; wait (bounded) for
+  // collectives that are mid-enqueue to leave RCCL before freeing the comm
+  std::unique_lock<std::shared_timed_mutex> ex(use_mu_, std::defer_lock);
+  if (!ex.try_lock_for(std::chrono::seconds(2))) {
+    // a call is blocked inside RCCL (e.g. lazy connection setup to a dead
+    // peer): ncclCommAbort is the one RCCL call allowed concurrently with it
+    // and is what makes that call return
+    LOG(WARNING) << "rank " << rank_ << ": aborting RCCL while a collective is blocked in it";
   }
+  (void)Api().CommAbort(C(comm_));
 }
 
 void Communicator::AbortOnTrackerFailure(TrackerClient* tracker) {

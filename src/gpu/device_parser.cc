@@ -439,7 +439,6 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     inflight_.pop_front();
     busy_ = 1;
     cur_slot_ = cur.slot;
-    cursor_ = cur.end_pos;
     const size_t nbytes = cur.size;
     const char* text = dtext_[cur.d]->template get<char>();
     hipStream_t s = compute_->get();
@@ -449,17 +448,29 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     const size_t nnz_base = append ? out->nnz_ : 0;
     ChunkPlan plan;
     const bool token_format = tcfg_.format != TextFormat::kCSV;
-    bool done = false;
-    if (token_format && cfg_.fast_path) {
-      done = FastParse(text, nbytes, out, row_base, nnz_base, &plan);
-      if (!done) stats_.exact_chunks += 1;
-    }
-    if (!done) {
-      ExactParse(text, nbytes, out, row_base, nnz_base, &plan, token_format && cfg_.fast_path);
+    try {
+      bool done = false;
+      if (token_format && cfg_.fast_path) {
+        done = FastParse(text, nbytes, out, row_base, nnz_base, &plan);
+        if (!done) stats_.exact_chunks += 1;
+      }
+      if (!done) {
+        ExactParse(text, nbytes, out, row_base, nnz_base, &plan, token_format && cfg_.fast_path);
+      }
+      DMLC_FAULT_POINT("parse_fill");
+    } catch (...) {
+      // the chunk was not delivered: the cursor stays at its start (a resume
+      // from Tell() replays it), its slots go back to the pipeline
+      (void)hipStreamSynchronize(s);
+      if (cur_slot_ != nullptr) iter_.Recycle(&cur_slot_);
+      parsed_[cur.d]->Record(s);
+      busy_ = 0;
+      throw;
     }
     if (cur_slot_ != nullptr) iter_.Recycle(&cur_slot_);
     parsed_[cur.d]->Record(s);
     busy_ = 0;
+    cursor_ = cur.end_pos;  // only once the chunk is delivered
     out->rows_ = row_base + plan.nrows;
     out->nnz_ = nnz_base + plan.nnz;
     if (acc_flags_ & kFlagWeight) out->has_weight_ = true;

@@ -777,7 +777,10 @@ PYBIND11_MODULE(_dmlc, m) {
              return py::str(reason);
            })
       .def("abort", &TrackerClient::Abort, py::call_guard<py::gil_scoped_release>())
-      .def("start_heartbeat", &TrackerClient::StartHeartbeat, py::arg("period") = 5.0)
+      // the first heartbeat is synchronous: never hold the GIL across it (an
+      // in-process Python tracker needs the GIL to answer)
+      .def("start_heartbeat", &TrackerClient::StartHeartbeat, py::arg("period") = 5.0,
+           py::call_guard<py::gil_scoped_release>())
       .def("stop_heartbeat", &TrackerClient::StopHeartbeat,
            py::call_guard<py::gil_scoped_release>())
       .def("rccl_put",

@@ -16,8 +16,17 @@ def _ptr(t):
 
 def test_rccl_collectives_world1():
     assert _dmlc.Communicator.available()
-    # torch (imported first by dmlc_core_amd) already loaded its RCCL
-    assert "torch" in _dmlc.Communicator.library_path(), _dmlc.Communicator.library_path()
+    # torch (imported first by dmlc_core_amd) already loaded its RCCL: the
+    # communicator must resolve to that same library, not load a second copy
+    import os
+    path = _dmlc.Communicator.library_path()
+    assert path and "rccl" in os.path.basename(path), path
+    loaded = set()
+    with open("/proc/self/maps") as f:
+        for line in f:
+            if "librccl" in line:
+                loaded.add(os.path.realpath(line.split()[-1]))
+    assert len(loaded) == 1 and os.path.realpath(path) in loaded, (path, loaded)
     uid = _dmlc.Communicator.new_unique_id()
     assert len(uid) == 128
     comm = _dmlc.Communicator(0, 1, 0, uid)

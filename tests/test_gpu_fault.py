@@ -49,3 +49,28 @@ def test_gpu_recordio_fault(tmp_path):
     _dmlc.fault_configure("")
     r = io.GPURecordIO(f, chunk_bytes=1 << 20)
     assert r.read_all()["size"] == 20000
+
+
+@pytest.mark.parametrize("zero_copy", [0, 1])
+def test_gpu_parse_failure_keeps_resume_cursor(tmp_path, zero_copy):
+    """A chunk that fails mid-parse is not delivered: tell() still points at
+    its start, so seeking there on the same parser replays it exactly."""
+    p = str(tmp_path / "c.libsvm")
+    data.write_synthetic(p, 0, 30000, seed=6)
+    g = data.GPUParser(p, chunk_bytes=1 << 20, zero_copy=zero_copy, read_threads=2)
+    blocks = []
+    assert g.next()
+    blocks.append(g.value_to_host())
+    before = g.tell()
+    _dmlc.fault_configure("parse_fill:1")
+    with pytest.raises(_dmlc.DMLCError, match='injected fault at "parse_fill"'):
+        g.next()
+    _dmlc.fault_configure("")
+    assert g.tell() == before
+    g.seek(before)
+    while g.next():
+        blocks.append(g.value_to_host())
+    got = pyref.concat_blocks(blocks)
+    c = _cpu(p)
+    for k in ("label", "offset", "index", "value"):
+        np.testing.assert_array_equal(got[k], c[k], err_msg=k)
