@@ -45,6 +45,10 @@ def parse_args():
     ap.add_argument("--device", choices=["auto", "gpu", "cpu"], default="auto")
     ap.add_argument("--zero-copy", default="auto", choices=["auto", "0", "1"],
                     help="mmap + hipHostRegister the shard (DMA from page cache)")
+    ap.add_argument("--mode", default="stream", choices=["stream", "hbm"],
+                    help="stream: every step re-reads the text from the page cache over PCIe; "
+                         "hbm: HBM epoch cache -- the warmup epoch keeps the text resident in "
+                         "HBM and timed epochs parse it from there (kernel-bound)")
     return ap.parse_args()
 
 
@@ -140,7 +144,10 @@ def main():
         parser = data.GPUParser(ddir, rank, world, format="libsvm", chunk_mb=args.chunk_mb,
                                 read_threads=read_threads, pinned_slots=args.pinned_slots,
                                 device_slots=args.device_slots, device=local_rank,
-                                zero_copy=args.zero_copy)
+                                zero_copy=args.zero_copy,
+                                hbm_cache=int(args.mode == "hbm"))
+        if args.mode == "hbm" and args.warmup < 1:
+            raise SystemExit("--mode hbm needs --warmup >= 1 (the warmup epoch fills the cache)")
         csr = data.DeviceCSR()
 
         def step():
@@ -211,11 +218,14 @@ def main():
                 "read_threads": read_threads,
                 "device": "gpu" if use_gpu else "cpu",
                 "numa_node_rank0": numa.get("numa_node", -1),
-                "ingest": ("zero-copy mmap+hipHostRegister DMA" if use_gpu and parser.stats().get("zero_copy")
+                "ingest": ("HBM epoch cache (text resident in HBM after the warmup epoch)"
+                           if use_gpu and args.mode == "hbm" else
+                           "zero-copy mmap+hipHostRegister DMA" if use_gpu and parser.stats().get("zero_copy")
                            else "parallel pread -> pinned ring -> hipMemcpyAsync"),
             },
             "per_gpu_rows_per_sec": round(value / max(1, world), 1),
             "input_GBps": round(nbytes * args.steps / elapsed / 1e9, 3),
+            "mode": args.mode,
         }
         if use_gpu:
             out["parser_stats_last_rank0"] = parser.stats()

@@ -56,8 +56,16 @@ struct DeviceParserConfig {
    *  pinned pread ring, 0 off, 1 required)
    */
   int zero_copy{-1};
+  /*!
+   * \brief HBM epoch cache: the first full pass also keeps every
+   *  chunk's text resident in one device arena (partition bytes of HBM); later
+   *  epochs (BeforeFirst, or Seek to a chunk boundary) parse straight from HBM
+   *  with no host I/O and no PCIe traffic.
+   */
+  bool hbm_cache{false};
   /*! \brief apply `?k=v` overrides (chunk_mb, pinned_slots, device_slots,
-   *  read_threads, device, format, label_column, weight_column, delimiter) */
+   *  read_threads, device, format, label_column, weight_column, delimiter,
+   *  fast_path, zero_copy, hbm_cache) */
   void Update(const std::map<std::string, std::string>& args);
 };
 

@@ -60,11 +60,17 @@ class InputSplitShuffle : public InputSplit {
       source_->BeforeFirst();
     }
   }
+  /*!
+   * \brief move to another rank's shard: the current visiting order is kept
+   *  (no reshuffle), as in the reference (:75-80); part_index_ is updated so
+   *  later sub-shards stay in the new shard (the reference keeps the old one).
+   */
   void ResetPartition(unsigned part_index, unsigned num_parts) override {
+    CHECK(num_parts == num_parts_) << "num_parts is not consistent!";
     CHECK(part_index < num_parts) << "invalid partition";
     part_index_ = part_index;
-    num_parts_ = num_parts;
-    BeforeFirst();
+    cur_shuffle_idx_ = 0;
+    source_->ResetPartition(SubPart(cur_shuffle_idx_), num_parts_ * num_shuffle_parts_);
   }
   bool NextRecord(Blob* out_rec) override {
     while (!source_->NextRecord(out_rec)) {

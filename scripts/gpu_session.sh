@@ -29,10 +29,26 @@ if [[ $STAGES == *bench* ]]; then
     [ $rc -eq 0 ] || exit $rc
   fi
 fi
+PROF_ARGS="${PROF_ARGS:---steps 2 --warmup 1}"
 if [[ $STAGES == *prof* ]]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
-    python3 bench.py --steps 2 --warmup 1 > $OUT/prof_bench.log 2>&1
+    python3 bench.py $PROF_ARGS > $OUT/prof_bench.log 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -3 $OUT/prof_bench.log
   find $OUT/prof -name '*kernel_stats*' | head -3
+  [ $rc -eq 0 ] || exit $rc
+fi
+# hardware counters: one rocprofv3 pass per counter group (slot limits:
+# FETCH_SIZE and WRITE_SIZE each need their own pass), counters only
+PMC_ARGS="${PMC_ARGS:---rows 2000000 --mode hbm --steps 3 --warmup 1}"
+if [[ $STAGES == *pmc* ]]; then
+  i=0
+  for grp in "FETCH_SIZE" "WRITE_SIZE" \
+             "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES"; do
+    i=$((i+1))
+    timeout -s KILL 240 rocprofv3 --pmc $grp -d $OUT/pmc$i -o run --output-format csv -- \
+      python3 bench.py $PMC_ARGS > $OUT/pmc$i.log 2>&1
+    rc=$?; echo "pmc pass $i ($grp) rc=$rc"; tail -2 $OUT/pmc$i.log
+    case $rc in 0|1|2) ;; *) exit $rc ;; esac
+  done
 fi
 exit 0

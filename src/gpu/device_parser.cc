@@ -70,6 +70,8 @@ void DeviceParserConfig::Update(const std::map<std::string, std::string>& args) 
       delimiter = v[0];
     } else if (k == "fast_path") {
       fast_path = v != "0" && v != "false";
+    } else if (k == "hbm_cache") {
+      hbm_cache = v != "0" && v != "false";
     } else if (k == "zero_copy") {
       zero_copy = (v == "auto" || v == "-1") ? -1 : ((v == "0" || v == "false") ? 0 : 1);
     }
@@ -132,9 +134,12 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       parsed_.back()->Record(compute_->get());
     }
     tiles_.Reserve(LineIndexTiles(cfg_.chunk_bytes) * sizeof(uint64_t));
+    tcounts_.Reserve(TileCount(cfg_.chunk_bytes) * sizeof(uint64_t));
+    tflags_.Reserve(TileCount(cfg_.chunk_bytes) * sizeof(uint32_t));
     meta_.Reserve(2 * sizeof(ChunkMeta));
     hmeta_.Reserve(2 * sizeof(ChunkMeta));
-    slots_.Reserve(kMaxPartialBlocks * sizeof(MetaPartial));
+    slots_.Reserve(std::max<size_t>(kMaxPartialBlocks, TileCount(cfg_.chunk_bytes)) *
+                   sizeof(MetaPartial));
     iter_.set_max_capacity(static_cast<size_t>(cfg_.pinned_slots));
     if (cfg_.zero_copy != 0) {
       zc_.reset(new ZeroCopySource());
@@ -148,6 +153,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       }
     }
     if (zc_ == nullptr) StartReader();
+    if (cfg_.hbm_cache) StartCaching();
   }
 
   ~DeviceParserImpl() override {
@@ -170,6 +176,27 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   void Seek(size_t cursor) override {
     CHECK_LE(cursor, PartitionBytes()) << "DeviceParser::Seek: cursor beyond the partition";
     DrainInflight();
+    replay_ = false;
+    caching_ = false;
+    if (cfg_.hbm_cache) {
+      if (cache_complete_) {
+        // replay from the cache when the cursor is a chunk boundary of it
+        for (size_t i = 0; i <= cached_.size(); ++i) {
+          const size_t b = i < cached_.size() ? cached_[i].begin_pos : PartitionBytes();
+          if (b == cursor) {
+            replay_ = true;
+            replay_idx_ = i;
+            cursor_ = cursor;
+            return;
+          }
+        }
+      } else if (cursor == 0) {
+        StartCaching();
+      } else {
+        cached_.clear();  // a partial pass cannot complete the cache
+        arena_fill_ = 0;
+      }
+    }
     if (zc_ != nullptr) {
       zc_->Seek(cursor);
     } else {
@@ -208,10 +235,15 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
 
  private:
   struct Inflight {
-    HostSlot* slot;  // nullptr in zero-copy mode
-    int d;
+    HostSlot* slot;  // nullptr in zero-copy / replay mode
+    int d;           // device slot (events), -1 when replayed from the HBM cache
     size_t size;
     size_t end_pos;  // resume cursor once this chunk is delivered
+    const char* text;  // device text of the chunk
+  };
+  /*! \brief a chunk held in the HBM epoch cache */
+  struct CachedChunk {
+    size_t off, size, begin_pos, end_pos;
   };
 
   void StartReader() {
@@ -239,6 +271,16 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
    *  recorded yet, so a copy queued into that slot would not wait for it.
    */
   void FillPipeline() {
+    if (replay_) {
+      // HBM epoch cache: chunks are already resident, no copy and no slot
+      while (static_cast<int>(inflight_.size()) < cfg_.device_slots &&
+             replay_idx_ < cached_.size()) {
+        const CachedChunk& c = cached_[replay_idx_++];
+        inflight_.push_back(Inflight{nullptr, -1, c.size, c.end_pos, arena_->get<char>() + c.off});
+      }
+      reader_done_ = replay_idx_ == cached_.size();
+      return;
+    }
     while (static_cast<int>(inflight_.size()) + busy_ < cfg_.device_slots && !reader_done_) {
       // fault points sit before a slot is taken, so a failure leaks nothing
       if (zc_ != nullptr) DMLC_FAULT_POINT("read");
@@ -250,6 +292,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
         ZeroCopySource::Piece piece;
         if (!zc_->Next(&piece)) {
           reader_done_ = true;
+          if (caching_) cache_complete_ = true;
           break;
         }
         src = piece.ptr;
@@ -259,6 +302,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
         const double t0 = GetTime();
         if (!iter_.Next(&slot)) {
           reader_done_ = true;
+          if (caching_) cache_complete_ = true;
           break;
         }
         stats_.wait_reader_sec += GetTime() - t0;
@@ -268,12 +312,32 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       }
       const int d = next_dslot_;
       next_dslot_ = (next_dslot_ + 1) % cfg_.device_slots;
+      char* dst = dtext_[d]->template get<char>();
+      if (caching_) {
+        // first pass of an hbm_cache epoch: the chunk lands in its arena slot
+        const size_t begin_pos = cached_.empty() ? 0 : cached_.back().end_pos;
+        CHECK_LE(arena_fill_ + size, arena_bytes_) << "HBM cache arena overflow";
+        dst = arena_->get<char>() + arena_fill_;
+        cached_.push_back(CachedChunk{arena_fill_, size, begin_pos, end_pos});
+        arena_fill_ += size;
+      }
       DMLC_HIP_CHECK(hipStreamWaitEvent(copy_->get(), parsed_[d]->get(), 0));
-      DMLC_HIP_CHECK(
-          hipMemcpyAsync(dtext_[d]->get(), src, size, hipMemcpyHostToDevice, copy_->get()));
+      DMLC_HIP_CHECK(hipMemcpyAsync(dst, src, size, hipMemcpyHostToDevice, copy_->get()));
       copied_[d]->Record(copy_->get());
-      inflight_.push_back(Inflight{slot, d, size, end_pos});
+      inflight_.push_back(Inflight{slot, d, size, end_pos, dst});
     }
+  }
+
+  void StartCaching() {
+    cached_.clear();
+    arena_fill_ = 0;
+    cache_complete_ = false;
+    if (arena_ == nullptr) {
+      arena_bytes_ = PartitionBytes();
+      arena_.reset(new DeviceBuffer(arena_bytes_ + kTextPadBytes));
+      DMLC_HIP_CHECK(hipMemset(arena_->get(), 0, arena_bytes_ + kTextPadBytes));
+    }
+    caching_ = true;
   }
 
   void DrainInflight() {
@@ -349,37 +413,41 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     return tgt;
   }
 
-  /*! \brief token-parallel parse; false when the chunk must take the exact path */
+  /*!
+   * \brief LDS-staged tile parse (tile_kernels.hip); false when the chunk must
+   *  take the exact path.  One blocking read-back (the chunk's sizes) before
+   *  the fill, one for the maxima / flags after it.
+   */
   bool FastParse(const char* text, size_t nbytes, DeviceCSR<IndexType>* out, size_t row_base,
                  size_t nnz_base, ChunkPlan* plan) {
     hipStream_t s = compute_->get();
     ChunkMeta* dmeta = meta_.get<ChunkMeta>();
-    uint64_t* packed = reinterpret_cast<uint64_t*>(dmeta + 1);
-    LaunchTokenCount(text, nbytes, tiles_.get<uint64_t>(), packed, s);
-    const uint64_t counts = ReadBack<uint64_t>(packed);
-    plan->nlines = counts >> 32;
-    plan->ntok = counts & 0xffffffffull;
+    LaunchTileCountScan(text, nbytes, tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(), dmeta, s);
+    const ChunkMeta sizes = ReadBack<ChunkMeta>(dmeta);
     AfterFirstSync();
-    EnsureLineBuffers(plan->nlines, plan->ntok);
-    LaunchTokenEmit(text, nbytes, tiles_.get<uint64_t>(), lines_.get<uint32_t>(),
-                    first_tok_.get<uint32_t>(), tok_pos_.get<uint32_t>(),
-                    tok_line_.get<uint32_t>(), s);
-    LaunchRowInfo(first_tok_.get<uint32_t>(), plan->nlines, plan->ntok, info_.get<uint64_t>(), s);
-    uint64_t* total = partials_.get<uint64_t>() + ScanPartials(plan->nlines) + 1;
-    LaunchScanU64(info_.get<uint64_t>(), plan->nlines, partials_.get<uint64_t>(), total, s);
-    const uint64_t t = ReadBack<uint64_t>(total);
-    plan->nrows = t >> 32;
-    plan->nnz = t & 0xffffffffull;
-    FillTarget<IndexType> tgt = PrepareOutput(out, row_base, nnz_base, *plan, true, nbytes);
-    DMLC_HIP_CHECK(hipMemsetAsync(dmeta, 0, sizeof(ChunkMeta), s));
-    LaunchTokenFill<IndexType>(text, nbytes, tcfg_.format, tok_pos_.get<uint32_t>(),
-                               tok_line_.get<uint32_t>(), plan->ntok, first_tok_.get<uint32_t>(),
-                               info_.get<uint64_t>(), tgt, plan->nrows, plan->nnz,
-                               slots_.get<MetaPartial>(), dmeta, s);
-    const ChunkMeta m = ReadBack<ChunkMeta>(dmeta);
-    if (m.flags & kFlagIrregular) return false;
-    Accumulate(m);
-    return true;
+    if (sizes.flags & kFlagIrregular) return false;
+    plan->nlines = sizes.nlines;
+    plan->nrows = sizes.nrows;
+    plan->nnz = sizes.nnz;
+    bool need_weight = false;
+    for (;;) {
+      FillTarget<IndexType> tgt = PrepareOutput(out, row_base, nnz_base, *plan, need_weight, nbytes);
+      LaunchTileFill<IndexType>(text, nbytes, tcfg_.format, tcounts_.get<uint64_t>(), tgt,
+                                slots_.get<MetaPartial>(), dmeta, s);
+      ChunkMeta m = ReadBack<ChunkMeta>(dmeta);
+      if (m.flags & kFlagIrregular) return false;
+      if ((m.flags & kFlagNeedWeight) && !need_weight) {
+        // first weighted row of the epoch: allocate the column (earlier rows
+        // get 1.0) and write this chunk again with it
+        need_weight = true;
+        m.flags &= ~kFlagNeedWeight;
+        DMLC_HIP_CHECK(hipMemcpyAsync(dmeta, &sizes, sizeof(ChunkMeta), hipMemcpyHostToDevice, s));
+        continue;
+      }
+      CHECK(!(m.flags & kFlagNeedWeight)) << "internal error: weight column not allocated";
+      Accumulate(m);
+      return true;
+    }
   }
 
   /*! \brief exact wave-per-line parse (any input) */
@@ -440,10 +508,10 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     busy_ = 1;
     cur_slot_ = cur.slot;
     const size_t nbytes = cur.size;
-    const char* text = dtext_[cur.d]->template get<char>();
+    const char* text = cur.text;
     hipStream_t s = compute_->get();
     ScopedRange range("parse_chunk");
-    DMLC_HIP_CHECK(hipStreamWaitEvent(s, copied_[cur.d]->get(), 0));
+    if (cur.d >= 0) DMLC_HIP_CHECK(hipStreamWaitEvent(s, copied_[cur.d]->get(), 0));
     const size_t row_base = append ? out->rows_ : 0;
     const size_t nnz_base = append ? out->nnz_ : 0;
     ChunkPlan plan;
@@ -463,12 +531,12 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       // from Tell() replays it), its slots go back to the pipeline
       (void)hipStreamSynchronize(s);
       if (cur_slot_ != nullptr) iter_.Recycle(&cur_slot_);
-      parsed_[cur.d]->Record(s);
+      if (cur.d >= 0) parsed_[cur.d]->Record(s);
       busy_ = 0;
       throw;
     }
     if (cur_slot_ != nullptr) iter_.Recycle(&cur_slot_);
-    parsed_[cur.d]->Record(s);
+    if (cur.d >= 0) parsed_[cur.d]->Record(s);
     busy_ = 0;
     cursor_ = cur.end_pos;  // only once the chunk is delivered
     out->rows_ = row_base + plan.nrows;
@@ -506,12 +574,19 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   std::vector<std::unique_ptr<DeviceBuffer>> dtext_;
   std::vector<std::unique_ptr<Event>> copied_, parsed_;
   DeviceBuffer tiles_, lines_, first_tok_, tok_pos_, tok_line_, info_, partials_, meta_;
+  /*! \brief tile parser scratch: per-tile counts (scanned in place) and flags */
+  DeviceBuffer tcounts_, tflags_;
   /*! \brief per-workgroup reduction slots (MetaPartial) */
   DeviceBuffer slots_;
   PinnedBuffer hmeta_;
   ThreadedIter<HostSlot> iter_;
   std::unique_ptr<ZeroCopySource> zc_;
   std::deque<Inflight> inflight_;
+  /*! \brief HBM epoch cache (cfg_.hbm_cache): the partition's chunks, resident */
+  std::unique_ptr<DeviceBuffer> arena_;
+  size_t arena_bytes_{0}, arena_fill_{0}, replay_idx_{0};
+  std::vector<CachedChunk> cached_;
+  bool caching_{false}, cache_complete_{false}, replay_{false};
   HostSlot* cur_slot_{nullptr};
   /*! \brief resume cursor (partition offset after the last delivered chunk) */
   size_t cursor_{0};

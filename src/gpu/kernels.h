@@ -170,6 +170,32 @@ void LaunchTokenFill(const char* text, size_t nbytes, TextFormat format, const u
                      const uint64_t* line_info, const FillTarget<IndexType>& out, uint64_t nrows,
                      uint64_t nnz, MetaPartial* partials, ChunkMeta* meta, hipStream_t stream);
 
+// --------------- LDS-staged tile parser (LibSVM/LibFM fast path) ---------------
+/*! \brief bytes of text per workgroup of the tile kernels */
+constexpr size_t kTileBytes = 8192;
+/*! \brief a weighted row met a FillTarget without a weight column (re-run with one) */
+constexpr unsigned kFlagNeedWeight = 2048u;
+/*! \brief tiles of a chunk (size of the tile count / flag scratch and MetaPartial slots) */
+size_t TileCount(size_t nbytes);
+/*!
+ * \brief C1 + C2: per-tile (line starts << 32 | token starts) and irregular
+ *  flags, exclusive-scanned in place; meta receives nlines, nrows = nlines,
+ *  nnz = tokens - lines, flags (kFlagIrregular) and zeroed maxima.
+ *  tile_counts / tile_flags need TileCount(nbytes) entries.
+ */
+void LaunchTileCountScan(const char* text, size_t nbytes, uint64_t* tile_counts,
+                         uint32_t* tile_flags, ChunkMeta* meta, hipStream_t stream);
+/*!
+ * \brief C3 + C4: parse every token of a regular chunk into out using the
+ *  scanned tile prefixes; merges max index / field and flags into meta and
+ *  writes offset[row_base + nrows].  partials needs TileCount(nbytes) slots.
+ *  Sets kFlagNeedWeight if a row is weighted and out.weight is null.
+ */
+template <typename IndexType>
+void LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
+                    const uint64_t* tile_prefix, const FillTarget<IndexType>& out,
+                    MetaPartial* partials, ChunkMeta* meta, hipStream_t stream);
+
 // ----------------------------- RecordIO (K7) -----------------------------
 /*! \brief error bits reported by the RecordIO kernels */
 constexpr uint32_t kRecErrTruncated = 1;   // a part runs past the chunk end

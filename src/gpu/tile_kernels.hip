@@ -1,0 +1,609 @@
+/*!
+ * \file src/gpu/tile_kernels.hip
+ * \brief LDS-staged tile parser: the LibSVM / LibFM fast path in three launches
+ *  and one host read-back of the chunk sizes.
+ *
+ *  Every row of a regular chunk is one line whose first byte starts its label
+ *  token, so with L(p) = line starts at or before byte p and T(p) = tokens
+ *  before p, the CSR position of a token follows from two prefix counts:
+ *      row(label token k of line l)   = l,        offset[l] = k - l
+ *      nnz(feature token k of line l) = k - l - 1
+ *  No per-line or per-token index arrays are materialised.
+ *
+ *  C1 k_tile_count (grid = tiles of 8 KiB): SWAR byte masks of 16 B per lane,
+ *     per tile (line starts << 32 | token starts) and an irregular bit (a line
+ *     that starts with a blank, a token that does not start with [0-9+-.]:
+ *     qid tokens, digit-less tokens, label-less lines).  Reads the chunk once.
+ *  C2 k_tile_scan  (one 1024-lane workgroup): exclusive scan of the tile
+ *     counts, OR of the flags; writes nlines / nrows / nnz / flags to the
+ *     ChunkMeta the host reads back (the single blocking read per chunk).
+ *  C3 k_tile_fill  (grid = tiles): stage the tile in LDS with coalesced 16 B
+ *     loads, recompute the masks from the same registers, workgroup-scan them
+ *     and compact (tile offset, line ordinal, label bit) of every token into an
+ *     LDS list; then lane i parses token i straight from the LDS tile with
+ *     strtonum.h's ParsePair / ParseTriple (bit-identical to the CPU parser)
+ *     over a separator-bounded byte iterator, and stores index / value /
+ *     label / offset directly.  Only a tile's last token, which may continue
+ *     into the next tile, is read from global memory.
+ *     K8 (max index / field, flags) is a per-workgroup slot.
+ *  C4 k_tile_finish (one workgroup): fold the slots into the ChunkMeta and
+ *     write the chunk's closing row pointer.
+ *  Traffic per chunk: text read twice (C1, C3) + the CSR written once.
+ */
+#include <hip/hip_runtime.h>
+
+#include "../data/strtonum.h"
+#include "./device_common.h"
+#include "./kernels.h"
+
+namespace dmlc {
+namespace gpu {
+
+namespace {
+constexpr int kThreads = 256;
+constexpr int kSub = static_cast<int>(kTileBytes / 4096);  // 4 KiB sub-tiles per tile
+constexpr unsigned kOffBits = 13;                            // tile offset < 8192
+constexpr unsigned kMaxTileTokens = static_cast<unsigned>(kTileBytes / 2);
+static_assert(kTileBytes == 8192, "entry packing assumes 8 KiB tiles");
+
+__device__ __forceinline__ uint32_t sep_masks(uint4 v, uint32_t* eol_out) {
+  const uint32_t eol = dev::byte_eq_mask(v, '\n') | dev::byte_eq_mask(v, '\r');
+  *eol_out = eol;
+  return eol | dev::byte_eq_mask(v, ' ') | dev::byte_eq_mask(v, '\t');
+}
+
+__device__ __forceinline__ bool num_start(uint32_t c) {
+  return (c >= '0' && c <= '9') || c == '+' || c == '-' || c == '.';
+}
+
+/*!
+ * \brief line-start / token-start masks of the 16 bytes v at chunk offset pos;
+ *  pc = the byte before pos ('\n' at 0).  Bytes at or past n are invalid.
+ *  Returns true when the lane saw an irregular construct.
+ */
+template <bool kCheck>
+__device__ __forceinline__ bool lane_masks(uint4 v, uint32_t pc, size_t pos, size_t n,
+                                           uint32_t* lm, uint32_t* tm) {
+  uint32_t eol;
+  const uint32_t sep = sep_masks(v, &eol);
+  const uint32_t prev_eol = (pc == '\n' || pc == '\r') ? 1u : 0u;
+  const uint32_t prev_sep = (prev_eol || pc == ' ' || pc == '\t') ? 1u : 0u;
+  uint32_t valid = 0xFFFFu;
+  if (pos >= n) {
+    valid = 0;
+  } else if (n - pos < 16) {
+    valid = (1u << (n - pos)) - 1u;
+  }
+  *lm = ~eol & ((eol << 1) | prev_eol) & valid & 0xFFFFu;
+  *tm = ~sep & ((sep << 1) | prev_sep) & valid & 0xFFFFu;
+  if (!kCheck) return false;
+  bool bad = (*lm & ~*tm) != 0;  // a line that starts with a blank
+  uint32_t t = *tm;
+  while (t != 0) {
+    const int j = __ffs(t) - 1;
+    t &= t - 1;
+    bad |= !num_start(dev::vec_byte(v, j));
+  }
+  return bad;
+}
+
+__device__ __forceinline__ uint4 load16(const uint8_t* __restrict__ text, size_t pos, size_t n) {
+  // a 16 B load that starts before n stays inside n + kTextPadBytes
+  if (pos < n) return *reinterpret_cast<const uint4*>(text + pos);
+  return make_uint4(0, 0, 0, 0);
+}
+
+/*! \brief byte before `pos` of this lane: lane t-1's last byte, or memory for lane 0 */
+__device__ __forceinline__ uint32_t prev_byte(const uint8_t* __restrict__ text, size_t pos,
+                                              uint4 v) {
+  const uint32_t from_left = __shfl_up(v.w >> 24, 1, dev::kWave);
+  if (dev::lane_id() != 0) return from_left;
+  return pos == 0 ? static_cast<uint32_t>('\n') : text[pos - 1];
+}
+
+__global__ __launch_bounds__(kThreads) void k_tile_count(const uint8_t* __restrict__ text,
+                                                         size_t n, uint64_t* __restrict__ counts,
+                                                         uint32_t* __restrict__ flags) {
+  __shared__ uint64_t smem[4];
+  __shared__ uint32_t sbad;
+  if (threadIdx.x == 0) sbad = 0;
+  uint64_t packed = 0;
+  bool bad = false;
+#pragma unroll
+  for (int s = 0; s < kSub; ++s) {
+    const size_t pos = blockIdx.x * kTileBytes + s * 4096 + threadIdx.x * 16;
+    const uint4 v = load16(text, pos, n);
+    const uint32_t pc = prev_byte(text, pos, v);
+    uint32_t lm, tm;
+    bad |= lane_masks<true>(v, pc, pos, n, &lm, &tm);
+    packed += (static_cast<uint64_t>(__popc(lm)) << 32) | __popc(tm);
+  }
+  const uint64_t total = dev::block_sum_256<uint64_t>(packed, smem);
+  // block_sum_256 ends with a barrier-separated read of smem: sbad's reset is ordered
+  if (__any(bad) && dev::lane_id() == 0) sbad = 1;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    counts[blockIdx.x] = total;
+    flags[blockIdx.x] = sbad ? kFlagIrregular : 0u;
+  }
+}
+
+constexpr int kScanThreads = 1024;
+constexpr int kScanPer = 8;
+
+/*! \brief exclusive scan of ntiles counts in place (one workgroup), meta totals */
+__global__ __launch_bounds__(kScanThreads) void k_tile_scan(uint64_t* __restrict__ counts,
+                                                            const uint32_t* __restrict__ flags,
+                                                            size_t ntiles, ChunkMeta* meta) {
+  __shared__ uint64_t swave[kScanThreads / 64];
+  __shared__ uint32_t sflag[kScanThreads / 64];
+  const int wid = threadIdx.x / dev::kWave;
+  uint64_t carry = 0;
+  uint32_t fl = 0;
+  for (size_t t0 = 0; t0 < ntiles; t0 += static_cast<size_t>(kScanThreads) * kScanPer) {
+    const size_t base = t0 + static_cast<size_t>(threadIdx.x) * kScanPer;
+    uint64_t v[kScanPer];
+    uint64_t s = 0;
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i) {
+      v[i] = base + i < ntiles ? counts[base + i] : 0;
+      if (base + i < ntiles) fl |= flags[base + i];
+      s += v[i];
+    }
+    uint64_t wtot;
+    const uint64_t wx = dev::wave_excl_scan(s, &wtot);
+    if (dev::lane_id() == 0) swave[wid] = wtot;
+    __syncthreads();
+    uint64_t before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < kScanThreads / 64; ++w) {
+      const uint64_t t = swave[w];
+      if (w < wid) before += t;
+      all += t;
+    }
+    uint64_t x = carry + before + wx;
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i) {
+      if (base + i < ntiles) counts[base + i] = x;
+      x += v[i];
+    }
+    carry += all;
+    __syncthreads();
+  }
+  fl = dev::wave_or(fl);
+  if (dev::lane_id() == 0) sflag[wid] = fl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t f = 0;
+    for (int w = 0; w < kScanThreads / 64; ++w) f |= sflag[w];
+    const uint64_t lines = carry >> 32, toks = carry & 0xffffffffull;
+    meta->nlines = lines;
+    meta->nrows = lines;
+    meta->nnz = toks - lines;
+    meta->max_index = 0;
+    meta->max_field = 0;
+    meta->flags = f;
+    meta->pad = 0;
+  }
+}
+
+/*!
+ * \brief byte iterator whose end is "the next separator" (blank / EOL) or a
+ *  hard limit.  strtonum.h's ParsePair / ParseTriple compare against an end
+ *  iterator; a `sentinel` end makes them stop at the token's own end without
+ *  knowing its length, so a token is parsed with one pass of byte loads
+ *  (ds_read_u8 from the LDS tile, or global loads for the last token of a
+ *  tile) instead of locating its end first.
+ */
+template <typename Ptr>
+struct SepIter {
+  Ptr p;
+  Ptr limit;
+  bool sentinel;
+  __device__ __forceinline__ char operator*() const { return static_cast<char>(*p); }
+  __device__ __forceinline__ SepIter& operator++() {
+    ++p;
+    return *this;
+  }
+  __device__ __forceinline__ bool at_end() const {
+    if (p >= limit) return true;
+    const uint8_t c = *p;
+    return c == ' ' || c == '\t' || c == '\n' || c == '\r';
+  }
+  __device__ __forceinline__ bool operator!=(const SepIter& o) const {
+    return o.sentinel ? !at_end() : p != o.p;
+  }
+  __device__ __forceinline__ bool operator==(const SepIter& o) const { return !(*this != o); }
+};
+
+template <typename Ptr>
+__device__ __forceinline__ SepIter<Ptr> sep_begin(Ptr p, Ptr limit) {
+  return SepIter<Ptr>{p, limit, false};
+}
+template <typename Ptr>
+__device__ __forceinline__ SepIter<Ptr> sep_end(Ptr limit) {
+  return SepIter<Ptr>{limit, limit, true};
+}
+
+/*! \brief 4 bytes starting at byte p of an LDS buffer (two aligned dword reads) */
+__device__ __forceinline__ uint32_t lds_u32_at(const uint8_t* lds, uint32_t p) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(lds + (p & ~3u));
+  return __builtin_amdgcn_alignbyte(w[1], w[0], (p & 3u) * 8u);
+}
+
+__device__ __forceinline__ uint32_t pow10_small(uint32_t k) {
+  return k >= 4 ? 10000u : (k == 3 ? 1000u : (k == 2 ? 100u : (k == 1 ? 10u : 1u)));
+}
+
+/*!
+ * \brief SWAR: number of leading ASCII digits (0..4) of the 4 bytes g (first
+ *  byte = lowest) and their decimal value.
+ */
+__device__ __forceinline__ uint32_t lead_digits(uint32_t g, uint32_t* val) {
+  const uint32_t hi = (g & 0xF0F0F0F0u) ^ 0x30303030u;           // high nibble != 3
+  const uint32_t lo = ((g & 0x0F0F0F0Fu) + 0x06060606u) & 0x10101010u;  // low nibble > 9
+  const uint32_t bad = hi | (lo << 3);
+  const uint32_t k = bad != 0 ? (static_cast<uint32_t>(__builtin_ctz(bad)) >> 3) : 4u;
+  uint32_t x = g & 0x0F0F0F0Fu;
+  x = k == 0 ? 0u : (x << (8u * (4u - k)));  // the k digits, right-aligned, leading zeros
+  const uint32_t t = (x * 10u + (x >> 8)) & 0x00FF00FFu;
+  *val = (t & 0xFFu) * 100u + (t >> 16);
+  return k;
+}
+
+/*! \brief a decimal number `[sign] digits [. digits]` read from LDS */
+struct FastNum {
+  uint64_t ip, fp, fpow;  // integer / fraction digits and 10^(fraction digits), mod 2^64
+  uint32_t nip;           // integer digit count
+  uint32_t term;          // the byte after the number
+  uint32_t end;           // its offset
+  bool neg, dot, ok;
+};
+
+__device__ __forceinline__ uint64_t digit_run(const uint8_t* lds, uint32_t* p, uint64_t acc,
+                                              uint32_t* ndig, uint64_t* pw, uint32_t* term,
+                                              bool* ok) {
+  for (int it = 0; it < 8; ++it) {
+    const uint32_t g = lds_u32_at(lds, *p);
+    uint32_t v;
+    const uint32_t k = lead_digits(g, &v);
+    const uint32_t m = pow10_small(k);
+    acc = acc * m + v;
+    *pw *= m;
+    *ndig += k;
+    *p += k;
+    if (k < 4) {
+      *term = (g >> (8u * k)) & 0xFFu;
+      return acc;
+    }
+  }
+  *ok = false;  // > 32 digits: generic path
+  return acc;
+}
+
+__device__ __forceinline__ FastNum fast_num(const uint8_t* lds, uint32_t p) {
+  FastNum r;
+  r.ip = r.fp = 0;
+  r.fpow = 1;
+  r.nip = 0;
+  r.neg = r.dot = false;
+  r.ok = true;
+  r.term = 0;
+  const uint32_t c0 = lds[p];
+  if (c0 == '-' || c0 == '+') {
+    r.neg = c0 == '-';
+    ++p;
+  }
+  uint64_t ipw = 1;
+  r.ip = digit_run(lds, &p, 0, &r.nip, &ipw, &r.term, &r.ok);
+  if (r.ok && r.term == '.') {
+    r.dot = true;
+    ++p;
+    uint32_t nfp = 0;
+    r.fp = digit_run(lds, &p, 0, &nfp, &r.fpow, &r.term, &r.ok);
+  }
+  r.end = p;
+  return r;
+}
+
+__device__ __forceinline__ bool is_sep(uint32_t c) {
+  return c == ' ' || c == '\t' || c == '\n' || c == '\r';
+}
+
+/*!
+ * \brief the reference StrToFloat of a FastNum (strtonum.h): integer digits
+ *  accumulated in float are exact below 2^24, so <= 7 of them equal the
+ *  integer converted once; the fraction is uint64 digits / uint64 10^n in
+ *  double, added as float.  False when the number needs the generic parser.
+ */
+__device__ __forceinline__ bool fast_float(const FastNum& n, float* out) {
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+  if (!n.ok || n.nip > 7) return false;
+  float v = static_cast<float>(static_cast<uint32_t>(n.ip));
+  if (n.dot) v += static_cast<float>(static_cast<double>(n.fp) / static_cast<double>(n.fpow));
+  *out = n.neg ? -v : v;
+  return true;
+}
+
+/*!
+ * \brief single-pass parse of a token starting at LDS offset `off` in the
+ *  common shapes: label `[+-]d[.d][:[+-]d[.d]]`, LibSVM feature `d[:[+-]d[.d]]`,
+ *  LibFM feature `d:d[:[+-]d[.d]]`, each ended by a separator.  Anything else
+ *  (exponents, signs on indices, junk bytes, over-long digit runs) returns
+ *  false and takes strtonum.h's generic ParsePair / ParseTriple; on the shapes
+ *  it accepts the results are identical.
+ */
+template <TextFormat F>
+__device__ __forceinline__ bool fast_token(const uint8_t* lds, uint32_t off, bool is_label,
+                                           int* r, uint64_t* u0, uint64_t* u1, float* f0,
+                                           float* f1) {
+  FastNum a = fast_num(lds, off);
+  if (!a.ok) return false;
+  if (is_label) {
+    if (!fast_float(a, f0)) return false;
+    if (is_sep(a.term)) {
+      *r = 1;
+      return true;
+    }
+    if (a.term != ':') return false;
+    FastNum w = fast_num(lds, a.end + 1);
+    if (!is_sep(w.term) || !fast_float(w, f1)) return false;
+    *r = 2;
+    return true;
+  }
+  if (a.neg || a.dot || a.nip == 0) return false;
+  *u0 = a.ip;
+  if (is_sep(a.term)) {
+    if (F == TextFormat::kLibFM) return false;  // r < 2: generic path flags it
+    *r = 1;
+    return true;
+  }
+  if (a.term != ':') return false;
+  if (F == TextFormat::kLibFM) {
+    FastNum b = fast_num(lds, a.end + 1);
+    if (!b.ok || b.neg || b.dot || b.nip == 0) return false;
+    *u1 = b.ip;
+    if (is_sep(b.term)) {
+      *r = 2;
+      return true;
+    }
+    if (b.term != ':') return false;
+    FastNum v = fast_num(lds, b.end + 1);
+    if (!is_sep(v.term) || !fast_float(v, f0)) return false;
+    *r = 3;
+    return true;
+  }
+  FastNum v = fast_num(lds, a.end + 1);
+  if (!is_sep(v.term) || !fast_float(v, f0)) return false;
+  *r = 2;
+  return true;
+}
+
+template <TextFormat F, typename IndexType>
+__global__ __launch_bounds__(kThreads) void k_tile_fill(const uint8_t* __restrict__ text, size_t n,
+                                                        const uint64_t* __restrict__ prefix,
+                                                        FillTarget<IndexType> out,
+                                                        MetaPartial* __restrict__ partials) {
+  __shared__ uint4 s_text[kTileBytes / 16 + 1];  // +16 B: 4-byte reads past a token
+  __shared__ uint32_t s_tok[kMaxTileTokens];
+  __shared__ uint64_t s_scan[4];
+  const uint8_t* lds = reinterpret_cast<const uint8_t*>(s_text);
+  const size_t tile0 = static_cast<size_t>(blockIdx.x) * kTileBytes;
+  const uint64_t pre = prefix[blockIdx.x];
+  const uint64_t line_base = pre >> 32;
+  const uint64_t tok_base = pre & 0xffffffffull;
+
+  // ---- stage: coalesced 16 B loads -> LDS; masks from the same registers
+  uint4 v[kSub];
+  uint32_t pc[kSub];
+#pragma unroll
+  for (int s = 0; s < kSub; ++s) {
+    const size_t pos = tile0 + s * 4096 + threadIdx.x * 16;
+    v[s] = load16(text, pos, n);
+    pc[s] = prev_byte(text, pos, v[s]);
+    s_text[s * 256 + threadIdx.x] = v[s];
+  }
+  // ---- compact the tile's tokens into s_tok in text order
+  uint64_t carry = 0;  // (lines << 32 | tokens) of earlier sub-tiles
+#pragma unroll
+  for (int s = 0; s < kSub; ++s) {
+    const size_t pos = tile0 + s * 4096 + threadIdx.x * 16;
+    uint32_t lm, tm;
+    (void)lane_masks<false>(v[s], pc[s], pos, n, &lm, &tm);
+    const uint64_t mine = (static_cast<uint64_t>(__popc(lm)) << 32) | __popc(tm);
+    uint64_t tot;
+    const uint64_t before = dev::block_excl_scan_256<uint64_t>(mine, s_scan, &tot) + carry;
+    uint32_t line = static_cast<uint32_t>(before >> 32);
+    uint32_t tok = static_cast<uint32_t>(before & 0xffffffffu);
+    uint32_t all = lm | tm;
+    while (all != 0) {
+      const int j = __ffs(all) - 1;
+      all &= all - 1;
+      const uint32_t bit = 1u << j;
+      if (lm & bit) ++line;  // lm implies tm on a regular chunk
+      if (tm & bit) {
+        const uint32_t off = static_cast<uint32_t>(s * 4096 + threadIdx.x * 16 + j);
+        const uint32_t label = (lm & bit) ? 1u : 0u;
+        s_tok[tok] = off | (line << kOffBits) | (label << (2 * kOffBits));
+        ++tok;
+      }
+    }
+    carry += tot;
+    __syncthreads();  // s_scan reuse by the next sub-tile; s_tok / s_text complete
+  }
+  const uint32_t ntok = static_cast<uint32_t>(carry & 0xffffffffu);
+
+  // ---- parse: lane i takes token i
+  uint64_t mx_index = 0, mx_field = 0;
+  bool any_value = false, any_weight = false, irregular = false, neg = false, need_w = false;
+  for (uint32_t i = threadIdx.x; i < ntok; i += kThreads) {
+    const uint32_t e = s_tok[i];
+    const uint32_t off = e & ((1u << kOffBits) - 1);
+    const uint32_t lcnt = (e >> kOffBits) & ((1u << kOffBits) - 1);
+    const bool is_label = (e >> (2 * kOffBits)) & 1u;
+    const uint64_t l = line_base + lcnt - 1;  // lcnt 0: line began in an earlier tile
+    const uint64_t k = tok_base + i;
+    const size_t gpos = tile0 + off;
+    bool bad = false;
+    int r = 0;
+    uint64_t u0 = 0, u1 = 0;
+    float f0 = 0.0f, f1 = 0.0f;
+    // every token but the tile's last ends inside the LDS tile
+    const bool in_lds = i + 1 < ntok;
+    bool done = in_lds && fast_token<F>(lds, off, is_label, &r, &u0, &u1, &f0, &f1);
+    if (!done) {
+      auto generic = [&](auto beg, auto end) {
+        if (is_label) {
+          r = data::ParsePair<float, float>(beg, end, &f0, &f1, &bad);
+        } else if constexpr (F == TextFormat::kLibSVM) {
+          IndexType idx = 0;
+          r = data::ParsePair<IndexType, float>(beg, end, &idx, &f0, &bad);
+          u0 = idx;
+        } else {
+          IndexType fid = 0, idx = 0;
+          r = data::ParseTriple<IndexType, IndexType, float>(beg, end, &fid, &idx, &f0, &bad);
+          u0 = fid;
+          u1 = idx;
+        }
+      };
+      if (in_lds) {
+        const uint8_t* lim = lds + kTileBytes;
+        generic(sep_begin(lds + off, lim), sep_end(lim));
+      } else {
+        const uint8_t* lim = text + n;
+        generic(sep_begin(text + gpos, lim), sep_end(lim));
+      }
+    }
+    if (is_label) {
+      const uint64_t row = out.row_base + l;
+      if (row < out.row_limit) {
+        out.label[row] = f0;
+        out.offset[row] = out.nnz_base + (k - l);
+        if (out.weight != nullptr) {
+          out.weight[row] = r == 2 ? f1 : 1.0f;
+        } else if (r == 2) {
+          need_w = true;
+        }
+        if (out.qid != nullptr) out.qid[row] = 0;  // qid lines take the exact path
+      } else {
+        irregular = true;
+      }
+      any_weight |= (r == 2);
+    } else {
+      const uint64_t pos = out.nnz_base + (k - l - 1);
+      if (pos >= out.nnz_limit) {
+        irregular = true;
+      } else if constexpr (F == TextFormat::kLibSVM) {
+        const IndexType idx = static_cast<IndexType>(u0);
+        out.index[pos] = idx;
+        out.value[pos] = r == 2 ? f0 : 1.0f;
+        any_value |= (r == 2);
+        if (static_cast<uint64_t>(idx) > mx_index) mx_index = idx;
+      } else {
+        if (r < 2) {
+          irregular = true;
+        } else {
+          const IndexType fid = static_cast<IndexType>(u0), idx = static_cast<IndexType>(u1);
+          out.field[pos] = fid;
+          out.index[pos] = idx;
+          out.value[pos] = r == 3 ? f0 : 1.0f;
+          any_value |= (r == 3);
+          if (static_cast<uint64_t>(idx) > mx_index) mx_index = idx;
+          if (static_cast<uint64_t>(fid) > mx_field) mx_field = fid;
+        }
+      }
+    }
+    neg |= bad;
+  }
+  unsigned fl = 0;
+  if (any_value) fl |= kFlagValue;
+  if (any_weight) fl |= kFlagWeight;
+  if (irregular) fl |= kFlagIrregular;
+  if (neg) fl |= kFlagNegIndex;
+  if (need_w) fl |= kFlagNeedWeight;
+  if (F == TextFormat::kLibFM) fl |= kFlagField;
+  dev::block_store_partial(static_cast<unsigned long long>(mx_index),
+                           static_cast<unsigned long long>(mx_field), fl, partials);
+}
+
+/*! \brief fold the per-workgroup slots into meta; closing row pointer */
+__global__ __launch_bounds__(kThreads) void k_tile_finish(const MetaPartial* __restrict__ p, int np,
+                                                          ChunkMeta* meta, uint64_t* offset,
+                                                          uint64_t row_base, uint64_t nnz_base) {
+  unsigned long long mi = 0, mf = 0;
+  unsigned fl = 0;
+  for (int i = threadIdx.x; i < np; i += kThreads) {
+    const MetaPartial q = p[i];
+    mi = q.max_index > mi ? q.max_index : mi;
+    mf = q.max_field > mf ? q.max_field : mf;
+    fl |= q.flags;
+  }
+  __shared__ unsigned long long s_mi[4], s_mf[4];
+  __shared__ unsigned s_fl[4];
+  mi = dev::wave_max(mi);
+  mf = dev::wave_max(mf);
+  fl = dev::wave_or(fl);
+  const int wid = threadIdx.x / dev::kWave;
+  if (dev::lane_id() == 0) {
+    s_mi[wid] = mi;
+    s_mf[wid] = mf;
+    s_fl[wid] = fl;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w) {
+      s_mi[0] = s_mi[w] > s_mi[0] ? s_mi[w] : s_mi[0];
+      s_mf[0] = s_mf[w] > s_mf[0] ? s_mf[w] : s_mf[0];
+      s_fl[0] |= s_fl[w];
+    }
+    meta->max_index = s_mi[0];
+    meta->max_field = s_mf[0];
+    meta->flags |= s_fl[0];
+    offset[row_base + meta->nrows] = nnz_base + meta->nnz;
+  }
+}
+}  // namespace
+
+size_t TileCount(size_t nbytes) { return (nbytes + kTileBytes - 1) / kTileBytes; }
+
+void LaunchTileCountScan(const char* text, size_t nbytes, uint64_t* tile_counts,
+                         uint32_t* tile_flags, ChunkMeta* meta, hipStream_t stream) {
+  const size_t ntiles = TileCount(nbytes);
+  if (ntiles != 0) {
+    hipLaunchKernelGGL(k_tile_count, dim3(ntiles), dim3(kThreads), 0, stream,
+                       reinterpret_cast<const uint8_t*>(text), nbytes, tile_counts, tile_flags);
+  }
+  hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kScanThreads), 0, stream, tile_counts, tile_flags,
+                     ntiles, meta);
+}
+
+template <typename IndexType>
+void LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
+                    const uint64_t* tile_prefix, const FillTarget<IndexType>& out,
+                    MetaPartial* partials, ChunkMeta* meta, hipStream_t stream) {
+  const size_t ntiles = TileCount(nbytes);
+  const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
+  if (ntiles != 0) {
+    if (format == TextFormat::kLibFM) {
+      hipLaunchKernelGGL((k_tile_fill<TextFormat::kLibFM, IndexType>), dim3(ntiles), dim3(kThreads),
+                         0, stream, t, nbytes, tile_prefix, out, partials);
+    } else {
+      hipLaunchKernelGGL((k_tile_fill<TextFormat::kLibSVM, IndexType>), dim3(ntiles),
+                         dim3(kThreads), 0, stream, t, nbytes, tile_prefix, out, partials);
+    }
+  }
+  hipLaunchKernelGGL(k_tile_finish, dim3(1), dim3(kThreads), 0, stream, partials,
+                     static_cast<int>(ntiles), meta, out.offset, out.row_base, out.nnz_base);
+}
+
+template void LaunchTileFill<uint32_t>(const char*, size_t, TextFormat, const uint64_t*,
+                                       const FillTarget<uint32_t>&, MetaPartial*, ChunkMeta*,
+                                       hipStream_t);
+template void LaunchTileFill<uint64_t>(const char*, size_t, TextFormat, const uint64_t*,
+                                       const FillTarget<uint64_t>&, MetaPartial*, ChunkMeta*,
+                                       hipStream_t);
+
+}  // namespace gpu
+}  // namespace dmlc

@@ -15,6 +15,7 @@
 #include <dmlc/gpu/device_parser.h>
 #include <dmlc/gpu/device_recordio.h>
 #include <dmlc/gpu/hip_utils.h>
+#include <dmlc/input_split_shuffle.h>
 #include <dmlc/io.h>
 #include <dmlc/logging.h>
 #include <dmlc/recordio.h>
@@ -211,8 +212,16 @@ class PyPartitionReader {
 class PyInputSplit {
  public:
   PyInputSplit(const std::string& uri, unsigned part, unsigned nparts, const std::string& type,
-               const std::string& index_uri, bool shuffle, int seed, size_t batch_size) {
+               const std::string& index_uri, bool shuffle, int seed, size_t batch_size,
+               unsigned num_shuffle_parts) {
     py::gil_scoped_release nogil;
+    if (num_shuffle_parts > 0) {
+      // coarse chunk shuffling (include/dmlc/input_split_shuffle.h)
+      CHECK(index_uri.empty()) << "num_shuffle_parts does not combine with an index file";
+      s_.reset(InputSplitShuffle::Create(uri.c_str(), part, nparts, type.c_str(),
+                                         num_shuffle_parts, seed));
+      return;
+    }
     s_.reset(index_uri.empty()
                  ? InputSplit::Create(uri.c_str(), part, nparts, type.c_str())
                  : InputSplit::Create(uri.c_str(), index_uri.c_str(), part, nparts, type.c_str(),
@@ -584,10 +593,10 @@ PYBIND11_MODULE(_dmlc, m) {
       .def("partition_bytes", &PyPartitionReader::PartitionBytes);
   py::class_<PyInputSplit>(m, "InputSplit")
       .def(py::init<const std::string&, unsigned, unsigned, const std::string&,
-                    const std::string&, bool, int, size_t>(),
+                    const std::string&, bool, int, size_t, unsigned>(),
            py::arg("uri"), py::arg("part") = 0, py::arg("nparts") = 1, py::arg("type") = "text",
            py::arg("index_uri") = "", py::arg("shuffle") = false, py::arg("seed") = 0,
-           py::arg("batch_size") = 256)
+           py::arg("batch_size") = 256, py::arg("num_shuffle_parts") = 0)
       .def("next_record", &PyInputSplit::NextRecord)
       .def("next_chunk", &PyInputSplit::NextChunk)
       .def("next_batch", &PyInputSplit::NextBatch)

@@ -79,6 +79,15 @@ def test_libsvm_negative_index_raises(tmp_path):
         list(data.iter_blocks(p, type="libsvm"))
 
 
+def test_libsvm_single_pass_token_path_matches_grammar(tmp_path):
+    """Tokens at the edge of the single-pass `digits[:number]` fast path (it must
+    hand every other shape to the general ParsePair grammar unchanged)."""
+    text = ("1 12.5:3 5: 5:abc +3:1 1e2:3 7:1.5.3 4:-2 9:.5x 3x:2 8:1e+2 6:0.5:9 2\n"
+            "0 10 11:7 12:-.25 13:+1.5e-3 4294967297:1 14:1e40\n")
+    p = write(str(tmp_path / "t.libsvm"), text)
+    check_libsvm(host_rows(p, "libsvm"), pyref.parse_libsvm(text))
+
+
 @pytest.mark.parametrize("nthread", [1, 3, 8])
 def test_libsvm_synthetic_matches_oracle(tmp_path, nthread):
     p = str(tmp_path / "s.libsvm")

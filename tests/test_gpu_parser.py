@@ -198,3 +198,109 @@ def test_negative_index_raises_on_gpu(tmp_path):
         f.write("1 -3:1\n")
     with pytest.raises(Exception):
         data.GPUParser(p).parse_all()
+
+
+@pytest.mark.parametrize("zero_copy", [0, 1])
+def test_hbm_epoch_cache_replay_and_resume(tmp_path, zero_copy):
+    """hbm_cache=1: epoch 1 streams and keeps the text in HBM; later epochs
+    (parse_all and streaming next) replay from HBM with identical output, and a
+    resume cursor that is a chunk boundary replays from there."""
+    d = tmp_path / "c"
+    d.mkdir()
+    for i in range(3):
+        data.write_synthetic(str(d / f"p{i}.libsvm"), i * 1500, (i + 1) * 1500, seed=31,
+                             weight_every=4 if i == 2 else 0)
+    c = cpu_rows(str(d), "libsvm")
+    gp = data.GPUParser(str(d), chunk_bytes=64 * 1024, zero_copy=zero_copy, hbm_cache=1)
+    csr = data.DeviceCSR()
+    for _ in range(3):
+        gp.before_first()
+        csr.clear()
+        gp.parse_all(csr)
+        assert_same(pyref.concat_blocks([csr.to_host()]), c)
+    gp.before_first()
+    head = [gp.value_to_host() for _ in range(2) if gp.next()]
+    cursor = gp.tell()
+    assert 0 < cursor < gp.partition_bytes
+    rest = []
+    while gp.next():
+        rest.append(gp.value_to_host())
+    assert_same(pyref.concat_blocks(head + rest), c)
+    gp.seek(cursor)
+    again = []
+    while gp.next():
+        again.append(gp.value_to_host())
+    assert_same(pyref.concat_blocks(head + again), c)
+
+
+def test_weight_column_first_seen_in_a_late_chunk(tmp_path):
+    """The tile fill learns about weights only when it meets one: the column
+    is allocated then (earlier rows 1.0) and that chunk is written again."""
+    p = str(tmp_path / "w.libsvm")
+    data.write_synthetic(p, 0, 3000, seed=17)
+    with open(p, "a") as f:
+        f.write("1:0.25 4:1 9:2\n0 3:1\n1:3.5 1:1\n")
+    g = gpu_rows(p, "libsvm", chunk_bytes=32 * 1024)
+    c = cpu_rows(p, "libsvm")
+    assert_same(g, c)
+    assert c["weight"][-3] == np.float32(0.25) and c["weight"][0] == 1.0
+
+
+def test_tokens_at_tile_and_window_edges(tmp_path):
+    """Tokens of every length 1..70 placed so they straddle the 8 KiB tile, the
+    64 B LDS halo and the 32 B parse window; the last line has no newline."""
+    rng = np.random.default_rng(3)
+    lines = []
+    for r in range(3000):
+        n = int(rng.integers(1, 12))
+        toks = []
+        for _ in range(n):
+            L = int(rng.integers(1, 70))
+            digits = "".join(str(int(x)) for x in rng.integers(0, 10, L))
+            toks.append(f"{int(rng.integers(0, 1 << 20))}:0.{digits}")
+        lines.append(f"{r % 3} " + " ".join(toks))
+    p = str(tmp_path / "edge.libsvm")
+    with open(p, "w") as f:
+        f.write("\n".join(lines))
+    for chunk in (8192, 40 * 1024, 1 << 20):
+        assert_same(gpu_rows(p, "libsvm", chunk_bytes=chunk), cpu_rows(p, "libsvm"))
+
+
+def test_token_shape_fuzz_matches_cpu(tmp_path):
+    """Labels / features in every shape the single-pass SWAR path accepts and
+    many it must hand to the generic grammar (signs, exponents, second dots,
+    junk bytes, empty values, long digit runs, weights)."""
+    rng = np.random.default_rng(12)
+    labels = ["1", "0", "-1", "+1", "0.5", "-0", "3.25", ".5", "1:0.25", "-1:2", "2:-0.5",
+              "1e2", "12345678", "1.5e-1:3", "7:", "1:2:3"]
+    values = ["1", "0.5", "-2", "+3.75", ".25", "5.", "", "1e3", "2.5E-2", "1.5.3", "3x",
+              "123456789.5", "0.000000000000000000000001", "-.5", "7:9", "12345678", "1234567"]
+    lines = []
+    for r in range(6000):
+        toks = [labels[int(rng.integers(len(labels)))]]
+        for _ in range(int(rng.integers(0, 9))):
+            idx = str(int(rng.integers(0, 1 << 31)))
+            if rng.random() < 0.1:
+                toks.append(idx)
+            else:
+                toks.append(idx + ":" + values[int(rng.integers(len(values)))])
+        lines.append(" ".join(toks))
+    p = str(tmp_path / "fuzz.libsvm")
+    with open(p, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    for chunk in (16 * 1024, 1 << 20):
+        assert_same(gpu_rows(p, "libsvm", chunk_bytes=chunk), cpu_rows(p, "libsvm"))
+    # the same for LibFM triples
+    fm = []
+    for r in range(3000):
+        toks = [labels[int(rng.integers(len(labels)))]]
+        for _ in range(int(rng.integers(1, 7))):
+            t = f"{int(rng.integers(0, 50))}:{int(rng.integers(0, 1 << 20))}"
+            if rng.random() < 0.85:
+                t += ":" + values[int(rng.integers(len(values)))]
+            toks.append(t)
+        fm.append(" ".join(toks))
+    q = str(tmp_path / "fuzz.libfm")
+    with open(q, "w") as f:
+        f.write("\n".join(fm) + "\n")
+    assert_same(gpu_rows(q, "libfm", chunk_bytes=16 * 1024), cpu_rows(q, "libfm"), field=True)
