@@ -33,7 +33,7 @@ CPU_SRCS := src/logging.cc src/fault.cc src/io.cc src/recordio.cc src/data.cc sr
   src/io/recordio_split.cc src/io/remote_filesys.cc \
   src/io/shard_reader.cc src/io/http.cc src/io/s3_filesys.cc src/io/azure_filesys.cc \
   src/io/hdfs_filesys.cc \
-  src/gpu/runtime.cc src/gpu/device_parser.cc src/gpu/device_recordio.cc \
+  src/gpu/runtime.cc src/gpu/device_parser.cc src/gpu/device_recordio.cc src/gpu/device_row_iter.cc \
   src/dist/tracker_client.cc src/dist/communicator.cc
 HIP_SRCS := $(wildcard src/gpu/*.hip)
 
@@ -115,8 +115,13 @@ $(BUILD)/dmlc_parameter_example: examples/parameter.cc $(LIB) $(HEADERS)
 	$(CXX) $(CXXFLAGS_BASE) $< -o $@ -L$(LIBDIR) -ldmlc -Wl,-rpath,$(abspath $(LIBDIR)) \
 	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64
 
+$(BUILD)/dmlc_gpu_api_check: tools/dmlc_gpu_api_check.cc $(LIB) $(HEADERS)
+	@mkdir -p $(BUILD)
+	$(CXX) $(CXXFLAGS_BASE) $< -o $@ -L$(LIBDIR) -ldmlc -Wl,-rpath,$(abspath $(LIBDIR)) \
+	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64
+
 tools: $(BUILD)/dmlc_parameter_example $(BUILD)/dmlc_gen $(BUILD)/dmlc_bench_cpu $(BUILD)/dmlc_recordio_dist $(BUILD)/dmlc_fs \
-  $(BUILD)/dmlc_recordio
+  $(BUILD)/dmlc_recordio $(BUILD)/dmlc_gpu_api_check
 
 clean:
 	rm -rf $(BUILD) $(LIB) $(PYMOD)

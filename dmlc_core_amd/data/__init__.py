@@ -19,18 +19,34 @@ __all__ = ["Parser", "RowBlockIter", "GPUParser", "DeviceCSR", "csr_to_torch", "
 write_synthetic = _dmlc.write_synthetic
 
 
+def _host_blocks_uri(uri: str) -> str:
+    """``?device=gpu`` URIs tokenise on the MI355X; the numpy views returned by
+    value() need host blocks, so ``to_host=1`` is added (device-resident blocks
+    are served by GPUParser / DeviceCSR instead)."""
+    q = uri.split("#", 1)[0]
+    if "?" not in q:
+        return uri
+    args = dict(kv.split("=", 1) for kv in q.split("?", 1)[1].split("&") if "=" in kv)
+    if not args.get("device", "").startswith("gpu") or "to_host" in args:
+        return uri
+    head, _, tail = uri.partition("#")
+    return head + "&to_host=1" + ("#" + tail if tail else "")
+
+
 def Parser(uri: str, part: int = 0, nparts: int = 1, type: str = "auto",  # noqa: N802,A002
            index64: bool = False):
-    """CPU streaming parser (LibSVM / LibFM / CSV), reference Parser<I>::Create."""
+    """Streaming parser (LibSVM / LibFM / CSV), reference Parser<I>::Create;
+    ``?device=gpu`` selects the HIP tokeniser (blocks copied back to the host)."""
     cls = _dmlc.Parser64 if index64 else _dmlc.Parser
-    return cls(uri, part, nparts, type)
+    return cls(_host_blocks_uri(uri), part, nparts, type)
 
 
 def RowBlockIter(uri: str, part: int = 0, nparts: int = 1, type: str = "auto",  # noqa: N802,A002
                  index64: bool = False):
-    """CPU in-memory (or ``#cache`` paged) iterator, reference RowBlockIter<I>::Create."""
+    """In-memory (or ``#cache`` paged) iterator, reference RowBlockIter<I>::Create;
+    ``?device=gpu`` parses the whole shard on the MI355X (DeviceRowIter)."""
     cls = _dmlc.RowBlockIter64 if index64 else _dmlc.RowBlockIter
-    return cls(uri, part, nparts, type)
+    return cls(_host_blocks_uri(uri), part, nparts, type)
 
 
 def iter_blocks(uri: str, part: int = 0, nparts: int = 1, type: str = "auto",  # noqa: A002

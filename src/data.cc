@@ -8,6 +8,8 @@
  * BasicRowIter (:87-107), uint32/uint64 specialisations (:112-147), registry
  * entries (:150-158).
  * Differences: CSV is registered for uint64 as well and threaded (§7.4 #4);
+ * `?device=gpu[:k]` routes both factories to the MI355X path
+ * (src/gpu/device_row_iter.cc: GPUParser per chunk, DeviceRowIter whole shard);
  * `?nthread=N` is honoured; RowBlockIter keeps `?k=v` args when a cache file
  * is used (the reference dropped them).
  */
@@ -20,6 +22,7 @@
 
 #include "./data/basic_row_iter.h"
 #include "./data/csv_parser.h"
+#include "./data/device_route.h"
 #include "./data/disk_row_iter.h"
 #include "./data/libfm_parser.h"
 #include "./data/libsvm_parser.h"
@@ -72,6 +75,10 @@ inline Parser<IndexType>* CreateParser_(const char* uri_, unsigned part_index,
     auto it = spec.args.find("format");
     ptype = it != spec.args.end() ? it->second : "libsvm";
   }
+  if (RoutesToDevice(spec.args)) {
+    CHECK(DeviceRoute<IndexType>::parser != nullptr) << "device=gpu: the GPU path is not built in";
+    return DeviceRoute<IndexType>::parser(spec.uri, spec.args, part_index, num_parts, ptype);
+  }
   const ParserFactoryReg<IndexType>* e = Registry<ParserFactoryReg<IndexType>>::Find(ptype);
   if (e == nullptr) {
     LOG(FATAL) << "Unknown data type " << ptype;
@@ -83,6 +90,15 @@ template <typename IndexType>
 inline RowBlockIter<IndexType>* CreateIter_(const char* uri_, unsigned part_index,
                                             unsigned num_parts, const char* type) {
   io::URISpec spec(uri_, part_index, num_parts);
+  if (RoutesToDevice(spec.args)) {
+    std::string ptype = type;
+    if (ptype == "auto") {
+      auto it = spec.args.find("format");
+      ptype = it != spec.args.end() ? it->second : "libsvm";
+    }
+    CHECK(DeviceRoute<IndexType>::iter != nullptr) << "device=gpu: the GPU path is not built in";
+    return DeviceRoute<IndexType>::iter(spec.uri, spec.args, part_index, num_parts, ptype);
+  }
   std::string parser_uri = uri_;
   const size_t hash = parser_uri.find('#');
   if (hash != std::string::npos) parser_uri = parser_uri.substr(0, hash);
@@ -95,6 +111,17 @@ inline RowBlockIter<IndexType>* CreateIter_(const char* uri_, unsigned part_inde
 }
 
 DMLC_REGISTER_PARAMETER(CSVParserParam);
+
+bool RoutesToDevice(const std::map<std::string, std::string>& args) {
+  auto it = args.find("device");
+  return it != args.end() && it->second.compare(0, 3, "gpu") == 0;
+}
+template <typename I>
+typename DeviceRoute<I>::ParserFn DeviceRoute<I>::parser = nullptr;
+template <typename I>
+typename DeviceRoute<I>::IterFn DeviceRoute<I>::iter = nullptr;
+template struct DeviceRoute<uint32_t>;
+template struct DeviceRoute<uint64_t>;
 }  // namespace data
 
 template <>

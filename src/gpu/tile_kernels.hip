@@ -228,7 +228,7 @@ __device__ __forceinline__ SepIter<Ptr> sep_end(Ptr limit) {
 /*! \brief 4 bytes starting at byte p of an LDS buffer (two aligned dword reads) */
 __device__ __forceinline__ uint32_t lds_u32_at(const uint8_t* lds, uint32_t p) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(lds + (p & ~3u));
-  return __builtin_amdgcn_alignbyte(w[1], w[0], (p & 3u) * 8u);
+  return __builtin_amdgcn_alignbyte(w[1], w[0], p & 3u);  // byte shift
 }
 
 __device__ __forceinline__ uint32_t pow10_small(uint32_t k) {
