@@ -63,9 +63,14 @@ struct DeviceParserConfig {
    *  with no host I/O and no PCIe traffic.
    */
   bool hbm_cache{false};
+  /*!
+   * \brief ParseAll over the HBM cache parses adjacent cached chunks together,
+   *  up to this many bytes per kernel pass (`?replay_chunk_mb=`)
+   */
+  size_t replay_chunk_bytes{1UL << 30};
   /*! \brief apply `?k=v` overrides (chunk_mb, pinned_slots, device_slots,
    *  read_threads, device, format, label_column, weight_column, delimiter,
-   *  fast_path, zero_copy, hbm_cache) */
+   *  fast_path, zero_copy, hbm_cache, replay_chunk_mb) */
   void Update(const std::map<std::string, std::string>& args);
 };
 

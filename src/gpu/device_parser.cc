@@ -6,15 +6,16 @@
  *   copy stream    : wait(parsed[d]) -> H2D(text[d]) -> record(copied[d])
  *   compute stream : wait(copied[d]) -> parse -> record(parsed[d])
  *
- * LibSVM / LibFM chunks take the token-parallel fast path
- * (token_kernels.hip: T1a count, T1b emit, T2 row info, K3 scan, T3 fill, one
- * lane per token).  A chunk the fast path flags as irregular (qid tokens,
- * digit-less tokens, label-less lines), and every CSV chunk, is parsed by the
- * exact wave-per-line kernels (text_kernels.hip: K1 line index, K2 count, K3
- * scan, K4 fill).  Both write bit-identical CSR for regular input.
- * The host reads three tiny results per chunk (counts, sizes, flags); the
- * H2D of the next chunks is queued before the current chunk is parsed, so
- * PCIe transfers overlap the kernels and the reader thread fills pinned slots
+ * LibSVM / LibFM chunks take the LDS-staged tile parser (tile_kernels.hip:
+ * C1 count, C2 scan, C3 fill, C4 finish; lane per token, SWAR number decode).
+ * A chunk it flags as irregular (qid tokens, digit-less tokens, label-less
+ * lines, control bytes), and every CSV chunk, is parsed by the exact
+ * wave-per-line kernels (text_kernels.hip: K1 line index, K2 count, K3 scan,
+ * K4 fill).  Both write bit-identical CSR for regular input.
+ * The tile kernels write the chunk's sizes and flags into mapped pinned
+ * memory (two stream synchronisations per chunk, no D2H copies); the H2D of
+ * the next chunks is queued before the current chunk is parsed, so PCIe
+ * transfers overlap the kernels and the reader thread fills pinned slots
  * further ahead.
  */
 #include <dmlc/gpu/device_parser.h>
@@ -70,6 +71,8 @@ void DeviceParserConfig::Update(const std::map<std::string, std::string>& args) 
       delimiter = v[0];
     } else if (k == "fast_path") {
       fast_path = v != "0" && v != "false";
+    } else if (k == "replay_chunk_mb") {
+      replay_chunk_bytes = static_cast<size_t>(std::atof(v.c_str()) * (1 << 20));
     } else if (k == "hbm_cache") {
       hbm_cache = v != "0" && v != "false";
     } else if (k == "zero_copy") {
@@ -88,6 +91,8 @@ namespace {
 /*! \brief a filled pinned host slot */
 struct HostSlot {
   PinnedBuffer buf;
+  /*! \brief usable bytes of buf (grows for records longer than chunk_bytes) */
+  size_t cap{0};
   size_t size{0};
   /*! \brief partition cursor after this chunk (ShardReader::Tell) */
   size_t end_pos{0};
@@ -138,6 +143,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     tflags_.Reserve(TileCount(cfg_.chunk_bytes) * sizeof(uint32_t));
     meta_.Reserve(2 * sizeof(ChunkMeta));
     hmeta_.Reserve(2 * sizeof(ChunkMeta));
+    hmap_.Reserve(sizeof(ChunkMeta), /*mapped=*/true);
     slots_.Reserve(std::max<size_t>(kMaxPartialBlocks, TileCount(cfg_.chunk_bytes)) *
                    sizeof(MetaPartial));
     iter_.set_max_capacity(static_cast<size_t>(cfg_.pinned_slots));
@@ -222,8 +228,15 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     ScopedRange range("DeviceParser::ParseAll");
     out->device_ = device_;
     ResetEpoch();
-    while (ProcessOne(out, /*append=*/true)) {
+    merge_replay_ = true;
+    try {
+      while (ProcessOne(out, /*append=*/true)) {
+      }
+    } catch (...) {
+      merge_replay_ = false;
+      throw;
     }
+    merge_replay_ = false;
     FinishEpoch(out);
   }
 
@@ -254,9 +267,19 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
           if (*dptr == nullptr) {
             *dptr = new HostSlot();
             (*dptr)->buf.Reserve(cap + kTextPadBytes);
+            (*dptr)->cap = cap;
           }
           ScopedRange r("pinned_fill");
-          (*dptr)->size = reader->Fill((*dptr)->buf.template get<char>(), cap);
+          HostSlot* slot = *dptr;
+          size_t n = reader->Fill(slot->buf.template get<char>(), slot->cap);
+          while (n == io::ShardReader::kNeedMore) {
+            // a record longer than the slot: grow it (the reader kept the bytes)
+            slot->cap = reader->NeedCapacity();
+            slot->buf.Free();
+            slot->buf.Reserve(slot->cap + kTextPadBytes);
+            n = reader->Fill(slot->buf.template get<char>(), slot->cap);
+          }
+          (*dptr)->size = n;
           (*dptr)->end_pos = reader->Tell();
           return (*dptr)->size != 0;
         },
@@ -276,7 +299,17 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       while (static_cast<int>(inflight_.size()) < cfg_.device_slots &&
              replay_idx_ < cached_.size()) {
         const CachedChunk& c = cached_[replay_idx_++];
-        inflight_.push_back(Inflight{nullptr, -1, c.size, c.end_pos, arena_->get<char>() + c.off});
+        size_t size = c.size, end_pos = c.end_pos;
+        // ParseAll over resident text: adjacent cached chunks are parsed as
+        // one larger chunk (fewer launches and host round trips per byte)
+        while (merge_replay_ && replay_idx_ < cached_.size() &&
+               cached_[replay_idx_].off == c.off + size &&
+               size + cached_[replay_idx_].size <= cfg_.replay_chunk_bytes) {
+          size += cached_[replay_idx_].size;
+          end_pos = cached_[replay_idx_].end_pos;
+          ++replay_idx_;
+        }
+        inflight_.push_back(Inflight{nullptr, -1, size, end_pos, arena_->get<char>() + c.off});
       }
       reader_done_ = replay_idx_ == cached_.size();
       return;
@@ -312,6 +345,13 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       }
       const int d = next_dslot_;
       next_dslot_ = (next_dslot_ + 1) % cfg_.device_slots;
+      if (size + kTextPadBytes > dtext_[d]->bytes()) {
+        // a chunk longer than chunk_bytes (one long record): grow this device
+        // slot once the parse that last used it has finished
+        parsed_[d]->Synchronize();
+        dtext_[d].reset(new DeviceBuffer(size + kTextPadBytes));
+        DMLC_HIP_CHECK(hipMemset(dtext_[d]->get(), 0, size + kTextPadBytes));
+      }
       char* dst = dtext_[d]->template get<char>();
       if (caching_) {
         // first pass of an hbm_cache epoch: the chunk lands in its arena slot
@@ -356,6 +396,16 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     acc_flags_ = 0;
   }
 
+  /*! \brief the ChunkMeta a kernel wrote into mapped pinned memory (synchronises) */
+  ChunkMeta WaitMapped(const ChunkMeta* hm) {
+    const double t0 = GetTime();
+    compute_->Synchronize();
+    stats_.wait_gpu_sec += GetTime() - t0;
+    ChunkMeta v;
+    std::memcpy(&v, const_cast<const ChunkMeta*>(hm), sizeof(v));
+    return v;
+  }
+
   /*! \brief device -> host copy of `bytes` at `src` (synchronises the compute stream) */
   template <typename T>
   T ReadBack(const void* src) {
@@ -369,15 +419,19 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     return v;
   }
 
-  void EnsureLineBuffers(size_t nlines, size_t ntok) {
+  /*! \brief per-chunk scratch for a chunk of nbytes (chunks may exceed chunk_bytes) */
+  void EnsureScratch(size_t nbytes) {
+    const size_t tiles = TileCount(nbytes);
+    tcounts_.Reserve(tiles * sizeof(uint64_t));
+    tflags_.Reserve(tiles * sizeof(uint32_t));
+    slots_.Reserve(std::max<size_t>(kMaxPartialBlocks, tiles) * sizeof(MetaPartial));
+    tiles_.Reserve(LineIndexTiles(nbytes) * sizeof(uint64_t));
+  }
+
+  void EnsureLineBuffers(size_t nlines) {
     lines_.Reserve((nlines + 1) * sizeof(uint32_t));
-    first_tok_.Reserve((nlines + 1) * sizeof(uint32_t));
     info_.Reserve((nlines + 1) * sizeof(uint64_t));
     partials_.Reserve((ScanPartials(nlines) + 2) * sizeof(uint64_t));
-    if (ntok != 0) {
-      tok_pos_.Reserve(ntok * sizeof(uint32_t));
-      tok_line_.Reserve(ntok * sizeof(uint32_t));
-    }
   }
 
   /*! \brief grow the output for this chunk and build the fill target */
@@ -422,8 +476,10 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
                  size_t nnz_base, ChunkPlan* plan) {
     hipStream_t s = compute_->get();
     ChunkMeta* dmeta = meta_.get<ChunkMeta>();
-    LaunchTileCountScan(text, nbytes, tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(), dmeta, s);
-    const ChunkMeta sizes = ReadBack<ChunkMeta>(dmeta);
+    ChunkMeta* hm = hmap_.get<ChunkMeta>();
+    LaunchTileCountScan(text, nbytes, tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(), dmeta, hm,
+                        s);
+    const ChunkMeta sizes = WaitMapped(hm);
     AfterFirstSync();
     if (sizes.flags & kFlagIrregular) return false;
     plan->nlines = sizes.nlines;
@@ -433,8 +489,8 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     for (;;) {
       FillTarget<IndexType> tgt = PrepareOutput(out, row_base, nnz_base, *plan, need_weight, nbytes);
       LaunchTileFill<IndexType>(text, nbytes, tcfg_.format, tcounts_.get<uint64_t>(), tgt,
-                                slots_.get<MetaPartial>(), dmeta, s);
-      ChunkMeta m = ReadBack<ChunkMeta>(dmeta);
+                                slots_.get<MetaPartial>(), dmeta, hm, s);
+      ChunkMeta m = WaitMapped(hm);
       if (m.flags & kFlagIrregular) return false;
       if ((m.flags & kFlagNeedWeight) && !need_weight) {
         // first weighted row of the epoch: allocate the column (earlier rows
@@ -459,7 +515,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     LaunchLineCount(text, nbytes, tiles_.get<uint64_t>(), dmeta, s);
     plan->nlines = ReadBack<ChunkMeta>(dmeta).nlines;
     if (!first_sync_done) AfterFirstSync();
-    EnsureLineBuffers(plan->nlines, 0);
+    EnsureLineBuffers(plan->nlines);
     LaunchLineEmit(text, nbytes, tiles_.get<uint64_t>(), lines_.get<uint32_t>(), s);
     LaunchTextCount(text, nbytes, lines_.get<uint32_t>(), plan->nlines, tcfg_,
                     info_.get<uint64_t>(), slots_.get<MetaPartial>(), dmeta, s);
@@ -509,6 +565,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     cur_slot_ = cur.slot;
     const size_t nbytes = cur.size;
     const char* text = cur.text;
+    EnsureScratch(nbytes);
     hipStream_t s = compute_->get();
     ScopedRange range("parse_chunk");
     if (cur.d >= 0) DMLC_HIP_CHECK(hipStreamWaitEvent(s, copied_[cur.d]->get(), 0));
@@ -573,12 +630,14 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   std::unique_ptr<Stream> compute_, copy_;
   std::vector<std::unique_ptr<DeviceBuffer>> dtext_;
   std::vector<std::unique_ptr<Event>> copied_, parsed_;
-  DeviceBuffer tiles_, lines_, first_tok_, tok_pos_, tok_line_, info_, partials_, meta_;
+  DeviceBuffer tiles_, lines_, info_, partials_, meta_;
   /*! \brief tile parser scratch: per-tile counts (scanned in place) and flags */
   DeviceBuffer tcounts_, tflags_;
   /*! \brief per-workgroup reduction slots (MetaPartial) */
   DeviceBuffer slots_;
   PinnedBuffer hmeta_;
+  /*! \brief mapped pinned ChunkMeta the tile kernels write directly */
+  PinnedBuffer hmap_;
   ThreadedIter<HostSlot> iter_;
   std::unique_ptr<ZeroCopySource> zc_;
   std::deque<Inflight> inflight_;
@@ -586,7 +645,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   std::unique_ptr<DeviceBuffer> arena_;
   size_t arena_bytes_{0}, arena_fill_{0}, replay_idx_{0};
   std::vector<CachedChunk> cached_;
-  bool caching_{false}, cache_complete_{false}, replay_{false};
+  bool caching_{false}, cache_complete_{false}, replay_{false}, merge_replay_{false};
   HostSlot* cur_slot_{nullptr};
   /*! \brief resume cursor (partition offset after the last delivered chunk) */
   size_t cursor_{0};

@@ -174,6 +174,12 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
         n = blob.size;
       }
       CHECK_EQ(n % 4, 0U) << "RecordIO chunk not 4-byte aligned";
+      if (n + 16 > s.text.bytes()) {
+        // a zero-copy piece holding one record longer than chunk_bytes
+        DMLC_HIP_CHECK(hipStreamSynchronize(copy_.get()));
+        DMLC_HIP_CHECK(hipStreamSynchronize(compute_.get()));
+        s.text.Reserve(n + 16);
+      }
       if (s.used) DMLC_HIP_CHECK(hipStreamWaitEvent(copy_.get(), s.parsed.get(), 0));
       DMLC_HIP_CHECK(hipMemcpyAsync(s.text.get<char>(), src, n, hipMemcpyHostToDevice, copy_.get()));
       s.copied.Record(copy_.get());

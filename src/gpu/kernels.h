@@ -143,32 +143,8 @@ void LaunchTextFill(const char* text, size_t nbytes, const uint32_t* line_starts
 /*! \brief offset[row_end] = nnz_end (closing row pointer of a chunk) */
 void LaunchCloseOffsets(uint64_t* offset, uint64_t row_end, uint64_t nnz_end, hipStream_t stream);
 
-// ------------------- token-parallel fast path (LibSVM/LibFM) -------------------
+/*! \brief a chunk the tile parser cannot take (the exact per-line kernels re-parse it) */
 constexpr unsigned kFlagIrregular = 1024u;
-/*!
- * \brief T1a: per-tile (line starts << 32 | token starts), scanned;
- *  *packed_total = (nlines << 32) | ntok.  tile_scratch as LaunchLineCount.
- */
-void LaunchTokenCount(const char* text, size_t nbytes, uint64_t* tile_scratch,
-                      uint64_t* packed_total, hipStream_t stream);
-/*! \brief T1b: line_starts / line_first_tok [nlines], tok_pos / tok_line [ntok] */
-void LaunchTokenEmit(const char* text, size_t nbytes, const uint64_t* tile_scratch,
-                     uint32_t* line_starts, uint32_t* line_first_tok, uint32_t* tok_pos,
-                     uint32_t* tok_line, hipStream_t stream);
-/*! \brief T2: line_info[i] = (tokens > 0) << 32 | (tokens - 1) */
-void LaunchRowInfo(const uint32_t* line_first_tok, size_t nlines, size_t ntok,
-                   uint64_t* line_info, hipStream_t stream);
-/*!
- * \brief T3: one lane per token; line_info must hold the scanned prefixes.
- *  Sets kFlagIrregular when a line breaks the label/feature assumption
- *  (the caller then re-parses the chunk with the exact per-line kernels).
- *  out.weight must be allocated (weights are discovered here).
- */
-template <typename IndexType>
-void LaunchTokenFill(const char* text, size_t nbytes, TextFormat format, const uint32_t* tok_pos,
-                     const uint32_t* tok_line, size_t ntok, const uint32_t* line_first_tok,
-                     const uint64_t* line_info, const FillTarget<IndexType>& out, uint64_t nrows,
-                     uint64_t nnz, MetaPartial* partials, ChunkMeta* meta, hipStream_t stream);
 
 // --------------- LDS-staged tile parser (LibSVM/LibFM fast path) ---------------
 /*! \brief bytes of text per workgroup of the tile kernels */
@@ -180,11 +156,14 @@ size_t TileCount(size_t nbytes);
 /*!
  * \brief C1 + C2: per-tile (line starts << 32 | token starts) and irregular
  *  flags, exclusive-scanned in place; meta receives nlines, nrows = nlines,
- *  nnz = tokens - lines, flags (kFlagIrregular) and zeroed maxima.
+ *  nnz = tokens - lines, flags (kFlagIrregular) and zeroed maxima; host_meta
+ *  (mapped pinned memory, may be null) receives a copy the host reads after
+ *  synchronising the stream, without a device-to-host copy.
  *  tile_counts / tile_flags need TileCount(nbytes) entries.
  */
 void LaunchTileCountScan(const char* text, size_t nbytes, uint64_t* tile_counts,
-                         uint32_t* tile_flags, ChunkMeta* meta, hipStream_t stream);
+                         uint32_t* tile_flags, ChunkMeta* meta, ChunkMeta* host_meta,
+                         hipStream_t stream);
 /*!
  * \brief C3 + C4: parse every token of a regular chunk into out using the
  *  scanned tile prefixes; merges max index / field and flags into meta and
@@ -194,7 +173,8 @@ void LaunchTileCountScan(const char* text, size_t nbytes, uint64_t* tile_counts,
 template <typename IndexType>
 void LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
                     const uint64_t* tile_prefix, const FillTarget<IndexType>& out,
-                    MetaPartial* partials, ChunkMeta* meta, hipStream_t stream);
+                    MetaPartial* partials, ChunkMeta* meta, ChunkMeta* host_meta,
+                    hipStream_t stream);
 
 // ----------------------------- RecordIO (K7) -----------------------------
 /*! \brief error bits reported by the RecordIO kernels */

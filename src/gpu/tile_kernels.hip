@@ -46,10 +46,35 @@ constexpr unsigned kOffBits = 13;                            // tile offset < 81
 constexpr unsigned kMaxTileTokens = static_cast<unsigned>(kTileBytes / 2);
 static_assert(kTileBytes == 8192, "entry packing assumes 8 KiB tiles");
 
-__device__ __forceinline__ uint32_t sep_masks(uint4 v, uint32_t* eol_out) {
-  const uint32_t eol = dev::byte_eq_mask(v, '\n') | dev::byte_eq_mask(v, '\r');
-  *eol_out = eol;
-  return eol | dev::byte_eq_mask(v, ' ') | dev::byte_eq_mask(v, '\t');
+/*! \brief the high bit of each byte of z (z & 0x80808080) as a 4-bit mask */
+__device__ __forceinline__ uint32_t gather_hi(uint32_t z) {
+  return (((z >> 7) & 0x01010101u) * 0x01020408u) >> 24;
+}
+
+/*!
+ * \brief byte classes of 16 bytes, branch-free SWAR (no cross-byte carries):
+ *  sep = byte <= 0x20, eol = sep with (byte & 6) != 0, ctl = byte < 0x20.
+ *  On text whose control bytes are only \t \n \r (verified per chunk by
+ *  k_tile_count through `ctl`), sep is exactly {' ', \t, \n, \r} and eol
+ *  exactly {\n, \r}.
+ */
+__device__ __forceinline__ void classify16(uint4 v, uint32_t* sep, uint32_t* eol, uint32_t* ctl) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t s = 0, e = 0, c = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t x = w[i];
+    const uint32_t lo7 = x & 0x7F7F7F7Fu;
+    const uint32_t le20 = ~((lo7 + 0x5F5F5F5Fu) | x) & 0x80808080u;    // <= 0x20
+    const uint32_t lt20 = ~((lo7 + 0x60606060u) | x) & 0x80808080u;    // <  0x20
+    const uint32_t b6 = ((x & 0x06060606u) + 0x7E7E7E7Eu) & 0x80808080u;  // (b & 6) != 0
+    s |= gather_hi(le20) << (4 * i);
+    e |= gather_hi(le20 & b6) << (4 * i);
+    c |= gather_hi(lt20) << (4 * i);
+  }
+  *sep = s;
+  *eol = e;
+  *ctl = c;
 }
 
 __device__ __forceinline__ bool num_start(uint32_t c) {
@@ -59,13 +84,15 @@ __device__ __forceinline__ bool num_start(uint32_t c) {
 /*!
  * \brief line-start / token-start masks of the 16 bytes v at chunk offset pos;
  *  pc = the byte before pos ('\n' at 0).  Bytes at or past n are invalid.
- *  Returns true when the lane saw an irregular construct.
+ *  kCheck: also return true when the lane saw an irregular construct (a
+ *  control byte other than \t \n \r, a line starting with a blank, a token
+ *  starting outside [0-9+-.]).
  */
 template <bool kCheck>
 __device__ __forceinline__ bool lane_masks(uint4 v, uint32_t pc, size_t pos, size_t n,
                                            uint32_t* lm, uint32_t* tm) {
-  uint32_t eol;
-  const uint32_t sep = sep_masks(v, &eol);
+  uint32_t sep, eol, ctl;
+  classify16(v, &sep, &eol, &ctl);
   const uint32_t prev_eol = (pc == '\n' || pc == '\r') ? 1u : 0u;
   const uint32_t prev_sep = (prev_eol || pc == ' ' || pc == '\t') ? 1u : 0u;
   uint32_t valid = 0xFFFFu;
@@ -84,6 +111,12 @@ __device__ __forceinline__ bool lane_masks(uint4 v, uint32_t pc, size_t pos, siz
     t &= t - 1;
     bad |= !num_start(dev::vec_byte(v, j));
   }
+  uint32_t c = ctl & valid;
+  while (c != 0) {
+    const int j = __ffs(c) - 1;
+    c &= c - 1;
+    bad |= !((0x2600u >> dev::vec_byte(v, j)) & 1u);  // only \t \n \r
+  }
   return bad;
 }
 
@@ -101,30 +134,42 @@ __device__ __forceinline__ uint32_t prev_byte(const uint8_t* __restrict__ text, 
   return pos == 0 ? static_cast<uint32_t>('\n') : text[pos - 1];
 }
 
+/*!
+ * \brief C1: one wave per 8 KiB tile, 8 x 16 B loads per lane all in flight,
+ *  wave-level reductions only (no LDS, no barrier).
+ */
+constexpr int kCountLoads = static_cast<int>(kTileBytes / 1024);
 __global__ __launch_bounds__(kThreads) void k_tile_count(const uint8_t* __restrict__ text,
-                                                         size_t n, uint64_t* __restrict__ counts,
+                                                         size_t n, size_t ntiles,
+                                                         uint64_t* __restrict__ counts,
                                                          uint32_t* __restrict__ flags) {
-  __shared__ uint64_t smem[4];
-  __shared__ uint32_t sbad;
-  if (threadIdx.x == 0) sbad = 0;
-  uint64_t packed = 0;
+  const int lane = dev::lane_id();
+  const size_t tile = static_cast<size_t>(blockIdx.x) * (kThreads / dev::kWave) +
+                      threadIdx.x / dev::kWave;
+  if (tile >= ntiles) return;  // whole waves leave; no barrier below
+  const size_t base = tile * kTileBytes;
+  uint4 v[kCountLoads];
+#pragma unroll
+  for (int j = 0; j < kCountLoads; ++j) v[j] = load16(text, base + j * 1024 + lane * 16, n);
+  const uint32_t first = base == 0 ? static_cast<uint32_t>('\n') : text[base - 1];
+  uint32_t lines = 0, toks = 0;
   bool bad = false;
 #pragma unroll
-  for (int s = 0; s < kSub; ++s) {
-    const size_t pos = blockIdx.x * kTileBytes + s * 4096 + threadIdx.x * 16;
-    const uint4 v = load16(text, pos, n);
-    const uint32_t pc = prev_byte(text, pos, v);
+  for (int j = 0; j < kCountLoads; ++j) {
+    const uint32_t left = __shfl_up(v[j].w >> 24, 1, dev::kWave);
+    const uint32_t wrap = j == 0 ? first : __shfl(v[j - 1].w >> 24, dev::kWave - 1, dev::kWave);
+    const uint32_t pc = lane == 0 ? wrap : left;
     uint32_t lm, tm;
-    bad |= lane_masks<true>(v, pc, pos, n, &lm, &tm);
-    packed += (static_cast<uint64_t>(__popc(lm)) << 32) | __popc(tm);
+    bad |= lane_masks<true>(v[j], pc, base + j * 1024 + lane * 16, n, &lm, &tm);
+    lines += __popc(lm);
+    toks += __popc(tm);
   }
-  const uint64_t total = dev::block_sum_256<uint64_t>(packed, smem);
-  // block_sum_256 ends with a barrier-separated read of smem: sbad's reset is ordered
-  if (__any(bad) && dev::lane_id() == 0) sbad = 1;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    counts[blockIdx.x] = total;
-    flags[blockIdx.x] = sbad ? kFlagIrregular : 0u;
+  lines = dev::wave_sum(lines);
+  toks = dev::wave_sum(toks);
+  const bool any_bad = __any(bad);
+  if (lane == 0) {
+    counts[tile] = (static_cast<uint64_t>(lines) << 32) | toks;
+    flags[tile] = any_bad ? kFlagIrregular : 0u;
   }
 }
 
@@ -134,7 +179,8 @@ constexpr int kScanPer = 8;
 /*! \brief exclusive scan of ntiles counts in place (one workgroup), meta totals */
 __global__ __launch_bounds__(kScanThreads) void k_tile_scan(uint64_t* __restrict__ counts,
                                                             const uint32_t* __restrict__ flags,
-                                                            size_t ntiles, ChunkMeta* meta) {
+                                                            size_t ntiles, ChunkMeta* meta,
+                                                            ChunkMeta* host_meta) {
   __shared__ uint64_t swave[kScanThreads / 64];
   __shared__ uint32_t sflag[kScanThreads / 64];
   const int wid = threadIdx.x / dev::kWave;
@@ -184,6 +230,7 @@ __global__ __launch_bounds__(kScanThreads) void k_tile_scan(uint64_t* __restrict
     meta->max_field = 0;
     meta->flags = f;
     meta->pad = 0;
+    if (host_meta != nullptr) *host_meta = *meta;  // mapped pinned copy: no D2H blit
   }
 }
 
@@ -388,7 +435,7 @@ __global__ __launch_bounds__(kThreads) void k_tile_fill(const uint8_t* __restric
                                                         MetaPartial* __restrict__ partials) {
   __shared__ uint4 s_text[kTileBytes / 16 + 1];  // +16 B: 4-byte reads past a token
   __shared__ uint32_t s_tok[kMaxTileTokens];
-  __shared__ uint64_t s_scan[4];
+  __shared__ uint32_t s_scan[4];
   const uint8_t* lds = reinterpret_cast<const uint8_t*>(s_text);
   const size_t tile0 = static_cast<size_t>(blockIdx.x) * kTileBytes;
   const uint64_t pre = prefix[blockIdx.x];
@@ -406,17 +453,17 @@ __global__ __launch_bounds__(kThreads) void k_tile_fill(const uint8_t* __restric
     s_text[s * 256 + threadIdx.x] = v[s];
   }
   // ---- compact the tile's tokens into s_tok in text order
-  uint64_t carry = 0;  // (lines << 32 | tokens) of earlier sub-tiles
+  uint32_t carry = 0;  // (lines << 16 | tokens) of earlier sub-tiles (each <= 4096)
 #pragma unroll
   for (int s = 0; s < kSub; ++s) {
     const size_t pos = tile0 + s * 4096 + threadIdx.x * 16;
     uint32_t lm, tm;
     (void)lane_masks<false>(v[s], pc[s], pos, n, &lm, &tm);
-    const uint64_t mine = (static_cast<uint64_t>(__popc(lm)) << 32) | __popc(tm);
-    uint64_t tot;
-    const uint64_t before = dev::block_excl_scan_256<uint64_t>(mine, s_scan, &tot) + carry;
-    uint32_t line = static_cast<uint32_t>(before >> 32);
-    uint32_t tok = static_cast<uint32_t>(before & 0xffffffffu);
+    const uint32_t mine = (static_cast<uint32_t>(__popc(lm)) << 16) | __popc(tm);
+    uint32_t tot;
+    const uint32_t before = dev::block_excl_scan_256<uint32_t>(mine, s_scan, &tot) + carry;
+    uint32_t line = before >> 16;
+    uint32_t tok = before & 0xffffu;
     uint32_t all = lm | tm;
     while (all != 0) {
       const int j = __ffs(all) - 1;
@@ -433,7 +480,22 @@ __global__ __launch_bounds__(kThreads) void k_tile_fill(const uint8_t* __restric
     carry += tot;
     __syncthreads();  // s_scan reuse by the next sub-tile; s_tok / s_text complete
   }
-  const uint32_t ntok = static_cast<uint32_t>(carry & 0xffffffffu);
+  const uint32_t ntok = carry & 0xffffu;
+  // WG-uniform bases: token k = tok_base + i of line l = line_base + lcnt - 1
+  // goes to nnz position C + (i - lcnt) (C = nnz_base + tok_base - line_base);
+  // its row is R + lcnt - 1 (R = row_base + line_base).  Per-lane offsets are
+  // 32-bit, the 64-bit parts stay scalar.
+  const uint64_t C = out.nnz_base + tok_base - line_base;
+  const uint64_t R = out.row_base + line_base;
+  const int64_t nnz_room = static_cast<int64_t>(out.nnz_limit) - static_cast<int64_t>(C);
+  const int64_t row_room = static_cast<int64_t>(out.row_limit) - static_cast<int64_t>(R);
+  IndexType* const idx_at = out.index + C;
+  float* const val_at = out.value + C;
+  IndexType* const fld_at = out.field != nullptr ? out.field + C : nullptr;
+  float* const lab_at = out.label + R - 1;
+  uint64_t* const off_at = out.offset + R - 1;
+  float* const wgt_at = out.weight != nullptr ? out.weight + R - 1 : nullptr;
+  uint64_t* const qid_at = out.qid != nullptr ? out.qid + R - 1 : nullptr;
 
   // ---- parse: lane i takes token i
   uint64_t mx_index = 0, mx_field = 0;
@@ -443,8 +505,6 @@ __global__ __launch_bounds__(kThreads) void k_tile_fill(const uint8_t* __restric
     const uint32_t off = e & ((1u << kOffBits) - 1);
     const uint32_t lcnt = (e >> kOffBits) & ((1u << kOffBits) - 1);
     const bool is_label = (e >> (2 * kOffBits)) & 1u;
-    const uint64_t l = line_base + lcnt - 1;  // lcnt 0: line began in an earlier tile
-    const uint64_t k = tok_base + i;
     const size_t gpos = tile0 + off;
     bool bad = false;
     int r = 0;
@@ -477,28 +537,27 @@ __global__ __launch_bounds__(kThreads) void k_tile_fill(const uint8_t* __restric
       }
     }
     if (is_label) {
-      const uint64_t row = out.row_base + l;
-      if (row < out.row_limit) {
-        out.label[row] = f0;
-        out.offset[row] = out.nnz_base + (k - l);
-        if (out.weight != nullptr) {
-          out.weight[row] = r == 2 ? f1 : 1.0f;
+      if (static_cast<int64_t>(lcnt) - 1 < row_room) {
+        lab_at[lcnt] = f0;
+        off_at[lcnt] = C + 1 + (static_cast<int64_t>(i) - static_cast<int64_t>(lcnt));
+        if (wgt_at != nullptr) {
+          wgt_at[lcnt] = r == 2 ? f1 : 1.0f;
         } else if (r == 2) {
           need_w = true;
         }
-        if (out.qid != nullptr) out.qid[row] = 0;  // qid lines take the exact path
+        if (qid_at != nullptr) qid_at[lcnt] = 0;  // qid lines take the exact path
       } else {
         irregular = true;
       }
       any_weight |= (r == 2);
     } else {
-      const uint64_t pos = out.nnz_base + (k - l - 1);
-      if (pos >= out.nnz_limit) {
+      const int32_t rel = static_cast<int32_t>(i) - static_cast<int32_t>(lcnt);
+      if (rel >= nnz_room) {
         irregular = true;
       } else if constexpr (F == TextFormat::kLibSVM) {
         const IndexType idx = static_cast<IndexType>(u0);
-        out.index[pos] = idx;
-        out.value[pos] = r == 2 ? f0 : 1.0f;
+        idx_at[rel] = idx;
+        val_at[rel] = r == 2 ? f0 : 1.0f;
         any_value |= (r == 2);
         if (static_cast<uint64_t>(idx) > mx_index) mx_index = idx;
       } else {
@@ -506,9 +565,9 @@ __global__ __launch_bounds__(kThreads) void k_tile_fill(const uint8_t* __restric
           irregular = true;
         } else {
           const IndexType fid = static_cast<IndexType>(u0), idx = static_cast<IndexType>(u1);
-          out.field[pos] = fid;
-          out.index[pos] = idx;
-          out.value[pos] = r == 3 ? f0 : 1.0f;
+          fld_at[rel] = fid;
+          idx_at[rel] = idx;
+          val_at[rel] = r == 3 ? f0 : 1.0f;
           any_value |= (r == 3);
           if (static_cast<uint64_t>(idx) > mx_index) mx_index = idx;
           if (static_cast<uint64_t>(fid) > mx_field) mx_field = fid;
@@ -528,20 +587,39 @@ __global__ __launch_bounds__(kThreads) void k_tile_fill(const uint8_t* __restric
                            static_cast<unsigned long long>(mx_field), fl, partials);
 }
 
-/*! \brief fold the per-workgroup slots into meta; closing row pointer */
-__global__ __launch_bounds__(kThreads) void k_tile_finish(const MetaPartial* __restrict__ p, int np,
-                                                          ChunkMeta* meta, uint64_t* offset,
-                                                          uint64_t row_base, uint64_t nnz_base) {
+/*!
+ * \brief fold the per-workgroup slots into meta; closing row pointer.  One
+ *  1024-lane workgroup, 8 independent slot loads per lane per step (a
+ *  latency-bound single-workgroup pass otherwise dominates small chunks).
+ */
+constexpr int kFinishThreads = 1024;
+constexpr int kFinishPer = 8;
+__global__ __launch_bounds__(kFinishThreads) void k_tile_finish(
+    const MetaPartial* __restrict__ p, int np, ChunkMeta* meta, ChunkMeta* host_meta,
+    uint64_t* offset, uint64_t row_base, uint64_t nnz_base) {
   unsigned long long mi = 0, mf = 0;
   unsigned fl = 0;
-  for (int i = threadIdx.x; i < np; i += kThreads) {
-    const MetaPartial q = p[i];
-    mi = q.max_index > mi ? q.max_index : mi;
-    mf = q.max_field > mf ? q.max_field : mf;
-    fl |= q.flags;
+  for (int i0 = threadIdx.x; i0 < np; i0 += kFinishThreads * kFinishPer) {
+    MetaPartial q[kFinishPer];
+#pragma unroll
+    for (int u = 0; u < kFinishPer; ++u) {
+      const int i = i0 + u * kFinishThreads;
+      if (i < np) {
+        q[u] = p[i];
+      } else {
+        q[u].max_index = q[u].max_field = 0;
+        q[u].flags = 0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kFinishPer; ++u) {
+      mi = q[u].max_index > mi ? q[u].max_index : mi;
+      mf = q[u].max_field > mf ? q[u].max_field : mf;
+      fl |= q[u].flags;
+    }
   }
-  __shared__ unsigned long long s_mi[4], s_mf[4];
-  __shared__ unsigned s_fl[4];
+  __shared__ unsigned long long s_mi[kFinishThreads / 64], s_mf[kFinishThreads / 64];
+  __shared__ unsigned s_fl[kFinishThreads / 64];
   mi = dev::wave_max(mi);
   mf = dev::wave_max(mf);
   fl = dev::wave_or(fl);
@@ -553,7 +631,7 @@ __global__ __launch_bounds__(kThreads) void k_tile_finish(const MetaPartial* __r
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int w = 1; w < 4; ++w) {
+    for (int w = 1; w < kFinishThreads / 64; ++w) {
       s_mi[0] = s_mi[w] > s_mi[0] ? s_mi[w] : s_mi[0];
       s_mf[0] = s_mf[w] > s_mf[0] ? s_mf[w] : s_mf[0];
       s_fl[0] |= s_fl[w];
@@ -562,6 +640,7 @@ __global__ __launch_bounds__(kThreads) void k_tile_finish(const MetaPartial* __r
     meta->max_field = s_mf[0];
     meta->flags |= s_fl[0];
     offset[row_base + meta->nrows] = nnz_base + meta->nnz;
+    if (host_meta != nullptr) *host_meta = *meta;
   }
 }
 }  // namespace
@@ -569,20 +648,24 @@ __global__ __launch_bounds__(kThreads) void k_tile_finish(const MetaPartial* __r
 size_t TileCount(size_t nbytes) { return (nbytes + kTileBytes - 1) / kTileBytes; }
 
 void LaunchTileCountScan(const char* text, size_t nbytes, uint64_t* tile_counts,
-                         uint32_t* tile_flags, ChunkMeta* meta, hipStream_t stream) {
+                         uint32_t* tile_flags, ChunkMeta* meta, ChunkMeta* host_meta,
+                         hipStream_t stream) {
   const size_t ntiles = TileCount(nbytes);
   if (ntiles != 0) {
-    hipLaunchKernelGGL(k_tile_count, dim3(ntiles), dim3(kThreads), 0, stream,
-                       reinterpret_cast<const uint8_t*>(text), nbytes, tile_counts, tile_flags);
+    const size_t per_block = kThreads / dev::kWave;
+    hipLaunchKernelGGL(k_tile_count, dim3((ntiles + per_block - 1) / per_block), dim3(kThreads), 0,
+                       stream, reinterpret_cast<const uint8_t*>(text), nbytes, ntiles, tile_counts,
+                       tile_flags);
   }
   hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kScanThreads), 0, stream, tile_counts, tile_flags,
-                     ntiles, meta);
+                     ntiles, meta, host_meta);
 }
 
 template <typename IndexType>
 void LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
                     const uint64_t* tile_prefix, const FillTarget<IndexType>& out,
-                    MetaPartial* partials, ChunkMeta* meta, hipStream_t stream) {
+                    MetaPartial* partials, ChunkMeta* meta, ChunkMeta* host_meta,
+                    hipStream_t stream) {
   const size_t ntiles = TileCount(nbytes);
   const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
   if (ntiles != 0) {
@@ -594,16 +677,17 @@ void LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
                          dim3(kThreads), 0, stream, t, nbytes, tile_prefix, out, partials);
     }
   }
-  hipLaunchKernelGGL(k_tile_finish, dim3(1), dim3(kThreads), 0, stream, partials,
-                     static_cast<int>(ntiles), meta, out.offset, out.row_base, out.nnz_base);
+  hipLaunchKernelGGL(k_tile_finish, dim3(1), dim3(kFinishThreads), 0, stream, partials,
+                     static_cast<int>(ntiles), meta, host_meta, out.offset, out.row_base,
+                     out.nnz_base);
 }
 
 template void LaunchTileFill<uint32_t>(const char*, size_t, TextFormat, const uint64_t*,
                                        const FillTarget<uint32_t>&, MetaPartial*, ChunkMeta*,
-                                       hipStream_t);
+                                       ChunkMeta*, hipStream_t);
 template void LaunchTileFill<uint64_t>(const char*, size_t, TextFormat, const uint64_t*,
                                        const FillTarget<uint64_t>&, MetaPartial*, ChunkMeta*,
-                                       hipStream_t);
+                                       ChunkMeta*, hipStream_t);
 
 }  // namespace gpu
 }  // namespace dmlc

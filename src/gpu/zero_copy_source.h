@@ -5,7 +5,8 @@
  *  H2D DMA reads the page cache directly -- no CPU memcpy into pinned slots
  *  (measured: 87.0M rows/s vs 55.3M with the pread ring, profiles/r01_zero_copy).
  *
- * Chunks never cross a file boundary and end on a record boundary:
+ * Chunks never cross a file boundary and end on a record boundary (a record
+ * longer than chunk_bytes makes its chunk longer):
  *  - text: after the last EOL of the window (reference LineSplitter,
  *    `src/io/line_split.cc:27-34`);
  *  - RecordIO: at the last aligned record head (magic word followed by an lrec
@@ -82,7 +83,10 @@ class ZeroCopySource {
     const Seg& s = segs_[seg_];
     const char* b = s.ptr + off_;
     size_t len = std::min(chunk_bytes_, s.size - off_);
-    if (off_ + len < s.size) len = cut_ == Cut::kLine ? CutLine(b, len) : CutRecord(b, len);
+    if (off_ + len < s.size) {
+      const size_t avail = s.size - off_;
+      len = cut_ == Cut::kLine ? CutLine(b, len, avail) : CutRecord(b, len, avail);
+    }
     out->ptr = b;
     out->size = len;
     off_ += len;
@@ -114,23 +118,37 @@ class ZeroCopySource {
   }
 
  private:
-  size_t CutLine(const char* b, size_t len) const {
+  /*!
+   * \brief end of the last whole line in [b, b+len); a line longer than the
+   *  window makes the piece longer instead (up to the line's end, or `avail`,
+   *  the bytes left in the segment), as the reference's InputSplitBase grows
+   *  its buffer for long records (src/io/input_split_base.cc:241-258)
+   */
+  size_t CutLine(const char* b, size_t len, size_t avail) const {
     size_t cut = len;
     while (cut > 0 && b[cut - 1] != '\n' && b[cut - 1] != '\r') --cut;
-    CHECK(cut != 0) << "a line is longer than chunk_bytes (" << chunk_bytes_ << ")";
+    if (cut != 0) return cut;
+    cut = len;
+    while (cut < avail && b[cut] != '\n' && b[cut] != '\r') ++cut;
+    while (cut < avail && (b[cut] == '\n' || b[cut] == '\r')) ++cut;
     return cut;
   }
-  size_t CutRecord(const char* b, size_t len) const {
+  static bool IsHead(const uint32_t* w, size_t p) {
+    return w[p] == RecordIOWriter::kMagic && RecordIOWriter::DecodeFlag(w[p + 1]) <= 1U;
+  }
+  /*! \brief last record head in the window; past it when one record fills it */
+  size_t CutRecord(const char* b, size_t len, size_t avail) const {
     // segments start 4-byte aligned (RecordIO partitions align to 4 bytes)
     const uint32_t* w = reinterpret_cast<const uint32_t*>(b);
-    size_t nw = len / 4;
+    const size_t nw = len / 4;
     for (size_t p = nw >= 2 ? nw - 2 : 0; p > 0; --p) {
-      if (w[p] == RecordIOWriter::kMagic && RecordIOWriter::DecodeFlag(w[p + 1]) <= 1U) {
-        return p * 4;
-      }
+      if (IsHead(w, p)) return p * 4;
     }
-    LOG(FATAL) << "a RecordIO record is longer than chunk_bytes (" << chunk_bytes_ << ")";
-    return 0;
+    const size_t aw = avail / 4;
+    for (size_t p = nw > 1 ? nw - 1 : 1; p + 1 < aw; ++p) {
+      if (IsHead(w, p)) return p * 4;
+    }
+    return avail;
   }
   struct Mapping {
     void* ptr;

@@ -171,9 +171,11 @@ void ShardReader::Reset() {
 
 size_t ShardReader::Fill(char* buf, size_t cap) {
   DMLC_FAULT_POINT("read");
-  CHECK(carry_.size() < cap) << "a single record (" << carry_.size()
-                             << " bytes) does not fit the chunk size " << cap
-                             << "; increase chunk_bytes";
+  if (carry_.size() >= cap) {
+    // the pending record alone fills the buffer: ask for a bigger one
+    need_cap_ = std::max(2 * cap, carry_.size() + 1);
+    return kNeedMore;
+  }
   size_t pos = carry_.size();
   if (pos != 0) std::memcpy(buf, carry_.data(), pos);
   carry_.clear();
@@ -237,8 +239,13 @@ size_t ShardReader::Fill(char* buf, size_t cap) {
   const bool at_end = seg_idx_ >= segs_.size() && !pending_newline_;
   if (at_end) return pos;
   const char* last = split_->FindLastRecordBegin(buf, buf + pos);
-  CHECK(last != buf) << "a single record does not fit the chunk size " << cap
-                     << "; increase chunk_bytes";
+  if (last == buf) {
+    // one record is longer than the buffer: keep what was read, grow, retry
+    // (the reference doubles its chunk buffer, src/io/input_split_base.cc:241-258)
+    carry_.assign(buf, pos);
+    need_cap_ = 2 * cap;
+    return kNeedMore;
+  }
   carry_.assign(last, buf + pos - last);
   return static_cast<size_t>(last - buf);
 }

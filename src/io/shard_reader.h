@@ -63,9 +63,14 @@ class ShardReader {
   /*!
    * \brief fill buf (capacity `cap`, multiple of the split's alignment) with
    *  whole records.
-   * \return bytes written; 0 at the end of the partition
+   * \return bytes written; 0 at the end of the partition; kNeedMore when a
+   *  single record is longer than `cap`: nothing is lost (the bytes read so
+   *  far are kept), call again with a buffer of at least NeedCapacity() bytes
    */
   size_t Fill(char* buf, size_t cap);
+  static constexpr size_t kNeedMore = ~static_cast<size_t>(0);
+  /*! \brief capacity the next Fill needs after it returned kNeedMore */
+  size_t NeedCapacity() const { return need_cap_; }
   /*! \brief rewind to the start of the partition */
   void Reset();
   /*! \brief bytes of the partition (excluding inserted newlines) */
@@ -96,6 +101,7 @@ class ShardReader {
   size_t seg_idx_{0}, seg_off_{0};
   bool pending_newline_{false};
   std::string carry_;
+  size_t need_cap_{0};
   size_t bytes_read_{0};
   int Fd(size_t file);
 };

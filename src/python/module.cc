@@ -195,6 +195,10 @@ class PyPartitionReader {
     {
       py::gil_scoped_release nogil;
       n = reader_->Fill(&buf_[0], buf_.size());
+      while (n == io::ShardReader::kNeedMore) {  // a record longer than the buffer
+        buf_.resize(reader_->NeedCapacity());
+        n = reader_->Fill(&buf_[0], buf_.size());
+      }
     }
     if (n == 0) return py::none();
     return py::bytes(buf_.data(), n);
@@ -737,7 +741,11 @@ PYBIND11_MODULE(_dmlc, m) {
           io::ShardReader reader(split.get(), nthread);
           std::string buf(chunk_bytes, '\0');
           for (;;) {
-            const size_t n = reader.Fill(&buf[0], buf.size());
+            size_t n = reader.Fill(&buf[0], buf.size());
+            while (n == io::ShardReader::kNeedMore) {
+              buf.resize(reader.NeedCapacity());
+              n = reader.Fill(&buf[0], buf.size());
+            }
             if (n == 0) break;
             chunks.emplace_back(buf.data(), n);
           }

@@ -74,3 +74,22 @@ def test_cache_file_written_and_replayed(tmp_path):
     e1 = _records(s)
     assert e0 == e1 == _records(io.InputSplit(path, 0, 1, "text"))
     assert os.path.getsize(cache) > os.path.getsize(path)
+
+
+def test_partition_reader_grows_for_a_record_longer_than_its_buffer(tmp_path):
+    """io.PartitionReader (the pinned-ring ShardReader) grows its buffer for a
+    line longer than chunk_bytes instead of failing; every byte arrives once."""
+    path = str(tmp_path / "g.txt")
+    lines = [b"short %d" % i for i in range(300)]
+    lines.insert(150, b"x" * (5 * 4096 + 7))
+    with open(path, "wb") as f:
+        f.write(b"\n".join(lines) + b"\n")
+    r = io.PartitionReader(path, 0, 1, "text", nthread=2, chunk_bytes=4096)
+    chunks = []
+    while True:
+        c = r.next()
+        if c is None:
+            break
+        chunks.append(c)
+    assert b"".join(chunks).split(b"\n")[:-1] == lines
+    assert max(len(c) for c in chunks) > 4096
