@@ -15,6 +15,8 @@ and re-parses the text.  Total work is fixed as N grows (strong scaling).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
+       dmlc-submit --cluster local --num-workers N --gpus-per-node N python bench.py --gpus N
+         (the dmlc tracker assigns ranks and bootstraps the RCCL/gloo group)
 """
 from __future__ import annotations
 
@@ -95,26 +97,22 @@ def ensure_dataset(args, rank: int, world: int, barrier) -> str:
 
 def main():
     args = parse_args()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
 
     import torch
 
+    from dmlc_core_amd.parallel import dist as ddist
+
     use_gpu = args.device == "gpu" or (args.device == "auto" and torch.cuda.is_available())
+    # torchrun (RANK/WORLD_SIZE/MASTER_*) or dmlc-submit (DMLC_TRACKER_URI/PORT:
+    # the tracker assigns the rank and brokers the process-group address)
+    info = ddist.init("nccl" if use_gpu else "gloo")
+    rank, world, local_rank = info["rank"], info["world_size"], info["local_rank"]
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but world size {world}", file=sys.stderr)
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: F811
-
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if use_gpu:
-            torch.cuda.set_device(local_rank)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        else:
-            dist.init_process_group("gloo")
-    elif use_gpu:
+    if use_gpu:
         torch.cuda.set_device(local_rank)
 
     dev = torch.device("cuda", local_rank) if use_gpu else torch.device("cpu")
@@ -140,6 +138,7 @@ def main():
     ddir = ensure_dataset(args, rank, world, barrier)
     read_threads = args.read_threads or max(4, min(16, len(os.sched_getaffinity(0))))
 
+    local = {}  # this rank's own counters, gathered to rank 0 after timing
     if use_gpu:
         parser = data.GPUParser(ddir, rank, world, format="libsvm", chunk_mb=args.chunk_mb,
                                 read_threads=read_threads, pinned_slots=args.pinned_slots,
@@ -154,11 +153,13 @@ def main():
             parser.before_first()
             csr.clear()
             parser.parse_all(csr)
+            local["rows"], local["bytes"] = csr.rows, parser.partition_bytes
             return csr.rows, csr.nnz, csr.max_index, parser.partition_bytes
     else:
         def step():
             p = data.Parser(ddir + "?format=libsvm", rank, world, "libsvm")
             rows, nnz, _ = p.drain()
+            local["rows"], local["bytes"] = rows, p.bytes_read()
             return rows, nnz, 0, p.bytes_read()
 
     def global_counts(rows, nnz, max_index, nbytes):
@@ -184,10 +185,24 @@ def main():
     barrier()
     sync()
     elapsed = time.perf_counter() - t0
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    # per-rank view (rows, bytes, own time, host waits) gathered to every rank
+    st = parser.stats() if use_gpu else {}
+    mine = torch.tensor([rank, local["rows"], local["bytes"], elapsed,
+                         st.get("wait_reader_sec", 0.0), st.get("wait_gpu_sec", 0.0)],
+                        dtype=torch.float64, device=dev)
+    gathered = [torch.zeros_like(mine) for _ in range(world)]
     if dist is not None:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+        dist.all_gather(gathered, mine)
+    else:
+        gathered = [mine]
+    per_rank = []
+    for g in sorted((x.tolist() for x in gathered), key=lambda v: v[0]):
+        r, rows_r, bytes_r, el_r, wr, wg = g
+        per_rank.append({"rank": int(r), "rows": int(rows_r), "bytes": int(bytes_r),
+                         "rows_per_sec": round(rows_r * args.steps / el_r, 1),
+                         "input_GBps": round(bytes_r * args.steps / el_r / 1e9, 3),
+                         "wait_reader_sec": round(wr, 4), "wait_gpu_sec": round(wg, 4)})
+    elapsed = max(float(x[3]) for x in gathered)  # the slowest rank sets the step time
     (rows, nnz, nbytes), max_index = totals
     ms = elapsed / max(1, args.steps) * 1e3
     value = rows * args.steps / elapsed
@@ -227,11 +242,11 @@ def main():
             "input_GBps": round(nbytes * args.steps / elapsed / 1e9, 3),
             "mode": args.mode,
         }
+        out["per_rank"] = per_rank
         if use_gpu:
             out["parser_stats_last_rank0"] = parser.stats()
         print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    ddist.finalize()
 
 
 if __name__ == "__main__":

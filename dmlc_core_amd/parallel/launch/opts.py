@@ -44,7 +44,7 @@ def _bool(s: str) -> bool:
 
 
 def build_parser() -> argparse.ArgumentParser:
-    p = argparse.ArgumentParser(description="DMLC job submission (MI355X build)")
+    p = argparse.ArgumentParser(description="DMLC job submission (MI355X build)", allow_abbrev=False)
     p.add_argument("--cluster", type=str, choices=BACKENDS,
                    help="cluster backend; defaults to ${DMLC_SUBMIT_CLUSTER}")
     p.add_argument("--num-workers", required=True, type=int)
@@ -86,12 +86,18 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--timeout", default=None, type=float, help="tracker job timeout (s)")
     p.add_argument("--heartbeat-timeout", default=None, type=float)
     p.add_argument("--dry-run", action="store_true", help="print the launch commands only")
-    p.add_argument("command", nargs="+", help="command to run on every task")
+    # everything from the first positional token on is the task's command,
+    # verbatim (its own --options included), as with the reference's
+    # parse_known_args + `command += unknown` (tracker/dmlc_tracker/opts.py:142-166)
+    p.add_argument("command", nargs=argparse.REMAINDER, help="command to run on every task")
     return p
 
 
 def get_opts(argv=None):
-    args = build_parser().parse_args(argv)
+    args, unknown = build_parser().parse_known_args(argv)
+    args.command = list(args.command) + unknown
+    if not args.command:
+        raise SystemExit("dmlc-submit: no command given")
     if args.cluster is None:
         args.cluster = os.environ.get("DMLC_SUBMIT_CLUSTER")
         if args.cluster is None:
