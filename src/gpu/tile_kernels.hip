@@ -135,6 +135,56 @@ __device__ __forceinline__ uint32_t prev_byte(const uint8_t* __restrict__ text, 
 }
 
 /*!
+ * \brief C1 lane step: line / token starts of 16 bytes as per-byte high-bit
+ *  masks (bit 7 of byte j), popcounted without gathering, plus the irregular
+ *  checks of lane_masks<true>.  pc: the byte before the 16.
+ */
+__device__ __forceinline__ bool count16(uint4 v, uint32_t pc, size_t pos, size_t n,
+                                        uint32_t* lines, uint32_t* toks) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  // bytes at or past n are "separators" (no starts there)
+  const size_t room = pos >= n ? 0 : (n - pos < 16 ? n - pos : 16);
+  uint32_t prev_sep = (pc <= 0x20u) ? 0x80u : 0u;  // sep bit of the byte before, at bit 7
+  uint32_t prev_eol = (pc == '\n' || pc == '\r') ? 0x80u : 0u;
+  bool bad = false;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t x = w[i];
+    const uint32_t lo7 = x & 0x7F7F7F7Fu;
+    const uint32_t le20 = ~((lo7 + 0x5F5F5F5Fu) | x) & 0x80808080u;
+    const uint32_t lt20 = ~((lo7 + 0x60606060u) | x) & 0x80808080u;
+    const uint32_t b6 = ((x & 0x06060606u) + 0x7E7E7E7Eu) & 0x80808080u;
+    const int valid_bytes = static_cast<int>(room) - 4 * i;
+    const uint32_t valid = valid_bytes >= 4 ? 0x80808080u
+                           : (valid_bytes <= 0 ? 0u : (0x80808080u >> (8 * (4 - valid_bytes))));
+    const uint32_t sep = le20 | (~valid & 0x80808080u);
+    const uint32_t eol = le20 & b6;
+    const uint32_t sep_before = (sep << 8) | prev_sep;
+    const uint32_t eol_before = (eol << 8) | prev_eol;
+    const uint32_t tm = ~sep & sep_before & 0x80808080u;
+    const uint32_t lm = ~eol & eol_before & valid & 0x80808080u;
+    *toks += __popc(tm);
+    *lines += __popc(lm);
+    bad |= (lm & ~tm) != 0;  // a line that starts with a blank
+    uint32_t t = tm;
+    while (t != 0) {  // token starts must be [0-9+-.]
+      const int j = (__ffs(t) - 1) >> 3;
+      t &= t - 1;
+      bad |= !num_start((x >> (8 * j)) & 0xFFu);
+    }
+    uint32_t c = lt20 & valid;
+    while (c != 0) {  // control bytes other than \t \n \r
+      const int j = (__ffs(c) - 1) >> 3;
+      c &= c - 1;
+      bad |= !((0x2600u >> ((x >> (8 * j)) & 0xFFu)) & 1u);
+    }
+    prev_sep = (sep >> 24) & 0x80u;
+    prev_eol = (eol >> 24) & 0x80u;
+  }
+  return bad;
+}
+
+/*!
  * \brief C1: one wave per 8 KiB tile, 8 x 16 B loads per lane all in flight,
  *  wave-level reductions only (no LDS, no barrier).
  */
@@ -159,10 +209,7 @@ __global__ __launch_bounds__(kThreads) void k_tile_count(const uint8_t* __restri
     const uint32_t left = __shfl_up(v[j].w >> 24, 1, dev::kWave);
     const uint32_t wrap = j == 0 ? first : __shfl(v[j - 1].w >> 24, dev::kWave - 1, dev::kWave);
     const uint32_t pc = lane == 0 ? wrap : left;
-    uint32_t lm, tm;
-    bad |= lane_masks<true>(v[j], pc, base + j * 1024 + lane * 16, n, &lm, &tm);
-    lines += __popc(lm);
-    toks += __popc(tm);
+    bad |= count16(v[j], pc, base + j * 1024 + lane * 16, n, &lines, &toks);
   }
   lines = dev::wave_sum(lines);
   toks = dev::wave_sum(toks);
@@ -307,10 +354,31 @@ struct FastNum {
   bool neg, dot, ok;
 };
 
-__device__ __forceinline__ uint64_t digit_run(const uint8_t* lds, uint32_t* p, uint64_t acc,
-                                              uint32_t* ndig, uint64_t* pw, uint32_t* term,
-                                              bool* ok) {
-  for (int it = 0; it < 8; ++it) {
+/*!
+ * \brief up to 8 leading digits at p from two speculative 4-byte groups
+ *  (branch-free); returns the digit count (8: more may follow), *val their
+ *  value, *term the byte that ended the run (when < 8 digits).
+ */
+__device__ __forceinline__ uint32_t run8(const uint8_t* lds, uint32_t p, uint32_t* val,
+                                         uint32_t* term) {
+  const uint32_t g0 = lds_u32_at(lds, p);
+  const uint32_t g1 = lds_u32_at(lds, p + 4);
+  uint32_t v0, v1;
+  const uint32_t k0 = lead_digits(g0, &v0);
+  uint32_t k1 = lead_digits(g1, &v1);
+  const bool full = k0 == 4;
+  k1 = full ? k1 : 0u;
+  v1 = full ? v1 : 0u;
+  *val = v0 * pow10_small(k1) + v1;
+  const uint32_t tg = full ? g1 : g0, tk = full ? k1 : k0;
+  *term = tk < 4 ? (tg >> (8u * tk)) & 0xFFu : static_cast<uint32_t>('0');
+  return k0 + k1;
+}
+
+/*! \brief continue a digit run past 8 digits in 64-bit (rare) */
+__device__ uint64_t digit_run_long(const uint8_t* lds, uint32_t* p, uint64_t acc, uint32_t* ndig,
+                                   uint64_t* pw, uint32_t* term, bool* ok) {
+  for (int it = 0; it < 6; ++it) {
     const uint32_t g = lds_u32_at(lds, *p);
     uint32_t v;
     const uint32_t k = lead_digits(g, &v);
@@ -328,27 +396,37 @@ __device__ __forceinline__ uint64_t digit_run(const uint8_t* lds, uint32_t* p, u
   return acc;
 }
 
+__device__ __forceinline__ uint32_t pow10_u32(uint32_t k) {  // k <= 8
+  return pow10_small(k < 4 ? k : 4u) * pow10_small(k > 4 ? k - 4u : 0u);
+}
+
 __device__ __forceinline__ FastNum fast_num(const uint8_t* lds, uint32_t p) {
   FastNum r;
-  r.ip = r.fp = 0;
-  r.fpow = 1;
-  r.nip = 0;
-  r.neg = r.dot = false;
   r.ok = true;
-  r.term = 0;
   const uint32_t c0 = lds[p];
-  if (c0 == '-' || c0 == '+') {
-    r.neg = c0 == '-';
-    ++p;
+  r.neg = c0 == '-';
+  p += (c0 == '-' || c0 == '+') ? 1u : 0u;
+  uint32_t v, term;
+  uint32_t k = run8(lds, p, &v, &term);
+  r.ip = v;
+  r.nip = k;
+  p += k;
+  if (k == 8) {
+    uint64_t unused = 1;
+    r.ip = digit_run_long(lds, &p, r.ip, &r.nip, &unused, &term, &r.ok);
   }
-  uint64_t ipw = 1;
-  r.ip = digit_run(lds, &p, 0, &r.nip, &ipw, &r.term, &r.ok);
-  if (r.ok && r.term == '.') {
-    r.dot = true;
+  r.dot = term == '.';
+  r.fp = 0;
+  r.fpow = 1;
+  if (r.dot) {
     ++p;
-    uint32_t nfp = 0;
-    r.fp = digit_run(lds, &p, 0, &nfp, &r.fpow, &r.term, &r.ok);
+    uint32_t nf = run8(lds, p, &v, &term);
+    r.fp = v;
+    r.fpow = pow10_u32(nf);
+    p += nf;
+    if (nf == 8) r.fp = digit_run_long(lds, &p, r.fp, &nf, &r.fpow, &term, &r.ok);
   }
+  r.term = term;
   r.end = p;
   return r;
 }
@@ -361,71 +439,62 @@ __device__ __forceinline__ bool is_sep(uint32_t c) {
  * \brief the reference StrToFloat of a FastNum (strtonum.h): integer digits
  *  accumulated in float are exact below 2^24, so <= 7 of them equal the
  *  integer converted once; the fraction is uint64 digits / uint64 10^n in
- *  double, added as float.  False when the number needs the generic parser.
+ *  double, added as float.  `ok` is false when the generic parser is needed.
  */
-__device__ __forceinline__ bool fast_float(const FastNum& n, float* out) {
+__device__ __forceinline__ float fast_float(const FastNum& n, bool* ok) {
 #if defined(__clang__)
 #pragma clang fp contract(off)
 #endif
-  if (!n.ok || n.nip > 7) return false;
+  *ok = n.ok && n.nip <= 7;
   float v = static_cast<float>(static_cast<uint32_t>(n.ip));
-  if (n.dot) v += static_cast<float>(static_cast<double>(n.fp) / static_cast<double>(n.fpow));
-  *out = n.neg ? -v : v;
-  return true;
+  const float frac = static_cast<float>(static_cast<double>(n.fp) / static_cast<double>(n.fpow));
+  if (n.dot) v += frac;
+  return n.neg ? -v : v;
 }
 
 /*!
  * \brief single-pass parse of a token starting at LDS offset `off` in the
  *  common shapes: label `[+-]d[.d][:[+-]d[.d]]`, LibSVM feature `d[:[+-]d[.d]]`,
- *  LibFM feature `d:d[:[+-]d[.d]]`, each ended by a separator.  Anything else
- *  (exponents, signs on indices, junk bytes, over-long digit runs) returns
- *  false and takes strtonum.h's generic ParsePair / ParseTriple; on the shapes
- *  it accepts the results are identical.
+ *  LibFM feature `d:d[:[+-]d[.d]]`, each ended by a separator.  Labels and
+ *  features run the same number decodes (no divergence inside a wave); the
+ *  second / third number is decoded speculatively and only used when the
+ *  first ended in ':'.  Anything else (exponents, signs on indices, junk
+ *  bytes, over-long digit runs) returns false and takes strtonum.h's generic
+ *  ParsePair / ParseTriple; on the shapes it accepts the results are identical.
  */
 template <TextFormat F>
 __device__ __forceinline__ bool fast_token(const uint8_t* lds, uint32_t off, bool is_label,
                                            int* r, uint64_t* u0, uint64_t* u1, float* f0,
                                            float* f1) {
-  FastNum a = fast_num(lds, off);
-  if (!a.ok) return false;
+  const FastNum a = fast_num(lds, off);
+  const FastNum b = fast_num(lds, a.end + 1);
+  const bool a_end = is_sep(a.term), a_col = a.term == ':';
+  const bool b_end = is_sep(b.term);
+  bool fa_ok, fb_ok;
+  const float fa = fast_float(a, &fa_ok);
+  const float fb = fast_float(b, &fb_ok);
   if (is_label) {
-    if (!fast_float(a, f0)) return false;
-    if (is_sep(a.term)) {
-      *r = 1;
-      return true;
-    }
-    if (a.term != ':') return false;
-    FastNum w = fast_num(lds, a.end + 1);
-    if (!is_sep(w.term) || !fast_float(w, f1)) return false;
-    *r = 2;
-    return true;
+    *f0 = fa;
+    *f1 = fb;
+    *r = a_end ? 1 : 2;
+    return fa_ok && (a_end || (a_col && b_end && fb_ok));
   }
-  if (a.neg || a.dot || a.nip == 0) return false;
+  const bool a_uint = a.ok && !a.neg && !a.dot && a.nip != 0;
   *u0 = a.ip;
-  if (is_sep(a.term)) {
-    if (F == TextFormat::kLibFM) return false;  // r < 2: generic path flags it
-    *r = 1;
-    return true;
+  if (F == TextFormat::kLibSVM) {
+    *f0 = fb;
+    *r = a_end ? 1 : 2;
+    return a_uint && (a_end || (a_col && b_end && fb_ok));
   }
-  if (a.term != ':') return false;
-  if (F == TextFormat::kLibFM) {
-    FastNum b = fast_num(lds, a.end + 1);
-    if (!b.ok || b.neg || b.dot || b.nip == 0) return false;
-    *u1 = b.ip;
-    if (is_sep(b.term)) {
-      *r = 2;
-      return true;
-    }
-    if (b.term != ':') return false;
-    FastNum v = fast_num(lds, b.end + 1);
-    if (!is_sep(v.term) || !fast_float(v, f0)) return false;
-    *r = 3;
-    return true;
-  }
-  FastNum v = fast_num(lds, a.end + 1);
-  if (!is_sep(v.term) || !fast_float(v, f0)) return false;
-  *r = 2;
-  return true;
+  // LibFM: field:index[:value]
+  const FastNum c = fast_num(lds, b.end + 1);
+  bool fc_ok;
+  const float fc = fast_float(c, &fc_ok);
+  const bool b_uint = b.ok && !b.neg && !b.dot && b.nip != 0;
+  *u1 = b.ip;
+  *f0 = fc;
+  *r = b_end ? 2 : 3;
+  return a_uint && a_col && b_uint && (b_end || (b.term == ':' && is_sep(c.term) && fc_ok));
 }
 
 template <TextFormat F, typename IndexType>
@@ -433,7 +502,7 @@ __global__ __launch_bounds__(kThreads) void k_tile_fill(const uint8_t* __restric
                                                         const uint64_t* __restrict__ prefix,
                                                         FillTarget<IndexType> out,
                                                         MetaPartial* __restrict__ partials) {
-  __shared__ uint4 s_text[kTileBytes / 16 + 1];  // +16 B: 4-byte reads past a token
+  __shared__ uint4 s_text[kTileBytes / 16 + 4];  // +64 B: speculative reads past a token
   __shared__ uint32_t s_tok[kMaxTileTokens];
   __shared__ uint32_t s_scan[4];
   const uint8_t* lds = reinterpret_cast<const uint8_t*>(s_text);
