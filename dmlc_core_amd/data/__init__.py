@@ -87,6 +87,21 @@ class GPUParser:
         self._p.parse_all(out)
         return out
 
+    def parse_all_hashed(self, dim: int, seed: int = 0, fp8: bool = True, scale: float = 1.0):
+        """Rest of the partition as a hashed dense batch, tokenised, hashed and
+        packed by ONE fused kernel per chunk (no CSR in between; BASELINE
+        config 5).  Returns ``{"x": [rows, dim] float8_e4m3fn (or float32),
+        "label": [rows] float32}`` as torch tensors on the device.  The hash
+        equals :func:`dmlc_core_amd.ops.hashed_dense` of the parsed CSR."""
+        import torch
+        import torch.utils.dlpack as tdl
+
+        d = self._p.parse_all_hashed(int(dim), float(scale), int(seed) & 0xFFFFFFFF, bool(fp8))
+        x = tdl.from_dlpack(d["x"]).view(d["rows"], d["dim"])
+        if fp8:
+            x = x.view(torch.float8_e4m3fn)
+        return {"x": x, "label": tdl.from_dlpack(d["label"])}
+
     def before_first(self):
         self._p.before_first()
 

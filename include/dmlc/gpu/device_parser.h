@@ -74,6 +74,21 @@ struct DeviceParserConfig {
   void Update(const std::map<std::string, std::string>& args);
 };
 
+/*!
+ * \brief a hashed dense batch in HBM (BASELINE config 5): row r of `x` is the
+ *  signed feature hash of line r into `dim` buckets, OCP fp8 e4m3 (1 byte) or
+ *  f32, `label` its label.  Grows by doubling, like DeviceCSR.
+ */
+struct DeviceHashedBatch {
+  DeviceBuffer x, label;
+  size_t rows{0}, row_cap{0};
+  int dim{0};
+  bool fp8{true};
+  int device{0};
+  /*! \brief capacity for `rows` rows, preserving the first this->rows */
+  void Reserve(size_t rows, hipStream_t stream);
+};
+
 /*! \brief cumulative pipeline counters */
 struct DeviceParserStats {
   size_t bytes{0};
@@ -125,6 +140,13 @@ class DeviceParser {
   virtual const DeviceRowBlock<IndexType>& Value() const = 0;
   /*! \brief parse the rest of the partition, appending to `out` */
   virtual void ParseAll(DeviceCSR<IndexType>* out) = 0;
+  /*!
+   * \brief parse the rest of the partition straight into a hashed dense batch
+   *  (tokenize -> hash -> fp8 in one kernel per chunk, no CSR materialised);
+   *  the hash is the one of ops.hashed_dense / LaunchHashedDense*
+   */
+  virtual void ParseAllHashed(DeviceHashedBatch* out, int dim, float scale, uint32_t seed,
+                              bool fp8) = 0;
   /*! \brief total bytes of this partition */
   virtual size_t PartitionBytes() const = 0;
   virtual const DeviceParserStats& Stats() const = 0;

@@ -149,6 +149,24 @@ __device__ __forceinline__ uint32_t byte_eq_mask(uint4 v, uint32_t c) {
   return m;
 }
 
+/*!
+ * \brief K9 feature hash (murmur3 fmix64 of the key mixed with the seed); the
+ *  low bits pick the bucket (h % dim), bit 31 the sign.  Shared by the CSR ->
+ *  dense kernel and the fused text -> dense kernel so both hash identically.
+ */
+__device__ __forceinline__ uint32_t hash_u64(uint64_t x, uint32_t seed) {
+  x ^= static_cast<uint64_t>(seed) * 0x9e3779b97f4a7c15ull;
+  x = (x ^ (x >> 33)) * 0xff51afd7ed558ccdull;
+  x = (x ^ (x >> 33)) * 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return static_cast<uint32_t>(x);
+}
+
+/*! \brief the K9 key of a (field, index) pair: fields occupy bits 40+ */
+__device__ __forceinline__ uint64_t hash_key(uint64_t index, uint64_t field, bool has_field) {
+  return has_field ? (index ^ (field << 40)) : index;
+}
+
 __device__ __forceinline__ uint8_t vec_byte(uint4 v, int j) {
   const uint32_t w = j < 4 ? v.x : (j < 8 ? v.y : (j < 12 ? v.z : v.w));
   return static_cast<uint8_t>(w >> (8 * (j & 3)));

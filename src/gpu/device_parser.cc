@@ -555,7 +555,13 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   }
 
   /*! \brief parse one chunk into out (append or replace); false at end */
-  bool ProcessOne(DeviceCSR<IndexType>* out, bool append) {
+  /*!
+   * \brief pop the next device-resident chunk and run body(text, nbytes) on it
+   *  (compute stream, after its H2D); false at the end.  Slot recycling and
+   *  the resume cursor are handled here, also when body throws.
+   */
+  template <typename Body>
+  bool WithNextChunk(Body body) {
     DMLC_FAULT_POINT("parse");
     FillPipeline();
     if (inflight_.empty()) return false;
@@ -563,25 +569,12 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     inflight_.pop_front();
     busy_ = 1;
     cur_slot_ = cur.slot;
-    const size_t nbytes = cur.size;
-    const char* text = cur.text;
-    EnsureScratch(nbytes);
+    EnsureScratch(cur.size);
     hipStream_t s = compute_->get();
     ScopedRange range("parse_chunk");
     if (cur.d >= 0) DMLC_HIP_CHECK(hipStreamWaitEvent(s, copied_[cur.d]->get(), 0));
-    const size_t row_base = append ? out->rows_ : 0;
-    const size_t nnz_base = append ? out->nnz_ : 0;
-    ChunkPlan plan;
-    const bool token_format = tcfg_.format != TextFormat::kCSV;
     try {
-      bool done = false;
-      if (token_format && cfg_.fast_path) {
-        done = FastParse(text, nbytes, out, row_base, nnz_base, &plan);
-        if (!done) stats_.exact_chunks += 1;
-      }
-      if (!done) {
-        ExactParse(text, nbytes, out, row_base, nnz_base, &plan, token_format && cfg_.fast_path);
-      }
+      body(cur.text, cur.size);
       DMLC_FAULT_POINT("parse_fill");
     } catch (...) {
       // the chunk was not delivered: the cursor stays at its start (a resume
@@ -596,16 +589,76 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     if (cur.d >= 0) parsed_[cur.d]->Record(s);
     busy_ = 0;
     cursor_ = cur.end_pos;  // only once the chunk is delivered
+    stats_.bytes += cur.size;
+    stats_.chunks += 1;
+    return true;
+  }
+
+  bool ProcessOne(DeviceCSR<IndexType>* out, bool append) {
+    const size_t row_base = append ? out->rows_ : 0;
+    const size_t nnz_base = append ? out->nnz_ : 0;
+    ChunkPlan plan;
+    const bool token_format = tcfg_.format != TextFormat::kCSV;
+    const bool more = WithNextChunk([&](const char* text, size_t nbytes) {
+      bool done = false;
+      if (token_format && cfg_.fast_path) {
+        done = FastParse(text, nbytes, out, row_base, nnz_base, &plan);
+        if (!done) stats_.exact_chunks += 1;
+      }
+      if (!done) {
+        ExactParse(text, nbytes, out, row_base, nnz_base, &plan, token_format && cfg_.fast_path);
+      }
+    });
+    if (!more) return false;
     out->rows_ = row_base + plan.nrows;
     out->nnz_ = nnz_base + plan.nnz;
     if (acc_flags_ & kFlagWeight) out->has_weight_ = true;
     if (tcfg_.format == TextFormat::kCSV) out->has_value_ = out->nnz_ != 0;
     if (tcfg_.format == TextFormat::kLibFM) out->has_field_ = true;
-    stats_.bytes += nbytes;
-    stats_.chunks += 1;
     stats_.rows += plan.nrows;
     stats_.nnz += plan.nnz;
     return true;
+  }
+
+  void ParseAllHashed(DeviceHashedBatch* out, int dim, float scale, uint32_t seed,
+                      bool fp8) override {
+    CHECK(tcfg_.format != TextFormat::kCSV) << "hashed batches are built from LibSVM / LibFM";
+    CHECK(dim > 0 && dim % 4 == 0 && dim <= 4096) << "dim must be a multiple of 4 in (0, 4096]";
+    ScopedRange range("DeviceParser::ParseAllHashed");
+    out->device = device_;
+    out->dim = dim;
+    out->fp8 = fp8;
+    out->rows = 0;
+    hipStream_t s = compute_->get();
+    while (WithNextChunk([&](const char* text, size_t nbytes) {
+      // K1 line index, K2 row validity + K3 scan (as the exact CSR path), then
+      // the fused hash kernel writes rows straight into the dense batch
+      ChunkMeta* dmeta = meta_.get<ChunkMeta>();
+      DMLC_HIP_CHECK(hipMemsetAsync(dmeta, 0, sizeof(ChunkMeta), s));
+      LaunchLineCount(text, nbytes, tiles_.get<uint64_t>(), dmeta, s);
+      const size_t nlines = ReadBack<ChunkMeta>(dmeta).nlines;
+      AfterFirstSync();
+      EnsureLineBuffers(nlines);
+      LaunchLineEmit(text, nbytes, tiles_.get<uint64_t>(), lines_.get<uint32_t>(), s);
+      LaunchTextCount(text, nbytes, lines_.get<uint32_t>(), nlines, tcfg_, info_.get<uint64_t>(),
+                      slots_.get<MetaPartial>(), dmeta, s);
+      uint64_t* total = partials_.get<uint64_t>() + ScanPartials(nlines) + 1;
+      LaunchScanU64(info_.get<uint64_t>(), nlines, partials_.get<uint64_t>(), total, s);
+      LaunchMetaFromTotal(total, dmeta, s);
+      const size_t nrows = ReadBack<ChunkMeta>(dmeta).nrows;
+      out->Reserve(out->rows + nrows, s);
+      DMLC_HIP_CHECK(hipMemsetAsync(dmeta, 0, sizeof(ChunkMeta), s));
+      LaunchTextHashed<IndexType>(text, nbytes, lines_.get<uint32_t>(), nlines, tcfg_.format,
+                                  info_.get<uint64_t>(), out->rows, dim, scale, seed, fp8,
+                                  out->x.get(), out->label.get<float>(), slots_.get<MetaPartial>(),
+                                  dmeta, s);
+      const ChunkMeta m = ReadBack<ChunkMeta>(dmeta);
+      CHECK(!(m.flags & kFlagNegIndex)) << "negative feature index in " << cfg_.format << " input";
+      out->rows += nrows;
+      stats_.rows += nrows;
+    })) {
+    }
+    compute_->Synchronize();
   }
 
   /*! \brief publish the accumulated max / flags of this epoch */

@@ -81,13 +81,6 @@ __global__ __launch_bounds__(kThreads) void k_spmvt(const uint64_t* __restrict__
   }
 }
 
-__device__ __forceinline__ uint32_t hash_u64(uint64_t x, uint32_t seed) {
-  x ^= static_cast<uint64_t>(seed) * 0x9e3779b97f4a7c15ull;
-  x = (x ^ (x >> 33)) * 0xff51afd7ed558ccdull;
-  x = (x ^ (x >> 33)) * 0xc4ceb9fe1a85ec53ull;
-  x ^= x >> 33;
-  return static_cast<uint32_t>(x);
-}
 
 /*! \brief one row per wave; LDS row buffer of `dim` floats per wave */
 template <typename IndexType, bool kFP8>
@@ -106,9 +99,10 @@ __global__ __launch_bounds__(kThreads) void k_hashed_dense(
     dev::wave_sync();
     const uint64_t b = offset[r], e = offset[r + 1];
     for (uint64_t j = b + lane; j < e; j += dev::kWave) {
-      uint64_t key = static_cast<uint64_t>(index[j]);
-      if (field != nullptr) key ^= static_cast<uint64_t>(field[j]) << 40;
-      const uint32_t h = hash_u64(key, seed);
+      const uint64_t key = dev::hash_key(static_cast<uint64_t>(index[j]),
+                                         field != nullptr ? static_cast<uint64_t>(field[j]) : 0,
+                                         field != nullptr);
+      const uint32_t h = dev::hash_u64(key, seed);
       const int bucket = static_cast<int>(h % static_cast<uint32_t>(dim));
       const float sign = (h & 0x80000000u) ? -1.0f : 1.0f;
       const float v = value != nullptr ? value[j] : 1.0f;

@@ -222,6 +222,19 @@ template <typename IndexType>
 void LaunchHashedDenseF32(const uint64_t* offset, const IndexType* index, const float* value,
                           const IndexType* field, size_t nrows, int dim, uint32_t seed,
                           float* out, hipStream_t stream);
+/*!
+ * \brief K9 fused with the text walk (BASELINE config 5): every valid line of a
+ *  LibSVM / LibFM chunk becomes row row_base + (line_info >> 32) of a dense
+ *  [rows x dim] batch -- OCP fp8 e4m3 (x scale) or f32 -- with features
+ *  hashed exactly as LaunchHashedDense* does, plus its label; no CSR is
+ *  written.  line_starts / line_info as for LaunchTextFill (K1, K2 + K3).
+ *  dim: multiple of 4, <= 4096 (LDS row per wave).  Merges kFlagNegIndex.
+ */
+template <typename IndexType>
+void LaunchTextHashed(const char* text, size_t nbytes, const uint32_t* line_starts, size_t nlines,
+                      TextFormat format, const uint64_t* line_info, uint64_t row_base, int dim,
+                      float scale, uint32_t seed, bool fp8, void* out, float* labels,
+                      MetaPartial* partials, ChunkMeta* meta, hipStream_t stream);
 /*! \brief K11: y[r] = sum_j value * w[index] (+ bias), row per wave */
 template <typename IndexType>
 void LaunchCSRSpMV(const uint64_t* offset, const IndexType* index, const float* value,

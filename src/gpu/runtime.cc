@@ -4,6 +4,7 @@
  *  device -> host copies.
  */
 #include <dlfcn.h>
+#include <dmlc/gpu/device_parser.h>
 #include <dmlc/gpu/device_row_block.h>
 #include <dmlc/gpu/hip_utils.h>
 
@@ -92,6 +93,23 @@ void DeviceCSR<IndexType>::Reserve(size_t rows, size_t nnz, bool with_field, hip
   } else if (with_field && field_.bytes() < nnz_cap_ * sizeof(IndexType)) {
     field_.Grow(nnz_cap_ * sizeof(IndexType), used_nnz * sizeof(IndexType), stream);
   }
+}
+
+void DeviceHashedBatch::Reserve(size_t want, hipStream_t stream) {
+  if (want <= row_cap) return;
+  const size_t cap = std::max(want, row_cap * 2);
+  const size_t esize = fp8 ? 1 : sizeof(float);
+  DeviceBuffer nx(cap * static_cast<size_t>(dim) * esize), nl(cap * sizeof(float));
+  if (rows != 0) {
+    DMLC_HIP_CHECK(hipMemcpyAsync(nx.get(), x.get(), rows * static_cast<size_t>(dim) * esize,
+                                  hipMemcpyDeviceToDevice, stream));
+    DMLC_HIP_CHECK(hipMemcpyAsync(nl.get(), label.get(), rows * sizeof(float),
+                                  hipMemcpyDeviceToDevice, stream));
+  }
+  // the old buffers are freed only after the copies (hipFree synchronises)
+  x = std::move(nx);
+  label = std::move(nl);
+  row_cap = cap;
 }
 
 template <typename IndexType>

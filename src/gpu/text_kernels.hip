@@ -541,6 +541,130 @@ struct LineVisitor {
   }
 };
 
+/*!
+ * \brief K9 fused into the per-line walk: feature tokens are hashed straight
+ *  into the wave's LDS row (dim floats, ds_add_f32) -- no CSR in between.
+ */
+template <TextFormat F, typename IndexType>
+struct HashVisitor {
+  float* row;  // this wave's LDS accumulator
+  uint32_t dim, seed;
+  bool is_label_lane{false}, label_ok{false};
+  float label{0.0f};
+  int row_state{0};
+  bool neg{false};
+
+  __device__ uint32_t classify(const TokenRef& t, uint32_t ord) {
+    if (ord == 0) {
+      is_label_lane = true;
+      float l = 0.0f, wgt = 0.0f;
+      int r = 0;
+      if (t.has_digit) {
+        bool bad;
+        t.with_bytes([&](auto p, auto end) { r = data::ParsePair<float, float>(p, end, &l, &wgt, &bad); });
+      }
+      label_ok = r >= 1;
+      if (r >= 1) label = l;
+      return 0;
+    }
+    if (!t.has_digit) return 0;
+    uint64_t key = 0;
+    float v = 1.0f;
+    bool bad = false;
+    if constexpr (F == TextFormat::kLibSVM) {
+      if (ord == 1 && tok_is_qid(t)) return 0;
+      IndexType idx = 0;
+      float val = 0.0f;
+      int r = 0;
+      t.with_bytes([&](auto p, auto end) { r = data::ParsePair<IndexType, float>(p, end, &idx, &val, &bad); });
+      key = dev::hash_key(static_cast<uint64_t>(idx), 0, false);
+      v = r == 2 ? val : 1.0f;
+    } else {
+      if (!tok_two_parts(t)) return 0;
+      IndexType fid = 0, idx = 0;
+      float val = 0.0f;
+      int r = 0;
+      t.with_bytes([&](auto p, auto end) {
+        r = data::ParseTriple<IndexType, IndexType, float>(p, end, &fid, &idx, &val, &bad);
+      });
+      key = dev::hash_key(static_cast<uint64_t>(idx), static_cast<uint64_t>(fid), true);
+      v = r == 3 ? val : 1.0f;
+    }
+    neg |= bad;
+    const uint32_t h = dev::hash_u64(key, seed);
+    atomicAdd(&row[h % dim], (h & 0x80000000u) ? -v : v);
+    return 0;
+  }
+  __device__ bool selected(const TokenRef&, uint32_t) const { return false; }
+  __device__ void after_classify(uint32_t tok_base, uint32_t ntok) {
+    if (row_state == 0 && tok_base + ntok > 0) row_state = __ballot(label_ok) != 0 ? 1 : -1;
+  }
+  __device__ bool emit_enabled() const { return false; }
+  __device__ void emit(const TokenRef&, uint32_t, uint32_t) {}
+};
+
+/*!
+ * \brief fused LibSVM / LibFM text -> hashed dense batch (BASELINE config 5):
+ *  one wave per line walks the line (exact tokenizer), hashes every feature
+ *  into its LDS row, then writes the row once -- OCP fp8 e4m3 (gfx950
+ *  v_cvt_pk_fp8_f32, 4 columns per 32-bit store) or f32 -- plus its label.
+ *  Rows are the valid lines (line_info scanned by K3, as for the CSR fill).
+ */
+template <TextFormat F, typename IndexType, bool kFP8>
+__global__ __launch_bounds__(kThreads) void k_text_hash(const uint8_t* __restrict__ text, size_t n,
+                                                        const uint32_t* __restrict__ line_starts,
+                                                        size_t nlines, const uint64_t* __restrict__ line_info,
+                                                        uint64_t row_base, int dim, float scale,
+                                                        uint32_t seed, void* __restrict__ out,
+                                                        float* __restrict__ labels,
+                                                        MetaPartial* __restrict__ partials) {
+  __shared__ uint4 lds[kWavesPerBlock][kWindow / 16];
+  extern __shared__ __attribute__((aligned(16))) float rows[];
+  const int wid = threadIdx.x / dev::kWave;
+  const int lane = dev::lane_id();
+  uint8_t* win = reinterpret_cast<uint8_t*>(lds[wid]);
+  float* row = rows + static_cast<size_t>(wid) * dim;
+  for (int c = lane; c < dim; c += dev::kWave) row[c] = 0.0f;
+  dev::wave_sync();
+  const size_t nwaves = static_cast<size_t>(gridDim.x) * kWavesPerBlock;
+  bool wneg = false;
+  for (size_t line = static_cast<size_t>(blockIdx.x) * kWavesPerBlock + wid; line < nlines;
+       line += nwaves) {
+    const uint32_t b = line_starts[line];
+    const uint32_t e = line + 1 < nlines ? line_starts[line + 1] : static_cast<uint32_t>(n);
+    HashVisitor<F, IndexType> vis;
+    vis.row = row;
+    vis.dim = static_cast<uint32_t>(dim);
+    vis.seed = seed;
+    walk_line<F, false>(text, b, e, win, ' ', vis);
+    wneg |= vis.neg;
+    dev::wave_sync();  // every ds_add of the line is done
+    if (vis.row_state == 1) {
+      const uint64_t r = row_base + (line_info[line] >> 32);
+      const uint64_t lmask = __ballot(vis.is_label_lane);
+      const int ll = lmask ? __ffsll(static_cast<long long>(lmask)) - 1 : 0;
+      const float label = lmask ? __shfl(vis.label, ll, dev::kWave) : 0.0f;
+      if (lane == 0) labels[r] = label;
+      if constexpr (kFP8) {
+        uint32_t* o = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(out) + r * dim);
+        for (int c = lane * 4; c < dim; c += dev::kWave * 4) {
+          int packed = __builtin_amdgcn_cvt_pk_fp8_f32(row[c] * scale, row[c + 1] * scale, 0, false);
+          packed = __builtin_amdgcn_cvt_pk_fp8_f32(row[c + 2] * scale, row[c + 3] * scale, packed,
+                                                   true);
+          o[c / 4] = static_cast<uint32_t>(packed);
+        }
+      } else {
+        float* o = static_cast<float*>(out) + r * dim;
+        for (int c = lane; c < dim; c += dev::kWave) o[c] = row[c];
+      }
+    }
+    dev::wave_sync();
+    for (int c = lane; c < dim; c += dev::kWave) row[c] = 0.0f;
+    dev::wave_sync();
+  }
+  dev::block_store_partial(0ull, 0ull, wneg ? kFlagNegIndex : 0u, partials);
+}
+
 // ------------------------------------------------------------------ K2
 template <TextFormat F>
 __global__ __launch_bounds__(kThreads) void k_text_count(const uint8_t* __restrict__ text, size_t n,
@@ -738,6 +862,43 @@ void LaunchTextFill(const char* text, size_t nbytes, const uint32_t* line_starts
   }
   LaunchCloseOffsets(out.offset, out.row_base + nrows, out.nnz_base + nnz, stream);
 }
+
+template <typename IndexType>
+void LaunchTextHashed(const char* text, size_t nbytes, const uint32_t* line_starts, size_t nlines,
+                      TextFormat format, const uint64_t* line_info, uint64_t row_base, int dim,
+                      float scale, uint32_t seed, bool fp8, void* out, float* labels,
+                      MetaPartial* partials, ChunkMeta* meta, hipStream_t stream) {
+  if (nlines == 0) return;
+  const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
+  const dim3 grid(LineGrid(nlines)), block(kThreads);
+  const size_t smem = static_cast<size_t>(kWavesPerBlock) * dim * sizeof(float);
+#define DMLC_HASH_LAUNCH(FMT, FP8)                                                              \
+  hipLaunchKernelGGL((k_text_hash<FMT, IndexType, FP8>), grid, block, smem, stream, t, nbytes, \
+                     line_starts, nlines, line_info, row_base, dim, scale, seed, out, labels,    \
+                     partials)
+  if (format == TextFormat::kLibFM) {
+    if (fp8) {
+      DMLC_HASH_LAUNCH(TextFormat::kLibFM, true);
+    } else {
+      DMLC_HASH_LAUNCH(TextFormat::kLibFM, false);
+    }
+  } else {
+    if (fp8) {
+      DMLC_HASH_LAUNCH(TextFormat::kLibSVM, true);
+    } else {
+      DMLC_HASH_LAUNCH(TextFormat::kLibSVM, false);
+    }
+  }
+#undef DMLC_HASH_LAUNCH
+  LaunchReducePartials(partials, static_cast<int>(grid.x), meta, stream);
+}
+
+template void LaunchTextHashed<uint32_t>(const char*, size_t, const uint32_t*, size_t, TextFormat,
+                                         const uint64_t*, uint64_t, int, float, uint32_t, bool,
+                                         void*, float*, MetaPartial*, ChunkMeta*, hipStream_t);
+template void LaunchTextHashed<uint64_t>(const char*, size_t, const uint32_t*, size_t, TextFormat,
+                                         const uint64_t*, uint64_t, int, float, uint32_t, bool,
+                                         void*, float*, MetaPartial*, ChunkMeta*, hipStream_t);
 
 void LaunchCloseOffsets(uint64_t* offset, uint64_t row_end, uint64_t nnz_end, hipStream_t stream) {
   hipLaunchKernelGGL(k_close_offsets, dim3(1), dim3(1), 0, stream, offset, row_end, nnz_end);

@@ -392,6 +392,26 @@ class PyDeviceParser {
     py::gil_scoped_release nogil;
     p_->ParseAll(out.csr_.get());
   }
+  /*! \brief fused tokenize -> hash -> fp8/f32 dense batch; DLPack capsules */
+  py::dict ParseAllHashed(int dim, float scale, uint32_t seed, bool fp8) {
+    auto batch = std::make_shared<gpu::DeviceHashedBatch>();
+    {
+      py::gil_scoped_release nogil;
+      p_->ParseAllHashed(batch.get(), dim, scale, seed, fp8);
+    }
+    py::dict d;
+    const int64_t n = static_cast<int64_t>(batch->rows) * dim;
+    if (fp8) {
+      d["x"] = ToCapsule(batch->x.get<uint8_t>(), n, batch->device, batch);
+    } else {
+      d["x"] = ToCapsule(batch->x.get<float>(), n, batch->device, batch);
+    }
+    d["label"] = ToCapsule(batch->label.get<float>(), static_cast<int64_t>(batch->rows),
+                           batch->device, batch);
+    d["rows"] = batch->rows;
+    d["dim"] = dim;
+    return d;
+  }
   bool Next() {
     py::gil_scoped_release nogil;
     return p_->Next();
@@ -482,6 +502,8 @@ void BindIndexType(py::module_& m, const std::string& suffix) {
       .def(py::init<const std::string&, unsigned, unsigned, py::dict>(), py::arg("uri"),
            py::arg("part") = 0, py::arg("nparts") = 1, py::arg("config") = py::dict())
       .def("parse_all", &PyDeviceParser<I>::ParseAll)
+      .def("parse_all_hashed", &PyDeviceParser<I>::ParseAllHashed, py::arg("dim"),
+           py::arg("scale") = 1.0f, py::arg("seed") = 0u, py::arg("fp8") = true)
       .def("next", &PyDeviceParser<I>::Next)
       .def("value_to_host", &PyDeviceParser<I>::ValueToHost)
       .def("value_shape", &PyDeviceParser<I>::ValueShape)

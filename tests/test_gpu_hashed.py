@@ -1,0 +1,110 @@
+"""BASELINE config 5: LibFM / LibSVM -> signed feature hash -> dense fp8 batch.
+
+* an independent numpy implementation of the K9 hash (murmur3 fmix64 of
+  index ^ field << 40 mixed with the seed; bucket = h % dim, sign = bit 31)
+  and an fp64 accumulation are the reference;
+* the CSR path (tile parser + ops.hashed_dense, K9) and the FUSED path
+  (GPUParser.parse_all_hashed: tokenize -> hash -> fp8 in one kernel, no CSR)
+  must both match it: identical buckets and signs, f32 sums to 1e-6, and fp8
+  equal to torch's e4m3fn cast of the reference (except at rounding ties of
+  buckets that several features share, where the f32 summation order shows);
+* HashedFM on the fused fp8 batch matches its fp32 reference.
+"""
+import numpy as np
+import pytest
+import torch
+
+from dmlc_core_amd import data, ops
+from dmlc_core_amd.models import HashedFM
+
+pytestmark = pytest.mark.gpu
+M64 = (1 << 64) - 1
+
+
+def ref_hash(keys: np.ndarray, seed: int) -> np.ndarray:
+    x = [int(k) for k in keys]
+    out = np.empty(len(x), dtype=np.uint64)
+    s = (seed * 0x9E3779B97F4A7C15) & M64
+    for i, v in enumerate(x):
+        v ^= s
+        v = ((v ^ (v >> 33)) * 0xFF51AFD7ED558CCD) & M64
+        v = ((v ^ (v >> 33)) * 0xC4CEB9FE1A85EC53) & M64
+        v ^= v >> 33
+        out[i] = v & 0xFFFFFFFF
+    return out
+
+
+def ref_dense(host, dim, seed, libfm):
+    rows = len(host["label"])
+    off = host["offset"].astype(np.int64)
+    idx = host["index"].astype(np.uint64)
+    val = (host["value"].astype(np.float64) if host.get("value") is not None
+           else np.ones(len(idx)))
+    keys = idx ^ (host["field"].astype(np.uint64) << np.uint64(40)) if libfm else idx
+    h = ref_hash(keys, seed)
+    bucket = (h % np.uint64(dim)).astype(np.int64)
+    sign = np.where(h & np.uint64(0x80000000), -1.0, 1.0)
+    rowid = np.repeat(np.arange(rows), np.diff(off))
+    out = np.zeros((rows, dim), dtype=np.float64)
+    np.add.at(out, (rowid, bucket), sign * val)
+    share = np.zeros((rows, dim), dtype=np.int64)
+    np.add.at(share, (rowid, bucket), 1)
+    return out, share
+
+
+@pytest.fixture(scope="module", params=["libfm", "libsvm"])
+def dataset(request, tmp_path_factory):
+    fmt = request.param
+    p = str(tmp_path_factory.mktemp("h") / f"d.{fmt}")
+    data.write_synthetic(p, 0, 1500, format=fmt, seed=9)
+    host = data.GPUParser(p, format=fmt, chunk_bytes=128 * 1024).parse_all().to_host()
+    return fmt, p, host
+
+
+@pytest.mark.parametrize("dim,seed", [(256, 0), (1024, 7)])
+def test_k9_and_fused_match_independent_hash(dataset, dim, seed):
+    fmt, p, host = dataset
+    libfm = fmt == "libfm"
+    ref, share = ref_dense(host, dim, seed, libfm)
+    # CSR path: tile parser -> K9
+    csr = data.csr_to_torch(data.GPUParser(p, format=fmt, chunk_bytes=128 * 1024).parse_all())
+    k9 = ops.hashed_dense(csr, dim, seed=seed, fp8=False).cpu().numpy().astype(np.float64)
+    # fused path, f32 and fp8
+    fused = data.GPUParser(p, format=fmt, chunk_bytes=128 * 1024).parse_all_hashed(
+        dim, seed=seed, fp8=False)
+    f32 = fused["x"].cpu().numpy().astype(np.float64)
+    np.testing.assert_array_equal(fused["label"].cpu().numpy(), host["label"])
+    for got in (k9, f32):
+        assert got.shape == ref.shape
+        np.testing.assert_array_equal(got != 0, ref != 0)  # same buckets, no extra mass
+        np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-6)
+    scale = 0.5
+    f8 = data.GPUParser(p, format=fmt, chunk_bytes=128 * 1024).parse_all_hashed(
+        dim, seed=seed, fp8=True, scale=scale)["x"]
+    assert f8.dtype == torch.float8_e4m3fn and tuple(f8.shape) == ref.shape
+    want = torch.from_numpy((ref * scale).astype(np.float32)).to(torch.float8_e4m3fn)
+    same = (f8.cpu().view(torch.uint8) == want.view(torch.uint8)).numpy()
+    assert same[share <= 2].all()  # one or two terms: the f32 sum is exact
+    assert same.mean() > 0.999
+
+
+def test_hashed_fm_on_fused_fp8_batch(dataset):
+    fmt, p, _ = dataset
+    scale = 0.25
+    b = data.GPUParser(p, format=fmt).parse_all_hashed(512, seed=1, fp8=True, scale=scale)
+    torch.manual_seed(0)
+    model = HashedFM(dim=512, rank=16).cuda()
+    with torch.no_grad():
+        model.w.normal_(0, 0.05)
+        model.bias.fill_(0.1)
+    y = model(b["x"], scale=scale)
+    x = b["x"].float() / scale
+    ref = HashedFM.reference(x, model.w.detach(), model.v.detach(), model.bias.detach())
+    err = (y.detach() - ref).abs().max().item() / (ref.abs().max().item() + 1e-6)
+    assert model.gemm in ("fp8", "bf16")
+    assert err < 0.05, (err, model.gemm)  # fp8 weights + bf16 interaction term
+    loss = torch.nn.functional.binary_cross_entropy_with_logits(y, b["label"].clamp(0, 1))
+    loss.backward()
+    assert model.w.grad is not None and torch.isfinite(model.w.grad).all()
+    assert model.v.grad is not None and torch.isfinite(model.v.grad).all()
+    print("HashedFM gemm path:", model.gemm)
