@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""BASELINE config 5: LibFM -> hashed fp8 dense batch on one MI355X.
+
+Times (a) the two-step path, tile parser -> device CSR -> K9 hashed_dense, and
+(b) the fused kernel (GPUParser.parse_all_hashed: tokenize -> hash -> fp8,
+no CSR), both over text already resident in HBM (hbm_cache, warm epoch
+first), plus HashedFM forward+backward on the batch.  Prints one JSON line.
+
+usage: python scripts/bench_hashed.py [--rows N] [--dim D] [--steps K]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=2_000_000)
+    ap.add_argument("--dim", type=int, default=1024)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--data", default="/tmp/dmlc_hashed_bench.libfm")
+    args = ap.parse_args()
+    import torch
+
+    from dmlc_core_amd import data, ops
+    from dmlc_core_amd.models import HashedFM
+
+    if not os.path.exists(args.data):
+        data.write_synthetic(args.data + ".tmp", 0, args.rows, format="libfm", seed=0, nthread=16)
+        os.replace(args.data + ".tmp", args.data)
+    nbytes = os.path.getsize(args.data)
+    two = data.GPUParser(args.data, format="libfm", hbm_cache=1)
+    fused = data.GPUParser(args.data, format="libfm", hbm_cache=1)
+
+    def step_two():
+        two.before_first()
+        csr = two.parse_all()
+        return ops.hashed_dense(data.csr_to_torch(csr), args.dim, seed=1, fp8=True, scale=0.5)
+
+    def step_fused():
+        fused.before_first()
+        return fused.parse_all_hashed(args.dim, seed=1, fp8=True, scale=0.5)["x"]
+
+    res = {}
+    for name, fn in (("csr_then_k9", step_two), ("fused", step_fused)):
+        fn()  # warm: fills the HBM cache
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            x = fn()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / args.steps
+        res[name] = {"ms": round(dt * 1e3, 3), "rows_per_sec": round(x.shape[0] / dt, 1),
+                     "text_GBps": round(nbytes / dt / 1e9, 2)}
+    a = step_two().view(torch.uint8)
+    b = step_fused().view(torch.uint8)
+    res["identical_fp8"] = bool(torch.equal(a, b))
+    res["mismatch_frac"] = float((a != b).float().mean())
+    model = HashedFM(dim=args.dim, rank=16).cuda()
+    fused.before_first()
+    batch = fused.parse_all_hashed(args.dim, seed=1, fp8=True, scale=0.5)
+    y = model(batch["x"], scale=0.5)
+    loss = torch.nn.functional.binary_cross_entropy_with_logits(y, batch["label"].clamp(0, 1))
+    loss.backward()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        model.zero_grad()
+        y = model(batch["x"], scale=0.5)
+        loss = torch.nn.functional.binary_cross_entropy_with_logits(y, batch["label"].clamp(0, 1))
+        loss.backward()
+    torch.cuda.synchronize()
+    res["hashed_fm_step_ms"] = round((time.perf_counter() - t0) / args.steps * 1e3, 3)
+    res["hashed_fm_gemm"] = model.gemm
+    res.update({"rows": int(batch["x"].shape[0]), "dim": args.dim, "text_bytes": nbytes,
+                "speedup_fused_vs_csr_k9": round(res["csr_then_k9"]["ms"] / res["fused"]["ms"], 3)})
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

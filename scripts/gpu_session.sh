@@ -29,6 +29,15 @@ if [[ $STAGES == *bench* ]]; then
     [ $rc -eq 0 ] || exit $rc
   fi
 fi
+if [[ $STAGES == *hashed* ]]; then
+  timeout -k 10 600 python scripts/bench_hashed.py ${HASHED_ARGS:-} > $OUT/hashed.json 2> $OUT/hashed.err
+  rc=$?; echo "hashed rc=$rc"; cat $OUT/hashed.json; tail -5 $OUT/hashed.err
+  [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_hashed -o run --output-format csv -- \
+    python3 scripts/bench_hashed.py --steps 1 ${HASHED_ARGS:-} > $OUT/prof_hashed.log 2>&1
+  rc=$?; echo "rocprof hashed rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+fi
 PROF_ARGS="${PROF_ARGS:---steps 2 --warmup 1}"
 if [[ $STAGES == *prof* ]]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \

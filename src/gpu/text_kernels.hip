@@ -576,7 +576,9 @@ struct HashVisitor {
       IndexType idx = 0;
       float val = 0.0f;
       int r = 0;
-      t.with_bytes([&](auto p, auto end) { r = data::ParsePair<IndexType, float>(p, end, &idx, &val, &bad); });
+      t.with_bytes([&](auto p, auto end) {
+        r = data::ParsePair<IndexType, float>(p, end, &idx, &val, &bad);
+      });
       key = dev::hash_key(static_cast<uint64_t>(idx), 0, false);
       v = r == 2 ? val : 1.0f;
     } else {
