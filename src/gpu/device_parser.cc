@@ -630,14 +630,44 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     out->fp8 = fp8;
     out->rows = 0;
     hipStream_t s = compute_->get();
+    merge_replay_ = true;  // resident text: parse adjacent cached chunks together
+    struct Unmerge {
+      bool* f;
+      ~Unmerge() { *f = false; }
+    } unmerge{&merge_replay_};
     while (WithNextChunk([&](const char* text, size_t nbytes) {
-      // K1 line index, K2 row validity + K3 scan (as the exact CSR path), then
-      // the fused hash kernel writes rows straight into the dense batch
       ChunkMeta* dmeta = meta_.get<ChunkMeta>();
+      if (cfg_.fast_path) {
+        // tile parser: C1 + C2 sizes, then the fused tile kernel builds the
+        // rows of the lines each workgroup owns
+        ChunkMeta* hm = hmap_.get<ChunkMeta>();
+        LaunchTileCountScan(text, nbytes, tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(), dmeta,
+                            hm, s);
+        const ChunkMeta sizes = WaitMapped(hm);
+        AfterFirstSync();
+        if (!(sizes.flags & kFlagIrregular)) {
+          out->Reserve(out->rows + sizes.nrows, s);
+          LaunchTileHashed<IndexType>(text, nbytes, tcfg_.format, tcounts_.get<uint64_t>(),
+                                      out->rows, dim, scale, seed, fp8, out->x.get(),
+                                      out->label.get<float>(), slots_.get<MetaPartial>(), dmeta,
+                                      hm, s);
+          const ChunkMeta m = WaitMapped(hm);
+          CHECK(!(m.flags & kFlagNegIndex)) << "negative feature index in " << cfg_.format
+                                            << " input";
+          if (!(m.flags & kFlagIrregular)) {
+            out->rows += sizes.nrows;
+            stats_.rows += sizes.nrows;
+            return;
+          }
+        }
+        stats_.exact_chunks += 1;
+      }
+      // K1 line index, K2 row validity + K3 scan (as the exact CSR path), then
+      // the fused per-line hash kernel writes rows straight into the batch
       DMLC_HIP_CHECK(hipMemsetAsync(dmeta, 0, sizeof(ChunkMeta), s));
       LaunchLineCount(text, nbytes, tiles_.get<uint64_t>(), dmeta, s);
       const size_t nlines = ReadBack<ChunkMeta>(dmeta).nlines;
-      AfterFirstSync();
+      if (!cfg_.fast_path) AfterFirstSync();
       EnsureLineBuffers(nlines);
       LaunchLineEmit(text, nbytes, tiles_.get<uint64_t>(), lines_.get<uint32_t>(), s);
       LaunchTextCount(text, nbytes, lines_.get<uint32_t>(), nlines, tcfg_, info_.get<uint64_t>(),

@@ -176,6 +176,20 @@ void LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
                     MetaPartial* partials, ChunkMeta* meta, ChunkMeta* host_meta,
                     hipStream_t stream);
 
+/*!
+ * \brief fused tokenize -> hash -> dense rows on the tile parser (config 5):
+ *  rows = the lines of a regular chunk (tile_prefix from LaunchTileCountScan),
+ *  row row_base + line of a [rows x dim] fp8 (x scale) or f32 batch, labels
+ *  alongside; no CSR is written.  Sets kFlagIrregular when a line runs more
+ *  than 4 KiB past its tile (re-run the chunk with LaunchTextHashed), merges
+ *  kFlagNegIndex.  dim: multiple of 4, <= 4096.
+ */
+template <typename IndexType>
+void LaunchTileHashed(const char* text, size_t nbytes, TextFormat format,
+                      const uint64_t* tile_prefix, uint64_t row_base, int dim, float scale,
+                      uint32_t seed, bool fp8, void* out, float* labels, MetaPartial* partials,
+                      ChunkMeta* meta, ChunkMeta* host_meta, hipStream_t stream);
+
 // ----------------------------- RecordIO (K7) -----------------------------
 /*! \brief error bits reported by the RecordIO kernels */
 constexpr uint32_t kRecErrTruncated = 1;   // a part runs past the chunk end

@@ -657,6 +657,230 @@ __global__ __launch_bounds__(kThreads) void k_tile_fill(const uint8_t* __restric
 }
 
 /*!
+ * \brief fused tokenize -> hash -> dense row (BASELINE config 5) on the tile
+ *  parser: workgroup t OWNS the lines that start in tile t.  It stages the
+ *  tile plus a 4 KiB extension (the rest of its last line) in LDS, compacts the
+ *  tokens of its own lines, and builds kRows rows at a time in LDS (dim floats
+ *  each, ds_add_f32 of +-value into bucket hash % dim), then writes each row
+ *  once -- OCP fp8 e4m3 (v_cvt_pk_fp8_f32, 4 columns per 32-bit store) or
+ *  f32 -- with its label.  No CSR is written.  A line running past the
+ *  extension sets kFlagIrregular (the caller re-runs the chunk on the exact
+ *  per-line kernel).
+ */
+constexpr int kHashExt = 4096;                            // bytes staged past the tile
+constexpr int kHashSegs = (static_cast<int>(kTileBytes) + kHashExt) / 4096;
+constexpr int kHashRows = 4;                              // rows built per LDS round
+constexpr unsigned kHashOffBits = 14;                     // staged offset < 12288
+
+template <TextFormat F, typename IndexType, bool kFP8>
+__global__ __launch_bounds__(kThreads) void k_tile_hash(const uint8_t* __restrict__ text, size_t n,
+                                                        const uint64_t* __restrict__ prefix,
+                                                        uint64_t row_base, int dim, float scale,
+                                                        uint32_t seed, void* __restrict__ out,
+                                                        float* __restrict__ labels,
+                                                        MetaPartial* __restrict__ partials) {
+  __shared__ uint4 s_text[(kTileBytes + kHashExt) / 16 + 4];
+  __shared__ uint32_t s_tok[(kTileBytes + kHashExt) / 2];
+  __shared__ uint32_t s_scan[4];
+  __shared__ uint32_t s_end;  // staged offset where the owned region ends
+  extern __shared__ __attribute__((aligned(16))) float s_rows[];
+  const uint8_t* lds = reinterpret_cast<const uint8_t*>(s_text);
+  const size_t tile0 = static_cast<size_t>(blockIdx.x) * kTileBytes;
+  const uint64_t line_base = prefix[blockIdx.x] >> 32;
+  const uint32_t staged_end = static_cast<uint32_t>(
+      n - tile0 < kTileBytes + kHashExt ? n - tile0 : kTileBytes + kHashExt);
+  if (threadIdx.x == 0) s_end = 0xFFFFFFFFu;
+
+  // ---- stage tile + extension; bytes at or past n are zero in LDS
+  uint4 v[kHashSegs];
+  uint32_t pc[kHashSegs];
+#pragma unroll
+  for (int s = 0; s < kHashSegs; ++s) {
+    const size_t pos = tile0 + s * 4096 + threadIdx.x * 16;
+    v[s] = load16(text, pos, n);
+    pc[s] = prev_byte(text, pos, v[s]);
+    if (pos < n && n - pos < 16) {  // the segment straddling n: clear its tail
+      uint32_t w[4] = {v[s].x, v[s].y, v[s].z, v[s].w};
+      const uint32_t keep = static_cast<uint32_t>(n - pos);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int lo = 4 * q;
+        if (static_cast<int>(keep) <= lo) {
+          w[q] = 0;
+        } else if (static_cast<int>(keep) < lo + 4) {
+          w[q] &= (1u << (8 * (keep - lo))) - 1u;
+        }
+      }
+      v[s] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    s_text[s * 256 + threadIdx.x] = v[s];
+  }
+  // ---- compact the tokens of the owned lines (line starts in the tile)
+  uint32_t carry = 0;
+  uint32_t nlines_tile = 0;
+#pragma unroll
+  for (int s = 0; s < kHashSegs; ++s) {
+    const size_t pos = tile0 + s * 4096 + threadIdx.x * 16;
+    uint32_t lm, tm;
+    (void)lane_masks<false>(v[s], pc[s], pos, n, &lm, &tm);
+    const bool ext = s * 4096 >= static_cast<int>(kTileBytes);
+    if (ext && lm != 0) atomicMin(&s_end, static_cast<uint32_t>(s * 4096 + threadIdx.x * 16 +
+                                                                 __ffs(lm) - 1));
+    const uint32_t mine = (static_cast<uint32_t>(__popc(lm)) << 16) | __popc(tm);
+    uint32_t tot;
+    const uint32_t before = dev::block_excl_scan_256<uint32_t>(mine, s_scan, &tot) + carry;
+    uint32_t line = before >> 16;
+    uint32_t tok = before & 0xffffu;
+    uint32_t all = lm | tm;
+    while (all != 0) {
+      const int j = __ffs(all) - 1;
+      all &= all - 1;
+      const uint32_t bit = 1u << j;
+      const uint32_t off = static_cast<uint32_t>(s * 4096 + threadIdx.x * 16 + j);
+      if (lm & bit) ++line;
+      if (tm & bit) {  // every token is listed; those at or past `end` are skipped later
+        const uint32_t label = (lm & bit) ? 1u : 0u;
+        s_tok[tok] = off | (line << kHashOffBits) | (label << 31);
+        ++tok;
+      }
+    }
+    carry += tot;
+    if (!ext) nlines_tile = carry >> 16;
+    __syncthreads();
+  }
+  const uint32_t end = s_end;  // first line start in the extension (barrier above)
+  const uint32_t ntok = carry & 0xffffu;
+  bool irregular = false;
+  if (end == 0xFFFFFFFFu && staged_end == kTileBytes + kHashExt && tile0 + staged_end < n &&
+      nlines_tile != 0) {
+    irregular = true;  // the last owned line runs past the extension
+  }
+  const uint32_t lim = end == 0xFFFFFFFFu ? staged_end : end;
+  float* rows = s_rows;
+  bool neg = false;
+  // ---- decode every owned token ONCE: labels are written out, features
+  // become (row in tile << 12 | bucket) in s_tok and their signed value in a
+  // register, later spilled to LDS over the (no longer needed) text
+  constexpr uint32_t kNone = 0xFFFFFFFFu;
+  constexpr int kPerLane = 4;  // tokens per lane held in registers (ntok <= 1024)
+  float vals[kPerLane];
+  const bool one_pass = ntok <= static_cast<uint32_t>(kPerLane * kThreads);
+  auto decode = [&](uint32_t i, uint32_t* res, float* sval) {
+    *res = kNone;
+    const uint32_t e = s_tok[i];
+    const uint32_t off = e & ((1u << kHashOffBits) - 1);
+    const uint32_t lcnt = (e >> kHashOffBits) & 0x1FFFu;
+    if (off >= lim || lcnt == 0) return;  // outside the owned lines
+    const bool is_label = (e >> 31) & 1u;
+    int r = 0;
+    uint64_t u0 = 0, u1 = 0;
+    float f0 = 0.0f, f1 = 0.0f;
+    bool bad = false;
+    if (!fast_token<F>(lds, off, is_label, &r, &u0, &u1, &f0, &f1)) {
+      const uint8_t* l = lds + lim;
+      auto b = sep_begin(lds + off, l);
+      auto en = sep_end(l);
+      if (is_label) {
+        r = data::ParsePair<float, float>(b, en, &f0, &f1, &bad);
+      } else if constexpr (F == TextFormat::kLibSVM) {
+        IndexType idx = 0;
+        r = data::ParsePair<IndexType, float>(b, en, &idx, &f0, &bad);
+        u0 = idx;
+      } else {
+        IndexType fid = 0, idx = 0;
+        r = data::ParseTriple<IndexType, IndexType, float>(b, en, &fid, &idx, &f0, &bad);
+        u0 = fid;
+        u1 = idx;
+      }
+    }
+    if (is_label) {
+      labels[row_base + line_base + lcnt - 1] = f0;
+      return;
+    }
+    uint64_t key;
+    float val;
+    if constexpr (F == TextFormat::kLibSVM) {
+      key = dev::hash_key(static_cast<uint64_t>(static_cast<IndexType>(u0)), 0, false);
+      val = r == 2 ? f0 : 1.0f;
+    } else {
+      if (r < 2) return;  // not a field:index token (the CPU parser skips it too)
+      key = dev::hash_key(static_cast<uint64_t>(static_cast<IndexType>(u1)),
+                          static_cast<uint64_t>(static_cast<IndexType>(u0)), true);
+      val = r == 3 ? f0 : 1.0f;
+    }
+    neg |= bad;
+    const uint32_t h = dev::hash_u64(key, seed);
+    *res = ((lcnt - 1) << 12) | (h % static_cast<uint32_t>(dim));
+    *sval = (h & 0x80000000u) ? -val : val;
+  };
+  float* s_val = reinterpret_cast<float*>(s_text);  // overlays the text after decoding
+  if (one_pass && !irregular) {
+#pragma unroll
+    for (int k = 0; k < kPerLane; ++k) {
+      const uint32_t i = threadIdx.x + k * kThreads;
+      vals[k] = 0.0f;
+      if (i < ntok) {
+        uint32_t res;
+        decode(i, &res, &vals[k]);
+        s_tok[i] = res;  // same lane reads and rewrites entry i
+      }
+    }
+    __syncthreads();  // every lane is done reading the text
+#pragma unroll
+    for (int k = 0; k < kPerLane; ++k) {
+      const uint32_t i = threadIdx.x + k * kThreads;
+      if (i < ntok) s_val[i] = vals[k];
+    }
+  }
+  for (uint32_t r0 = 0; r0 < nlines_tile && !irregular; r0 += kHashRows) {
+    for (int c = threadIdx.x; c < kHashRows * dim; c += kThreads) rows[c] = 0.0f;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < ntok; i += kThreads) {
+      uint32_t res;
+      float sv = 0.0f;
+      if (one_pass) {
+        res = s_tok[i];
+        if (res == kNone) continue;
+        sv = s_val[i];
+      } else {
+        // many tiny tokens: decode again in every round (rare)
+        const uint32_t lcnt = (s_tok[i] >> kHashOffBits) & 0x1FFFu;
+        if (lcnt - 1 - r0 >= static_cast<uint32_t>(kHashRows)) continue;
+        decode(i, &res, &sv);
+        if (res == kNone) continue;
+      }
+      const uint32_t lr = (res >> 12) - r0;
+      if (lr >= static_cast<uint32_t>(kHashRows)) continue;
+      atomicAdd(&rows[lr * dim + (res & 0xFFFu)], sv);
+    }
+    __syncthreads();
+    const uint32_t nr = nlines_tile - r0 < static_cast<uint32_t>(kHashRows) ? nlines_tile - r0
+                                                                           : kHashRows;
+    for (uint32_t j = 0; j < nr; ++j) {
+      const uint64_t row = row_base + line_base + r0 + j;
+      const float* src = rows + j * dim;
+      if constexpr (kFP8) {
+        uint32_t* o = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(out) + row * dim);
+        for (int c = threadIdx.x * 4; c < dim; c += kThreads * 4) {
+          int packed = __builtin_amdgcn_cvt_pk_fp8_f32(src[c] * scale, src[c + 1] * scale, 0, false);
+          packed = __builtin_amdgcn_cvt_pk_fp8_f32(src[c + 2] * scale, src[c + 3] * scale, packed,
+                                                   true);
+          o[c / 4] = static_cast<uint32_t>(packed);
+        }
+      } else {
+        float* o = static_cast<float*>(out) + row * dim;
+        for (int c = threadIdx.x; c < dim; c += kThreads) o[c] = src[c];
+      }
+    }
+    __syncthreads();
+  }
+  unsigned fl = 0;
+  if (irregular) fl |= kFlagIrregular;
+  if (neg) fl |= kFlagNegIndex;
+  dev::block_store_partial(0ull, 0ull, fl, partials);
+}
+
+/*!
  * \brief fold the per-workgroup slots into meta; closing row pointer.  One
  *  1024-lane workgroup, 8 independent slot loads per lane per step (a
  *  latency-bound single-workgroup pass otherwise dominates small chunks).
@@ -708,7 +932,7 @@ __global__ __launch_bounds__(kFinishThreads) void k_tile_finish(
     meta->max_index = s_mi[0];
     meta->max_field = s_mf[0];
     meta->flags |= s_fl[0];
-    offset[row_base + meta->nrows] = nnz_base + meta->nnz;
+    if (offset != nullptr) offset[row_base + meta->nrows] = nnz_base + meta->nnz;
     if (host_meta != nullptr) *host_meta = *meta;
   }
 }
@@ -750,6 +974,45 @@ void LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
                      static_cast<int>(ntiles), meta, host_meta, out.offset, out.row_base,
                      out.nnz_base);
 }
+
+template <typename IndexType>
+void LaunchTileHashed(const char* text, size_t nbytes, TextFormat format,
+                      const uint64_t* tile_prefix, uint64_t row_base, int dim, float scale,
+                      uint32_t seed, bool fp8, void* out, float* labels, MetaPartial* partials,
+                      ChunkMeta* meta, ChunkMeta* host_meta, hipStream_t stream) {
+  const size_t ntiles = TileCount(nbytes);
+  const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
+  const size_t smem = static_cast<size_t>(kHashRows) * dim * sizeof(float);
+  if (ntiles != 0) {
+#define DMLC_TILE_HASH(FMT, FP8)                                                               \
+  hipLaunchKernelGGL((k_tile_hash<FMT, IndexType, FP8>), dim3(ntiles), dim3(kThreads), smem,  \
+                     stream, t, nbytes, tile_prefix, row_base, dim, scale, seed, out, labels,  \
+                     partials)
+    if (format == TextFormat::kLibFM) {
+      if (fp8) {
+        DMLC_TILE_HASH(TextFormat::kLibFM, true);
+      } else {
+        DMLC_TILE_HASH(TextFormat::kLibFM, false);
+      }
+    } else {
+      if (fp8) {
+        DMLC_TILE_HASH(TextFormat::kLibSVM, true);
+      } else {
+        DMLC_TILE_HASH(TextFormat::kLibSVM, false);
+      }
+    }
+#undef DMLC_TILE_HASH
+  }
+  hipLaunchKernelGGL(k_tile_finish, dim3(1), dim3(kFinishThreads), 0, stream, partials,
+                     static_cast<int>(ntiles), meta, host_meta, nullptr, 0ull, 0ull);
+}
+
+template void LaunchTileHashed<uint32_t>(const char*, size_t, TextFormat, const uint64_t*,
+                                         uint64_t, int, float, uint32_t, bool, void*, float*,
+                                         MetaPartial*, ChunkMeta*, ChunkMeta*, hipStream_t);
+template void LaunchTileHashed<uint64_t>(const char*, size_t, TextFormat, const uint64_t*,
+                                         uint64_t, int, float, uint32_t, bool, void*, float*,
+                                         MetaPartial*, ChunkMeta*, ChunkMeta*, hipStream_t);
 
 template void LaunchTileFill<uint32_t>(const char*, size_t, TextFormat, const uint64_t*,
                                        const FillTarget<uint32_t>&, MetaPartial*, ChunkMeta*,

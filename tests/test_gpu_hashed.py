@@ -69,12 +69,14 @@ def test_k9_and_fused_match_independent_hash(dataset, dim, seed):
     # CSR path: tile parser -> K9
     csr = data.csr_to_torch(data.GPUParser(p, format=fmt, chunk_bytes=128 * 1024).parse_all())
     k9 = ops.hashed_dense(csr, dim, seed=seed, fp8=False).cpu().numpy().astype(np.float64)
-    # fused path, f32 and fp8
-    fused = data.GPUParser(p, format=fmt, chunk_bytes=128 * 1024).parse_all_hashed(
-        dim, seed=seed, fp8=False)
-    f32 = fused["x"].cpu().numpy().astype(np.float64)
-    np.testing.assert_array_equal(fused["label"].cpu().numpy(), host["label"])
-    for got in (k9, f32):
+    # fused paths (tile kernel, and the exact per-line kernel), f32
+    outs = [k9]
+    for fast in (1, 0):
+        fused = data.GPUParser(p, format=fmt, chunk_bytes=128 * 1024, fast_path=fast
+                               ).parse_all_hashed(dim, seed=seed, fp8=False)
+        outs.append(fused["x"].cpu().numpy().astype(np.float64))
+        np.testing.assert_array_equal(fused["label"].cpu().numpy(), host["label"])
+    for got in outs:
         assert got.shape == ref.shape
         np.testing.assert_array_equal(got != 0, ref != 0)  # same buckets, no extra mass
         np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-6)
@@ -108,3 +110,24 @@ def test_hashed_fm_on_fused_fp8_batch(dataset):
     assert model.w.grad is not None and torch.isfinite(model.w.grad).all()
     assert model.v.grad is not None and torch.isfinite(model.v.grad).all()
     print("HashedFM gemm path:", model.gemm)
+
+
+def test_fused_tile_kernel_long_lines_fall_back(tmp_path):
+    """Lines longer than the tile kernel's 4 KiB extension are rebuilt by the
+    exact per-line kernel; short and long lines mixed, output equals K9."""
+    rng = np.random.default_rng(2)
+    lines = []
+    for r in range(300):
+        n = int(rng.integers(5, 40)) if r % 50 else 1500  # every 50th line ~ 20 KB
+        toks = [f"{int(rng.integers(0, 30))}:{int(rng.integers(0, 1 << 20))}:{rng.random():.4f}"
+                for _ in range(n)]
+        lines.append(f"{r % 2} " + " ".join(toks))
+    p = str(tmp_path / "long.libfm")
+    with open(p, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    g = data.GPUParser(p, format="libfm", chunk_bytes=256 * 1024)
+    fused = g.parse_all_hashed(256, seed=3, fp8=False)
+    assert g.stats()["exact_chunks"] > 0
+    csr = data.csr_to_torch(data.GPUParser(p, format="libfm").parse_all())
+    k9 = ops.hashed_dense(csr, 256, seed=3, fp8=False)
+    np.testing.assert_allclose(fused["x"].cpu().numpy(), k9.cpu().numpy(), rtol=1e-5, atol=1e-5)
