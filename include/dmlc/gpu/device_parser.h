@@ -57,6 +57,14 @@ struct DeviceParserConfig {
    */
   int zero_copy{-1};
   /*!
+   * \brief zero-copy pinning: partitions up to zc_pin_budget bytes are
+   *  registered whole, larger ones in sliding windows of zc_window_bytes (at
+   *  most two pinned, the next prepared in the background)
+   *  (`?zc_pin_budget_mb=`, `?zc_window_mb=`)
+   */
+  size_t zc_pin_budget{64UL << 30};
+  size_t zc_window_bytes{1UL << 30};
+  /*!
    * \brief HBM epoch cache: the first full pass also keeps every
    *  chunk's text resident in one device arena (partition bytes of HBM); later
    *  epochs (BeforeFirst, or Seek to a chunk boundary) parse straight from HBM
@@ -70,7 +78,7 @@ struct DeviceParserConfig {
   size_t replay_chunk_bytes{1UL << 30};
   /*! \brief apply `?k=v` overrides (chunk_mb, pinned_slots, device_slots,
    *  read_threads, device, format, label_column, weight_column, delimiter,
-   *  fast_path, zero_copy, hbm_cache, replay_chunk_mb) */
+   *  fast_path, zero_copy, zc_pin_budget_mb, zc_window_mb, hbm_cache, replay_chunk_mb) */
   void Update(const std::map<std::string, std::string>& args);
 };
 

@@ -73,6 +73,10 @@ void DeviceParserConfig::Update(const std::map<std::string, std::string>& args) 
       fast_path = v != "0" && v != "false";
     } else if (k == "replay_chunk_mb") {
       replay_chunk_bytes = static_cast<size_t>(std::atof(v.c_str()) * (1 << 20));
+    } else if (k == "zc_pin_budget_mb") {
+      zc_pin_budget = static_cast<size_t>(std::atof(v.c_str()) * (1 << 20));
+    } else if (k == "zc_window_mb") {
+      zc_window_bytes = static_cast<size_t>(std::atof(v.c_str()) * (1 << 20));
     } else if (k == "hbm_cache") {
       hbm_cache = v != "0" && v != "false";
     } else if (k == "zero_copy") {
@@ -150,7 +154,8 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     if (cfg_.zero_copy != 0) {
       zc_.reset(new ZeroCopySource());
       const double t0 = GetTime();
-      if (!zc_->Init(split_.get(), cfg_.chunk_bytes)) {
+      zc_->SetDrain([this]() { copy_->Synchronize(); });
+      if (!zc_->Init(split_.get(), cfg_.chunk_bytes, cfg_.zc_pin_budget, cfg_.zc_window_bytes)) {
         CHECK(cfg_.zero_copy != 1) << "zero_copy=1 but the input cannot be mmap'ed + registered";
         zc_.reset();
       } else {
@@ -637,7 +642,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     } unmerge{&merge_replay_};
     while (WithNextChunk([&](const char* text, size_t nbytes) {
       ChunkMeta* dmeta = meta_.get<ChunkMeta>();
-      if (cfg_.fast_path) {
+      if (cfg_.fast_path && dim % 16 == 0) {
         // tile parser: C1 + C2 sizes, then the fused tile kernel builds the
         // rows of the lines each workgroup owns
         ChunkMeta* hm = hmap_.get<ChunkMeta>();
@@ -667,7 +672,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       DMLC_HIP_CHECK(hipMemsetAsync(dmeta, 0, sizeof(ChunkMeta), s));
       LaunchLineCount(text, nbytes, tiles_.get<uint64_t>(), dmeta, s);
       const size_t nlines = ReadBack<ChunkMeta>(dmeta).nlines;
-      if (!cfg_.fast_path) AfterFirstSync();
+      if (!(cfg_.fast_path && dim % 16 == 0)) AfterFirstSync();
       EnsureLineBuffers(nlines);
       LaunchLineEmit(text, nbytes, tiles_.get<uint64_t>(), lines_.get<uint32_t>(), s);
       LaunchTextCount(text, nbytes, lines_.get<uint32_t>(), nlines, tcfg_, info_.get<uint64_t>(),

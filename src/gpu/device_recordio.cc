@@ -63,6 +63,7 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
                                           nparts));
     if (cfg_.zero_copy != 0) {
       zc_.reset(new ZeroCopySource(ZeroCopySource::Cut::kRecordIO));
+      zc_->SetDrain([this]() { (void)hipStreamSynchronize(copy_.get()); });
       if (!zc_->Init(split_.get(), cfg_.chunk_bytes)) {
         CHECK_NE(cfg_.zero_copy, 1) << "zero_copy=1 but mmap/hipHostRegister failed";
         zc_.reset();

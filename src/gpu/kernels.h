@@ -182,7 +182,7 @@ void LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
  *  row row_base + line of a [rows x dim] fp8 (x scale) or f32 batch, labels
  *  alongside; no CSR is written.  Sets kFlagIrregular when a line runs more
  *  than 4 KiB past its tile (re-run the chunk with LaunchTextHashed), merges
- *  kFlagNegIndex.  dim: multiple of 4, <= 4096.
+ *  kFlagNegIndex.  dim: multiple of 16, <= 4096.
  */
 template <typename IndexType>
 void LaunchTileHashed(const char* text, size_t nbytes, TextFormat format,

@@ -671,6 +671,7 @@ constexpr int kHashExt = 4096;                            // bytes staged past t
 constexpr int kHashSegs = (static_cast<int>(kTileBytes) + kHashExt) / 4096;
 constexpr int kHashRows = 4;                              // rows built per LDS round
 constexpr unsigned kHashOffBits = 14;                     // staged offset < 12288
+constexpr uint32_t kHashMaxTok = 3072;  // listed tokens per tile (more: exact kernel)
 
 template <TextFormat F, typename IndexType, bool kFP8>
 __global__ __launch_bounds__(kThreads) void k_tile_hash(const uint8_t* __restrict__ text, size_t n,
@@ -680,7 +681,7 @@ __global__ __launch_bounds__(kThreads) void k_tile_hash(const uint8_t* __restric
                                                         float* __restrict__ labels,
                                                         MetaPartial* __restrict__ partials) {
   __shared__ uint4 s_text[(kTileBytes + kHashExt) / 16 + 4];
-  __shared__ uint32_t s_tok[(kTileBytes + kHashExt) / 2];
+  __shared__ uint32_t s_tok[kHashMaxTok];
   __shared__ uint32_t s_scan[4];
   __shared__ uint32_t s_end;  // staged offset where the owned region ends
   extern __shared__ __attribute__((aligned(16))) float s_rows[];
@@ -740,7 +741,7 @@ __global__ __launch_bounds__(kThreads) void k_tile_hash(const uint8_t* __restric
       if (lm & bit) ++line;
       if (tm & bit) {  // every token is listed; those at or past `end` are skipped later
         const uint32_t label = (lm & bit) ? 1u : 0u;
-        s_tok[tok] = off | (line << kHashOffBits) | (label << 31);
+        if (tok < kHashMaxTok) s_tok[tok] = off | (line << kHashOffBits) | (label << 31);
         ++tok;
       }
     }
@@ -749,8 +750,9 @@ __global__ __launch_bounds__(kThreads) void k_tile_hash(const uint8_t* __restric
     __syncthreads();
   }
   const uint32_t end = s_end;  // first line start in the extension (barrier above)
-  const uint32_t ntok = carry & 0xffffu;
-  bool irregular = false;
+  const uint32_t ntok_all = carry & 0xffffu;
+  const uint32_t ntok = ntok_all < kHashMaxTok ? ntok_all : kHashMaxTok;
+  bool irregular = ntok_all > kHashMaxTok;  // very many tiny tokens: exact kernel
   if (end == 0xFFFFFFFFu && staged_end == kTileBytes + kHashExt && tile0 + staged_end < n &&
       nlines_tile != 0) {
     irregular = true;  // the last owned line runs past the extension
@@ -856,20 +858,31 @@ __global__ __launch_bounds__(kThreads) void k_tile_hash(const uint8_t* __restric
     __syncthreads();
     const uint32_t nr = nlines_tile - r0 < static_cast<uint32_t>(kHashRows) ? nlines_tile - r0
                                                                            : kHashRows;
-    for (uint32_t j = 0; j < nr; ++j) {
+    // wave w writes row w of the round: 16 columns per lane -> one 16 B store
+    const uint32_t j = threadIdx.x / dev::kWave;
+    if (j < nr) {
       const uint64_t row = row_base + line_base + r0 + j;
       const float* src = rows + j * dim;
+      const int lane = dev::lane_id();
       if constexpr (kFP8) {
-        uint32_t* o = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(out) + row * dim);
-        for (int c = threadIdx.x * 4; c < dim; c += kThreads * 4) {
-          int packed = __builtin_amdgcn_cvt_pk_fp8_f32(src[c] * scale, src[c + 1] * scale, 0, false);
-          packed = __builtin_amdgcn_cvt_pk_fp8_f32(src[c + 2] * scale, src[c + 3] * scale, packed,
-                                                   true);
-          o[c / 4] = static_cast<uint32_t>(packed);
+        uint4* o = reinterpret_cast<uint4*>(static_cast<uint8_t*>(out) + row * dim);
+        for (int c = lane * 16; c < dim; c += dev::kWave * 16) {
+          const float4* f = reinterpret_cast<const float4*>(src + c);
+          uint32_t w[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 x = f[q];
+            int pk = __builtin_amdgcn_cvt_pk_fp8_f32(x.x * scale, x.y * scale, 0, false);
+            pk = __builtin_amdgcn_cvt_pk_fp8_f32(x.z * scale, x.w * scale, pk, true);
+            w[q] = static_cast<uint32_t>(pk);
+          }
+          o[c / 16] = make_uint4(w[0], w[1], w[2], w[3]);
         }
       } else {
-        float* o = static_cast<float*>(out) + row * dim;
-        for (int c = threadIdx.x; c < dim; c += kThreads) o[c] = src[c];
+        float4* o = reinterpret_cast<float4*>(static_cast<float*>(out) + row * dim);
+        for (int c = lane * 4; c < dim; c += dev::kWave * 4) {
+          o[c / 4] = *reinterpret_cast<const float4*>(src + c);
+        }
       }
     }
     __syncthreads();

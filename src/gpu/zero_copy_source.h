@@ -5,6 +5,16 @@
  *  H2D DMA reads the page cache directly -- no CPU memcpy into pinned slots
  *  (measured: 87.0M rows/s vs 55.3M with the pread ring, profiles/r01_zero_copy).
  *
+ * Two modes:
+ *  - eager: a partition of at most `pin_budget` bytes is mapped and registered
+ *    once, up front (registration is paid once per parser, not per epoch);
+ *  - windowed: larger partitions (a 288 GB shard per GPU) are mapped and
+ *    registered in sliding windows of `window_bytes`; the next window is
+ *    prepared on a background thread while the current one is consumed, and at
+ *    most two are pinned at once (plus the one being prefetched).  A window is
+ *    released only after the owner's drain callback (the copy stream's
+ *    synchronisation) has run, so no DMA still reads it.
+ *
  * Chunks never cross a file boundary and end on a record boundary (a record
  * longer than chunk_bytes makes its chunk longer):
  *  - text: after the last EOL of the window (reference LineSplitter,
@@ -25,6 +35,10 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <deque>
+#include <functional>
+#include <future>
+#include <memory>
 #include <vector>
 
 #include "../io/filesys.h"
@@ -41,38 +55,62 @@ class ZeroCopySource {
     size_t size;
   };
   explicit ZeroCopySource(Cut cut = Cut::kLine) : cut_(cut) {}
-  ~ZeroCopySource() { Release(); }
+  ~ZeroCopySource() {
+    JoinPending();
+    for (auto& w : windows_) Unmap(&w);
+    windows_.clear();
+    for (auto& m : eager_) Unmap(&m);
+    eager_.clear();
+    for (int fd : fds_) {
+      if (fd >= 0) ::close(fd);
+    }
+  }
   ZeroCopySource(const ZeroCopySource&) = delete;
   ZeroCopySource& operator=(const ZeroCopySource&) = delete;
 
-  /*! \brief map + register every segment; false (and unmapped) on failure */
-  bool Init(io::InputSplitBase* split, size_t chunk_bytes) {
+  /*!
+   * \brief prepare the partition; false (nothing left mapped) when it cannot be
+   *  mmap'ed + registered
+   * \param pin_budget partitions up to this size are pinned whole (eager)
+   * \param window_bytes window size of the windowed mode
+   */
+  bool Init(io::InputSplitBase* split, size_t chunk_bytes, size_t pin_budget = 64UL << 30,
+            size_t window_bytes = 1UL << 30) {
     chunk_bytes_ = chunk_bytes;
-    const long page = sysconf(_SC_PAGESIZE);
+    page_ = static_cast<size_t>(sysconf(_SC_PAGESIZE));
+    window_bytes_ = std::max(window_bytes, 2 * chunk_bytes);
     for (const auto& seg : split->ShardSegments()) {
       if (seg.end <= seg.begin) continue;
       const int fd = split->filesystem()->OpenRawFd(split->files()[seg.file_index].path);
       if (fd < 0) return Fail();
-      const size_t map_off = seg.begin & ~static_cast<size_t>(page - 1);
-      const size_t map_len = seg.end - map_off;
-      void* p = mmap(nullptr, map_len, PROT_READ, MAP_SHARED | MAP_POPULATE, fd, map_off);
-      ::close(fd);
-      if (p == MAP_FAILED) return Fail();
-      maps_.push_back(Mapping{p, map_len, false});
-      hipError_t err = hipHostRegister(p, map_len, hipHostRegisterReadOnly);
-      if (err != hipSuccess) {
-        (void)hipGetLastError();
-        return Fail();
+      fds_.push_back(fd);
+      segs_.push_back(Seg{fds_.size() - 1, seg.begin, seg.end - seg.begin, nullptr});
+    }
+    windowed_ = PartitionBytes() > pin_budget;
+    if (windowed_) {
+      // probe once: a file that cannot be mapped + registered fails here
+      if (!segs_.empty()) {
+        Mapping probe;
+        if (!MapRange(segs_[0], 0, std::min(segs_[0].size, page_), &probe)) return Fail();
+        Unmap(&probe);
       }
-      maps_.back().registered = true;
-      segs_.push_back(Seg{static_cast<const char*>(p) + (seg.begin - map_off), seg.end - seg.begin});
+      return true;
+    }
+    for (auto& s : segs_) {
+      Mapping m;
+      if (!MapRange(s, 0, s.size, &m)) return Fail();
+      s.eager = m.data;
+      eager_.push_back(m);
     }
     return true;
   }
-  void Reset() {
-    seg_ = 0;
-    off_ = 0;
-  }
+  /*!
+   * \brief called before a window is released: must wait until no transfer
+   *  reads pieces handed out earlier (the owner's copy-stream sync)
+   */
+  void SetDrain(std::function<void()> drain) { drain_ = std::move(drain); }
+  bool windowed() const { return windowed_; }
+  void Reset() { Seek(0); }
   /*! \brief next chunk of whole records; false at the end */
   bool Next(Piece* out) {
     while (seg_ < segs_.size() && off_ >= segs_[seg_].size) {
@@ -81,16 +119,33 @@ class ZeroCopySource {
     }
     if (seg_ >= segs_.size()) return false;
     const Seg& s = segs_[seg_];
-    const char* b = s.ptr + off_;
-    size_t len = std::min(chunk_bytes_, s.size - off_);
-    if (off_ + len < s.size) {
-      const size_t avail = s.size - off_;
-      len = cut_ == Cut::kLine ? CutLine(b, len, avail) : CutRecord(b, len, avail);
+    const size_t remain = s.size - off_;
+    size_t want = std::min(chunk_bytes_, remain);
+    for (;;) {
+      const char* b = nullptr;
+      size_t avail = 0;  // bytes of the segment visible from b
+      if (!windowed_) {
+        b = s.eager + off_;
+        avail = remain;
+      } else {
+        const Mapping* w = Window(seg_, off_, want);
+        b = w->data + (off_ - w->seg_off);
+        avail = w->seg_off + w->len - off_;
+      }
+      size_t len = want;
+      if (off_ + len < s.size) {
+        len = cut_ == Cut::kLine ? CutLine(b, len, avail) : CutRecord(b, len, avail);
+        if (len == avail && off_ + avail < s.size) {
+          // one record runs past the mapped window: map a larger one
+          want = std::min(remain, 2 * avail);
+          continue;
+        }
+      }
+      out->ptr = b;
+      out->size = len;
+      off_ += len;
+      return true;
     }
-    out->ptr = b;
-    out->size = len;
-    off_ += len;
-    return true;
   }
   /*!
    * \brief partition byte offset of the next piece (same cursor space as
@@ -103,6 +158,12 @@ class ZeroCopySource {
   }
   /*! \brief continue from a Tell() cursor */
   void Seek(size_t pos) {
+    if (windowed_) {
+      JoinPending();
+      if (!windows_.empty() && drain_) drain_();
+      for (auto& w : windows_) Unmap(&w);
+      windows_.clear();
+    }
     seg_ = 0;
     off_ = pos;
     while (seg_ < segs_.size() && off_ >= segs_[seg_].size) {
@@ -116,18 +177,118 @@ class ZeroCopySource {
     for (const auto& s : segs_) n += s.size;
     return n;
   }
+  /*! \brief bytes currently registered with HIP (for stats and tests) */
+  size_t PinnedBytes() const {
+    size_t n = 0;
+    for (const auto& m : eager_) n += m.map_len;
+    for (const auto& w : windows_) n += w.map_len;
+    return n;
+  }
 
  private:
-  /*!
-   * \brief end of the last whole line in [b, b+len); a line longer than the
-   *  window makes the piece longer instead (up to the line's end, or `avail`,
-   *  the bytes left in the segment), as the reference's InputSplitBase grows
-   *  its buffer for long records (src/io/input_split_base.cc:241-258)
-   */
+  struct Seg {
+    size_t fd_index;
+    size_t file_begin;  // first byte of the segment in its file
+    size_t size;
+    const char* eager;  // eager mode: mapped segment start
+  };
+  struct Mapping {
+    void* map{nullptr};
+    size_t map_len{0};
+    const char* data{nullptr};  // segment byte seg_off
+    size_t seg_index{0}, seg_off{0}, len{0};
+    bool registered{false};
+  };
+
+  bool MapRange(const Seg& s, size_t seg_off, size_t len, Mapping* m) {
+    const size_t file_off = s.file_begin + seg_off;
+    const size_t map_off = file_off & ~(page_ - 1);
+    m->map_len = file_off + len - map_off;
+    m->map = mmap(nullptr, m->map_len, PROT_READ, MAP_SHARED | MAP_POPULATE, fds_[s.fd_index],
+                  static_cast<off_t>(map_off));
+    if (m->map == MAP_FAILED) {
+      m->map = nullptr;
+      return false;
+    }
+    if (hipHostRegister(m->map, m->map_len, hipHostRegisterReadOnly) != hipSuccess) {
+      (void)hipGetLastError();
+      munmap(m->map, m->map_len);
+      m->map = nullptr;
+      return false;
+    }
+    m->registered = true;
+    m->data = static_cast<const char*>(m->map) + (file_off - map_off);
+    m->seg_off = seg_off;
+    m->len = len;
+    return true;
+  }
+  static void Unmap(Mapping* m) {
+    if (m->map == nullptr) return;
+    if (m->registered) (void)hipHostUnregister(m->map);
+    munmap(m->map, m->map_len);
+    m->map = nullptr;
+  }
+  void JoinPending() {
+    if (pending_.valid()) {
+      Mapping m = pending_.get();
+      Unmap(&m);
+    }
+  }
+  /*! \brief the window of segment si holding [off, off + want), mapped on demand */
+  const Mapping* Window(size_t si, size_t off, size_t want) {
+    for (const auto& w : windows_) {
+      if (w.seg_index == si && off >= w.seg_off && off + want <= w.seg_off + w.len) return &w;
+    }
+    const Seg& s = segs_[si];
+    const size_t len = std::min(s.size - off, std::max(window_bytes_, want));
+    Mapping m;
+    bool have = false;
+    if (pending_.valid()) {
+      Mapping p = pending_.get();  // prefetched by the background thread
+      if (p.map != nullptr && p.seg_index == si && off >= p.seg_off &&
+          off + want <= p.seg_off + p.len) {
+        m = p;
+        have = true;
+      } else {
+        Unmap(&p);
+      }
+    }
+    if (!have) {
+      CHECK(MapRange(s, off, len, &m)) << "zero-copy: cannot map + register a window";
+      m.seg_index = si;
+    }
+    // at most two windows pinned: release the oldest once its DMAs are done
+    if (windows_.size() >= 2) {
+      if (drain_) drain_();
+      Unmap(&windows_.front());
+      windows_.pop_front();
+    }
+    windows_.push_back(m);
+    // the next window overlaps this one by two chunks, so the piece that no
+    // longer fits here starts inside the prefetched window
+    const size_t overlap = std::min(m.len, 2 * chunk_bytes_);
+    if (m.seg_off + m.len < s.size) Prefetch(si, m.seg_off + m.len - overlap);
+    return &windows_.back();
+  }
+  /*! \brief map + register the window after this one on a background thread */
+  void Prefetch(size_t si, size_t off) {
+    if (si >= segs_.size() || off >= segs_[si].size) return;
+    const Seg s = segs_[si];
+    const size_t len = std::min(s.size - off, window_bytes_);
+    pending_ = std::async(std::launch::async, [this, s, si, off, len]() {
+      Mapping m;
+      if (!MapRange(s, off, len, &m)) m.map = nullptr;
+      m.seg_index = si;
+      return m;
+    });
+  }
   size_t CutLine(const char* b, size_t len, size_t avail) const {
     size_t cut = len;
     while (cut > 0 && b[cut - 1] != '\n' && b[cut - 1] != '\r') --cut;
     if (cut != 0) return cut;
+    // one line fills the window: extend to its end (up to what is mapped),
+    // as the reference's InputSplitBase grows its buffer for long records
+    // (src/io/input_split_base.cc:241-258)
     cut = len;
     while (cut < avail && b[cut] != '\n' && b[cut] != '\r') ++cut;
     while (cut < avail && (b[cut] == '\n' || b[cut] == '\r')) ++cut;
@@ -150,31 +311,26 @@ class ZeroCopySource {
     }
     return avail;
   }
-  struct Mapping {
-    void* ptr;
-    size_t len;
-    bool registered;
-  };
-  struct Seg {
-    const char* ptr;
-    size_t size;
-  };
   bool Fail() {
-    Release();
+    for (auto& m : eager_) Unmap(&m);
+    eager_.clear();
+    for (int fd : fds_) {
+      if (fd >= 0) ::close(fd);
+    }
+    fds_.clear();
+    segs_.clear();
     return false;
   }
-  void Release() {
-    for (auto& m : maps_) {
-      if (m.registered) (void)hipHostUnregister(m.ptr);
-      munmap(m.ptr, m.len);
-    }
-    maps_.clear();
-    segs_.clear();
-  }
+
   Cut cut_;
-  size_t chunk_bytes_{0};
-  std::vector<Mapping> maps_;
+  size_t chunk_bytes_{0}, page_{4096}, window_bytes_{1UL << 30};
+  bool windowed_{false};
+  std::vector<int> fds_;
   std::vector<Seg> segs_;
+  std::vector<Mapping> eager_;
+  std::deque<Mapping> windows_;
+  std::future<Mapping> pending_;
+  std::function<void()> drain_;
   size_t seg_{0}, off_{0};
 };
 

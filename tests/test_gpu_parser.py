@@ -304,3 +304,25 @@ def test_token_shape_fuzz_matches_cpu(tmp_path):
     with open(q, "w") as f:
         f.write("\n".join(fm) + "\n")
     assert_same(gpu_rows(q, "libfm", chunk_bytes=16 * 1024), cpu_rows(q, "libfm"), field=True)
+
+
+@pytest.mark.parametrize("hbm_cache", [0, 1])
+def test_zero_copy_windowed_pinning(tmp_path, hbm_cache):
+    """A partition above the pin budget is mapped + registered in sliding
+    windows (background prefetch, at most two pinned); output unchanged."""
+    d = tmp_path / "w"
+    d.mkdir()
+    for i in range(3):
+        data.write_synthetic(str(d / f"p{i}.libsvm"), i * 4000, (i + 1) * 4000, seed=19)
+    c = cpu_rows(str(d), "libsvm")
+    g = data.GPUParser(str(d), chunk_bytes=96 * 1024, zero_copy=1, zc_pin_budget_mb=1,
+                       zc_window_mb=0.5, hbm_cache=hbm_cache)
+    for _ in range(2):
+        g.before_first()
+        assert_same(pyref.concat_blocks([g.parse_all().to_host()]), c)
+    assert g.stats()["zero_copy"]
+    g.before_first()
+    blocks = []
+    while g.next():
+        blocks.append(g.value_to_host())
+    assert_same(pyref.concat_blocks(blocks), c)
