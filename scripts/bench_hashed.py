@@ -22,6 +22,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=2_000_000)
     ap.add_argument("--dim", type=int, default=1024)
+    ap.add_argument("--sweep", default="128,256,1024",
+                    help="extra dims timed for fused vs CSR+K9 (comma list, '' to skip)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--data", default="/tmp/dmlc_hashed_bench.libfm")
     args = ap.parse_args()
@@ -79,6 +81,25 @@ def main():
     res["hashed_fm_gemm"] = model.gemm
     res.update({"rows": int(batch["x"].shape[0]), "dim": args.dim, "text_bytes": nbytes,
                 "speedup_fused_vs_csr_k9": round(res["csr_then_k9"]["ms"] / res["fused"]["ms"], 3)})
+    sweep = {}
+    for d in [int(x) for x in args.sweep.split(",") if x]:
+        t = {}
+        for name, fn in (("csr_then_k9", lambda: ops.hashed_dense(
+                data.csr_to_torch(two.parse_all()), d, seed=1, fp8=True, scale=0.5)),
+                         ("fused", lambda: fused.parse_all_hashed(d, seed=1, fp8=True,
+                                                                  scale=0.5)["x"])):
+            (two if name == "csr_then_k9" else fused).before_first()
+            fn()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                (two if name == "csr_then_k9" else fused).before_first()
+                fn()
+            torch.cuda.synchronize()
+            t[name] = round((time.perf_counter() - t0) / args.steps * 1e3, 3)
+        t["speedup"] = round(t["csr_then_k9"] / t["fused"], 3)
+        sweep[str(d)] = t
+    res["dim_sweep_ms"] = sweep
     print(json.dumps(res), flush=True)
 
 
