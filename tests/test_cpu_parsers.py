@@ -97,8 +97,13 @@ def test_libsvm_synthetic_matches_oracle(tmp_path, nthread):
     check_libsvm(got, pyref.parse_libsvm(text))
 
 
-def test_libfm_matches_oracle(tmp_path):
-    text = "1 1:2:0.5 3:4 5:6:7e1 junk 2\n0:2 7:8:9\n\n1 1:1:1\n"
+@pytest.mark.parametrize("text", [
+    "1 1:2:0.5 3:4 5:6:7e1 junk 2\n0:2 7:8:9\n\n1 1:1:1\n",
+    # shapes at the edge of the single-pass field:index[:value] path
+    "1 3:4:0.5 3:4 3:4: 3x:4:1 3:4:-1.5 3:4:1e2 +3:4:1 3:4:abc 3:4:1.5.2 3:4:2:9 12.5:3:1\n"
+    "0 10:20 11:21:.25 4294967297:5:1 7:8:+2.5e-1 9:9:5.\n",
+])
+def test_libfm_matches_oracle(tmp_path, text):
     p = write(str(tmp_path / "f.libfm"), text)
     got = pyref.concat_blocks(list(data.iter_blocks(p, type="libfm")))
     rows = pyref.parse_libfm(text)
