@@ -203,6 +203,19 @@ def main():
                          "input_GBps": round(bytes_r * args.steps / el_r / 1e9, 3),
                          "wait_reader_sec": round(wr, 4), "wait_gpu_sec": round(wg, 4)})
     elapsed = max(float(x[3]) for x in gathered)  # the slowest rank sets the step time
+    # structured per-stage metrics ($DMLC_METRICS_FILE, JSONL, one file per rank
+    # with "{rank}" in the path) and their cross-rank reduction
+    from dmlc_core_amd.utils.metrics import MetricsLogger, parser_record, reduce_across_ranks
+
+    rec = {"rows": local["rows"], "bytes": local["bytes"], "elapsed_sec": float(mine[3])}
+    rec.update(parser_record(st))
+    reduced = reduce_across_ranks(rec, device=dev)
+    with MetricsLogger() as ml:
+        ml.log("ingest", steps=args.steps, **rec)
+        if rank == 0:
+            ml.log("ingest_reduced", steps=args.steps,
+                   **{f"{k}_{agg}": v[agg] for k, v in reduced.items()
+                      for agg in ("sum", "min", "max")})
     (rows, nnz, nbytes), max_index = totals
     ms = elapsed / max(1, args.steps) * 1e3
     value = rows * args.steps / elapsed
