@@ -9,12 +9,16 @@
  * New: libhdfs (JNI) is resolved at run time (HADOOP_HOME/lib/native or the
  * loader path), so libdmlc has no link-time Hadoop/JVM dependency and hdfs://
  * fails with a clear message where Hadoop is not installed.
+ * New: webhdfs:// and swebhdfs:// (the namenode REST API over libcurl), also
+ * used for hdfs:// where libhdfs is absent and DMLC_WEBHDFS_ENDPOINT is set,
+ * so HDFS works without a JVM on the node.
  */
 #include <dlfcn.h>
 #include <dmlc/logging.h>
 #include <errno.h>
 #include <fcntl.h>
 
+#include <cctype>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -24,6 +28,7 @@
 #include <vector>
 
 #include "./filesys.h"
+#include "./http.h"
 #include "./remote_filesys.h"
 
 namespace dmlc {
@@ -101,10 +106,16 @@ struct HdfsApi {
   bool ok() const { return handle != nullptr && error.empty(); }
 };
 
-HdfsApi& Api() {
+HdfsApi& RawApi() {
   static HdfsApi* api = new HdfsApi();
-  CHECK(api->ok()) << "hdfs:// unavailable: " << api->error;
   return *api;
+}
+bool HdfsLoadable() { return RawApi().ok(); }
+HdfsApi& Api() {
+  HdfsApi& api = RawApi();
+  CHECK(api.ok()) << "hdfs:// unavailable: " << api.error
+                  << " (or set DMLC_WEBHDFS_ENDPOINT=http://namenode:9870 for WebHDFS)";
+  return api;
 }
 
 /*! \brief one namenode connection shared by the filesystem and its streams */
@@ -228,13 +239,416 @@ class HdfsFileSystem : public FileSystem {
   std::shared_ptr<Connection> conn_;
 };
 
-FileSystem* CreateHdfs(const URI& path) { return new HdfsFileSystem(path); }
+// ---------------------------------------------------------------------------
+// WebHDFS: the namenode's REST interface (http://nn:9870/webhdfs/v1/<path>?op=)
+// over the same dlopen'ed libcurl client as s3:// and azure://.  Reads are
+// ranged OPENs (offset/length) fed to RangedReadStream, so InputSplit's
+// parallel ranged pieces work exactly as for S3; writes CREATE the file with
+// the first buffered block and APPEND the rest.  Both follow the namenode's
+// 307 redirect to a datanode by hand (the HTTP client never auto-follows, so
+// the request body is re-sent only to the datanode).
+// ---------------------------------------------------------------------------
+
+/*! \brief minimal JSON value tree for WebHDFS replies */
+struct JVal {
+  enum Kind { kNull, kBool, kNum, kStr, kArr, kObj } kind{kNull};
+  double num{0};
+  std::string str;
+  std::vector<JVal> arr;
+  std::vector<std::pair<std::string, JVal>> obj;
+  const JVal* Get(const std::string& k) const {
+    for (const auto& kv : obj) {
+      if (kv.first == k) return &kv.second;
+    }
+    return nullptr;
+  }
+};
+
+class JParser {
+ public:
+  explicit JParser(const std::string& s) : s_(s) {}
+  JVal Parse() {
+    JVal v = Value();
+    Ws();
+    CHECK_EQ(i_, s_.size()) << "WebHDFS: trailing bytes in JSON reply";
+    return v;
+  }
+
+ private:
+  void Ws() {
+    while (i_ < s_.size() && std::isspace(static_cast<unsigned char>(s_[i_]))) ++i_;
+  }
+  char Peek() {
+    Ws();
+    CHECK_LT(i_, s_.size()) << "WebHDFS: truncated JSON reply";
+    return s_[i_];
+  }
+  void Expect(char c) {
+    CHECK_EQ(Peek(), c) << "WebHDFS: malformed JSON reply at byte " << i_;
+    ++i_;
+  }
+  std::string Str() {
+    Expect('"');
+    std::string out;
+    while (i_ < s_.size() && s_[i_] != '"') {
+      char c = s_[i_++];
+      if (c == '\\' && i_ < s_.size()) {
+        const char e = s_[i_++];
+        switch (e) {
+          case 'n': c = '\n'; break;
+          case 't': c = '\t'; break;
+          case 'r': c = '\r'; break;
+          case 'b': c = '\b'; break;
+          case 'f': c = '\f'; break;
+          case 'u': {  // BMP code point -> UTF-8
+            CHECK_LE(i_ + 4, s_.size());
+            const unsigned cp = std::stoul(s_.substr(i_, 4), nullptr, 16);
+            i_ += 4;
+            if (cp < 0x80) {
+              out += static_cast<char>(cp);
+            } else if (cp < 0x800) {
+              out += static_cast<char>(0xC0 | (cp >> 6));
+              out += static_cast<char>(0x80 | (cp & 0x3F));
+            } else {
+              out += static_cast<char>(0xE0 | (cp >> 12));
+              out += static_cast<char>(0x80 | ((cp >> 6) & 0x3F));
+              out += static_cast<char>(0x80 | (cp & 0x3F));
+            }
+            continue;
+          }
+          default: c = e;
+        }
+      }
+      out += c;
+    }
+    Expect('"');
+    return out;
+  }
+  JVal Value() {
+    JVal v;
+    const char c = Peek();
+    if (c == '{') {
+      v.kind = JVal::kObj;
+      ++i_;
+      if (Peek() == '}') {
+        ++i_;
+        return v;
+      }
+      for (;;) {
+        std::string k = Str();
+        Expect(':');
+        v.obj.emplace_back(std::move(k), Value());
+        if (Peek() == ',') {
+          ++i_;
+          continue;
+        }
+        Expect('}');
+        return v;
+      }
+    }
+    if (c == '[') {
+      v.kind = JVal::kArr;
+      ++i_;
+      if (Peek() == ']') {
+        ++i_;
+        return v;
+      }
+      for (;;) {
+        v.arr.push_back(Value());
+        if (Peek() == ',') {
+          ++i_;
+          continue;
+        }
+        Expect(']');
+        return v;
+      }
+    }
+    if (c == '"') {
+      v.kind = JVal::kStr;
+      v.str = Str();
+      return v;
+    }
+    if (s_.compare(i_, 4, "true") == 0 || s_.compare(i_, 5, "false") == 0) {
+      v.kind = JVal::kBool;
+      v.num = s_[i_] == 't';
+      i_ += s_[i_] == 't' ? 4 : 5;
+      return v;
+    }
+    if (s_.compare(i_, 4, "null") == 0) {
+      i_ += 4;
+      return v;
+    }
+    char* end = nullptr;
+    v.kind = JVal::kNum;
+    v.num = std::strtod(s_.c_str() + i_, &end);
+    CHECK(end != s_.c_str() + i_) << "WebHDFS: malformed JSON number at byte " << i_;
+    i_ = static_cast<size_t>(end - s_.c_str());
+    return v;
+  }
+  const std::string& s_;
+  size_t i_{0};
+};
+
+std::string PercentEncodePath(const std::string& p) {
+  static const char* hex = "0123456789ABCDEF";
+  std::string out;
+  for (unsigned char c : p) {
+    if (std::isalnum(c) || c == '/' || c == '-' || c == '_' || c == '.' || c == '~') {
+      out += static_cast<char>(c);
+    } else {
+      out += '%';
+      out += hex[c >> 4];
+      out += hex[c & 15];
+    }
+  }
+  return out;
+}
+
+[[noreturn]] void WebFail(const std::string& what, const HttpResponse& r) {
+  std::string msg = r.error;
+  if (msg.empty()) {
+    msg = "HTTP " + std::to_string(r.status);
+    // RemoteException {"exception": ..., "message": ...}
+    try {
+      JVal j = JParser(r.body).Parse();
+      if (const JVal* e = j.Get("RemoteException")) {
+        const JVal* m = e->Get("message");
+        const JVal* x = e->Get("exception");
+        msg += std::string(" ") + (x ? x->str : "") + ": " + (m ? m->str : "");
+      }
+    } catch (const dmlc::Error&) {
+      msg += " " + r.body.substr(0, 300);
+    }
+  }
+  LOG(FATAL) << what << ": " << msg;
+  std::abort();
+}
+
+/*! \brief REST endpoint of one namenode */
+class WebHdfsClient {
+ public:
+  /*! \param endpoint "http(s)://host:port" */
+  explicit WebHdfsClient(std::string endpoint) : endpoint_(std::move(endpoint)) {
+    if (const char* u = std::getenv("HADOOP_USER_NAME")) user_ = u;
+    if (const char* t = std::getenv("DMLC_WEBHDFS_TOKEN")) token_ = t;
+    if (const char* v = std::getenv("DMLC_WEBHDFS_VERIFY_SSL")) verify_ssl_ = std::atoi(v) != 0;
+  }
+  std::string Url(const std::string& path, const std::string& op,
+                  const std::vector<std::pair<std::string, std::string>>& q = {}) const {
+    std::string url = endpoint_ + "/webhdfs/v1" + PercentEncodePath(path.empty() ? "/" : path) +
+                      "?op=" + op;
+    for (const auto& kv : q) url += "&" + kv.first + "=" + kv.second;
+    if (!token_.empty()) {
+      url += "&delegation=" + token_;
+    } else if (!user_.empty()) {
+      url += "&user.name=" + user_;
+    }
+    return url;
+  }
+  HttpRequest Make(const std::string& method, const std::string& url) const {
+    HttpRequest r;
+    r.method = method;
+    r.url = url;
+    r.verify_ssl = verify_ssl_;
+    r.follow_redirects = false;
+    return r;
+  }
+  /*! \brief namenode request; a 307 (datanode redirect) is followed once, with the body */
+  HttpResponse Call(const std::string& method, const std::string& url, const char* body = nullptr,
+                    size_t len = 0, char* out = nullptr, size_t out_cap = 0, int retries = 3) const {
+    HttpRequest req = Make(method, url);
+    if (body != nullptr) req.headers.push_back("Content-Type: application/octet-stream");
+    // the namenode gets no body: it only answers with the datanode location
+    HttpResponse r = Http::PerformRetry(req, retries);
+    if (r.status == 307 || r.status == 302 || r.status == 301) {
+      auto loc = r.headers.find("location");
+      CHECK(loc != r.headers.end()) << "WebHDFS redirect without Location: " << url;
+      HttpRequest dn = Make(method, loc->second);
+      dn.body = body;
+      dn.body_len = len;
+      dn.out = out;
+      dn.out_cap = out_cap;
+      if (body != nullptr) dn.headers.push_back("Content-Type: application/octet-stream");
+      return Http::PerformRetry(dn, retries);
+    }
+    return r;
+  }
+  const std::string& endpoint() const { return endpoint_; }
+
+ private:
+  std::string endpoint_, user_, token_;
+  bool verify_ssl_{true};
+};
+
+/*! \brief CREATE with the first block, APPEND for every later one */
+class WebHdfsWriteStream : public Stream {
+ public:
+  WebHdfsWriteStream(std::shared_ptr<WebHdfsClient> c, std::string path, bool append)
+      : c_(std::move(c)), path_(std::move(path)), created_(append) {
+    const char* mb = std::getenv("DMLC_WEBHDFS_WRITE_BUFFER_MB");
+    block_ = (mb != nullptr ? std::strtoull(mb, nullptr, 10) : 64) << 20;
+    if (block_ == 0) block_ = 1 << 20;
+  }
+  ~WebHdfsWriteStream() override {
+    try {
+      Flush(true);
+    } catch (const dmlc::Error& e) {
+      LOG(ERROR) << "WebHDFS write of " << path_ << " failed: " << e.what();
+    }
+  }
+  size_t Read(void*, size_t) override {
+    LOG(FATAL) << "WebHDFS write stream is write-only";
+    return 0;
+  }
+  void Write(const void* ptr, size_t size) override {
+    buf_.append(static_cast<const char*>(ptr), size);
+    if (buf_.size() >= block_) Flush(false);
+  }
+
+ private:
+  void Flush(bool final) {
+    if (buf_.empty() && (created_ || !final)) return;
+    HttpResponse r;
+    if (!created_) {
+      r = c_->Call("PUT", c_->Url(path_, "CREATE", {{"overwrite", "true"}}), buf_.data(),
+                   buf_.size());
+      if (r.status != 201 && !r.ok()) WebFail("WebHDFS CREATE " + path_, r);
+      created_ = true;
+    } else {
+      r = c_->Call("POST", c_->Url(path_, "APPEND"), buf_.data(), buf_.size());
+      if (!r.ok()) WebFail("WebHDFS APPEND " + path_, r);
+    }
+    buf_.clear();
+  }
+  std::shared_ptr<WebHdfsClient> c_;
+  std::string path_, buf_;
+  size_t block_;
+  bool created_;
+};
+
+class WebHdfsFileSystem : public FileSystem {
+ public:
+  WebHdfsFileSystem(const URI& path, const std::string& endpoint)
+      : protocol_(path.protocol), host_(path.host),
+        c_(std::make_shared<WebHdfsClient>(endpoint)) {}
+
+  FileInfo GetPathInfo(const URI& path) override {
+    auto r = c_->Call("GET", c_->Url(path.name, "GETFILESTATUS"));
+    if (!r.ok()) WebFail("WebHDFS GETFILESTATUS " + path.str(), r);
+    const JVal j = JParser(r.body).Parse();
+    const JVal* st = j.Get("FileStatus");
+    CHECK(st != nullptr) << "WebHDFS GETFILESTATUS: no FileStatus in reply";
+    FileInfo fi = ToInfo(*st, path.name);
+    fi.path.name = path.name;
+    return fi;
+  }
+  void ListDirectory(const URI& path, std::vector<FileInfo>* out) override {
+    out->clear();
+    std::string dir = path.name;
+    while (dir.size() > 1 && dir.back() == '/') dir.pop_back();
+    std::string after;  // LISTSTATUS_BATCH cursor (large directories)
+    for (;;) {
+      auto r = c_->Call("GET", after.empty() ? c_->Url(dir, "LISTSTATUS_BATCH")
+                                             : c_->Url(dir, "LISTSTATUS_BATCH",
+                                                       {{"startAfter", PercentEncodePath(after)}}));
+      if (r.status == 400 || r.status == 501) {  // pre-2.8 namenode: one-shot LISTSTATUS
+        r = c_->Call("GET", c_->Url(dir, "LISTSTATUS"));
+      }
+      if (!r.ok()) WebFail("WebHDFS LISTSTATUS " + path.str(), r);
+      const JVal j = JParser(r.body).Parse();
+      const JVal* list = j.Get("DirectoryListing");
+      // LISTSTATUS_BATCH: {"DirectoryListing": {"partialListing": {"FileStatuses": {..}},
+      // "remainingEntries": n}}; LISTSTATUS: {"FileStatuses": {"FileStatus": [..]}}
+      const JVal* part = list != nullptr ? list->Get("partialListing") : &j;
+      const JVal* statuses = part != nullptr ? part->Get("FileStatuses") : nullptr;
+      const JVal* arr = statuses != nullptr ? statuses->Get("FileStatus") : nullptr;
+      CHECK(arr != nullptr) << "WebHDFS LISTSTATUS: no FileStatus array in reply";
+      for (const JVal& st : arr->arr) {
+        const JVal* suffix = st.Get("pathSuffix");
+        const std::string name = suffix != nullptr ? suffix->str : "";
+        out->push_back(ToInfo(st, name.empty() ? dir : (dir == "/" ? "/" : dir + "/") + name));
+        if (!name.empty()) after = name;
+      }
+      const JVal* rem = list != nullptr ? list->Get("remainingEntries") : nullptr;
+      if (rem == nullptr || rem->num <= 0 || arr->arr.empty()) break;
+    }
+  }
+  Stream* Open(const URI& path, const char* const flag, bool allow_null) override {
+    if (!std::strcmp(flag, "r") || !std::strcmp(flag, "rb")) return OpenForRead(path, allow_null);
+    const bool append = !std::strcmp(flag, "a") || !std::strcmp(flag, "ab");
+    CHECK(append || !std::strcmp(flag, "w") || !std::strcmp(flag, "wb"))
+        << "WebHDFS: bad mode " << flag;
+    return new WebHdfsWriteStream(c_, path.name, append);
+  }
+  SeekStream* OpenForRead(const URI& path, bool allow_null) override {
+    auto r = c_->Call("GET", c_->Url(path.name, "GETFILESTATUS"));
+    if (!r.ok()) {
+      if (allow_null) return nullptr;
+      WebFail("WebHDFS open " + path.str(), r);
+    }
+    const JVal j = JParser(r.body).Parse();
+    const JVal* st = j.Get("FileStatus");
+    CHECK(st != nullptr && st->Get("length") != nullptr) << "WebHDFS: no length for " << path.str();
+    return OpenForReadSized(path, static_cast<size_t>(st->Get("length")->num));
+  }
+  SeekStream* OpenForReadSized(const URI& path, size_t size) override {
+    auto c = c_;
+    const std::string name = path.name;
+    return new RangedReadStream(size, [c, name](size_t off, size_t len, char* dst) -> size_t {
+      auto r = c->Call("GET", c->Url(name, "OPEN", {{"offset", std::to_string(off)},
+                                                    {"length", std::to_string(len)}}),
+                       nullptr, 0, dst, len, 0);
+      if (r.status == 404 || r.status == 403) WebFail("WebHDFS OPEN " + name, r);
+      return r.status == 200 ? r.out_written : 0;
+    });
+  }
+
+ private:
+  FileInfo ToInfo(const JVal& st, const std::string& name) const {
+    FileInfo fi;
+    fi.path.protocol = protocol_;
+    fi.path.host = host_;
+    fi.path.name = name;
+    const JVal* len = st.Get("length");
+    const JVal* type = st.Get("type");
+    fi.size = len != nullptr ? static_cast<size_t>(len->num) : 0;
+    fi.type = type != nullptr && type->str == "DIRECTORY" ? kDirectory : kFile;
+    return fi;
+  }
+  std::string protocol_, host_;
+  std::shared_ptr<WebHdfsClient> c_;
+};
+
+FileSystem* CreateWebHdfs(const URI& path) {
+  const std::string scheme = path.protocol == "swebhdfs://" ? "https://" : "http://";
+  return new WebHdfsFileSystem(path, scheme + path.host);
+}
+
+/*!
+ * hdfs:// / viewfs://: libhdfs (JNI) when it loads; otherwise, when
+ * DMLC_WEBHDFS_ENDPOINT names the namenode's HTTP address, the REST backend
+ * (DMLC_HDFS_BACKEND=libhdfs|webhdfs forces one).
+ */
+FileSystem* CreateHdfs(const URI& path) {
+  const char* be = std::getenv("DMLC_HDFS_BACKEND");
+  const std::string backend = be != nullptr ? be : "auto";
+  const char* ep = std::getenv("DMLC_WEBHDFS_ENDPOINT");
+  if (backend == "webhdfs" || (backend == "auto" && ep != nullptr && *ep != '\0' &&
+                               !HdfsLoadable())) {
+    CHECK(ep != nullptr && *ep != '\0')
+        << "DMLC_HDFS_BACKEND=webhdfs needs DMLC_WEBHDFS_ENDPOINT=http://namenode:9870";
+    return new WebHdfsFileSystem(path, ep);
+  }
+  return new HdfsFileSystem(path);
+}
 
 }  // namespace
 
 void RegisterHDFSFileSystem() {
   RegisterFileSystem("hdfs://", &CreateHdfs);
   RegisterFileSystem("viewfs://", &CreateHdfs);
+  RegisterFileSystem("webhdfs://", &CreateWebHdfs);
+  RegisterFileSystem("swebhdfs://", &CreateWebHdfs);
 }
 
 }  // namespace io

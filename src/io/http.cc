@@ -158,7 +158,7 @@ HttpResponse Http::Perform(const HttpRequest& req) {
   c.easy_setopt(h, kOptHeaderFunction, &OnHeader);
   c.easy_setopt(h, kOptHeaderData, &t);
   c.easy_setopt(h, kOptNoSignal, 1L);
-  c.easy_setopt(h, kOptFollow, 1L);
+  c.easy_setopt(h, kOptFollow, req.follow_redirects ? 1L : 0L);
   c.easy_setopt(h, kOptConnectTimeout, 30L);
   c.easy_setopt(h, kOptTimeout, req.timeout_sec);
   c.easy_setopt(h, kOptSslVerifyPeer, req.verify_ssl ? 1L : 0L);

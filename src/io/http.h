@@ -35,6 +35,8 @@ struct HttpRequest {
   char* out{nullptr};
   size_t out_cap{0};
   bool verify_ssl{true};
+  /*! \brief follow 3xx Location (off for WebHDFS, which re-sends the body itself) */
+  bool follow_redirects{true};
   long timeout_sec{300};
 };
 

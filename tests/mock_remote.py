@@ -310,6 +310,114 @@ class PlainHandler(_Base):
             self._serve_object(data, self.headers.get("Range"))
 
 
+# ------------------------------------------------------------------------ WebHDFS
+class WebHdfsHandler(_Base):
+    """Namenode + datanode in one server: namenode ops OPEN/CREATE/APPEND answer
+    307 with a Location under /dn/ (the datanode), as a real cluster does.
+    Listings come in pages of 2 via LISTSTATUS_BATCH unless `batch` is off
+    (then the op is rejected with 400, as pre-2.8 namenodes do)."""
+    store: Dict[str, bytes] = {}
+    batch = True
+    namenode_bodies = 0  # requests that sent data to the namenode (must stay 0)
+    users: set = set()
+
+    def _split(self):
+        u = urllib.parse.urlsplit(self.path)
+        q = dict(urllib.parse.parse_qsl(u.query))
+        return urllib.parse.unquote(u.path), q
+
+    def _json(self, code, obj):
+        import json
+        self._send(code, json.dumps(obj).encode(), None)
+
+    def _missing(self, p):
+        self._json(404, {"RemoteException": {"exception": "FileNotFoundException",
+                                             "javaClassName": "java.io.FileNotFoundException",
+                                             "message": f"File does not exist: {p}"}})
+
+    def _status(self, p, suffix):
+        if p in self.store:
+            return {"pathSuffix": suffix, "type": "FILE", "length": len(self.store[p]),
+                    "ecPolicyObj": {"name": "RS-6-3", "schema": {"codecName": "rs"}}}
+        return {"pathSuffix": suffix, "type": "DIRECTORY", "length": 0}
+
+    def _is_dir(self, p):
+        pre = p.rstrip("/") + "/"
+        return p == "/" or any(k.startswith(pre) for k in self.store)
+
+    def _children(self, p):
+        pre = p.rstrip("/") + "/"
+        names = sorted({k[len(pre):].split("/")[0] for k in self.store if k.startswith(pre)})
+        return [(n, pre + n) for n in names]
+
+    def _redirect(self, path, q):
+        self.users.add(q.get("user.name", ""))
+        if int(self.headers.get("Content-Length", "0") or 0):
+            type(self).namenode_bodies += 1
+            self._body()
+        host = self.headers["Host"]
+        loc = f"http://{host}/dn{urllib.parse.quote(path)}?" + urllib.parse.urlencode(q)
+        self._send(307, b"", {"Location": loc, "Content-Length": "0"})
+
+    def do_GET(self):
+        path, q = self._split()
+        if path.startswith("/dn/"):
+            data = self.store[path[3:]]
+            off, n = int(q.get("offset", 0)), int(q.get("length", len(data)))
+            return self._send(200, data[off:off + n])
+        assert path.startswith("/webhdfs/v1")
+        p = path[len("/webhdfs/v1"):] or "/"
+        op = q["op"]
+        self.users.add(q.get("user.name", ""))
+        if op == "GETFILESTATUS":
+            if p not in self.store and not self._is_dir(p):
+                return self._missing(p)
+            return self._json(200, {"FileStatus": self._status(p, "")})
+        if op in ("LISTSTATUS", "LISTSTATUS_BATCH"):
+            if op == "LISTSTATUS_BATCH" and not self.batch:
+                return self._json(400, {"RemoteException": {"exception": "IllegalArgumentException",
+                                                            "message": "Invalid value for webhdfs parameter \"op\""}})
+            if p in self.store:
+                kids = [("", p)]
+            elif self._is_dir(p):
+                kids = self._children(p)
+            else:
+                return self._missing(p)
+            if op == "LISTSTATUS":
+                return self._json(200, {"FileStatuses": {"FileStatus": [self._status(f, n) for n, f in kids]}})
+            after = q.get("startAfter")
+            if after:
+                kids = [k for k in kids if k[0] > after]
+            page = kids[:2]
+            return self._json(200, {"DirectoryListing": {
+                "partialListing": {"FileStatuses": {"FileStatus": [self._status(f, n) for n, f in page]}},
+                "remainingEntries": len(kids) - len(page)}})
+        if op == "OPEN":
+            if p not in self.store:
+                return self._missing(p)
+            return self._redirect(p, q)
+        self._send(400)
+
+    def do_PUT(self):
+        path, q = self._split()
+        if path.startswith("/dn/"):
+            assert q["op"] == "CREATE"
+            self.store[path[3:]] = self._body()
+            return self._send(201, b"", {"Location": "webhdfs://" + path[3:]})
+        self._redirect(path[len("/webhdfs/v1"):], q)
+
+    def do_POST(self):
+        path, q = self._split()
+        if path.startswith("/dn/"):
+            assert q["op"] == "APPEND"
+            p = path[3:]
+            if p not in self.store:
+                return self._missing(p)
+            self.store[p] = self.store[p] + self._body()
+            return self._send(200)
+        self._redirect(path[len("/webhdfs/v1"):], q)
+
+
 def serve(handler):
     """Start a server on 127.0.0.1:<free port> in a daemon thread."""
     srv = ThreadingHTTPServer(("127.0.0.1", 0), handler)

@@ -174,3 +174,83 @@ def test_http_ranged_reads():
 def test_hdfs_fails_loudly_without_libhdfs():
     with pytest.raises(_dmlc.DMLCError, match="libhdfs"):
         io.Stream("hdfs://namenode:8020/x", "r")
+
+
+@pytest.fixture()
+def webhdfs():
+    mock_remote.WebHdfsHandler.store = {}
+    mock_remote.WebHdfsHandler.namenode_bodies = 0
+    mock_remote.WebHdfsHandler.batch = True
+    srv = mock_remote.serve(mock_remote.WebHdfsHandler)
+    os.environ["HADOOP_USER_NAME"] = "dmlc"
+    os.environ["DMLC_WEBHDFS_WRITE_BUFFER_MB"] = "1"
+    yield mock_remote.WebHdfsHandler, f"127.0.0.1:{srv.server_address[1]}"
+    srv.shutdown()
+    for k in ("HADOOP_USER_NAME", "DMLC_WEBHDFS_WRITE_BUFFER_MB", "DMLC_WEBHDFS_ENDPOINT",
+              "DMLC_HDFS_BACKEND"):
+        os.environ.pop(k, None)
+
+
+def test_webhdfs_create_append_open_roundtrip(webhdfs):
+    """Writes CREATE with the first 1 MiB block and APPEND the rest, each via
+    the namenode's 307 to the datanode (no data ever sent to the namenode);
+    reads are ranged OPENs, through both the direct and the read-ahead path."""
+    h, addr = webhdfs
+    payload = _blob((3 << 20) + 4321, seed=11)
+    w = io.Stream(f"webhdfs://{addr}/user/dmlc/blob.bin", "w")
+    for i in range(0, len(payload), 700_000):
+        w.write(payload[i:i + 700_000])
+    w.close()
+    assert h.store["/user/dmlc/blob.bin"] == payload
+    assert h.namenode_bodies == 0
+    assert h.users == {"dmlc"}
+    assert _read_all(f"webhdfs://{addr}/user/dmlc/blob.bin", chunk=16 << 20) == payload
+    assert _read_all(f"webhdfs://{addr}/user/dmlc/blob.bin", chunk=5000) == payload
+    # "a" mode appends to an existing file
+    a = io.Stream(f"webhdfs://{addr}/user/dmlc/blob.bin", "a")
+    a.write(b"tail")
+    a.close()
+    assert h.store["/user/dmlc/blob.bin"] == payload + b"tail"
+    # an empty "w" stream still creates the file
+    io.Stream(f"webhdfs://{addr}/user/dmlc/empty", "w").close()
+    assert h.store["/user/dmlc/empty"] == b""
+
+
+@pytest.mark.parametrize("batch", [True, False])
+def test_webhdfs_listing_and_sharded_parser(webhdfs, tmp_path, batch):
+    """A directory of 5 LibSVM parts (+ a subdirectory, not descended into) is
+    listed in pages of 2 (LISTSTATUS_BATCH / startAfter) or, on an older
+    namenode, with one LISTSTATUS; sharded parsing equals the local files."""
+    h, addr = webhdfs
+    h.batch = batch
+    local = tmp_path / "d"
+    local.mkdir()
+    for i in range(5):
+        f = local / f"part-{i}.libsvm"
+        data.write_synthetic(str(f), i * 400, (i + 1) * 400, seed=21)
+        h.store[f"/data/train/part-{i}.libsvm"] = f.read_bytes()
+    h.store["/data/train/sub/x.libsvm"] = b"1 1:1\n"
+    import pyref
+    for nparts in (1, 3):
+        for part in range(nparts):
+            a = pyref.concat_blocks(list(data.iter_blocks(f"webhdfs://{addr}/data/train", part, nparts,
+                                                          type="libsvm")))
+            b = pyref.concat_blocks(list(data.iter_blocks(str(local), part, nparts, type="libsvm")))
+            np.testing.assert_array_equal(a["index"], b["index"])
+            np.testing.assert_array_equal(a["value"], b["value"])
+            np.testing.assert_array_equal(a["offset"], b["offset"])
+
+
+def test_hdfs_routes_to_webhdfs_without_libhdfs(webhdfs):
+    h, addr = webhdfs
+    h.store["/x/y.txt"] = b"a\nbb\nccc\n"
+    os.environ["DMLC_WEBHDFS_ENDPOINT"] = f"http://{addr}"
+    # a namenode address not seen before, so a fresh hdfs:// instance is made
+    recs = [r.rstrip(b"\x00\n") for r in io.iter_records("hdfs://nn-web:8020/x/y.txt", 0, 1, "text")]
+    assert recs == [b"a", b"bb", b"ccc"]
+
+
+def test_webhdfs_missing_file_reports_remote_exception(webhdfs):
+    _, addr = webhdfs
+    with pytest.raises(_dmlc.DMLCError, match="FileNotFoundException"):
+        io.Stream(f"webhdfs://{addr}/nope", "r")
