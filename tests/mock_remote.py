@@ -375,8 +375,9 @@ class WebHdfsHandler(_Base):
             return self._json(200, {"FileStatus": self._status(p, "")})
         if op in ("LISTSTATUS", "LISTSTATUS_BATCH"):
             if op == "LISTSTATUS_BATCH" and not self.batch:
-                return self._json(400, {"RemoteException": {"exception": "IllegalArgumentException",
-                                                            "message": "Invalid value for webhdfs parameter \"op\""}})
+                exc = {"exception": "IllegalArgumentException",
+                       "message": "Invalid value for webhdfs parameter \"op\""}
+                return self._json(400, {"RemoteException": exc})
             if p in self.store:
                 kids = [("", p)]
             elif self._is_dir(p):
@@ -384,7 +385,8 @@ class WebHdfsHandler(_Base):
             else:
                 return self._missing(p)
             if op == "LISTSTATUS":
-                return self._json(200, {"FileStatuses": {"FileStatus": [self._status(f, n) for n, f in kids]}})
+                sts = [self._status(f, n) for n, f in kids]
+                return self._json(200, {"FileStatuses": {"FileStatus": sts}})
             after = q.get("startAfter")
             if after:
                 kids = [k for k in kids if k[0] > after]
