@@ -1,0 +1,173 @@
+"""YARN: the dmlc ApplicationMaster policy (reference
+tracker/yarn/.../ApplicationMaster.java:482-610) over local process
+containers, and the JVM-free Services REST submission against a mock RM."""
+import json
+import os
+import sys
+import threading
+import urllib.parse
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+import pytest
+
+from dmlc_core_amd.parallel.launch import yarn, yarn_am
+from dmlc_core_amd.parallel.launch.opts import get_opts
+
+PY = sys.executable
+
+
+def _task_cmd(tmp_path, body):
+    script = tmp_path / "task.py"
+    script.write_text("import os, sys\n" + body)
+    return [PY, str(script)]
+
+
+def test_am_runs_every_task_once_with_dmlc_env(tmp_path):
+    out = tmp_path / "out"
+    out.mkdir()
+    cmd = _task_cmd(tmp_path, f"open(os.path.join({str(out)!r}, os.environ['DMLC_TASK_ID']), 'w')"
+                              ".write(os.environ['DMLC_ROLE'] + ' ' + os.environ['DMLC_NODE_HOST'] + ' '"
+                              " + os.environ['DMLC_NUM_ATTEMPT'] + ' ' + os.environ['DMLC_TRACKER_URI'])\n")
+    be = yarn_am.LocalContainerBackend(nodes=["n0", "n1"])
+    env = {"DMLC_NUM_WORKER": "3", "DMLC_NUM_SERVER": "1", "DMLC_TRACKER_URI": "10.0.0.1",
+           "DMLC_WORKER_MEMORY_MB": "2048", "OTHER": "x"}
+    am = yarn_am.ApplicationMaster.from_env(be, cmd, env)
+    assert am.res["worker"].memory_mb == 2048
+    res = am.run(timeout=60)
+    assert res.success and res.finished == 4 and res.failed == 0
+    got = {int(p.name): p.read_text().split() for p in out.iterdir()}
+    assert sorted(got) == [0, 1, 2, 3]
+    assert [got[i][0] for i in range(4)] == ["worker", "worker", "worker", "server"]
+    assert all(g[2] == "0" and g[3] == "10.0.0.1" for g in got.values())
+    assert all("OTHER" not in e for _, _, e in be.launched)  # only DMLC_* is forwarded
+
+
+def test_am_retries_on_another_node_and_blacklists(tmp_path):
+    """Every container on n0 fails: the task is retried (attempt 1), n0 is
+    blacklisted, later n0 containers are released unused, the job succeeds."""
+    cmd = _task_cmd(tmp_path, "sys.exit(0)\n")
+    be = yarn_am.LocalContainerBackend(nodes=["n0", "n1", "n2"], fail_nodes={"n0": 1})
+    am = yarn_am.ApplicationMaster(be, cmd, num_worker=3, max_attempt=3, env={})
+    res = am.run(timeout=60)
+    assert res.success, res.diagnostics
+    assert res.blacklist == ["n0"]
+    assert res.attempts[0] == 1 and res.attempts[1] == 0 and res.attempts[2] == 0
+    assert be.released  # a later allocation on n0 was handed back
+    retried = [e for _, node, e in be.launched if e["DMLC_TASK_ID"] == "0"]
+    assert [e["DMLC_NUM_ATTEMPT"] for e in retried] == ["0", "1"]
+
+
+def test_am_aborts_after_max_attempts(tmp_path):
+    cmd = _task_cmd(tmp_path, "sys.exit(int(os.environ['DMLC_TASK_ID'] == '1') * 3)\n")
+    be = yarn_am.LocalContainerBackend(nodes=[f"n{i}" for i in range(8)])
+    am = yarn_am.ApplicationMaster(be, cmd, num_worker=2, max_attempt=2, env={})
+    res = am.run(timeout=60)
+    assert not res.success
+    assert "Task 1 failed more than 2 times" in res.diagnostics
+    assert res.finished == 1 and res.failed == 1
+    assert res.diagnostics.startswith("Diagnostics., num_tasks2, finished=1, failed=1")
+
+
+@pytest.mark.parametrize("status,word", [(yarn_am.KILLED_EXCEEDED_PMEM, "physical"),
+                                         (yarn_am.KILLED_EXCEEDED_VMEM, "virtual")])
+def test_am_memory_kill_aborts_immediately(tmp_path, status, word):
+    cmd = _task_cmd(tmp_path, "import time; time.sleep(30)\n")
+    be = yarn_am.LocalContainerBackend(nodes=["bad", "ok1", "ok2"], fail_nodes={"bad": status})
+    am = yarn_am.ApplicationMaster(be, cmd, num_worker=3, max_attempt=5, env={})
+    res = am.run(timeout=60)
+    assert not res.success
+    assert f"exceeding allocated {word} memory" in res.diagnostics
+    assert res.failed == 3 and res.finished == 0  # the sleeping tasks were stopped
+    assert not be.procs
+
+
+# ------------------------------------------------------------ Services REST API
+class _RM(BaseHTTPRequestHandler):
+    protocol_version = "HTTP/1.1"
+    services = {}
+    script = []  # successive container states returned by GET
+    deleted = []
+
+    def log_message(self, *a):
+        pass
+
+    def _send(self, code, obj=None):
+        b = json.dumps(obj).encode() if obj is not None else b""
+        self.send_response(code)
+        self.send_header("Content-Length", str(len(b)))
+        self.end_headers()
+        self.wfile.write(b)
+
+    def do_POST(self):
+        n = int(self.headers["Content-Length"])
+        spec = json.loads(self.rfile.read(n))
+        assert urllib.parse.urlsplit(self.path).query == "user.name=alice"
+        self.services[spec["name"]] = spec
+        self._send(202, {"uri": "/app/v1/services/" + spec["name"]})
+
+    def do_GET(self):
+        name = urllib.parse.urlsplit(self.path).path.rsplit("/", 1)[1]
+        st = self.script.pop(0) if len(self.script) > 1 else self.script[0]
+        self._send(200, dict(st, name=name))
+
+    def do_DELETE(self):
+        self.deleted.append(urllib.parse.urlsplit(self.path).path.rsplit("/", 1)[1])
+        self._send(200, {})
+
+
+@pytest.fixture()
+def rm():
+    srv = ThreadingHTTPServer(("127.0.0.1", 0), _RM)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    _RM.services, _RM.deleted = {}, []
+    os.environ["HADOOP_USER_NAME"] = "alice"
+    yield f"http://127.0.0.1:{srv.server_address[1]}"
+    os.environ.pop("HADOOP_USER_NAME", None)
+    srv.shutdown()
+
+
+def _args(*extra):
+    return get_opts(["--cluster", "yarn", "--num-workers", "4", "--num-servers", "1",
+                     "--worker-memory", "2g", "--gpus-per-node", "8", "--env", "FOO=bar",
+                     *extra, "python", "train.py"])
+
+
+def test_service_spec_shapes_components():
+    spec = yarn.service_spec(_args(), {"DMLC_TRACKER_URI": "1.2.3.4", "DMLC_TRACKER_PORT": 9091},
+                             "job")
+    comps = {c["name"]: c for c in spec["components"]}
+    w, s = comps["worker"], comps["server"]
+    assert w["number_of_containers"] == 4 and s["number_of_containers"] == 1
+    assert w["resource"]["memory"] == "2048" and w["resource"]["additional"]["amd.com/gpu"]["value"] == 8
+    assert "additional" not in s["resource"]
+    assert w["configuration"]["env"]["DMLC_TRACKER_PORT"] == "9091"
+    assert w["configuration"]["env"]["DMLC_ROLE"] == "worker" and w["configuration"]["env"]["FOO"] == "bar"
+    assert w["launch_command"].endswith("python train.py")
+
+
+def test_service_job_success_and_memory_abort(rm):
+    job = yarn.YarnServiceJob(rm, "j1")
+    job.submit(yarn.service_spec(_args(), {}, "j1"))
+    assert "j1" in _RM.services
+    _RM.script = [{"state": "ACCEPTED"}, {"state": "STARTED", "components": []},
+                  {"state": "SUCCEEDED"}]
+    assert job.wait(poll=0.01) == (True, "SUCCEEDED")
+    # a container killed by the NM memory monitor aborts the service at once
+    _RM.script = [{"state": "STARTED", "components": [{"name": "worker", "containers": [
+        {"id": "c1", "state": "FAILED",
+         "diagnostics": "Container is running 2.1GB beyond physical memory limits"}]}]}]
+    ok, diag = job.wait(poll=0.01)
+    assert not ok and "exceeding allocated memory" in diag and _RM.deleted == ["j1"]
+
+
+def test_service_job_aborts_after_repeated_failures(rm):
+    job = yarn.YarnServiceJob(rm, "j2")
+    def failed(cid):
+        return {"state": "STARTED", "components": [{"name": "worker", "containers": [
+            {"id": cid, "component_instance_name": "worker-0", "state": "FAILED",
+             "diagnostics": "exit 1"}]}]}
+    # the same failed container seen on several polls counts once
+    _RM.script = [failed("c7"), failed("c7"), failed("c8"), failed("c8"), failed("c9")]
+    ok, diag = job.wait(poll=0.01, max_attempt=3)
+    assert not ok and "worker/worker-0 failed more than 3 times" in diag
+    assert _RM.deleted == ["j2"]
