@@ -61,7 +61,7 @@ def dataset(request, tmp_path_factory):
     return fmt, p, host
 
 
-@pytest.mark.parametrize("dim,seed", [(256, 0), (1024, 7)])
+@pytest.mark.parametrize("dim,seed", [(48, 3), (64, 1), (256, 0), (1024, 7), (2048, 5)])
 def test_k9_and_fused_match_independent_hash(dataset, dim, seed):
     fmt, p, host = dataset
     libfm = fmt == "libfm"
