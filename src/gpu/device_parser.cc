@@ -136,19 +136,22 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     copy_.reset(new Stream());
     for (int d = 0; d < cfg_.device_slots; ++d) {
       dtext_.emplace_back(new DeviceBuffer(cfg_.chunk_bytes + kTextPadBytes));
-      // the pad is read (never used) by 16-byte loads past the chunk end
-      DMLC_HIP_CHECK(hipMemset(dtext_.back()->get(), 0, cfg_.chunk_bytes + kTextPadBytes));
+      // the pad is read (never used) by 16-byte loads past the chunk end.  The
+      // memsets go on the copy stream: the streams are non-blocking, so a
+      // null-stream hipMemset is not ordered before the H2D copy into the slot
+      DMLC_HIP_CHECK(hipMemsetAsync(dtext_.back()->get(), 0, cfg_.chunk_bytes + kTextPadBytes,
+                                    copy_->get()));
       copied_.emplace_back(new Event());
       parsed_.emplace_back(new Event());
       parsed_.back()->Record(compute_->get());
     }
     tiles_.Reserve(LineIndexTiles(cfg_.chunk_bytes) * sizeof(uint64_t));
-    tcounts_.Reserve(TileCount(cfg_.chunk_bytes) * sizeof(uint64_t));
-    tflags_.Reserve(TileCount(cfg_.chunk_bytes) * sizeof(uint32_t));
+    tcounts_.Reserve(TileScratchWords(TileCount(cfg_.chunk_bytes)) * sizeof(uint64_t));
+    tflags_.Reserve(TileScratchWords(TileCount(cfg_.chunk_bytes)) * sizeof(uint32_t));
     meta_.Reserve(2 * sizeof(ChunkMeta));
     hmeta_.Reserve(2 * sizeof(ChunkMeta));
     hmap_.Reserve(sizeof(ChunkMeta), /*mapped=*/true);
-    slots_.Reserve(std::max<size_t>(kMaxPartialBlocks, TileCount(cfg_.chunk_bytes)) *
+    slots_.Reserve(std::max<size_t>(kMaxPartialBlocks, TileScratchSlots(TileCount(cfg_.chunk_bytes))) *
                    sizeof(MetaPartial));
     iter_.set_max_capacity(static_cast<size_t>(cfg_.pinned_slots));
     if (cfg_.zero_copy != 0) {
@@ -355,7 +358,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
         // slot once the parse that last used it has finished
         parsed_[d]->Synchronize();
         dtext_[d].reset(new DeviceBuffer(size + kTextPadBytes));
-        DMLC_HIP_CHECK(hipMemset(dtext_[d]->get(), 0, size + kTextPadBytes));
+        DMLC_HIP_CHECK(hipMemsetAsync(dtext_[d]->get(), 0, size + kTextPadBytes, copy_->get()));
       }
       char* dst = dtext_[d]->template get<char>();
       if (caching_) {
@@ -380,7 +383,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     if (arena_ == nullptr) {
       arena_bytes_ = PartitionBytes();
       arena_.reset(new DeviceBuffer(arena_bytes_ + kTextPadBytes));
-      DMLC_HIP_CHECK(hipMemset(arena_->get(), 0, arena_bytes_ + kTextPadBytes));
+      DMLC_HIP_CHECK(hipMemsetAsync(arena_->get(), 0, arena_bytes_ + kTextPadBytes, copy_->get()));
     }
     caching_ = true;
   }
@@ -427,9 +430,9 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   /*! \brief per-chunk scratch for a chunk of nbytes (chunks may exceed chunk_bytes) */
   void EnsureScratch(size_t nbytes) {
     const size_t tiles = TileCount(nbytes);
-    tcounts_.Reserve(tiles * sizeof(uint64_t));
-    tflags_.Reserve(tiles * sizeof(uint32_t));
-    slots_.Reserve(std::max<size_t>(kMaxPartialBlocks, tiles) * sizeof(MetaPartial));
+    tcounts_.Reserve(TileScratchWords(tiles) * sizeof(uint64_t));
+    tflags_.Reserve(TileScratchWords(tiles) * sizeof(uint32_t));
+    slots_.Reserve(std::max<size_t>(kMaxPartialBlocks, TileScratchSlots(tiles)) * sizeof(MetaPartial));
     tiles_.Reserve(LineIndexTiles(nbytes) * sizeof(uint64_t));
   }
 

@@ -153,6 +153,10 @@ constexpr size_t kTileBytes = 8192;
 constexpr unsigned kFlagNeedWeight = 2048u;
 /*! \brief tiles of a chunk (size of the tile count / flag scratch and MetaPartial slots) */
 size_t TileCount(size_t nbytes);
+/*! \brief u64 tile_counts / u32 tile_flags entries to reserve for ntiles tiles (scan scratch) */
+size_t TileScratchWords(size_t ntiles);
+/*! \brief MetaPartial slots to reserve for ntiles tiles (finish-fold scratch) */
+size_t TileScratchSlots(size_t ntiles);
 /*!
  * \brief C1 + C2: per-tile (line starts << 32 | token starts) and irregular
  *  flags, exclusive-scanned in place; meta receives nlines, nrows = nlines,

@@ -26,6 +26,8 @@
  *     label / offset directly.  Only a tile's last token, which may continue
  *     into the next tile, is read from global memory.
  *     K8 (max index / field, flags) is a per-workgroup slot.
+ *  (C2 and C4 become two-level -- many workgroups, then one -- above 8192
+ *  tiles, i.e. for the 1 GiB passes over HBM-resident text.)
  *  C4 k_tile_finish (one workgroup): fold the slots into the ChunkMeta and
  *     write the chunk's closing row pointer.
  *  Traffic per chunk: text read twice (C1, C3) + the CSR written once.
@@ -279,6 +281,87 @@ __global__ __launch_bounds__(kScanThreads) void k_tile_scan(uint64_t* __restrict
     meta->pad = 0;
     if (host_meta != nullptr) *host_meta = *meta;  // mapped pinned copy: no D2H blit
   }
+}
+
+/*!
+ * \brief two-level scan for large chunks (a 1 GiB HBM-resident pass has 131 K
+ *  tiles; one workgroup reading them all is bound by a single CU's load path).
+ *  Level 1: workgroup g scans tiles [4096 g, 4096 (g+1)) in place -- coalesced
+ *  loads into LDS, a blocked 4-per-lane scan, coalesced stores -- and writes
+ *  its total and flag OR.  Level 2 is k_tile_scan over the block totals (it
+ *  also fills the ChunkMeta).  Level 3 adds each block's prefix to its tiles.
+ */
+constexpr int kScanBlockPer = 4;
+constexpr size_t kScanBlockTiles = static_cast<size_t>(kScanThreads) * kScanBlockPer;
+__global__ __launch_bounds__(kScanThreads) void k_tile_scan_local(uint64_t* __restrict__ counts,
+                                                                  const uint32_t* __restrict__ flags,
+                                                                  size_t ntiles,
+                                                                  uint64_t* __restrict__ bsum,
+                                                                  uint32_t* __restrict__ bflag) {
+  __shared__ uint64_t sbuf[kScanBlockTiles];
+  __shared__ uint64_t swave[kScanThreads / 64];
+  __shared__ uint32_t sfl[kScanThreads / 64];
+  const int wid = threadIdx.x / dev::kWave;
+  const size_t t0 = static_cast<size_t>(blockIdx.x) * kScanBlockTiles;
+  uint32_t fl = 0;
+#pragma unroll
+  for (int k = 0; k < kScanBlockPer; ++k) {
+    const size_t idx = t0 + static_cast<size_t>(k) * kScanThreads + threadIdx.x;
+    uint64_t c = 0;
+    if (idx < ntiles) {
+      c = counts[idx];
+      fl |= flags[idx];
+    }
+    sbuf[k * kScanThreads + threadIdx.x] = c;
+  }
+  __syncthreads();
+  uint64_t v[kScanBlockPer];
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanBlockPer; ++i) {
+    v[i] = sbuf[threadIdx.x * kScanBlockPer + i];
+    s += v[i];
+  }
+  uint64_t wtot;
+  const uint64_t wx = dev::wave_excl_scan(s, &wtot);
+  fl = dev::wave_or(fl);
+  if (dev::lane_id() == 0) {
+    swave[wid] = wtot;
+    sfl[wid] = fl;
+  }
+  __syncthreads();
+  uint64_t before = 0, all = 0;
+  uint32_t f = 0;
+#pragma unroll
+  for (int w = 0; w < kScanThreads / 64; ++w) {
+    const uint64_t t = swave[w];
+    if (w < wid) before += t;
+    all += t;
+    f |= sfl[w];
+  }
+  uint64_t x = before + wx;
+#pragma unroll
+  for (int i = 0; i < kScanBlockPer; ++i) {  // each lane rewrites only its own 4 entries
+    sbuf[threadIdx.x * kScanBlockPer + i] = x;
+    x += v[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kScanBlockPer; ++k) {
+    const size_t idx = t0 + static_cast<size_t>(k) * kScanThreads + threadIdx.x;
+    if (idx < ntiles) counts[idx] = sbuf[k * kScanThreads + threadIdx.x];
+  }
+  if (threadIdx.x == 0) {
+    bsum[blockIdx.x] = all;
+    bflag[blockIdx.x] = f;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_tile_scan_add(uint64_t* __restrict__ counts,
+                                                            size_t ntiles,
+                                                            const uint64_t* __restrict__ bprefix) {
+  const size_t t = static_cast<size_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (t < ntiles) counts[t] += bprefix[t / kScanBlockTiles];
 }
 
 /*!
@@ -949,6 +1032,67 @@ __global__ __launch_bounds__(kFinishThreads) void k_tile_finish(
     if (host_meta != nullptr) *host_meta = *meta;
   }
 }
+/*! \brief level 1 of the finish fold: workgroup g folds slots g, g+G, ... into out[g] */
+__global__ __launch_bounds__(kFinishThreads) void k_tile_finish_partial(
+    const MetaPartial* __restrict__ p, size_t np, MetaPartial* __restrict__ out) {
+  unsigned long long mi = 0, mf = 0;
+  unsigned fl = 0;
+  const size_t stride = static_cast<size_t>(gridDim.x) * kFinishThreads;
+  for (size_t i = static_cast<size_t>(blockIdx.x) * kFinishThreads + threadIdx.x; i < np;
+       i += stride) {
+    const MetaPartial q = p[i];
+    mi = q.max_index > mi ? q.max_index : mi;
+    mf = q.max_field > mf ? q.max_field : mf;
+    fl |= q.flags;
+  }
+  __shared__ unsigned long long s_mi[kFinishThreads / 64], s_mf[kFinishThreads / 64];
+  __shared__ unsigned s_fl[kFinishThreads / 64];
+  mi = dev::wave_max(mi);
+  mf = dev::wave_max(mf);
+  fl = dev::wave_or(fl);
+  const int wid = threadIdx.x / dev::kWave;
+  if (dev::lane_id() == 0) {
+    s_mi[wid] = mi;
+    s_mf[wid] = mf;
+    s_fl[wid] = fl;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kFinishThreads / 64; ++w) {
+      mi = s_mi[w] > mi ? s_mi[w] : mi;
+      mf = s_mf[w] > mf ? s_mf[w] : mf;
+    }
+    mi = s_mi[0] > mi ? s_mi[0] : mi;
+    mf = s_mf[0] > mf ? s_mf[0] : mf;
+    unsigned f = 0;
+    for (int w = 0; w < kFinishThreads / 64; ++w) f |= s_fl[w];
+    MetaPartial r;
+    r.max_index = mi;
+    r.max_field = mf;
+    r.flags = f;
+    r.pad = 0;
+    out[blockIdx.x] = r;
+  }
+}
+
+// chunks above this many tiles take the multi-workgroup scan / finish
+constexpr size_t kTwoLevelTiles = 2 * kScanBlockTiles;
+constexpr int kFinishGroups = 128;
+
+void LaunchFinish(MetaPartial* partials, size_t ntiles, ChunkMeta* meta, ChunkMeta* host_meta,
+                  uint64_t* offset, uint64_t row_base, uint64_t nnz_base, hipStream_t stream) {
+  const MetaPartial* src = partials;
+  int np = static_cast<int>(ntiles);
+  if (ntiles > kTwoLevelTiles) {
+    MetaPartial* folded = partials + ntiles;  // TileScratchSlots(ntiles) leaves room
+    hipLaunchKernelGGL(k_tile_finish_partial, dim3(kFinishGroups), dim3(kFinishThreads), 0, stream,
+                       partials, ntiles, folded);
+    src = folded;
+    np = kFinishGroups;
+  }
+  hipLaunchKernelGGL(k_tile_finish, dim3(1), dim3(kFinishThreads), 0, stream, src, np, meta,
+                     host_meta, offset, row_base, nnz_base);
+}
 }  // namespace
 
 size_t TileCount(size_t nbytes) { return (nbytes + kTileBytes - 1) / kTileBytes; }
@@ -963,9 +1107,28 @@ void LaunchTileCountScan(const char* text, size_t nbytes, uint64_t* tile_counts,
                        stream, reinterpret_cast<const uint8_t*>(text), nbytes, ntiles, tile_counts,
                        tile_flags);
   }
-  hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kScanThreads), 0, stream, tile_counts, tile_flags,
-                     ntiles, meta, host_meta);
+  if (ntiles <= kTwoLevelTiles) {
+    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kScanThreads), 0, stream, tile_counts,
+                       tile_flags, ntiles, meta, host_meta);
+    return;
+  }
+  // block totals / flags live past the tiles (TileScratchWords reserves them)
+  const size_t nblk = (ntiles + kScanBlockTiles - 1) / kScanBlockTiles;
+  uint64_t* bsum = tile_counts + ntiles;
+  uint32_t* bflag = tile_flags + ntiles;
+  hipLaunchKernelGGL(k_tile_scan_local, dim3(nblk), dim3(kScanThreads), 0, stream, tile_counts,
+                     tile_flags, ntiles, bsum, bflag);
+  hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kScanThreads), 0, stream, bsum, bflag, nblk, meta,
+                     host_meta);
+  hipLaunchKernelGGL(k_tile_scan_add, dim3((ntiles + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                     stream, tile_counts, ntiles, bsum);
 }
+
+size_t TileScratchWords(size_t ntiles) {
+  return ntiles + (ntiles + kScanBlockTiles - 1) / kScanBlockTiles + 64;
+}
+
+size_t TileScratchSlots(size_t ntiles) { return ntiles + kFinishGroups; }
 
 template <typename IndexType>
 void LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
@@ -983,9 +1146,7 @@ void LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
                          dim3(kThreads), 0, stream, t, nbytes, tile_prefix, out, partials);
     }
   }
-  hipLaunchKernelGGL(k_tile_finish, dim3(1), dim3(kFinishThreads), 0, stream, partials,
-                     static_cast<int>(ntiles), meta, host_meta, out.offset, out.row_base,
-                     out.nnz_base);
+  LaunchFinish(partials, ntiles, meta, host_meta, out.offset, out.row_base, out.nnz_base, stream);
 }
 
 template <typename IndexType>
@@ -1016,8 +1177,7 @@ void LaunchTileHashed(const char* text, size_t nbytes, TextFormat format,
     }
 #undef DMLC_TILE_HASH
   }
-  hipLaunchKernelGGL(k_tile_finish, dim3(1), dim3(kFinishThreads), 0, stream, partials,
-                     static_cast<int>(ntiles), meta, host_meta, nullptr, 0ull, 0ull);
+  LaunchFinish(partials, ntiles, meta, host_meta, nullptr, 0ull, 0ull, stream);
 }
 
 template void LaunchTileHashed<uint32_t>(const char*, size_t, TextFormat, const uint64_t*,

@@ -326,3 +326,26 @@ def test_zero_copy_windowed_pinning(tmp_path, hbm_cache):
     while g.next():
         blocks.append(g.value_to_host())
     assert_same(pyref.concat_blocks(blocks), c)
+
+
+def test_two_level_scan_and_finish_on_large_chunks(tmp_path):
+    """Chunks above 8192 tiles (64 MiB) take the multi-workgroup tile scan and
+    finish fold: one 192 MiB chunk, and HBM-cache replay passes merged up to
+    1 GiB, must equal the CPU parser; the fused hashed batch of one big chunk
+    must equal the one built from 4 MiB chunks."""
+    p = str(tmp_path / "big.libsvm")
+    data.write_synthetic(p, 0, 250_000, format="libsvm", seed=5)
+    assert os.path.getsize(p) > 100 << 20
+    c = cpu_rows(p, "libsvm")
+    assert_same(gpu_rows(p, "libsvm", chunk_bytes=192 << 20), c)
+    gp = data.GPUParser(p, format="libsvm", chunk_bytes=16 << 20, hbm_cache=1)
+    for _ in range(2):  # epoch 1 streams 16 MiB chunks, epoch 2 replays one merged pass
+        gp.before_first()
+        csr = data.DeviceCSR()
+        gp.parse_all(csr)
+        assert_same(pyref.concat_blocks([csr.to_host()]), c)
+    # f32 rows (LDS accumulation order may differ between runs in the last bit)
+    big = data.GPUParser(p, format="libsvm", chunk_bytes=192 << 20).parse_all_hashed(256, seed=1, fp8=False)
+    small = data.GPUParser(p, format="libsvm", chunk_bytes=4 << 20).parse_all_hashed(256, seed=1, fp8=False)
+    np.testing.assert_allclose(big["x"].cpu().numpy(), small["x"].cpu().numpy(), rtol=1e-6, atol=1e-6)
+    np.testing.assert_array_equal(big["label"].cpu().numpy(), c["label"])
