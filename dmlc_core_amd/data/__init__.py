@@ -87,14 +87,33 @@ class GPUParser:
         self._p.parse_all(out)
         return out
 
-    def parse_all_hashed(self, dim: int, seed: int = 0, fp8: bool = True, scale: float = 1.0):
-        """Rest of the partition as a hashed dense batch, tokenised, hashed and
-        packed by ONE fused kernel per chunk (no CSR in between; BASELINE
-        config 5).  Returns ``{"x": [rows, dim] float8_e4m3fn (or float32),
-        "label": [rows] float32}`` as torch tensors on the device.  The hash
-        equals :func:`dmlc_core_amd.ops.hashed_dense` of the parsed CSR."""
+    #: widest dim at which the fused kernel beats tile CSR + K9 on MI355X
+    #: (profiles/r02_session5: 1.35x at dim 128-256, 0.88x at dim 1024, where
+    #: the per-tile LDS row buffers cost more than writing the CSR once)
+    FUSED_HASH_MAX_DIM = 512
+
+    def parse_all_hashed(self, dim: int, seed: int = 0, fp8: bool = True, scale: float = 1.0,
+                         strategy: str = "auto"):
+        """Rest of the partition as a hashed dense batch (BASELINE config 5).
+        Returns ``{"x": [rows, dim] float8_e4m3fn (or float32), "label": [rows]
+        float32}`` as torch tensors on the device.
+
+        ``strategy``: ``"fused"`` tokenises, hashes and packs with ONE kernel
+        per chunk (no CSR in between); ``"csr"`` parses to a device CSR and
+        runs :func:`dmlc_core_amd.ops.hashed_dense` (K9); ``"auto"`` takes the
+        faster of the two for ``dim`` (fused up to FUSED_HASH_MAX_DIM).  Both
+        compute the same hash."""
         import torch
         import torch.utils.dlpack as tdl
+
+        if strategy not in ("auto", "fused", "csr"):
+            raise ValueError(f"strategy must be auto, fused or csr, not {strategy!r}")
+        if strategy == "csr" or (strategy == "auto" and dim > self.FUSED_HASH_MAX_DIM):
+            from .. import ops
+
+            t = csr_to_torch(self.parse_all())
+            x = ops.hashed_dense(t, int(dim), seed=seed, fp8=fp8, scale=scale)
+            return {"x": x, "label": t["label"].clone()}  # the CSR buffers are released
 
         d = self._p.parse_all_hashed(int(dim), float(scale), int(seed) & 0xFFFFFFFF, bool(fp8))
         x = tdl.from_dlpack(d["x"]).view(d["rows"], d["dim"])

@@ -46,7 +46,7 @@ def main():
 
     def step_fused():
         fused.before_first()
-        return fused.parse_all_hashed(args.dim, seed=1, fp8=True, scale=0.5)["x"]
+        return fused.parse_all_hashed(args.dim, seed=1, fp8=True, scale=0.5, strategy="fused")["x"]
 
     res = {}
     for name, fn in (("csr_then_k9", step_two), ("fused", step_fused)):
@@ -65,7 +65,7 @@ def main():
     res["mismatch_frac"] = float((a != b).float().mean())
     model = HashedFM(dim=args.dim, rank=16).cuda()
     fused.before_first()
-    batch = fused.parse_all_hashed(args.dim, seed=1, fp8=True, scale=0.5)
+    batch = fused.parse_all_hashed(args.dim, seed=1, fp8=True, scale=0.5, strategy="fused")
     y = model(batch["x"], scale=0.5)
     loss = torch.nn.functional.binary_cross_entropy_with_logits(y, batch["label"].clamp(0, 1))
     loss.backward()
@@ -86,8 +86,8 @@ def main():
         t = {}
         for name, fn in (("csr_then_k9", lambda: ops.hashed_dense(
                 data.csr_to_torch(two.parse_all()), d, seed=1, fp8=True, scale=0.5)),
-                         ("fused", lambda: fused.parse_all_hashed(d, seed=1, fp8=True,
-                                                                  scale=0.5)["x"])):
+                         ("fused", lambda: fused.parse_all_hashed(d, seed=1, fp8=True, scale=0.5,
+                                                                  strategy="fused")["x"])):
             (two if name == "csr_then_k9" else fused).before_first()
             fn()
             torch.cuda.synchronize()

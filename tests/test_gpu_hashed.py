@@ -73,7 +73,7 @@ def test_k9_and_fused_match_independent_hash(dataset, dim, seed):
     outs = [k9]
     for fast in (1, 0):
         fused = data.GPUParser(p, format=fmt, chunk_bytes=128 * 1024, fast_path=fast
-                               ).parse_all_hashed(dim, seed=seed, fp8=False)
+                               ).parse_all_hashed(dim, seed=seed, fp8=False, strategy="fused")
         outs.append(fused["x"].cpu().numpy().astype(np.float64))
         np.testing.assert_array_equal(fused["label"].cpu().numpy(), host["label"])
     for got in outs:
@@ -82,7 +82,7 @@ def test_k9_and_fused_match_independent_hash(dataset, dim, seed):
         np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-6)
     scale = 0.5
     f8 = data.GPUParser(p, format=fmt, chunk_bytes=128 * 1024).parse_all_hashed(
-        dim, seed=seed, fp8=True, scale=scale)["x"]
+        dim, seed=seed, fp8=True, scale=scale, strategy="fused")["x"]
     assert f8.dtype == torch.float8_e4m3fn and tuple(f8.shape) == ref.shape
     want = torch.from_numpy((ref * scale).astype(np.float32)).to(torch.float8_e4m3fn)
     same = (f8.cpu().view(torch.uint8) == want.view(torch.uint8)).numpy()
@@ -131,3 +131,20 @@ def test_fused_tile_kernel_long_lines_fall_back(tmp_path):
     csr = data.csr_to_torch(data.GPUParser(p, format="libfm").parse_all())
     k9 = ops.hashed_dense(csr, 256, seed=3, fp8=False)
     np.testing.assert_allclose(fused["x"].cpu().numpy(), k9.cpu().numpy(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("dim", [256, 1024])
+def test_hashed_strategies_agree(dataset, dim):
+    """auto / csr / fused return the same batch (f32: exact up to the order of
+    colliding terms) and the same labels."""
+    fmt, p, host = dataset
+    got = {}
+    for strat in ("auto", "csr", "fused"):
+        got[strat] = data.GPUParser(p, format=fmt, chunk_bytes=128 * 1024).parse_all_hashed(
+            dim, seed=2, fp8=False, strategy=strat)
+        np.testing.assert_array_equal(got[strat]["label"].cpu().numpy(), host["label"])
+    for strat in ("auto", "fused"):
+        np.testing.assert_allclose(got[strat]["x"].cpu().numpy(), got["csr"]["x"].cpu().numpy(),
+                                   rtol=1e-6, atol=1e-6)
+    with pytest.raises(ValueError):
+        data.GPUParser(p, format=fmt).parse_all_hashed(dim, strategy="nope")

@@ -345,7 +345,9 @@ def test_two_level_scan_and_finish_on_large_chunks(tmp_path):
         gp.parse_all(csr)
         assert_same(pyref.concat_blocks([csr.to_host()]), c)
     # f32 rows (LDS accumulation order may differ between runs in the last bit)
-    big = data.GPUParser(p, format="libsvm", chunk_bytes=192 << 20).parse_all_hashed(256, seed=1, fp8=False)
-    small = data.GPUParser(p, format="libsvm", chunk_bytes=4 << 20).parse_all_hashed(256, seed=1, fp8=False)
+    big = data.GPUParser(p, format="libsvm", chunk_bytes=192 << 20).parse_all_hashed(
+        256, seed=1, fp8=False, strategy="fused")
+    small = data.GPUParser(p, format="libsvm", chunk_bytes=4 << 20).parse_all_hashed(
+        256, seed=1, fp8=False, strategy="fused")
     np.testing.assert_allclose(big["x"].cpu().numpy(), small["x"].cpu().numpy(), rtol=1e-6, atol=1e-6)
     np.testing.assert_array_equal(big["label"].cpu().numpy(), c["label"])
