@@ -254,3 +254,50 @@ def test_webhdfs_missing_file_reports_remote_exception(webhdfs):
     _, addr = webhdfs
     with pytest.raises(_dmlc.DMLCError, match="FileNotFoundException"):
         io.Stream(f"webhdfs://{addr}/nope", "r")
+
+
+def test_hdfs_through_libhdfs_abi(tmp_path):
+    """hdfs:// over the dlopen'ed libhdfs C API, using a stand-in libhdfs.so
+    (tests/fake_libhdfs.c: the hdfs.h functions over a local directory, short
+    reads and one EINTR): write (short writes looped), append, read back,
+    GetPathInfo sizes, and a sharded parse of a directory equal to local."""
+    import subprocess
+    import sys
+    lib = tmp_path / "hadoop" / "lib" / "native"
+    lib.mkdir(parents=True)
+    src = os.path.join(os.path.dirname(__file__), "fake_libhdfs.c")
+    subprocess.check_call(["gcc", "-O1", "-shared", "-fPIC", "-o", str(lib / "libhdfs.so"), src])
+    root = tmp_path / "root"
+    (root / "data").mkdir(parents=True)
+    for i in range(3):
+        data.write_synthetic(str(root / "data" / f"part-{i}.libsvm"), i * 500, (i + 1) * 500, seed=4)
+    code = f"""
+import numpy as np, pyref
+from dmlc_core_amd import data, io
+blob = bytes(range(256)) * 40
+w = io.Stream("hdfs://nn:8020/out/blob.bin", "w"); w.write(blob); w.close()
+a = io.Stream("hdfs://nn:8020/out/blob.bin", "a"); a.write(b"tail"); a.close()
+s = io.Stream("hdfs://nn:8020/out/blob.bin", "r")
+got = b""
+while True:
+    b = s.read(3000)
+    if not b:
+        break
+    got += b
+assert got == blob + b"tail", len(got)
+for nparts in (1, 2):
+    for part in range(nparts):
+        x = pyref.concat_blocks(list(data.iter_blocks("hdfs://nn:8020/data", part, nparts, type="libsvm")))
+        y = pyref.concat_blocks(list(data.iter_blocks({str(root / 'data')!r}, part, nparts, type="libsvm")))
+        for k in ("offset", "index", "value", "label"):
+            np.testing.assert_array_equal(x[k], y[k])
+print("ok")
+"""
+    env = dict(os.environ, HADOOP_HOME=str(tmp_path / "hadoop"), FAKE_HDFS_ROOT=str(root),
+               PYTHONPATH=os.pathsep.join([os.path.dirname(__file__),
+                                           os.path.dirname(os.path.dirname(__file__))]))
+    env.pop("DMLC_WEBHDFS_ENDPOINT", None)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+    assert (root / "out" / "blob.bin").read_bytes() == bytes(range(256)) * 40 + b"tail"
