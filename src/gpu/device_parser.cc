@@ -29,6 +29,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -151,6 +152,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     meta_.Reserve(2 * sizeof(ChunkMeta));
     hmeta_.Reserve(2 * sizeof(ChunkMeta));
     hmap_.Reserve(sizeof(ChunkMeta), /*mapped=*/true);
+    std::memset(hmap_.get(), 0, sizeof(ChunkMeta));  // WaitMapped polls its pad word
     slots_.Reserve(std::max<size_t>(kMaxPartialBlocks, TileScratchSlots(TileCount(cfg_.chunk_bytes))) *
                    sizeof(MetaPartial));
     iter_.set_max_capacity(static_cast<size_t>(cfg_.pinned_slots));
@@ -405,12 +407,23 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   }
 
   /*! \brief the ChunkMeta a kernel wrote into mapped pinned memory (synchronises) */
-  ChunkMeta WaitMapped(const ChunkMeta* hm) {
+  ChunkMeta WaitMapped(ChunkMeta* hm) {
     const double t0 = GetTime();
-    compute_->Synchronize();
+    // the publishing kernel raises hm->pad last (after a system fence): poll
+    // it rather than pay a blocking stream synchronise per chunk; bounded, so
+    // a kernel that never publishes (a fault) still surfaces through the sync
+    volatile unsigned* flag = &hm->pad;
+    bool seen = false;
+    for (uint32_t i = 0; !seen; ++i) {
+      seen = *flag != 0;
+      if (!seen && (i & 1023u) == 1023u && GetTime() - t0 > 0.05) break;
+    }
+    if (!seen) compute_->Synchronize();
+    std::atomic_thread_fence(std::memory_order_acquire);
     stats_.wait_gpu_sec += GetTime() - t0;
     ChunkMeta v;
     std::memcpy(&v, const_cast<const ChunkMeta*>(hm), sizeof(v));
+    *flag = 0;  // re-armed before the next publishing kernel is launched
     return v;
   }
 

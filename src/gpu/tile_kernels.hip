@@ -222,6 +222,18 @@ __global__ __launch_bounds__(kThreads) void k_tile_count(const uint8_t* __restri
   }
 }
 
+/*!
+ * \brief copy the ChunkMeta to mapped pinned host memory, then raise its
+ *  `pad` word (after a system-scope fence) so the host can poll for it
+ *  instead of a blocking stream synchronise (DeviceParser::WaitMapped)
+ */
+__device__ __forceinline__ void publish_host_meta(ChunkMeta* host_meta, ChunkMeta m) {
+  m.pad = 0;
+  *host_meta = m;
+  __threadfence_system();
+  *reinterpret_cast<volatile unsigned*>(&host_meta->pad) = 1u;
+}
+
 constexpr int kScanThreads = 1024;
 constexpr int kScanPer = 8;
 
@@ -279,7 +291,7 @@ __global__ __launch_bounds__(kScanThreads) void k_tile_scan(uint64_t* __restrict
     meta->max_field = 0;
     meta->flags = f;
     meta->pad = 0;
-    if (host_meta != nullptr) *host_meta = *meta;  // mapped pinned copy: no D2H blit
+    if (host_meta != nullptr) publish_host_meta(host_meta, *meta);  // no D2H blit
   }
 }
 
@@ -1029,7 +1041,7 @@ __global__ __launch_bounds__(kFinishThreads) void k_tile_finish(
     meta->max_field = s_mf[0];
     meta->flags |= s_fl[0];
     if (offset != nullptr) offset[row_base + meta->nrows] = nnz_base + meta->nnz;
-    if (host_meta != nullptr) *host_meta = *meta;
+    if (host_meta != nullptr) publish_host_meta(host_meta, *meta);
   }
 }
 /*! \brief level 1 of the finish fold: workgroup g folds slots g, g+G, ... into out[g] */
