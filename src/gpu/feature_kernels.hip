@@ -93,10 +93,12 @@ __global__ __launch_bounds__(kThreads) void k_hashed_dense(
   const int lane = dev::lane_id();
   float* row = smem + static_cast<size_t>(wid) * dim;
   const size_t nwaves = static_cast<size_t>(gridDim.x) * (kThreads / dev::kWave);
+  // rows are zeroed once here, then by the readout that consumes them
+  for (int c = lane; c < dim; c += dev::kWave) row[c] = 0.0f;
+  dev::wave_sync();
+  const bool wide = (dim & 15) == 0;  // 16 columns per lane: b128 LDS ops, 16 B stores
   for (size_t r = blockIdx.x * static_cast<size_t>(kThreads / dev::kWave) + wid; r < nrows;
        r += nwaves) {
-    for (int c = lane; c < dim; c += dev::kWave) row[c] = 0.0f;
-    dev::wave_sync();
     const uint64_t b = offset[r], e = offset[r + 1];
     for (uint64_t j = b + lane; j < e; j += dev::kWave) {
       const uint64_t key = dev::hash_key(static_cast<uint64_t>(index[j]),
@@ -109,17 +111,47 @@ __global__ __launch_bounds__(kThreads) void k_hashed_dense(
       atomicAdd(&row[bucket], sign * v);
     }
     dev::wave_sync();
-    if constexpr (kFP8) {
+    if (wide) {
+      float4* r4 = reinterpret_cast<float4*>(row);
+      const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      for (int c = lane * 16; c < dim; c += dev::kWave * 16) {
+        float4 x[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          x[q] = r4[c / 4 + q];
+          r4[c / 4 + q] = z;
+        }
+        if constexpr (kFP8) {
+          uint32_t w[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            int pk = __builtin_amdgcn_cvt_pk_fp8_f32(x[q].x * scale, x[q].y * scale, 0, false);
+            pk = __builtin_amdgcn_cvt_pk_fp8_f32(x[q].z * scale, x[q].w * scale, pk, true);
+            w[q] = static_cast<uint32_t>(pk);
+          }
+          *reinterpret_cast<uint4*>(static_cast<uint8_t*>(out) + r * dim + c) =
+              make_uint4(w[0], w[1], w[2], w[3]);
+        } else {
+          float4* o = reinterpret_cast<float4*>(static_cast<float*>(out) + r * dim + c);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o[q] = x[q];
+        }
+      }
+    } else if constexpr (kFP8) {
       // 4 columns per lane-iteration -> one 32-bit store of 4 fp8 (e4m3, OCP on gfx950)
       uint32_t* o = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(out) + r * dim);
       for (int c = lane * 4; c < dim; c += dev::kWave * 4) {
         int packed = __builtin_amdgcn_cvt_pk_fp8_f32(row[c] * scale, row[c + 1] * scale, 0, false);
         packed = __builtin_amdgcn_cvt_pk_fp8_f32(row[c + 2] * scale, row[c + 3] * scale, packed, true);
         o[c / 4] = static_cast<uint32_t>(packed);
+        row[c] = row[c + 1] = row[c + 2] = row[c + 3] = 0.0f;
       }
     } else {
       float* o = static_cast<float*>(out) + r * dim;
-      for (int c = lane; c < dim; c += dev::kWave) o[c] = row[c];
+      for (int c = lane; c < dim; c += dev::kWave) {
+        o[c] = row[c];
+        row[c] = 0.0f;
+      }
     }
     dev::wave_sync();
   }
