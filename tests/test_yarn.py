@@ -171,3 +171,14 @@ def test_service_job_aborts_after_repeated_failures(rm):
     ok, diag = job.wait(poll=0.01, max_attempt=3)
     assert not ok and "worker/worker-0 failed more than 3 times" in diag
     assert _RM.deleted == ["j2"]
+
+
+def test_submit_dry_run_uses_services_api_without_jar(monkeypatch, capsys):
+    """With YARN_RM_ADDRESS set and no dmlc-yarn.jar, dmlc-submit --cluster
+    yarn builds a Services spec instead of a hadoop jar command."""
+    monkeypatch.setenv("YARN_RM_ADDRESS", "http://rm.invalid:8088")
+    monkeypatch.delenv("DMLC_YARN_APP_DIR", raising=False)
+    assert yarn.submit(_args("--dry-run")) == 0
+    spec = json.loads(capsys.readouterr().out)
+    assert {c["name"] for c in spec["components"]} == {"worker", "server"}
+    assert spec["queue"] == "default"
