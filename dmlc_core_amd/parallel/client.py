@@ -112,6 +112,7 @@ class TrackerClient:
         ch = self._connect("abort")
         try:
             ch.send_str(msg)
+            ch.wait_closed()  # the tracker closes after recording the failure
         finally:
             ch.close()
 

@@ -90,6 +90,14 @@ class Channel:
     def send_str(self, s: str) -> None:
         self.send_bytes(s.encode())
 
+    def wait_closed(self) -> None:
+        """Block until the peer closes the connection (or the socket times out)."""
+        try:
+            while self.sock.recv(1):
+                pass
+        except OSError:
+            pass
+
     def close(self) -> None:
         try:
             self.sock.close()
@@ -388,9 +396,11 @@ class RabitTracker:
             return
         if w.cmd == "abort":
             msg = w.ch.recv_str()
-            w.ch.close()
             with self._mu:
                 self._fail(st, f"rank {w.rank} aborted: {msg}", w.rank)
+            # closed only once recorded: a client waiting for the close knows
+            # every later heartbeat reply carries the failure
+            w.ch.close()
             return
         if w.cmd == "shutdown":
             with self._mu:

@@ -267,10 +267,11 @@ inline bool ThreadedIter<DType>::Next(DType** out_dptr) {
 
 template <typename DType>
 inline void ThreadedIter<DType>::Recycle(DType** inout_dptr) {
-  ThrowExceptionIfSet();
+  // take the cell back BEFORE reporting a producer failure: throwing first
+  // (as the reference does) leaks the cell the consumer was handing back
   {
     std::lock_guard<std::mutex> lock(mutex_);
-    free_cells_.push_back(*inout_dptr);
+    if (*inout_dptr != nullptr) free_cells_.push_back(*inout_dptr);
     *inout_dptr = nullptr;
     producer_cond_.notify_one();
   }

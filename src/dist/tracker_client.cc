@@ -84,6 +84,15 @@ class TrackerClient::Conn {
       n -= static_cast<size_t>(k);
     }
   }
+  /*! \brief block until the peer closes (EOF) or the socket times out */
+  void WaitClosed() {
+    char b;
+    for (;;) {
+      const ssize_t k = recv(fd_, &b, 1, 0);
+      if (k < 0 && errno == EINTR) continue;
+      if (k <= 0) return;
+    }
+  }
   void SendInt(int32_t v) { SendAll(&v, sizeof(v)); }
   int32_t RecvInt() {
     int32_t v;
@@ -190,6 +199,7 @@ bool TrackerClient::Heartbeat(std::string* reason) {
 void TrackerClient::Abort(const std::string& msg) {
   auto c = Connect("abort");
   c->SendStr(msg);
+  c->WaitClosed();  // the tracker closes once the failure is recorded
 }
 
 void TrackerClient::SetFailureHandler(std::function<void(const std::string&)> handler) {
