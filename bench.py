@@ -17,6 +17,13 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
        dmlc-submit --cluster local --num-workers N --gpus-per-node N python bench.py --gpus N
          (the dmlc tracker assigns ranks and bootstraps the RCCL/gloo group)
+
+With ``--gpus N > 1`` and no launcher in the environment, this process is only
+a launcher: before touching torch or the HIP runtime it starts the N ranks
+through ``dmlc-submit --cluster local`` (reference
+`tracker/dmlc_tracker/local.py:47-72`), forwards their output (rank 0's JSON
+line) and exits with their status.  Every rank checks that the world it joined
+has exactly ``--gpus`` ranks.
 """
 from __future__ import annotations
 
@@ -95,8 +102,46 @@ def ensure_dataset(args, rank: int, world: int, barrier) -> str:
     return d
 
 
+def _launcher_present() -> bool:
+    env = os.environ
+    return ("RANK" in env and "WORLD_SIZE" in env) or "DMLC_TRACKER_URI" in env
+
+
+def _parent_maps_hip() -> bool:
+    try:
+        with open("/proc/self/maps") as f:
+            return "libamdhip64" in f.read()
+    except OSError:
+        return False
+
+
+def launch_ranks(args) -> int:
+    """Start --gpus ranks via dmlc-submit (tracker-assigned ranks, one process
+    per GPU bound by local index) and wait for them.  Runs with neither torch
+    nor the native extension imported: a process that has initialised the GPU
+    must not fork/exec the ranks."""
+    import shlex
+    import subprocess
+
+    n = args.gpus
+    child = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
+    cmd = [sys.executable, "-m", "dmlc_core_amd.parallel.launch.submit", "--cluster", "local",
+           "--num-workers", str(n), "--gpus-per-node", str(n), "--host-ip", "127.0.0.1",
+           "--auto-file-cache", "0"] + [shlex.quote(c) for c in child]
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    rc = subprocess.call(cmd, env=env, cwd=ROOT)
+    if os.environ.get("DMLC_BENCH_CHECK_MAPS") == "1":
+        print(f"bench launcher: libamdhip64 mapped = {_parent_maps_hip()}", file=sys.stderr)
+    return rc
+
+
 def main():
     args = parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and not _launcher_present():
+        sys.exit(launch_ranks(args))
 
     import torch
 
@@ -107,8 +152,9 @@ def main():
     # the tracker assigns the rank and brokers the process-group address)
     info = ddist.init("nccl" if use_gpu else "gloo")
     rank, world, local_rank = info["rank"], info["world_size"], info["local_rank"]
-    if args.gpus != world and world > 1:
-        print(f"warning: --gpus {args.gpus} but world size {world}", file=sys.stderr)
+    if args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started a world of "
+                         f"{world} rank(s)")
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: F811
@@ -224,7 +270,7 @@ def main():
             "metric": "parsed rows/sec (LibSVM->CSR in device memory), aggregate over GPUs",
             "value": round(value, 1),
             "unit": "rows/s",
-            "n_gpus": world if use_gpu else 0,
+            "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 3),

@@ -10,14 +10,21 @@ multi-GPU sharding.
 The native runtime lives in ``dmlc_core_amd/lib/libdmlc.so`` (C++17 + HIP for
 gfx950) and is exposed through ``dmlc_core_amd._dmlc`` (pybind11).  Build it
 with ``make -j8`` (or ``python -c "import __graft_entry__ as g; g.build()"``).
+
+Subpackages load lazily (PEP 562): ``import dmlc_core_amd`` alone touches
+neither torch nor the HIP runtime, so a launcher process
+(``python -m dmlc_core_amd.parallel.launch.submit``, or ``bench.py --gpus N``
+spawning its ranks) never maps ``libamdhip64`` -- only the ranks it starts do.
 """
 from __future__ import annotations
 
+import importlib
 import os
 
 __version__ = "0.1.0"
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+_SUBMODULES = ("utils", "io", "data", "ops", "parallel", "models")
 
 
 def _load_native():
@@ -30,16 +37,22 @@ def _load_native():
     except ImportError:  # pragma: no cover - torch is optional for the C++-only path
         pass
     try:
-        from . import _dmlc  # noqa: F401
+        return importlib.import_module(__name__ + "._dmlc")
     except ImportError as err:  # pragma: no cover - exercised only when unbuilt
         raise ImportError(
             "dmlc_core_amd native extension is not built; run `make -j8` in the repo root "
             f"({err})") from err
-    return _dmlc
 
 
-_native = _load_native()
+def __getattr__(name):
+    if name == "_dmlc":
+        mod = _load_native()
+    elif name in _SUBMODULES:
+        mod = importlib.import_module(f"{__name__}.{name}")
+    else:
+        raise AttributeError(f"module {__name__!r} has no attribute {name!r}")
+    globals()[name] = mod
+    return mod
 
-from . import utils, io, data, ops, parallel, models  # noqa: E402,F401
 
-__all__ = ["utils", "io", "data", "ops", "parallel", "models", "__version__"]
+__all__ = list(_SUBMODULES) + ["__version__"]

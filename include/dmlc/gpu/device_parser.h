@@ -76,6 +76,11 @@ struct DeviceParserConfig {
    *  up to this many bytes per kernel pass (`?replay_chunk_mb=`)
    */
   size_t replay_chunk_bytes{1UL << 30};
+  /*!
+   * \brief busy-poll budget (us) of a chunk-metadata wait before the host
+   *  thread falls back to 20 us sleeps (src/gpu/host_wait.h)
+   */
+  double wait_spin_us{50};
   /*! \brief apply `?k=v` overrides (chunk_mb, pinned_slots, device_slots,
    *  read_threads, device, format, label_column, weight_column, delimiter,
    *  fast_path, zero_copy, zc_pin_budget_mb, zc_window_mb, hbm_cache, replay_chunk_mb) */
@@ -112,6 +117,8 @@ struct DeviceParserStats {
   /*! \brief zero-copy mode active, and the one-time mmap + register cost */
   bool zero_copy{false};
   double register_sec{0};
+  /*! \brief metadata waits that ended spinning / sleeping / at the bound */
+  size_t waits_spun{0}, waits_slept{0}, waits_timed_out{0};
 };
 
 /*!

@@ -157,7 +157,9 @@ class PinnedBuffer {
     if (bytes <= bytes_) return;
     Free();
     unsigned flags = hipHostMallocDefault;
-    if (mapped) flags |= hipHostMallocMapped;
+    // mapped buffers are polled by the host while kernels write them:
+    // coherent explicitly, whatever HIP_HOST_COHERENT says
+    if (mapped) flags |= hipHostMallocMapped | hipHostMallocCoherent;
     DMLC_HIP_CHECK(hipHostMalloc(&ptr_, bytes == 0 ? 1 : bytes, flags));
     bytes_ = bytes;
   }

@@ -39,6 +39,7 @@
 #include "../io/line_split.h"
 #include "../io/shard_reader.h"
 #include "../io/uri_spec.h"
+#include "./host_wait.h"
 #include "./kernels.h"
 #include "./zero_copy_source.h"
 
@@ -80,6 +81,8 @@ void DeviceParserConfig::Update(const std::map<std::string, std::string>& args) 
       zc_window_bytes = static_cast<size_t>(std::atof(v.c_str()) * (1 << 20));
     } else if (k == "hbm_cache") {
       hbm_cache = v != "0" && v != "false";
+    } else if (k == "wait_spin_us") {
+      wait_spin_us = std::atof(v.c_str());
     } else if (k == "zero_copy") {
       zero_copy = (v == "auto" || v == "-1") ? -1 : ((v == "0" || v == "false") ? 0 : 1);
     }
@@ -87,6 +90,9 @@ void DeviceParserConfig::Update(const std::map<std::string, std::string>& args) 
   chunk_bytes = (chunk_bytes + 4095) & ~size_t(4095);
   CHECK_GE(chunk_bytes, 4096U) << "chunk_bytes too small";
   CHECK_LT(chunk_bytes, size_t(1) << 31) << "chunk_bytes must be < 2 GiB";
+  // merged replay chunks go through the same kernels: 32-bit line offsets on
+  // the exact path, 32-bit packed token counts on the tile path
+  CHECK_LT(replay_chunk_bytes, size_t(1) << 31) << "replay_chunk_bytes must be < 2 GiB";
   CHECK_GE(pinned_slots, 1);
   CHECK_GE(device_slots, 1);
 }
@@ -410,17 +416,17 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   ChunkMeta WaitMapped(ChunkMeta* hm) {
     const double t0 = GetTime();
     // the publishing kernel raises hm->pad last (after a system fence): poll
-    // it rather than pay a blocking stream synchronise per chunk; bounded, so
-    // a kernel that never publishes (a fault) still surfaces through the sync
+    // it rather than pay a blocking stream synchronise per chunk -- a short
+    // spin, then short sleeps (host_wait.h); bounded, so a kernel that never
+    // publishes (a fault) still surfaces through the sync
     volatile unsigned* flag = &hm->pad;
-    bool seen = false;
-    for (uint32_t i = 0; !seen; ++i) {
-      seen = *flag != 0;
-      if (!seen && (i & 1023u) == 1023u && GetTime() - t0 > 0.05) break;
-    }
+    const bool seen = WaitHostFlag(flag, cfg_.wait_spin_us, 0.05, &wait_stats_);
     if (!seen) compute_->Synchronize();
     std::atomic_thread_fence(std::memory_order_acquire);
     stats_.wait_gpu_sec += GetTime() - t0;
+    stats_.waits_spun = wait_stats_.spun;
+    stats_.waits_slept = wait_stats_.slept;
+    stats_.waits_timed_out = wait_stats_.timed_out;
     ChunkMeta v;
     std::memcpy(&v, const_cast<const ChunkMeta*>(hm), sizeof(v));
     *flag = 0;  // re-armed before the next publishing kernel is launched
@@ -599,11 +605,18 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       DMLC_FAULT_POINT("parse_fill");
     } catch (...) {
       // the chunk was not delivered: the cursor stays at its start (a resume
-      // from Tell() replays it), its slots go back to the pipeline
+      // from Tell() replays it), its slots go back to the pipeline.  The
+      // event and busy_ are settled first, and a producer error Recycle may
+      // rethrow is dropped: the parse error is the one the caller sees
       (void)hipStreamSynchronize(s);
-      if (cur_slot_ != nullptr) iter_.Recycle(&cur_slot_);
-      if (cur.d >= 0) parsed_[cur.d]->Record(s);
+      if (cur.d >= 0) (void)hipEventRecord(parsed_[cur.d]->get(), s);
       busy_ = 0;
+      if (cur_slot_ != nullptr) {
+        try {
+          iter_.Recycle(&cur_slot_);
+        } catch (...) {
+        }
+      }
       throw;
     }
     if (cur_slot_ != nullptr) iter_.Recycle(&cur_slot_);
@@ -763,6 +776,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   DeviceCSR<IndexType> block_;
   DeviceRowBlock<IndexType> view_;
   DeviceParserStats stats_;
+  HostWaitStats wait_stats_;
 };
 
 }  // namespace

@@ -8,15 +8,19 @@
  *
  *  URI arguments (besides every DeviceParserConfig key):
  *    device=gpu | gpu:<k>   route to the GPU path (current device / device k)
- *    to_host=1              copy every block back into host memory, so code
- *                           written against host RowBlocks runs unchanged;
- *                           default 0: the RowBlock's pointers are DEVICE
- *                           pointers (HBM-resident, stream-ordered and ready
- *                           when Next() returns), `offset` is 64-bit.
+ *    device_ptrs=1          (or to_host=0) serve the HBM-resident blocks: the
+ *                           RowBlock's pointers are DEVICE pointers (stream-
+ *                           ordered and ready when Next() returns), `offset`
+ *                           is 64-bit.  Default: every block is copied back
+ *                           into host memory, so code written against the
+ *                           reference's host RowBlock API (Row access, SGD
+ *                           loops) runs unchanged and never dereferences a
+ *                           device pointer by accident.
  *  GPUParser<I>   : one block per chunk (the reference's ThreadedParser shape).
  *  DeviceRowIter<I>: the whole partition parsed into one HBM-resident CSR
- *                   (ParseAll), served as a single block, NumCol = max index
- *                   + 1 (the reference's BasicRowIter, src/data/basic_row_iter.h).
+ *                   (ParseAll), served as a single block (also when it is
+ *                   empty), NumCol = max index + 1 (the reference's
+ *                   BasicRowIter, src/data/basic_row_iter.h:35-48).
  */
 #include <dmlc/data.h>
 #include <dmlc/gpu/device_parser.h>
@@ -36,7 +40,7 @@ namespace {
 
 struct RouteArgs {
   gpu::DeviceParserConfig cfg;
-  bool to_host{false};
+  bool to_host{true};
 };
 
 RouteArgs ParseRoute(const std::map<std::string, std::string>& args, const std::string& type) {
@@ -49,6 +53,8 @@ RouteArgs ParseRoute(const std::map<std::string, std::string>& args, const std::
       r.cfg.device = v.size() > 4 && v[3] == ':' ? std::atoi(v.c_str() + 4) : -1;
     } else if (kv.first == "to_host") {
       r.to_host = kv.second != "0" && kv.second != "false";
+    } else if (kv.first == "device_ptrs") {
+      r.to_host = kv.second == "0" || kv.second == "false";
     } else if (kv.first != "format" && kv.first != "nthread") {
       rest.insert(kv);
     }
@@ -111,7 +117,7 @@ class DeviceRowIter : public RowBlockIter<IndexType> {
         gpu::DeviceParser<IndexType>::Create(uri, part, nparts, r.cfg));
     p->ParseAll(&csr_);
     const gpu::DeviceRowBlock<IndexType> d = csr_.View();
-    num_col_ = d.size == 0 && d.max_index == 0 ? 0 : static_cast<size_t>(d.max_index) + 1;
+    num_col_ = static_cast<size_t>(d.max_index) + 1;
     if (r.to_host) {
       host_ = gpu::CopyToHost(d);
       block_ = host_.GetBlock();
@@ -123,7 +129,7 @@ class DeviceRowIter : public RowBlockIter<IndexType> {
   }
   void BeforeFirst() override { at_ = 0; }
   bool Next() override {
-    if (at_ != 0 || block_.size == 0) return false;
+    if (at_ != 0) return false;
     at_ = 1;
     return true;
   }

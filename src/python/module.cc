@@ -446,6 +446,9 @@ class PyDeviceParser {
     d["wait_gpu_sec"] = s.wait_gpu_sec;
     d["zero_copy"] = s.zero_copy;
     d["register_sec"] = s.register_sec;
+    d["waits_spun"] = s.waits_spun;
+    d["waits_slept"] = s.waits_slept;
+    d["waits_timed_out"] = s.waits_timed_out;
     return d;
   }
   uintptr_t Stream() const { return reinterpret_cast<uintptr_t>(p_->stream()); }

@@ -42,3 +42,22 @@ def test_python_parser_device_gpu_matches_cpu(tmp_path):
         np.testing.assert_array_equal(gpu[k], cpu[k], err_msg=k)
     it = data.RowBlockIter(p + "?device=gpu")
     assert it.num_col() == data.RowBlockIter(p).num_col()
+
+
+def test_device_row_iter_empty_partition_matches_cpu(tmp_path):
+    """An empty shard behaves as the reference BasicRowIter's
+    (src/data/basic_row_iter.h:35-48): Next() yields one (empty) block and
+    NumCol() is max_index + 1."""
+    p = str(tmp_path / "two.libsvm")
+    with open(p, "w") as f:
+        f.write("1 3:1 7:2\n0 2:5\n")
+    for part in range(8):
+        cpu = data.RowBlockIter(p, part, 8, "libsvm")
+        gpu = data.RowBlockIter(p + "?device=gpu", part, 8, "libsvm")
+        assert gpu.num_col() == cpu.num_col(), part
+        n_cpu = n_gpu = 0
+        while cpu.next():
+            n_cpu += 1
+        while gpu.next():
+            n_gpu += 1
+        assert n_gpu == n_cpu == 1, (part, n_gpu, n_cpu)

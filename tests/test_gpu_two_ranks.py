@@ -1,0 +1,41 @@
+"""Two GPU processes against one MI355X: the only pre-scale check of
+concurrent hipHostRegister windows, concurrent zero-copy DMA and per-process
+HIP state available on a one-GPU box.  Two tracker-launched ranks share
+cuda:0 (gloo control plane); their shards must be disjoint and complete and
+each must equal the CPU parser's shard."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from dmlc_core_amd import data
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_two_ranks_share_one_gpu(tmp_path):
+    path = str(tmp_path / "d.libsvm")
+    data.write_synthetic(path, 0, 60000, format="libsvm", seed=21)  # ~38 MB
+    out = str(tmp_path / "ranks.json")
+    env = dict(os.environ, PYTHONPATH=ROOT, DMLC_HEARTBEAT_PERIOD="1")
+    cmd = [sys.executable, "-m", "dmlc_core_amd.parallel.launch.submit", "--cluster", "local",
+           "--num-workers", "2", "--gpus-per-node", "1", "--host-ip", "127.0.0.1",
+           "--timeout", "150", "--auto-file-cache", "0", sys.executable, "-u",
+           os.path.join(ROOT, "tests", "two_rank_gpu_worker.py"), path, out]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=180, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-5000:]
+    res = json.load(open(out))
+    ranks = sorted(res["ranks"])
+    assert [r[0] for r in ranks] == [0, 1]
+    assert all(r[1] > 0 for r in ranks)
+    cpu = list(data.iter_blocks(path, 0, 1, "libsvm"))
+    rows = sum(len(b["label"]) for b in cpu)
+    nnz = sum(len(b["index"]) for b in cpu)
+    csum = int(sum(b["index"].astype(np.uint64).sum() for b in cpu))
+    assert sum(r[1] for r in ranks) == rows  # complete and disjoint
+    assert sum(r[2] for r in ranks) == nnz
+    assert sum(r[3] for r in ranks) == csum

@@ -1,6 +1,7 @@
 // dmlc_gpu_api_check: the reference's public data API on the GPU path.
-//   Parser<I>::Create(uri + "?device=gpu", part, nparts, type)   (device blocks)
-//   RowBlockIter<I>::Create(uri + "?device=gpu", ...)             (whole shard in HBM)
+//   Parser<I>::Create(uri + "?device=gpu", part, nparts, type)   (host blocks; device
+//                                                  blocks with &device_ptrs=1)
+//   RowBlockIter<I>::Create(uri + "?device=gpu&device_ptrs=1", ...) (whole shard in HBM)
 // Every block is copied back with hipMemcpy and compared value by value with
 // the CPU parser over the same partition.  Exit 0 = identical.
 //
@@ -100,14 +101,15 @@ int main(int argc, char** argv) {
     const Rows ref = Drain(cpu.get(), false);
     const std::string g = uri + sep + "device=gpu" + extra;
     std::unique_ptr<dmlc::Parser<uint32_t>> gp(
-        dmlc::Parser<uint32_t>::Create(g.c_str(), part, nparts, type.c_str()));
-    ok &= Same(Drain(gp.get(), true), ref, "Parser device=gpu");
+        dmlc::Parser<uint32_t>::Create((g + "&device_ptrs=1").c_str(), part, nparts, type.c_str()));
+    ok &= Same(Drain(gp.get(), true), ref, "Parser device=gpu&device_ptrs=1");
     std::unique_ptr<dmlc::Parser<uint32_t>> gh(
-        dmlc::Parser<uint32_t>::Create((g + "&to_host=1").c_str(), part, nparts, type.c_str()));
-    ok &= Same(Drain(gh.get(), false), ref, "Parser device=gpu&to_host=1");
+        dmlc::Parser<uint32_t>::Create(g.c_str(), part, nparts, type.c_str()));
+    ok &= Same(Drain(gh.get(), false), ref, "Parser device=gpu (host blocks by default)");
     std::unique_ptr<dmlc::RowBlockIter<uint32_t>> it(
-        dmlc::RowBlockIter<uint32_t>::Create(g.c_str(), part, nparts, type.c_str()));
-    ok &= Same(Drain(it.get(), true), ref, "RowBlockIter device=gpu");
+        dmlc::RowBlockIter<uint32_t>::Create((g + "&device_ptrs=1").c_str(), part, nparts,
+                                             type.c_str()));
+    ok &= Same(Drain(it.get(), true), ref, "RowBlockIter device=gpu&device_ptrs=1");
     std::unique_ptr<dmlc::RowBlockIter<uint32_t>> cit(
         dmlc::RowBlockIter<uint32_t>::Create(uri.c_str(), part, nparts, type.c_str()));
     if (it->NumCol() != cit->NumCol()) {
