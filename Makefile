@@ -25,7 +25,7 @@ WARN := -Wall -Wno-unknown-pragmas -Wno-sign-compare
 CXXFLAGS_BASE := -std=c++17 -O3 -fPIC -fopenmp -ffp-contract=off -g1 $(WARN) -Iinclude -Isrc \
   -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
 HIPFLAGS := -std=c++17 -O3 -fPIC --offload-arch=$(GPU_ARCH) -ffp-contract=off -Iinclude -Isrc \
-  -Wno-unused-result -munsafe-fp-atomics
+  -Wno-unused-result -munsafe-fp-atomics $(HIPFLAGS_EXTRA)
 LDFLAGS_LIB := -shared -fopenmp -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64 -lrccl -ldl -lpthread
 
 CPU_SRCS := src/logging.cc src/fault.cc src/io.cc src/recordio.cc src/data.cc src/config.cc src/synthetic.cc \

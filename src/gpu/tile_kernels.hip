@@ -37,6 +37,7 @@
 #include "../data/strtonum.h"
 #include "./device_common.h"
 #include "./kernels.h"
+#include "./token_decode.h"
 
 namespace dmlc {
 namespace gpu {
@@ -592,63 +593,171 @@ __device__ __forceinline__ bool fast_token(const uint8_t* lds, uint32_t off, boo
   return a_uint && a_col && b_uint && (b_end || (b.term == ':' && is_sep(c.term) && fc_ok));
 }
 
+/*!
+ * \brief generic (strtonum.h ParsePair / ParseTriple) parse of the token at
+ *  global offset gpos: tokens the register-window decoder does not cover.
+ *  Out of line: it is rare, and inlined it would raise the register
+ *  allocation of the whole fill kernel.
+ */
 template <TextFormat F, typename IndexType>
-__global__ __launch_bounds__(kThreads) void k_tile_fill(const uint8_t* __restrict__ text, size_t n,
+__device__ __noinline__ void generic_token(const uint8_t* __restrict__ text, size_t n, size_t gpos,
+                                           bool is_label, tok::Token* t, bool* bad) {
+  const uint8_t* lim = text + n;
+  auto beg = sep_begin(text + gpos, lim);
+  auto end = sep_end(lim);
+  float f0 = 0.0f, f1 = 0.0f;
+  *bad = false;
+  if (is_label) {
+    t->r = data::ParsePair<float, float>(beg, end, &f0, &f1, bad);
+    t->f0 = f0;
+    t->f1 = f1;
+  } else if constexpr (F == TextFormat::kLibSVM) {
+    IndexType idx = 0;
+    t->r = data::ParsePair<IndexType, float>(beg, end, &idx, &f0, bad);
+    t->u0 = static_cast<uint32_t>(idx);
+    t->u0_hi = static_cast<uint32_t>(static_cast<uint64_t>(idx) >> 32);
+    t->f0 = f0;
+  } else {
+    IndexType fid = 0, idx = 0;
+    t->r = data::ParseTriple<IndexType, IndexType, float>(beg, end, &fid, &idx, &f0, bad);
+    t->u0 = static_cast<uint32_t>(fid);
+    t->u0_hi = static_cast<uint32_t>(static_cast<uint64_t>(fid) >> 32);
+    t->u1 = static_cast<uint32_t>(idx);
+    t->u1_hi = static_cast<uint32_t>(static_cast<uint64_t>(idx) >> 32);
+    t->f0 = f0;
+  }
+}
+
+/*!
+ * \brief C3: wave-autonomous tile fill.  Each wave of the workgroup owns one
+ *  8 KiB tile and never synchronises with the others (no __syncthreads):
+ *   1. all 8 KiB (+ the 64 bytes after it) are loaded into registers at once;
+ *   2. per 2 KiB step the step is staged in the wave's LDS region, the
+ *      line / token start masks of each lane's two 16 B slices come from the
+ *      same registers, and a wave scan (DPP) places each token's LDS offset
+ *      (and its line-start bit) in a wave-private list, in text order;
+ *   3. 64 list entries at a time, lane i decodes token i from the LDS text in
+ *      registers (token_decode.h: two aligned ds_read_b128 per number), its
+ *      line ordinal comes from a ballot of the line-start bits, and it writes
+ *      index / value (consecutive lanes -> consecutive nnz slots) or label /
+ *      offset / weight directly.
+ *  Tokens the fast decoder does not take use the generic strtonum.h parser
+ *  from global memory (bit-identical by construction).
+ */
+constexpr int kFillWaves = kThreads / 64;
+#ifndef DMLC_FILL_WAVES
+#define DMLC_FILL_WAVES 8
+#endif
+constexpr uint32_t kStepBytes = 2048;
+constexpr int kSteps = static_cast<int>(kTileBytes / kStepBytes);
+constexpr uint32_t kStageVecs = (kStepBytes + 64) / 16;   // a step + 64 B of the next
+constexpr uint32_t kListCap = kStepBytes / 2;              // tokens of a step, at most
+
+/*!
+ * \brief the 16 B at chunk offset pos, bytes at or past n zeroed (the
+ *  decoder's end marker), without branches: lanes past n load from a clamped
+ *  in-bounds address and mask everything
+ */
+__device__ __forceinline__ uint4 load16_clip(const uint8_t* __restrict__ text, size_t pos, size_t n) {
+  const size_t at = pos < n ? pos : 0;
+  const uint4 v = *reinterpret_cast<const uint4*>(text + at);
+  const uint32_t keep = pos < n ? static_cast<uint32_t>(n - pos < 16 ? n - pos : 16) : 0u;
+  // byte mask of the first `keep` bytes, per word
+  const uint64_t m_lo = keep >= 8 ? ~0ull : ((1ull << (8 * keep)) - 1ull);
+  const uint64_t m_hi = keep >= 16 ? ~0ull : (keep <= 8 ? 0ull : ((1ull << (8 * (keep - 8))) - 1ull));
+  return make_uint4(v.x & static_cast<uint32_t>(m_lo), v.y & static_cast<uint32_t>(m_lo >> 32),
+                    v.z & static_cast<uint32_t>(m_hi), v.w & static_cast<uint32_t>(m_hi >> 32));
+}
+
+/*!
+ * \brief append the token starts of one lane's 16 B slice to the wave's list
+ *  (`at` = its first list position; `line0` = line starts of the step before
+ *  this slice).  An entry is  offset (11 bits) | line start (bit 11) | line
+ *  ordinal in the step, this token's line included (bits 12..23), so a round
+ *  can take the entries in any lane order.  The first two starts are written
+ *  unconditionally -- a lane with fewer writes a private dummy slot past
+ *  kListCap -- so the common case has no per-lane loop; slices with more
+ *  starts (tokens shorter than 8 B) take the loop.
+ */
+__device__ __forceinline__ uint32_t list_entry(uint32_t tm_bit_j, uint32_t lm, uint32_t base,
+                                               uint32_t line0) {
+  const uint32_t j = tm_bit_j;
+  const uint32_t upto = lm & ((2u << j) - 1u);  // line starts up to byte j of the slice
+  return (base + j) | (((lm >> j) & 1u) << 11) | ((line0 + __popc(upto)) << 12);
+}
+
+__device__ __forceinline__ void list_slice(uint32_t* sl, uint32_t tm, uint32_t lm, uint32_t at,
+                                           uint32_t base, uint32_t line0, int lane) {
+  uint32_t m = tm;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const uint32_t j = static_cast<uint32_t>(__builtin_ctz(m | 0x10000u));
+    const bool has = m != 0;
+    sl[has ? at : kListCap + lane] = list_entry(j & 15u, lm, base, line0);
+    at += has ? 1u : 0u;
+    m &= m - 1;
+  }
+  if (__any(m != 0)) {
+    for (; m != 0; m &= m - 1) {
+      sl[at++] = list_entry(static_cast<uint32_t>(__builtin_ctz(m)), lm, base, line0);
+    }
+  }
+}
+
+/*!
+ * \brief token slot of `lane` in a decode round: the four 16-lane groups of a
+ *  ds_read_b128 ({0-3,12-15,20-27}, {4-11,16-19,28-31} and the same + 32)
+ *  take 16 consecutive tokens each, which start ~16 B apart -- distinct bank
+ *  quads, where lane-ordered slots put tokens 256 B apart into one group
+ */
+__device__ __forceinline__ uint32_t round_slot(int lane) {
+  // rank within its group + 16 * group, for lanes 0..31 (4 bits per entry)
+  const uint32_t l = static_cast<uint32_t>(lane) & 31u;
+  uint32_t k;
+  if (l < 4) {
+    k = l;
+  } else if (l < 12) {
+    k = 16u + (l - 4u);
+  } else if (l < 16) {
+    k = 4u + (l - 12u);
+  } else if (l < 20) {
+    k = 24u + (l - 16u);
+  } else if (l < 28) {
+    k = 8u + (l - 20u);
+  } else {
+    k = 28u + (l - 28u);
+  }
+  return (static_cast<uint32_t>(lane) & 32u) + k;
+}
+
+template <TextFormat F, typename IndexType>
+__global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(const uint8_t* __restrict__ text, size_t n,
+                                                        size_t ntiles,
                                                         const uint64_t* __restrict__ prefix,
                                                         FillTarget<IndexType> out,
-                                                        MetaPartial* __restrict__ partials) {
-  __shared__ uint4 s_text[kTileBytes / 16 + 4];  // +64 B: speculative reads past a token
-  __shared__ uint32_t s_tok[kMaxTileTokens];
-  __shared__ uint32_t s_scan[4];
-  const uint8_t* lds = reinterpret_cast<const uint8_t*>(s_text);
-  const size_t tile0 = static_cast<size_t>(blockIdx.x) * kTileBytes;
-  const uint64_t pre = prefix[blockIdx.x];
+                                                        MetaPartial* __restrict__ partials,
+                                                        int exp_mode) {
+  __shared__ uint4 s_text[kFillWaves][kStageVecs];
+  __shared__ uint32_t s_list[kFillWaves][kListCap + 64];  // + a dummy slot per lane
+  const int wave = threadIdx.x / dev::kWave;
+  const int lane = dev::lane_id();
+  const size_t tile = static_cast<size_t>(blockIdx.x) * kFillWaves + wave;
+  if (tile >= ntiles) return;  // whole waves leave; nothing below synchronises waves
+  uint4* const st = s_text[wave];
+  uint32_t* const sl = s_list[wave];
+  const uint32_t slot = round_slot(lane);
+  const size_t tile0 = tile * kTileBytes;
+
+  // ---- 1. the first step in flight; each step prefetches the next (the
+  // last one prefetches the 64 bytes past the tile)
+  uint4 a = load16_clip(text, tile0 + lane * 16, n);
+  uint4 b = load16_clip(text, tile0 + 1024 + lane * 16, n);
+  uint32_t carry_pc = tile0 == 0 ? static_cast<uint32_t>('\n') : text[tile0 - 1];
+  const uint64_t pre = prefix[tile];
   const uint64_t line_base = pre >> 32;
   const uint64_t tok_base = pre & 0xffffffffull;
-
-  // ---- stage: coalesced 16 B loads -> LDS; masks from the same registers
-  uint4 v[kSub];
-  uint32_t pc[kSub];
-#pragma unroll
-  for (int s = 0; s < kSub; ++s) {
-    const size_t pos = tile0 + s * 4096 + threadIdx.x * 16;
-    v[s] = load16(text, pos, n);
-    pc[s] = prev_byte(text, pos, v[s]);
-    s_text[s * 256 + threadIdx.x] = v[s];
-  }
-  // ---- compact the tile's tokens into s_tok in text order
-  uint32_t carry = 0;  // (lines << 16 | tokens) of earlier sub-tiles (each <= 4096)
-#pragma unroll
-  for (int s = 0; s < kSub; ++s) {
-    const size_t pos = tile0 + s * 4096 + threadIdx.x * 16;
-    uint32_t lm, tm;
-    (void)lane_masks<false>(v[s], pc[s], pos, n, &lm, &tm);
-    const uint32_t mine = (static_cast<uint32_t>(__popc(lm)) << 16) | __popc(tm);
-    uint32_t tot;
-    const uint32_t before = dev::block_excl_scan_256<uint32_t>(mine, s_scan, &tot) + carry;
-    uint32_t line = before >> 16;
-    uint32_t tok = before & 0xffffu;
-    uint32_t all = lm | tm;
-    while (all != 0) {
-      const int j = __ffs(all) - 1;
-      all &= all - 1;
-      const uint32_t bit = 1u << j;
-      if (lm & bit) ++line;  // lm implies tm on a regular chunk
-      if (tm & bit) {
-        const uint32_t off = static_cast<uint32_t>(s * 4096 + threadIdx.x * 16 + j);
-        const uint32_t label = (lm & bit) ? 1u : 0u;
-        s_tok[tok] = off | (line << kOffBits) | (label << (2 * kOffBits));
-        ++tok;
-      }
-    }
-    carry += tot;
-    __syncthreads();  // s_scan reuse by the next sub-tile; s_tok / s_text complete
-  }
-  const uint32_t ntok = carry & 0xffffu;
-  // WG-uniform bases: token k = tok_base + i of line l = line_base + lcnt - 1
-  // goes to nnz position C + (i - lcnt) (C = nnz_base + tok_base - line_base);
-  // its row is R + lcnt - 1 (R = row_base + line_base).  Per-lane offsets are
-  // 32-bit, the 64-bit parts stay scalar.
+  // token k = tok_base + i of line l = line_base + lcnt - 1 goes to nnz
+  // position C + (i - lcnt); its row is R + lcnt - 1 (as k_tile_scan defines)
   const uint64_t C = out.nnz_base + tok_base - line_base;
   const uint64_t R = out.row_base + line_base;
   const int64_t nnz_room = static_cast<int64_t>(out.nnz_limit) - static_cast<int64_t>(C);
@@ -661,84 +770,128 @@ __global__ __launch_bounds__(kThreads) void k_tile_fill(const uint8_t* __restric
   float* const wgt_at = out.weight != nullptr ? out.weight + R - 1 : nullptr;
   uint64_t* const qid_at = out.qid != nullptr ? out.qid + R - 1 : nullptr;
 
-  // ---- parse: lane i takes token i
+  uint32_t tok_i = 0;  // tokens of this tile before the current step
+  uint32_t lcnt = 0;   // line starts of this tile so far
   uint64_t mx_index = 0, mx_field = 0;
   bool any_value = false, any_weight = false, irregular = false, neg = false, need_w = false;
-  for (uint32_t i = threadIdx.x; i < ntok; i += kThreads) {
-    const uint32_t e = s_tok[i];
-    const uint32_t off = e & ((1u << kOffBits) - 1);
-    const uint32_t lcnt = (e >> kOffBits) & ((1u << kOffBits) - 1);
-    const bool is_label = (e >> (2 * kOffBits)) & 1u;
-    const size_t gpos = tile0 + off;
-    bool bad = false;
-    int r = 0;
-    uint64_t u0 = 0, u1 = 0;
-    float f0 = 0.0f, f1 = 0.0f;
-    // every token but the tile's last ends inside the LDS tile
-    const bool in_lds = i + 1 < ntok;
-    bool done = in_lds && fast_token<F>(lds, off, is_label, &r, &u0, &u1, &f0, &f1);
-    if (!done) {
-      auto generic = [&](auto beg, auto end) {
-        if (is_label) {
-          r = data::ParsePair<float, float>(beg, end, &f0, &f1, &bad);
-        } else if constexpr (F == TextFormat::kLibSVM) {
-          IndexType idx = 0;
-          r = data::ParsePair<IndexType, float>(beg, end, &idx, &f0, &bad);
-          u0 = idx;
-        } else {
-          IndexType fid = 0, idx = 0;
-          r = data::ParseTriple<IndexType, IndexType, float>(beg, end, &fid, &idx, &f0, &bad);
-          u0 = fid;
-          u1 = idx;
-        }
-      };
-      if (in_lds) {
-        const uint8_t* lim = lds + kTileBytes;
-        generic(sep_begin(lds + off, lim), sep_end(lim));
-      } else {
-        const uint8_t* lim = text + n;
-        generic(sep_begin(text + gpos, lim), sep_end(lim));
-      }
-    }
-    if (is_label) {
-      if (static_cast<int64_t>(lcnt) - 1 < row_room) {
-        lab_at[lcnt] = f0;
-        off_at[lcnt] = C + 1 + (static_cast<int64_t>(i) - static_cast<int64_t>(lcnt));
-        if (wgt_at != nullptr) {
-          wgt_at[lcnt] = r == 2 ? f1 : 1.0f;
-        } else if (r == 2) {
-          need_w = true;
-        }
-        if (qid_at != nullptr) qid_at[lcnt] = 0;  // qid lines take the exact path
-      } else {
-        irregular = true;
-      }
-      any_weight |= (r == 2);
+
+#pragma unroll 1
+  for (int s = 0; s < kSteps; ++s) {
+    // prefetch: the next step (lanes 0..3 of it are also this step's tail)
+    const size_t nxt = tile0 + (s + 1) * kStepBytes;
+    const bool last = s + 1 == kSteps;
+    uint4 na, nb = make_uint4(0, 0, 0, 0);
+    if (nxt + kStepBytes <= n) {  // wave-uniform: no byte of the next step is past n
+      na = *reinterpret_cast<const uint4*>(text + nxt + lane * 16);
+      if (!last) nb = *reinterpret_cast<const uint4*>(text + nxt + 1024 + lane * 16);
     } else {
-      const int32_t rel = static_cast<int32_t>(i) - static_cast<int32_t>(lcnt);
-      if (rel >= nnz_room) {
-        irregular = true;
-      } else if constexpr (F == TextFormat::kLibSVM) {
-        const IndexType idx = static_cast<IndexType>(u0);
-        idx_at[rel] = idx;
-        val_at[rel] = r == 2 ? f0 : 1.0f;
-        any_value |= (r == 2);
-        if (static_cast<uint64_t>(idx) > mx_index) mx_index = idx;
-      } else {
-        if (r < 2) {
-          irregular = true;
-        } else {
-          const IndexType fid = static_cast<IndexType>(u0), idx = static_cast<IndexType>(u1);
-          fld_at[rel] = fid;
-          idx_at[rel] = idx;
-          val_at[rel] = r == 3 ? f0 : 1.0f;
-          any_value |= (r == 3);
-          if (static_cast<uint64_t>(idx) > mx_index) mx_index = idx;
-          if (static_cast<uint64_t>(fid) > mx_field) mx_field = fid;
-        }
-      }
+      na = load16_clip(text, nxt + lane * 16, n);
+      if (!last) nb = load16_clip(text, nxt + 1024 + lane * 16, n);
     }
-    neg |= bad;
+    if (last && lane >= 4) na = make_uint4(0, 0, 0, 0);
+    // ---- 2. stage the step (+ the next 64 B) and list its tokens
+    st[lane] = a;
+    st[64 + lane] = b;
+    if (lane < 4) st[128 + lane] = na;
+    const size_t pos_a = tile0 + s * kStepBytes + lane * 16;
+    const uint32_t left_a = __shfl_up(a.w >> 24, 1, dev::kWave);
+    const uint32_t pc_a = lane == 0 ? carry_pc : left_a;
+    const uint32_t left_b = __shfl_up(b.w >> 24, 1, dev::kWave);
+    // cross-lane reads run in every lane (a shuffle inside `lane == 0 ? :`
+    // would execute with only lane 0 active and read an inactive lane)
+    const uint32_t last_a = __shfl(a.w >> 24, dev::kWave - 1, dev::kWave);
+    const uint32_t pc_b = lane == 0 ? last_a : left_b;
+    carry_pc = __shfl(b.w >> 24, dev::kWave - 1, dev::kWave);
+    uint32_t lm_a, tm_a, lm_b, tm_b;
+    (void)lane_masks<false>(a, pc_a, pos_a, n, &lm_a, &tm_a);
+    (void)lane_masks<false>(b, pc_b, pos_a + 1024, n, &lm_b, &tm_b);
+    // one 64-bit scan of four 16-bit counts: tokens / lines of both slices
+    const uint64_t cnt = static_cast<uint64_t>(__popc(tm_a)) |
+                         (static_cast<uint64_t>(__popc(tm_b)) << 16) |
+                         (static_cast<uint64_t>(__popc(lm_a)) << 32) |
+                         (static_cast<uint64_t>(__popc(lm_b)) << 48);
+    uint64_t tot;
+    const uint64_t before = dev::wave_excl_scan(cnt, &tot);
+    const uint32_t ntok_a = static_cast<uint32_t>(tot & 0xFFFFu);
+    const uint32_t ntok = ntok_a + static_cast<uint32_t>((tot >> 16) & 0xFFFFu);
+    const uint32_t nline_a = static_cast<uint32_t>((tot >> 32) & 0xFFFFu);
+    const uint32_t nline = nline_a + static_cast<uint32_t>(tot >> 48);
+    list_slice(sl, tm_a, lm_a, static_cast<uint32_t>(before & 0xFFFFu), lane * 16,
+               static_cast<uint32_t>((before >> 32) & 0xFFFFu), lane);
+    list_slice(sl, tm_b, lm_b, ntok_a + static_cast<uint32_t>((before >> 16) & 0xFFFFu),
+               1024 + lane * 16, nline_a + static_cast<uint32_t>(before >> 48), lane);
+    dev::wave_sync();  // the staged text and the list are visible to every lane
+
+    // ---- 3. decode 64 listed tokens per round
+    for (uint32_t r0 = 0; r0 < (exp_mode == 3 ? 0u : ntok); r0 += dev::kWave) {
+      const uint32_t li = r0 + slot;
+      const bool active = li < ntok;
+      const uint32_t e = active ? sl[li] : 0u;
+      const bool is_label = active && ((e >> 11) & 1u) != 0;
+      const uint32_t off = e & 0x7FFu;  // 0 in idle lanes: they decode harmless bytes
+      const uint32_t lc = lcnt + (e >> 12);
+      const uint32_t i = tok_i + li;
+      tok::Token t;
+      t.u0_hi = t.u1_hi = 0;
+      t.u1 = 0;
+      bool bad = false;
+      bool ok;
+      if (exp_mode >= 1) {
+        t.u0 = off;
+        t.f0 = 1.0f;
+        t.f1 = 0.0f;
+        t.r = 1;
+        ok = true;
+      } else {
+        ok = tok::decode<F>(st, off, is_label, &t);
+      }
+      if (active & !ok) {
+        generic_token<F, IndexType>(text, n, tile0 + s * kStepBytes + off, is_label, &t, &bad);
+      }
+      const int32_t rel = static_cast<int32_t>(i) - static_cast<int32_t>(lc);
+      const bool row_ok = static_cast<int64_t>(lc) - 1 < row_room;
+      const bool nnz_ok = rel < nnz_room;
+      bool field_ok = true;
+      if (F == TextFormat::kLibFM) field_ok = is_label || t.r >= 2;
+      irregular |= active & (is_label ? !row_ok : (!nnz_ok | !field_ok));
+      if (active & is_label & row_ok & (exp_mode != 2)) {
+        lab_at[lc] = t.f0;
+        off_at[lc] = C + 1 + (static_cast<int64_t>(i) - static_cast<int64_t>(lc));
+        if (wgt_at != nullptr) wgt_at[lc] = t.r == 2 ? t.f1 : 1.0f;
+        if (qid_at != nullptr) qid_at[lc] = 0;  // qid lines take the exact path
+      }
+      need_w |= active & is_label & (wgt_at == nullptr) & (t.r == 2);
+      any_weight |= active & is_label & (t.r == 2);
+      const bool feat = active & !is_label & nnz_ok & field_ok & (exp_mode != 2);
+      const uint64_t u0 = (static_cast<uint64_t>(t.u0_hi) << 32) | t.u0;
+      if constexpr (F == TextFormat::kLibSVM) {
+        if (feat) {
+          idx_at[rel] = static_cast<IndexType>(u0);
+          val_at[rel] = t.r == 2 ? t.f0 : 1.0f;
+        }
+        any_value |= feat && t.r == 2;
+        const uint64_t iu = static_cast<uint64_t>(static_cast<IndexType>(u0));
+        mx_index = feat && iu > mx_index ? iu : mx_index;
+      } else {
+        const uint64_t u1 = (static_cast<uint64_t>(t.u1_hi) << 32) | t.u1;
+        if (feat) {
+          fld_at[rel] = static_cast<IndexType>(u0);
+          idx_at[rel] = static_cast<IndexType>(u1);
+          val_at[rel] = t.r == 3 ? t.f0 : 1.0f;
+        }
+        any_value |= feat && t.r == 3;
+        const uint64_t iu = static_cast<uint64_t>(static_cast<IndexType>(u1));
+        const uint64_t fu = static_cast<uint64_t>(static_cast<IndexType>(u0));
+        mx_index = feat && iu > mx_index ? iu : mx_index;
+        mx_field = feat && fu > mx_field ? fu : mx_field;
+      }
+      neg |= active && bad;
+    }
+    tok_i += ntok;
+    lcnt += nline;
+    a = na;
+    b = nb;
+    dev::wave_sync();  // every lane is done with this step's text and list
   }
   unsigned fl = 0;
   if (any_value) fl |= kFlagValue;
@@ -747,8 +900,17 @@ __global__ __launch_bounds__(kThreads) void k_tile_fill(const uint8_t* __restric
   if (neg) fl |= kFlagNegIndex;
   if (need_w) fl |= kFlagNeedWeight;
   if (F == TextFormat::kLibFM) fl |= kFlagField;
-  dev::block_store_partial(static_cast<unsigned long long>(mx_index),
-                           static_cast<unsigned long long>(mx_field), fl, partials);
+  const unsigned long long mi = dev::wave_max(static_cast<unsigned long long>(mx_index));
+  const unsigned long long mf = dev::wave_max(static_cast<unsigned long long>(mx_field));
+  fl = dev::wave_or(fl);
+  if (lane == 0) {
+    MetaPartial p;
+    p.max_index = mi;
+    p.max_field = mf;
+    p.flags = fl;
+    p.pad = 0;
+    partials[tile] = p;
+  }
 }
 
 /*!
@@ -1150,12 +1312,14 @@ void LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
   const size_t ntiles = TileCount(nbytes);
   const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
   if (ntiles != 0) {
+    const dim3 grid(static_cast<unsigned>((ntiles + kFillWaves - 1) / kFillWaves));
+    static const int exp_mode = getenv("DMLC_FILL_EXP") ? atoi(getenv("DMLC_FILL_EXP")) : 0;
     if (format == TextFormat::kLibFM) {
-      hipLaunchKernelGGL((k_tile_fill<TextFormat::kLibFM, IndexType>), dim3(ntiles), dim3(kThreads),
-                         0, stream, t, nbytes, tile_prefix, out, partials);
+      hipLaunchKernelGGL((k_tile_fill<TextFormat::kLibFM, IndexType>), grid, dim3(kThreads), 0,
+                         stream, t, nbytes, ntiles, tile_prefix, out, partials, exp_mode);
     } else {
-      hipLaunchKernelGGL((k_tile_fill<TextFormat::kLibSVM, IndexType>), dim3(ntiles),
-                         dim3(kThreads), 0, stream, t, nbytes, tile_prefix, out, partials);
+      hipLaunchKernelGGL((k_tile_fill<TextFormat::kLibSVM, IndexType>), grid, dim3(kThreads), 0,
+                         stream, t, nbytes, ntiles, tile_prefix, out, partials, exp_mode);
     }
   }
   LaunchFinish(partials, ntiles, meta, host_meta, out.offset, out.row_base, out.nnz_base, stream);

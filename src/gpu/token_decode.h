@@ -1,0 +1,212 @@
+/*!
+ * \file src/gpu/token_decode.h
+ * \brief Register-window decoding of one LibSVM / LibFM token on gfx950 (the
+ *  fast path of the tile fill kernel, src/gpu/tile_kernels.hip).
+ *
+ *  A token's bytes are read from the LDS-staged text 16 at a time: two
+ *  16-byte-aligned ds_read_b128 cover any 16-byte window, which is then
+ *  funnel-shifted into place with v_alignbyte (ext16).  Lanes of a wave take
+ *  consecutive tokens (about 16 B apart), so the four 16-lane groups of a
+ *  ds_read_b128 read nearly disjoint bank quads -- the unaligned dword reads
+ *  of the round-2 kernel were 4-way conflicted at that stride.
+ *  Digit runs are decoded 4 bytes at a time (SWAR, lead_digits); every
+ *  number takes one window, a value's fraction digits come out of the same
+ *  window when they fit.
+ *
+ *  Arithmetic parity with src/data/strtonum.h (reference src/data/strtonum.h:
+ *  37-97): an integer part of <= 7 digits accumulated in float is exact, so it
+ *  equals the integer converted once; the fraction float(double(F) /
+ *  double(10^k)) equals the correctly rounded float quotient F / 10^k for
+ *  k <= 8 (the quotient's distance to a float rounding boundary exceeds the
+ *  double rounding error), and for k <= 7 (F < 2^24, exact in float) that
+ *  quotient is q0 = F * r, q1 = fma(F - q0 * 10^k, r, q0) with r = RN(1 / 10^k)
+ *  -- checked exhaustively for every F < 10^k, k = 1..7.  Shapes outside the
+ *  fast path (exponents, > 7 integer or fraction digits, over-long indices,
+ *  signs on indices, tokens longer than the windows) return false and take
+ *  the generic ParsePair / ParseTriple.
+ */
+#ifndef DMLC_SRC_GPU_TOKEN_DECODE_H_
+#define DMLC_SRC_GPU_TOKEN_DECODE_H_
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "./kernels.h"
+
+namespace dmlc {
+namespace gpu {
+namespace tok {
+
+/*! \brief 16 bytes starting at byte `a` of a 16-byte-aligned LDS buffer
+ *  (the buffer must hold 32 bytes from a & ~15) */
+__device__ __forceinline__ uint4 ext16(const uint4* lds, uint32_t a) {
+  const uint4 x = lds[a >> 4];
+  const uint4 y = lds[(a >> 4) + 1];
+  const uint32_t q = (a >> 2) & 3u, r = a & 3u;
+  // words q .. q+4 of (x, y)
+  const uint32_t w0 = q == 0 ? x.x : (q == 1 ? x.y : (q == 2 ? x.z : x.w));
+  const uint32_t w1 = q == 0 ? x.y : (q == 1 ? x.z : (q == 2 ? x.w : y.x));
+  const uint32_t w2 = q == 0 ? x.z : (q == 1 ? x.w : (q == 2 ? y.x : y.y));
+  const uint32_t w3 = q == 0 ? x.w : (q == 1 ? y.x : (q == 2 ? y.y : y.z));
+  const uint32_t w4 = q == 0 ? y.x : (q == 1 ? y.y : (q == 2 ? y.z : y.w));
+  return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, r), __builtin_amdgcn_alignbyte(w2, w1, r),
+                    __builtin_amdgcn_alignbyte(w3, w2, r), __builtin_amdgcn_alignbyte(w4, w3, r));
+}
+
+/*! \brief 10^k for k = 0..7 from its bits: three selects, two 24-bit multiplies */
+__device__ __forceinline__ uint32_t pow10_u(uint32_t k) {
+  const uint32_t a = (k & 1u) ? 10u : 1u;
+  const uint32_t b = (k & 2u) ? 100u : 1u;
+  const uint32_t c = (k & 4u) ? 10000u : 1u;
+  return __umul24(__umul24(a, b), c);
+}
+
+/*!
+ * \brief SWAR: number of leading ASCII digits (0..4) of the 4 bytes g (first
+ *  byte = lowest) and their decimal value.
+ */
+__device__ __forceinline__ uint32_t lead_digits(uint32_t g, uint32_t* val) {
+  const uint32_t lo4 = g & 0x0F0F0F0Fu;
+  const uint32_t hi = (g & 0xF0F0F0F0u) ^ 0x30303030u;        // high nibble != 3
+  const uint32_t lo = (lo4 + 0x06060606u) & 0x10101010u;      // low nibble > 9
+  const uint32_t bad = hi | (lo << 3);
+  // no non-digit byte: 4 digits
+  const uint32_t k = static_cast<uint32_t>(__builtin_ctzg(bad, 32)) >> 3;
+  // k digits right-aligned (a 64-bit shift: k = 0 shifts them all out)
+  const uint32_t x = static_cast<uint32_t>((static_cast<uint64_t>(lo4) << (8u * (4u - k))));
+  const uint32_t t = ((x << 3) + (x << 1) + (x >> 8)) & 0x00FF00FFu;  // x * 10 without v_mul_lo
+  *val = (t & 0xFFu) * 100u + (t >> 16);
+  return k;
+}
+
+/*! \brief RN(1 / 10^k) and 10^k in float, k = 0..7 (branch-free selects) */
+__device__ __forceinline__ void pow10f(uint32_t k, float* p, float* inv) {
+  *p = static_cast<float>(pow10_u(k));
+  const float i_lo = k == 0 ? 1.0f : (k == 1 ? 0.1f : (k == 2 ? 0.01f : 0.001f));
+  const float i_hi = k == 4 ? 1e-4f : (k == 5 ? 1e-5f : (k == 6 ? 1e-6f : 1e-7f));
+  *inv = k < 4 ? i_lo : i_hi;
+}
+
+/*!
+ * \brief one number `[+-] digits [. digits]` at LDS byte a, decoded without
+ *  branches (every lane of a wave runs the same instructions; the caller
+ *  selects what it needs):
+ *   ival  the integer digits (valid as an index when ok_uint)
+ *   fval  the reference StrToFloat value (valid when ok_float)
+ *   end / term  the byte after the number and its LDS offset
+ */
+struct Num {
+  uint32_t ival;
+  float fval;
+  uint32_t end, term;
+  bool ok_float, ok_uint;
+};
+
+__device__ __forceinline__ Num parse_num(const uint4* lds, uint32_t a) {
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+  Num o;
+  const uint4 g = ext16(lds, a);
+  const uint32_t c0 = g.x & 0xFFu;
+  const bool neg = c0 == '-';
+  const uint32_t s = (neg || c0 == '+') ? 1u : 0u;
+  const uint32_t h0 = __builtin_amdgcn_alignbyte(g.y, g.x, s);
+  const uint32_t h1 = __builtin_amdgcn_alignbyte(g.z, g.y, s);
+  const uint32_t h2 = __builtin_amdgcn_alignbyte(g.w, g.z, s);
+  const uint32_t h3 = g.w >> (8u * s);
+  // integer digits (<= 8) and the byte after them
+  uint32_t v0, v1;
+  const uint32_t k0 = lead_digits(h0, &v0);
+  const uint32_t k1 = lead_digits(h1, &v1);
+  const uint32_t k = k0 == 4 ? 4u + k1 : k0;
+  const uint32_t iv = k0 == 4 ? v0 * pow10_u(k1) + v1 : v0;
+  const uint32_t tw = k < 4 ? h0 : (k < 8 ? h1 : h2);
+  const uint32_t term = (tw >> (8u * (k & 3u))) & 0xFFu;
+  // fraction digits: 8 bytes at fs = k + 1 (1..9) of h0..h3
+  const uint32_t fs = k + 1u;
+  const uint32_t q = fs >> 2, r = fs & 3u;
+  const uint32_t a0 = q == 0 ? h0 : (q == 1 ? h1 : h2);
+  const uint32_t a1 = q == 0 ? h1 : (q == 1 ? h2 : h3);
+  const uint32_t a2 = q == 0 ? h2 : (q == 1 ? h3 : 0u);
+  const uint32_t lo = __builtin_amdgcn_alignbyte(a1, a0, r);
+  const uint32_t hi = __builtin_amdgcn_alignbyte(a2, a1, r);
+  uint32_t w0, w1;
+  const uint32_t f0 = lead_digits(lo, &w0);
+  const uint32_t f1 = lead_digits(hi, &w1);
+  const uint32_t nf = f0 == 4 ? 4u + f1 : f0;
+  const uint32_t fv = f0 == 4 ? w0 * pow10_u(f1) + w1 : w0;
+  const uint32_t fw = nf < 4 ? lo : hi;
+  const uint32_t fterm = nf < 8 ? (fw >> (8u * (nf & 3u))) & 0xFFu : 0x30u;
+  const bool dot = term == '.';
+  // the fraction and its terminator must lie inside the 16 - s window bytes
+  const bool frac_ok = (nf <= 7) & (fs + nf < 16u - s) & ((k | nf) != 0);
+  o.ok_float = (k <= 7) & (dot ? frac_ok : k != 0);
+  o.ok_uint = (s == 0) & !dot & (k != 0) & !((k == 8) & ((h2 & 0xFFu) - '0' < 10u));
+  o.term = dot ? fterm : term;
+  o.end = a + s + k + (dot ? 1u + nf : 0u);
+  o.ival = iv;
+  // StrToFloat: float(int digits) + float(F / 10^nf) (see file comment)
+  float p, inv;
+  pow10f(nf, &p, &inv);
+  const float ff = static_cast<float>(fv);
+  const float q0 = ff * inv;
+  const float rem = __builtin_fmaf(-q0, p, ff);
+  const float frac = __builtin_fmaf(rem, inv, q0);
+  float v = static_cast<float>(iv);
+  v = dot ? v + frac : v;
+  o.fval = neg ? -v : v;
+  return o;
+}
+
+__device__ __forceinline__ bool is_end(uint32_t c) {
+  // separators, or the zero padding past the chunk end (the count pass sends
+  // chunks with other control bytes to the exact kernels)
+  return (c == ' ') | (c == '\t') | (c == '\n') | (c == '\r') | (c == 0);
+}
+
+/*! \brief fast-path result of one token */
+struct Token {
+  uint32_t u0, u1;        // LibSVM index / LibFM field, LibFM index
+  uint32_t u0_hi, u1_hi;  // high words (generic path, 64-bit indices)
+  float f0, f1;           // label & weight, or the feature value
+  int r;                  // values parsed (ParsePair / ParseTriple convention)
+};
+
+/*!
+ * \brief decode a label `f[:f]`, LibSVM feature `u[:f]` or LibFM feature
+ *  `u:u[:f]` starting at LDS byte a, branch-free: the numbers are decoded
+ *  unconditionally (the next one from wherever the previous ended) and the
+ *  token shape is selected afterwards.  false: the generic parser is needed.
+ */
+template <TextFormat F>
+__device__ __forceinline__ bool decode(const uint4* lds, uint32_t a, bool is_label, Token* t) {
+  const Num n1 = parse_num(lds, a);
+  const bool c1 = n1.term == ':';
+  const Num n2 = parse_num(lds, n1.end + (c1 ? 1u : 0u));
+  // label f[:f] (either format) or LibSVM feature u[:f]
+  const bool first = is_label ? n1.ok_float : n1.ok_uint;
+  const bool pair_ok = first & (c1 ? (n2.ok_float & is_end(n2.term)) : is_end(n1.term));
+  t->u0 = n1.ival;
+  t->f1 = n2.fval;
+  if (F == TextFormat::kLibSVM) {
+    t->f0 = is_label ? n1.fval : n2.fval;
+    t->r = c1 ? 2 : 1;
+    return pair_ok;
+  }
+  // LibFM feature field:index[:value]
+  const bool c2 = n2.term == ':';
+  const Num n3 = parse_num(lds, n2.end + (c2 ? 1u : 0u));
+  const bool triple_ok =
+      c1 & n1.ok_uint & n2.ok_uint & (c2 ? (n3.ok_float & is_end(n3.term)) : is_end(n2.term));
+  t->u1 = n2.ival;
+  t->f0 = is_label ? n1.fval : n3.fval;
+  t->r = is_label ? (c1 ? 2 : 1) : (c2 ? 3 : 2);
+  return is_label ? pair_ok : triple_ok;
+}
+
+}  // namespace tok
+}  // namespace gpu
+}  // namespace dmlc
+#endif  // DMLC_SRC_GPU_TOKEN_DECODE_H_
