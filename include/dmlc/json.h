@@ -1,17 +1,25 @@
 /*!
  * \file dmlc/json.h
- * \brief Streaming JSON reader/writer with STL handlers and dmlc::any support.
+ * \brief Streaming JSON reader / writer with STL handlers and dmlc::any.
  *
- * Parity: reference `include/dmlc/json.h` — JSONReader (:43-183) with
- * ReadString / ReadNumber / BeginObject / BeginArray / NextObjectItem /
- * NextArrayItem / line_info; JSONWriter (:188-292); JSONObjectReadHelper with
- * DeclareField / DeclareOptionalField / ReadAllFields (:310-368, unknown field
- * and missing required field are errors); handlers for numbers, strings,
- * vectors, lists, maps, pairs and classes with Save(JSONWriter*) /
- * Load(JSONReader*) (:393-525); AnyJSONManager + DMLC_JSON_ENABLE_ANY writing
- * `["TypeKey", value]` (:370-384, :530-613).
+ * Public surface kept from the reference (`include/dmlc/json.h`): JSONReader
+ * {ReadString, ReadNumber, BeginObject, BeginArray, NextObjectItem,
+ * NextArrayItem, Read, line_info}, JSONWriter {WriteNoEscape, WriteString,
+ * WriteNumber, BeginArray, EndArray, BeginObject, EndObject,
+ * WriteObjectKeyValue, WriteArraySeperator (sic), WriteArrayItem, Write},
+ * JSONObjectReadHelper {DeclareField, DeclareOptionalField, ReadAllFields:
+ * an unknown key or a missing required key is an error}, and
+ * DMLC_JSON_ENABLE_ANY(Type, Key) which stores an `any` as `["Key", value]`.
  *
- * New implementation: single constexpr-dispatch handler, no SFINAE class tree.
+ * Layout written: objects put each member on its own line,
+ * indented two spaces per open scope; arrays of class-typed elements do the
+ * same, arrays of scalars / strings stay on one line ("[1, 2, 3]"); pairs and
+ * `any` are one-line two-element arrays.
+ *
+ * Implementation (new): the reader keeps a stack of open scopes and advances
+ * arrays and objects through one routine (`Advance`); the writer keeps a
+ * stack of frames {multi-line, members written}; values dispatch through one
+ * `json::Handler<T>` with `if constexpr`.
  */
 #ifndef DMLC_JSON_H_
 #define DMLC_JSON_H_
@@ -20,6 +28,7 @@
 #include <cstdio>
 #include <functional>
 #include <istream>
+#include <limits>
 #include <list>
 #include <map>
 #include <ostream>
@@ -46,288 +55,352 @@ template <typename T>
 struct Handler;
 }  // namespace json
 
-/*! \brief pull-style JSON reader over a std::istream */
+/*! \brief pull parser over a std::istream */
 class JSONReader {
  public:
-  explicit JSONReader(std::istream* is) : is_(is) {}
+  explicit JSONReader(std::istream* is) : in_(is) {}
 
-  /*! \brief read a quoted string (supports \" \\ \/ \n \r \t \b \f \uXXXX<128) */
-  inline void ReadString(std::string* out_str);
-  /*! \brief read a number (or bool for ValueType=bool) */
+  /*! \brief a quoted string; escapes \" \\ \/ \b \f \n \r \t and \uXXXX (BMP, as UTF-8) */
+  inline void ReadString(std::string* out);
+  /*! \brief a number (true / false / 1 / 0 for bool) */
   template <typename ValueType>
-  inline void ReadNumber(ValueType* out_value);
-  inline void BeginObject();
-  inline void BeginArray();
-  /*! \brief advance to the next key of the current object; false at '}' */
+  inline void ReadNumber(ValueType* out);
+  inline void BeginObject() { Open('{', '}'); }
+  inline void BeginArray() { Open('[', ']'); }
+  /*! \brief move to the next member of the innermost object; false once it closed */
   inline bool NextObjectItem(std::string* out_key);
-  /*! \brief advance to the next element of the current array; false at ']' */
-  inline bool NextArrayItem();
-  /*! \brief read any value with a registered handler */
+  /*! \brief move to the next element of the innermost array; false once it closed */
+  inline bool NextArrayItem() { return Advance(']'); }
+  /*! \brief any value with a json::Handler */
   template <typename ValueType>
-  inline void Read(ValueType* out_value);
-  /*! \brief "Line N, around ^`...`" for error messages */
+  inline void Read(ValueType* out);
+  /*! \brief where the reader is, for error messages */
   inline std::string line_info() const {
     std::ostringstream os;
-    os << " Line " << std::max(line_count_r_, line_count_n_)
-       << ", around ^`" << last_chars_ << "`";
+    os << " (line " << line_ + 1 << ", after \"" << recent_ << "\")";
     return os.str();
   }
-  /*! \brief peek next non-space char without consuming it */
+  /*! \brief next non-blank character, not consumed */
   inline int PeekNextNonSpace() {
-    int ch;
-    while (true) {
-      ch = is_->peek();
-      if (ch == '\n') ++line_count_n_;
-      if (ch == '\r') ++line_count_r_;
-      if (!std::isspace(ch)) break;
-      is_->get();
-    }
-    return ch;
+    SkipBlanks();
+    return in_->peek();
   }
-  /*! \brief consume and return next non-space char */
+  /*! \brief next non-blank character, consumed */
   inline int NextNonSpace() {
-    int ch;
-    do {
-      ch = NextChar();
-      if (ch == '\n') ++line_count_n_;
-      if (ch == '\r') ++line_count_r_;
-    } while (std::isspace(ch));
-    return ch;
+    SkipBlanks();
+    return Take();
   }
 
  private:
-  inline int NextChar() {
-    int ch = is_->get();
-    if (ch != EOF) {
-      last_chars_.push_back(static_cast<char>(ch));
-      if (last_chars_.size() > 32) last_chars_.erase(0, last_chars_.size() - 32);
-    }
-    return ch;
+  struct Scope {
+    char close;
+    size_t items;
+  };
+  inline int Take() {
+    const int c = in_->get();
+    if (c == EOF) return c;
+    if (c == '\n') ++line_;
+    recent_.push_back(static_cast<char>(c));
+    if (recent_.size() > 24) recent_.erase(0, recent_.size() - 24);
+    return c;
   }
-  std::istream* is_;
-  size_t line_count_r_{0};
-  size_t line_count_n_{0};
-  std::string last_chars_;
-  /*! \brief element counters of the open scopes */
-  std::vector<size_t> scope_counter_;
+  inline void SkipBlanks() {
+    while (std::isspace(in_->peek())) Take();
+  }
+  inline void Expect(int got, char want) {
+    if (got != want) {
+      LOG(FATAL) << "JSON: wanted '" << want << "' but read "
+                 << (got == EOF ? std::string("end of input")
+                                : std::string("'") + static_cast<char>(got) + "'")
+                 << line_info();
+    }
+  }
+  inline void Open(char open, char close) {
+    Expect(NextNonSpace(), open);
+    scopes_.push_back(Scope{close, 0});
+  }
+  /*!
+   * \brief shared step of NextArrayItem / NextObjectItem: consume the closing
+   *  bracket (scope done) or, after the first item, the separating comma
+   */
+  inline bool Advance(char close) {
+    CHECK(!scopes_.empty() && scopes_.back().close == close)
+        << "JSON: no open '" << (close == ']' ? '[' : '{') << "' to iterate" << line_info();
+    Scope& sc = scopes_.back();
+    const int c = PeekNextNonSpace();
+    if (c == close || c == EOF) {
+      Take();
+      scopes_.pop_back();
+      return false;
+    }
+    if (sc.items != 0) Expect(Take(), ',');
+    ++sc.items;
+    return true;
+  }
+  inline unsigned HexDigit() {
+    const int h = Take();
+    if (h >= '0' && h <= '9') return static_cast<unsigned>(h - '0');
+    if (h >= 'a' && h <= 'f') return static_cast<unsigned>(h - 'a' + 10);
+    if (h >= 'A' && h <= 'F') return static_cast<unsigned>(h - 'A' + 10);
+    LOG(FATAL) << "JSON: bad \\u escape digit" << line_info();
+    return 0;
+  }
+  static inline void AppendUtf8(unsigned cp, std::string* s) {
+    if (cp < 0x80) {
+      s->push_back(static_cast<char>(cp));
+    } else if (cp < 0x800) {
+      s->push_back(static_cast<char>(0xC0 | (cp >> 6)));
+      s->push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+    } else {
+      s->push_back(static_cast<char>(0xE0 | (cp >> 12)));
+      s->push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
+      s->push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+    }
+  }
+
+  std::istream* in_;
+  size_t line_{0};
+  std::string recent_;
+  std::vector<Scope> scopes_;
 };
 
-/*! \brief JSON writer with optional multi-line indentation */
+/*! \brief writer producing the layout described in the file comment */
 class JSONWriter {
  public:
-  explicit JSONWriter(std::ostream* os) : os_(os) {}
-  inline void WriteNoEscape(const std::string& s) { *os_ << '\"' << s << '\"'; }
+  explicit JSONWriter(std::ostream* os) : out_(os) {}
+  inline void WriteNoEscape(const std::string& s) { *out_ << '"' << s << '"'; }
   inline void WriteString(const std::string& s);
   template <typename ValueType>
   inline void WriteNumber(const ValueType& v) {
     if constexpr (std::is_same<ValueType, bool>::value) {
-      *os_ << (v ? "true" : "false");
+      *out_ << (v ? "true" : "false");
     } else if constexpr (std::is_floating_point<ValueType>::value) {
-      std::ostringstream tmp;
-      tmp.precision(std::is_same<ValueType, float>::value ? 9 : 17);
-      tmp << v;
-      *os_ << tmp.str();
+      // enough digits to read the same value back
+      std::ostringstream num;
+      num.precision(std::numeric_limits<ValueType>::max_digits10);
+      num << v;
+      *out_ << num.str();
     } else {
-      *os_ << v;
+      *out_ << v;
     }
   }
-  inline void BeginArray(bool multi_line = true);
-  inline void EndArray();
-  inline void BeginObject(bool multi_line = true);
-  inline void EndObject();
+  inline void BeginArray(bool multi_line = true) { Push('[', multi_line); }
+  inline void EndArray() { Pop(']'); }
+  inline void BeginObject(bool multi_line = true) { Push('{', multi_line); }
+  inline void EndObject() { Pop('}'); }
   template <typename ValueType>
   inline void WriteObjectKeyValue(const std::string& key, const ValueType& value);
+  /*! \brief the separator before the next array element (name kept from the reference API) */
   inline void WriteArraySeperator();
   template <typename ValueType>
-  inline void WriteArrayItem(const ValueType& value);
+  inline void WriteArrayItem(const ValueType& value) {
+    WriteArraySeperator();
+    json::Handler<ValueType>::Write(this, value);
+  }
   template <typename ValueType>
   inline void Write(const ValueType& value);
 
  private:
-  inline void WriteSeperator() {
-    if (scope_multi_line_.empty() || scope_multi_line_.back()) {
-      *os_ << '\n' << std::string(scope_multi_line_.size() * 2, ' ');
-    }
+  struct Frame {
+    char close;
+    bool multi_line;
+    size_t written;
+  };
+  inline void NewLine() {
+    *out_ << '\n';
+    for (size_t i = 0; i < frames_.size(); ++i) *out_ << "  ";
   }
-  std::ostream* os_;
-  std::vector<size_t> scope_counter_;
-  std::vector<bool> scope_multi_line_;
+  inline void Push(char open, bool multi_line) {
+    *out_ << open;
+    frames_.push_back(Frame{open == '[' ? ']' : '}', multi_line, 0});
+  }
+  inline void Pop(char close) {
+    CHECK(!frames_.empty() && frames_.back().close == close)
+        << "JSONWriter: '" << close << "' does not close the innermost scope";
+    const Frame f = frames_.back();
+    frames_.pop_back();
+    if (f.multi_line && f.written != 0) NewLine();
+    *out_ << close;
+  }
+  std::ostream* out_;
+  std::vector<Frame> frames_;
 };
 
-/*! \brief declarative reader of a fixed set of object fields */
+/*! \brief reads one object into declared fields */
 class JSONObjectReadHelper {
  public:
   template <typename T>
   inline void DeclareField(const std::string& key, T* addr) {
-    DeclareFieldInternal(key, addr, false);
+    Declare(key, addr, true);
   }
   template <typename T>
   inline void DeclareOptionalField(const std::string& key, T* addr) {
-    DeclareFieldInternal(key, addr, true);
+    Declare(key, addr, false);
   }
-  /*! \brief read the object; unknown keys and missing required keys are fatal */
+  /*! \brief read the object; an undeclared key or a missing required key is fatal */
   inline void ReadAllFields(JSONReader* reader);
 
  private:
-  template <typename T>
-  inline void DeclareFieldInternal(const std::string& key, T* addr, bool optional) {
-    CHECK(map_.count(key) == 0) << "Adding duplicate field " << key;
-    Entry e;
-    e.func = [](JSONReader* reader, void* a) { reader->Read(static_cast<T*>(a)); };
-    e.addr = addr;
-    e.optional = optional;
-    map_[key] = e;
-  }
-  struct Entry {
-    std::function<void(JSONReader*, void*)> func;
-    void* addr;
-    bool optional;
+  struct Slot {
+    std::function<void(JSONReader*)> read;
+    bool required;
   };
-  std::map<std::string, Entry> map_;
+  template <typename T>
+  inline void Declare(const std::string& key, T* addr, bool required) {
+    CHECK(slots_.find(key) == slots_.end()) << "JSONObjectReadHelper: '" << key
+                                            << "' declared twice";
+    slots_[key] = Slot{[addr](JSONReader* r) { r->Read(addr); }, required};
+  }
+  std::map<std::string, Slot> slots_;
 };
 
 namespace json {
 
-/*! \brief registry of types storable inside dmlc::any for JSON I/O */
+/*! \brief types allowed inside dmlc::any for JSON I/O, by key name */
 class AnyJSONManager {
  public:
-  template <typename T>
-  inline AnyJSONManager& EnableType(const std::string& type_name) {
-    std::type_index tp = std::type_index(typeid(T));
-    if (type_name_.count(tp) != 0) {
-      CHECK(type_name_.at(tp) == type_name)
-          << "Type has already been registered as another typename "
-          << type_name_.at(tp);
-      return *this;
-    }
-    CHECK(type_map_.count(type_name) == 0)
-        << "Type name " << type_name << " already registered in registry";
-    Entry e;
-    e.read = [](JSONReader* reader, any* data) {
-      T v;
-      reader->Read(&v);
-      *data = std::move(v);
-    };
-    e.write = [](JSONWriter* writer, const any& data) {
-      writer->Write(dmlc::get<T>(data));
-    };
-    type_name_[tp] = type_name;
-    type_map_[type_name] = e;
-    return *this;
-  }
-  static AnyJSONManager* Global() {
-    static AnyJSONManager inst;
-    return &inst;
-  }
   struct Entry {
     std::function<void(JSONReader*, any*)> read;
     std::function<void(JSONWriter*, const any&)> write;
   };
-  std::unordered_map<std::type_index, std::string> type_name_;
-  std::unordered_map<std::string, Entry> type_map_;
+  template <typename T>
+  inline AnyJSONManager& EnableType(const std::string& key) {
+    const std::type_index tid(typeid(T));
+    auto known = key_of_.find(tid);
+    if (known != key_of_.end()) {
+      CHECK_EQ(known->second, key) << "type already enabled for JSON as " << known->second;
+      return *this;
+    }
+    CHECK(by_key_.count(key) == 0) << "JSON any key " << key << " is taken by another type";
+    key_of_[tid] = key;
+    by_key_[key] = Entry{[](JSONReader* r, any* dst) {
+                           T v;
+                           r->Read(&v);
+                           *dst = std::move(v);
+                         },
+                         [](JSONWriter* w, const any& src) { w->Write(dmlc::get<T>(src)); }};
+    return *this;
+  }
+  static AnyJSONManager* Global() {
+    static AnyJSONManager registry;
+    return &registry;
+  }
+  /*! \brief key of a stored type; fatal if it was never enabled */
+  const std::string& KeyOf(const std::type_info& t) const {
+    auto hit = key_of_.find(std::type_index(t));
+    CHECK(hit != key_of_.end()) << "type " << Demangle(t.name())
+                                << " is not enabled for JSON (DMLC_JSON_ENABLE_ANY)";
+    return hit->second;
+  }
+  const Entry& ByKey(const std::string& key) const {
+    auto hit = by_key_.find(key);
+    CHECK(hit != by_key_.end()) << "JSON any key " << key
+                                << " is not enabled (DMLC_JSON_ENABLE_ANY)";
+    return hit->second;
+  }
+
+ private:
+  std::unordered_map<std::type_index, std::string> key_of_;
+  std::unordered_map<std::string, Entry> by_key_;
 };
 
 template <typename T>
-struct is_vector_like : std::false_type {};
+struct IsSequence : std::false_type {};
 template <typename T, typename A>
-struct is_vector_like<std::vector<T, A>> : std::true_type {};
+struct IsSequence<std::vector<T, A>> : std::true_type {};
 template <typename T, typename A>
-struct is_vector_like<std::list<T, A>> : std::true_type {};
+struct IsSequence<std::list<T, A>> : std::true_type {};
 
 template <typename T>
-struct is_str_map : std::false_type {};
+struct IsStringKeyed : std::false_type {};
 template <typename V, typename C, typename A>
-struct is_str_map<std::map<std::string, V, C, A>> : std::true_type {};
+struct IsStringKeyed<std::map<std::string, V, C, A>> : std::true_type {};
 template <typename V, typename H, typename E, typename A>
-struct is_str_map<std::unordered_map<std::string, V, H, E, A>> : std::true_type {};
+struct IsStringKeyed<std::unordered_map<std::string, V, H, E, A>> : std::true_type {};
 
 template <typename T>
-struct is_pair_t : std::false_type {};
+struct IsPair : std::false_type {};
 template <typename A, typename B>
-struct is_pair_t<std::pair<A, B>> : std::true_type {};
+struct IsPair<std::pair<A, B>> : std::true_type {};
+
+/*! \brief read one element of a two-element array (pair, any) */
+template <typename E>
+inline void ReadSlot(JSONReader* r, E* dst, const char* what) {
+  CHECK(r->NextArrayItem()) << "JSON: " << what << " needs two elements" << r->line_info();
+  r->Read(dst);
+}
 
 template <typename T>
 struct Handler {
-  inline static void Write(JSONWriter* writer, const T& value) {
+  static void Write(JSONWriter* w, const T& v) {
     if constexpr (std::is_same<T, std::string>::value) {
-      writer->WriteString(value);
+      w->WriteString(v);
     } else if constexpr (std::is_arithmetic<T>::value) {
-      writer->WriteNumber(value);
+      w->WriteNumber(v);
     } else if constexpr (std::is_same<T, any>::value) {
-      std::type_index tp(value.type());
-      auto* mgr = AnyJSONManager::Global();
-      CHECK(mgr->type_name_.count(tp) != 0)
-          << "Type " << Demangle(value.type().name())
-          << " has not been registered via DMLC_JSON_ENABLE_ANY";
-      const std::string& name = mgr->type_name_.at(tp);
-      writer->BeginArray(false);
-      writer->WriteArrayItem(name);
-      writer->WriteArraySeperator();
-      mgr->type_map_.at(name).write(writer, value);
-      writer->EndArray();
-    } else if constexpr (is_vector_like<T>::value) {
-      writer->BeginArray(std::is_class<typename T::value_type>::value);
-      for (const auto& v : value) writer->WriteArrayItem(v);
-      writer->EndArray();
-    } else if constexpr (is_str_map<T>::value) {
-      writer->BeginObject(true);
-      for (const auto& kv : value) writer->WriteObjectKeyValue(kv.first, kv.second);
-      writer->EndObject();
-    } else if constexpr (is_pair_t<T>::value) {
-      writer->BeginArray(false);
-      writer->WriteArrayItem(value.first);
-      writer->WriteArrayItem(value.second);
-      writer->EndArray();
+      AnyJSONManager* reg = AnyJSONManager::Global();
+      const std::string& key = reg->KeyOf(v.type());
+      w->BeginArray(false);
+      w->WriteArrayItem(key);
+      w->WriteArraySeperator();
+      reg->ByKey(key).write(w, v);
+      w->EndArray();
+    } else if constexpr (IsSequence<T>::value) {
+      w->BeginArray(std::is_class<typename T::value_type>::value);
+      for (const auto& e : v) w->WriteArrayItem(e);
+      w->EndArray();
+    } else if constexpr (IsStringKeyed<T>::value) {
+      w->BeginObject(true);
+      for (const auto& kv : v) w->WriteObjectKeyValue(kv.first, kv.second);
+      w->EndObject();
+    } else if constexpr (IsPair<T>::value) {
+      w->BeginArray(false);
+      w->WriteArrayItem(v.first);
+      w->WriteArrayItem(v.second);
+      w->EndArray();
     } else {
-      value.Save(writer);
+      v.Save(w);
     }
   }
-  inline static void Read(JSONReader* reader, T* value) {
+  static void Read(JSONReader* r, T* v) {
     if constexpr (std::is_same<T, std::string>::value) {
-      reader->ReadString(value);
+      r->ReadString(v);
     } else if constexpr (std::is_arithmetic<T>::value) {
-      reader->ReadNumber(value);
+      r->ReadNumber(v);
     } else if constexpr (std::is_same<T, any>::value) {
-      std::string type_name;
-      reader->BeginArray();
-      CHECK(reader->NextArrayItem()) << "invalid any json format";
-      reader->ReadString(&type_name);
-      auto* mgr = AnyJSONManager::Global();
-      auto it = mgr->type_map_.find(type_name);
-      CHECK(it != mgr->type_map_.end())
-          << "JSONReader: cannot find type " << type_name
-          << " (register it with DMLC_JSON_ENABLE_ANY)";
-      CHECK(reader->NextArrayItem()) << "invalid any json format";
-      it->second.read(reader, value);
-      CHECK(!reader->NextArrayItem()) << "invalid any json format";
-    } else if constexpr (is_vector_like<T>::value) {
-      using E = typename T::value_type;
-      value->clear();
-      reader->BeginArray();
-      while (reader->NextArrayItem()) {
-        E e;
-        Handler<E>::Read(reader, &e);
-        value->push_back(std::move(e));
-      }
-    } else if constexpr (is_str_map<T>::value) {
-      using V = typename T::mapped_type;
-      value->clear();
-      reader->BeginObject();
+      r->BeginArray();
       std::string key;
-      while (reader->NextObjectItem(&key)) {
-        V v;
-        Handler<V>::Read(reader, &v);
-        (*value)[key] = std::move(v);
+      ReadSlot(r, &key, "an any value");
+      CHECK(r->NextArrayItem()) << "JSON: an any value needs two elements" << r->line_info();
+      AnyJSONManager::Global()->ByKey(key).read(r, v);
+      CHECK(!r->NextArrayItem()) << "JSON: an any value has exactly two elements"
+                                 << r->line_info();
+    } else if constexpr (IsSequence<T>::value) {
+      T out;
+      r->BeginArray();
+      while (r->NextArrayItem()) {
+        typename T::value_type e;
+        r->Read(&e);
+        out.push_back(std::move(e));
       }
-    } else if constexpr (is_pair_t<T>::value) {
-      reader->BeginArray();
-      CHECK(reader->NextArrayItem()) << "Expect array of length 2";
-      Handler<typename T::first_type>::Read(reader, &value->first);
-      CHECK(reader->NextArrayItem()) << "Expect array of length 2";
-      Handler<typename T::second_type>::Read(reader, &value->second);
-      CHECK(!reader->NextArrayItem()) << "Expect array of length 2";
+      *v = std::move(out);
+    } else if constexpr (IsStringKeyed<T>::value) {
+      T out;
+      r->BeginObject();
+      std::string key;
+      while (r->NextObjectItem(&key)) {
+        typename T::mapped_type e;
+        r->Read(&e);
+        out[key] = std::move(e);
+      }
+      *v = std::move(out);
+    } else if constexpr (IsPair<T>::value) {
+      r->BeginArray();
+      ReadSlot(r, &v->first, "a pair");
+      ReadSlot(r, &v->second, "a pair");
+      CHECK(!r->NextArrayItem()) << "JSON: a pair has exactly two elements" << r->line_info();
     } else {
-      value->Load(reader);
+      v->Load(r);
     }
   }
 };
@@ -336,274 +409,152 @@ struct Handler {
 #define DMLC_JSON_ENABLE_ANY_VAR_DEF(KeyName) \
   static DMLC_ATTRIBUTE_UNUSED ::dmlc::json::AnyJSONManager& __make_AnyJSONType##_##KeyName##__
 
-/*! \brief allow values of `Type` inside dmlc::any to be saved/loaded as JSON */
+/*! \brief let dmlc::any values of `Type` be written / read as ["KeyName", value] */
 #define DMLC_JSON_ENABLE_ANY(Type, KeyName) \
   DMLC_JSON_ENABLE_ANY_VAR_DEF(KeyName) =   \
       ::dmlc::json::AnyJSONManager::Global()->EnableType<Type>(#KeyName)
 
-// ---------------------------------------------------------------------------
-// implementation
-// ---------------------------------------------------------------------------
-inline void JSONReader::ReadString(std::string* out_str) {
-  int ch = NextNonSpace();
-  CHECK_EQ(ch, '\"') << "Error at" << line_info() << ", Expect \'\"\' but get \'"
-                     << static_cast<char>(ch) << '\'';
-  std::string out;
-  while (true) {
-    ch = NextChar();
-    if (ch == '\\') {
-      int sch = NextChar();
-      switch (sch) {
-        case 'r': out.push_back('\r'); break;
-        case 'n': out.push_back('\n'); break;
-        case 't': out.push_back('\t'); break;
-        case 'b': out.push_back('\b'); break;
-        case 'f': out.push_back('\f'); break;
-        case '\\': out.push_back('\\'); break;
-        case '\"': out.push_back('\"'); break;
-        case '/': out.push_back('/'); break;
-        case 'u': {
-          unsigned code = 0;
-          for (int i = 0; i < 4; ++i) {
-            int h = NextChar();
-            code = code * 16 + static_cast<unsigned>(
-                std::isdigit(h) ? h - '0' : (std::tolower(h) - 'a' + 10));
-          }
-          if (code < 0x80) {
-            out.push_back(static_cast<char>(code));
-          } else if (code < 0x800) {
-            out.push_back(static_cast<char>(0xC0 | (code >> 6)));
-            out.push_back(static_cast<char>(0x80 | (code & 0x3F)));
-          } else {
-            out.push_back(static_cast<char>(0xE0 | (code >> 12)));
-            out.push_back(static_cast<char>(0x80 | ((code >> 6) & 0x3F)));
-            out.push_back(static_cast<char>(0x80 | (code & 0x3F)));
-          }
-          break;
-        }
-        default: LOG(FATAL) << "unknown string escape \\" << static_cast<char>(sch);
+// ------------------------------------------------------------------ reader
+inline void JSONReader::ReadString(std::string* out) {
+  Expect(NextNonSpace(), '"');
+  std::string s;
+  for (;;) {
+    const int c = Take();
+    if (c == '"') break;
+    CHECK(c != EOF && c != '\n' && c != '\r') << "JSON: unterminated string" << line_info();
+    if (c != '\\') {
+      s.push_back(static_cast<char>(c));
+      continue;
+    }
+    const int e = Take();
+    switch (e) {
+      case '"':
+      case '\\':
+      case '/':
+        s.push_back(static_cast<char>(e));
+        break;
+      case 'b': s.push_back('\b'); break;
+      case 'f': s.push_back('\f'); break;
+      case 'n': s.push_back('\n'); break;
+      case 'r': s.push_back('\r'); break;
+      case 't': s.push_back('\t'); break;
+      case 'u': {
+        unsigned cp = 0;
+        for (int i = 0; i < 4; ++i) cp = (cp << 4) | HexDigit();
+        AppendUtf8(cp, &s);
+        break;
       }
-    } else {
-      if (ch == '\"') break;
-      CHECK(ch != EOF && ch != '\r' && ch != '\n')
-          << "Error at" << line_info() << ", string is not terminated";
-      out.push_back(static_cast<char>(ch));
+      default:
+        LOG(FATAL) << "JSON: unknown escape \\" << static_cast<char>(e) << line_info();
     }
   }
-  *out_str = std::move(out);
+  *out = std::move(s);
 }
 
 template <typename ValueType>
-inline void JSONReader::ReadNumber(ValueType* out_value) {
+inline void JSONReader::ReadNumber(ValueType* out) {
   if constexpr (std::is_same<ValueType, bool>::value) {
-    int ch = NextNonSpace();
-    std::string tok(1, static_cast<char>(ch));
-    while (std::isalpha(is_->peek())) tok.push_back(static_cast<char>(NextChar()));
-    if (tok == "true") {
-      *out_value = true;
-    } else if (tok == "false") {
-      *out_value = false;
+    std::string word;
+    word.push_back(static_cast<char>(NextNonSpace()));
+    while (std::isalnum(in_->peek())) word.push_back(static_cast<char>(Take()));
+    if (word == "true" || word == "1") {
+      *out = true;
+    } else if (word == "false" || word == "0") {
+      *out = false;
     } else {
-      // also accept 0/1
-      CHECK(tok == "1" || tok == "0") << "Error at" << line_info()
-                                      << ", expect boolean, got " << tok;
-      *out_value = tok == "1";
+      LOG(FATAL) << "JSON: '" << word << "' is not a boolean" << line_info();
     }
   } else {
-    PeekNextNonSpace();
-    *is_ >> *out_value;
-    CHECK(!is_->fail()) << "Error at" << line_info() << ", Expect number";
+    SkipBlanks();
+    *in_ >> *out;
+    CHECK(!in_->fail()) << "JSON: expected a number" << line_info();
   }
-}
-
-inline void JSONReader::BeginObject() {
-  int ch = NextNonSpace();
-  CHECK_EQ(ch, '{') << "Error at" << line_info() << ", Expect \'{\' but get \'"
-                    << static_cast<char>(ch) << '\'';
-  scope_counter_.push_back(0);
-}
-
-inline void JSONReader::BeginArray() {
-  int ch = NextNonSpace();
-  CHECK_EQ(ch, '[') << "Error at" << line_info() << ", Expect \'[\' but get \'"
-                    << static_cast<char>(ch) << '\'';
-  scope_counter_.push_back(0);
 }
 
 inline bool JSONReader::NextObjectItem(std::string* out_key) {
-  bool next = true;
-  if (scope_counter_.back() != 0) {
-    int ch = NextNonSpace();
-    if (ch == EOF || ch == '}') {
-      next = false;
-    } else {
-      CHECK_EQ(ch, ',') << "Error at" << line_info()
-                        << ", JSON object expect \'}\' or \',\' but get \'"
-                        << static_cast<char>(ch) << '\'';
-    }
-  } else {
-    int ch = PeekNextNonSpace();
-    if (ch == '}') {
-      NextChar();
-      next = false;
-    }
-  }
-  if (!next) {
-    scope_counter_.pop_back();
-    return false;
-  }
-  scope_counter_.back() += 1;
+  if (!Advance('}')) return false;
   ReadString(out_key);
-  int ch = NextNonSpace();
-  CHECK_EQ(ch, ':') << "Error at" << line_info() << ", Expect \':\' but get \'"
-                    << static_cast<char>(ch) << '\'';
-  return true;
-}
-
-inline bool JSONReader::NextArrayItem() {
-  bool next = true;
-  if (scope_counter_.back() != 0) {
-    int ch = NextNonSpace();
-    if (ch == EOF || ch == ']') {
-      next = false;
-    } else {
-      CHECK_EQ(ch, ',') << "Error at" << line_info()
-                        << ", JSON array expect \']\' or \',\'. Get \'"
-                        << static_cast<char>(ch) << "\' instead";
-    }
-  } else {
-    int ch = PeekNextNonSpace();
-    if (ch == ']') {
-      NextChar();
-      next = false;
-    }
-  }
-  if (!next) {
-    scope_counter_.pop_back();
-    return false;
-  }
-  scope_counter_.back() += 1;
+  Expect(NextNonSpace(), ':');
   return true;
 }
 
 template <typename ValueType>
-inline void JSONReader::Read(ValueType* out_value) {
-  json::Handler<ValueType>::Read(this, out_value);
+inline void JSONReader::Read(ValueType* out) {
+  json::Handler<ValueType>::Read(this, out);
 }
 
+// ------------------------------------------------------------------ writer
 inline void JSONWriter::WriteString(const std::string& s) {
-  std::ostream& os = *os_;
-  os << '\"';
-  for (char c : s) {
-    switch (c) {
-      case '\r': os << "\\r"; break;
-      case '\n': os << "\\n"; break;
-      case '\t': os << "\\t"; break;
-      case '\b': os << "\\b"; break;
-      case '\f': os << "\\f"; break;
-      case '\\': os << "\\\\"; break;
-      case '\"': os << "\\\""; break;
-      default:
-        if (static_cast<unsigned char>(c) < 0x20) {
-          char buf[8];
-          std::snprintf(buf, sizeof(buf), "\\u%04x", static_cast<unsigned>(c));
-          os << buf;
-        } else {
-          os << c;
-        }
+  std::ostream& os = *out_;
+  os << '"';
+  for (const char c : s) {
+    const unsigned char u = static_cast<unsigned char>(c);
+    if (c == '"' || c == '\\') {
+      os << '\\' << c;
+    } else if (c == '\n') {
+      os << "\\n";
+    } else if (c == '\r') {
+      os << "\\r";
+    } else if (c == '\t') {
+      os << "\\t";
+    } else if (c == '\b') {
+      os << "\\b";
+    } else if (c == '\f') {
+      os << "\\f";
+    } else if (u < 0x20) {
+      char hex[8];
+      std::snprintf(hex, sizeof(hex), "\\u%04x", u);
+      os << hex;
+    } else {
+      os << c;
     }
   }
-  os << '\"';
-}
-
-inline void JSONWriter::BeginArray(bool multi_line) {
-  *os_ << '[';
-  scope_multi_line_.push_back(multi_line);
-  scope_counter_.push_back(0);
-}
-
-inline void JSONWriter::EndArray() {
-  CHECK_NE(scope_multi_line_.size(), 0U);
-  CHECK_NE(scope_counter_.size(), 0U);
-  bool newline = scope_multi_line_.back();
-  size_t nelem = scope_counter_.back();
-  scope_multi_line_.pop_back();
-  scope_counter_.pop_back();
-  if (newline && nelem != 0) WriteSeperator();
-  *os_ << ']';
-}
-
-inline void JSONWriter::BeginObject(bool multi_line) {
-  *os_ << '{';
-  scope_multi_line_.push_back(multi_line);
-  scope_counter_.push_back(0);
-}
-
-inline void JSONWriter::EndObject() {
-  CHECK_NE(scope_multi_line_.size(), 0U);
-  CHECK_NE(scope_counter_.size(), 0U);
-  bool newline = scope_multi_line_.back();
-  size_t nelem = scope_counter_.back();
-  scope_multi_line_.pop_back();
-  scope_counter_.pop_back();
-  if (newline && nelem != 0) WriteSeperator();
-  *os_ << '}';
-}
-
-template <typename ValueType>
-inline void JSONWriter::WriteObjectKeyValue(const std::string& key,
-                                           const ValueType& value) {
-  std::ostream& os = *os_;
-  if (scope_counter_.back() != 0) os << ",";
-  WriteSeperator();
-  WriteString(key);
-  os << ": ";
-  scope_counter_.back() += 1;
-  json::Handler<ValueType>::Write(this, value);
+  os << '"';
 }
 
 inline void JSONWriter::WriteArraySeperator() {
-  std::ostream& os = *os_;
-  if (scope_counter_.back() != 0) os << ", ";
-  scope_counter_.back() += 1;
-  if (scope_multi_line_.back()) WriteSeperator();
+  CHECK(!frames_.empty()) << "JSONWriter: array element outside an array";
+  Frame& f = frames_.back();
+  if (f.written++ != 0) *out_ << ", ";
+  if (f.multi_line) NewLine();
 }
 
 template <typename ValueType>
-inline void JSONWriter::WriteArrayItem(const ValueType& value) {
-  this->WriteArraySeperator();
+inline void JSONWriter::WriteObjectKeyValue(const std::string& key, const ValueType& value) {
+  CHECK(!frames_.empty()) << "JSONWriter: object member outside an object";
+  Frame& f = frames_.back();
+  if (f.written++ != 0) *out_ << ',';
+  if (f.multi_line) NewLine();
+  WriteString(key);
+  *out_ << ": ";
   json::Handler<ValueType>::Write(this, value);
 }
 
 template <typename ValueType>
 inline void JSONWriter::Write(const ValueType& value) {
-  size_t nscope = scope_multi_line_.size();
+  const size_t depth = frames_.size();
   json::Handler<ValueType>::Write(this, value);
-  CHECK_EQ(nscope, scope_multi_line_.size()) << "Uneven scope, did you call EndArray/EndObject?";
+  CHECK_EQ(depth, frames_.size()) << "JSONWriter: a Begin* without its End*";
 }
 
 inline void JSONObjectReadHelper::ReadAllFields(JSONReader* reader) {
+  std::map<std::string, bool> seen;
   reader->BeginObject();
-  std::map<std::string, int> visited;
   std::string key;
   while (reader->NextObjectItem(&key)) {
-    auto it = map_.find(key);
-    if (it != map_.end()) {
-      it->second.func(reader, it->second.addr);
-      visited[key] = 0;
-    } else {
-      std::ostringstream err;
-      err << "JSONReader: Unknown field " << key << ", candidates are: \n";
-      for (const auto& kv : map_) err << '\"' << kv.first << "\"\n";
-      LOG(FATAL) << err.str();
+    auto slot = slots_.find(key);
+    if (slot == slots_.end()) {
+      std::ostringstream known;
+      for (const auto& kv : slots_) known << " \"" << kv.first << '"';
+      LOG(FATAL) << "JSON: unexpected member \"" << key << "\"; expected one of" << known.str()
+                 << reader->line_info();
     }
+    slot->second.read(reader);
+    seen[key] = true;
   }
-  for (const auto& kv : map_) {
-    if (!kv.second.optional) {
-      CHECK(visited.count(kv.first) != 0)
-          << "JSONReader: Missing field \"" << kv.first << "\"\n At "
-          << reader->line_info();
-    }
+  for (const auto& kv : slots_) {
+    CHECK(!kv.second.required || seen.count(kv.first) != 0)
+        << "JSON: required member \"" << kv.first << "\" is missing" << reader->line_info();
   }
 }
 

@@ -413,3 +413,61 @@ TEST(Registry, FindAliasList) {
   EXPECT_EQ(dmlc::Registry<TestFactory>::List().size(), 2U);
   EXPECT_EQ(dmlc::Registry<TestFactory>::ListAllNames().size(), 3U);  // names include aliases
 }
+
+// ------------------------------------------------- parameter / json (round 3)
+TEST(Parameter, UpdateOptionalBoolAndDocs) {
+  TestParam p;
+  p.Init(std::map<std::string, std::string>{{"name", "a"}, {"nthread", "6"}});
+  // UpdateAllowUnknown touches only the given fields and applies no defaults
+  auto rest = p.UpdateAllowUnknown(
+      std::map<std::string, std::string>{{"lr", "0.25"}, {"zzz", "1"}});
+  ASSERT_EQ(rest.size(), 1U);
+  EXPECT_EQ(rest[0].first, "zzz");
+  EXPECT_EQ(p.nthread, 6);
+  EXPECT_NEAR(p.lr, 0.25f, 1e-7);
+  // optional<int> with enums: "None" empties it and prints back as None
+  p.Init(std::map<std::string, std::string>{{"name", "a"}, {"maybe", "None"}, {"flag", " FALSE"}});
+  EXPECT_FALSE(p.maybe.has_value());
+  EXPECT_EQ(p.__DICT__()["maybe"], "None");
+  EXPECT_FALSE(*p.flag);
+  // trailing garbage after a number is an error; trailing blanks are not
+  EXPECT_THROW(p.Init(std::map<std::string, std::string>{{"name", "a"}, {"nthread", "3x"}}),
+               dmlc::ParamError);
+  EXPECT_NO_THROW(p.Init(std::map<std::string, std::string>{{"name", "a"}, {"nthread", "3 "}}));
+  EXPECT_EQ(p.nthread, 3);
+  // field docs: required vs default, enum listing
+  auto fields = TestParam::__FIELDS__();
+  ASSERT_EQ(fields.size(), 6U);
+  EXPECT_EQ(fields[2].name, "name");
+  EXPECT_TRUE(fields[2].type_info_str.find("required") != std::string::npos);
+  EXPECT_TRUE(fields[3].type_info_str.find("'exact'") != std::string::npos);
+  EXPECT_TRUE(fields[3].type_info_str.find("default=fast") != std::string::npos);
+  // kAllMatch rejects hidden keys too
+  EXPECT_THROW(p.Init(std::map<std::string, std::string>{{"name", "a"}, {"__h__", "1"}},
+                      dmlc::kAllMatch),
+               dmlc::ParamError);
+}
+
+TEST(Json, WriterLayoutAndReaderErrors) {
+  std::ostringstream os;
+  dmlc::JSONWriter w(&os);
+  std::map<std::string, std::vector<int>> m{{"a", {1, 2}}, {"b", {}}};
+  w.Write(m);
+  EXPECT_EQ(os.str(), "{\n  \"a\": [1, 2],\n  \"b\": []\n}");
+  std::ostringstream os2;
+  dmlc::JSONWriter w2(&os2);
+  std::vector<std::map<std::string, int>> vm{{{"k", 1}}};
+  w2.Write(vm);
+  EXPECT_EQ(os2.str(), "[\n  {\n    \"k\": 1\n  }\n]");
+  // \u escapes decode to UTF-8, a missing comma is an error
+  std::istringstream is("[\"\\u00e9\\u0041\"]");
+  dmlc::JSONReader r(&is);
+  std::vector<std::string> v;
+  r.Read(&v);
+  ASSERT_EQ(v.size(), 1U);
+  EXPECT_EQ(v[0], "\xc3\xa9" "A");
+  std::istringstream bad("[1 2]");
+  dmlc::JSONReader rb(&bad);
+  std::vector<int> vi;
+  EXPECT_THROW(rb.Read(&vi), dmlc::Error);
+}
