@@ -39,13 +39,36 @@ sys.path.insert(0, ROOT)
 BASELINE_ROWS_PER_SEC = 2.20e6  # reference CPU parser, 8 threads
 NUM_PARTS = 16
 
+# per format: the reference number it is compared with (measured
+# CPU reference), the metric name and the default dataset size
+FORMATS = {
+    "libsvm": dict(baseline=2.201e6, rows=10_000_000,
+                   metric="parsed rows/sec (LibSVM->CSR in device memory), aggregate over GPUs",
+                   model="LibSVM tokenize -> device CSR RowBlock (synthetic 10M-row sparse file)",
+                   dtype="fp32 values / u32 indices (text parse, no matmul)"),
+    "libfm": dict(baseline=1.954e6, rows=10_000_000,
+                  metric="parsed rows/sec (LibFM->CSR in device memory), aggregate over GPUs",
+                  model="LibFM tokenize -> device CSR RowBlock with fields (synthetic 10M rows)",
+                  dtype="fp32 values / u32 indices and fields (text parse, no matmul)"),
+    "csv": dict(baseline=6.61e6, rows=10_000_000,
+                metric="parsed rows/sec (CSV->CSR in device memory, label_column=0), aggregate over GPUs",
+                model="CSV (29 columns) -> device CSR RowBlock (synthetic 10M rows)",
+                dtype="fp32 values / u32 indices (text parse, no matmul)"),
+    "recordio": dict(baseline=11.31e6, rows=4_000_000,
+                     metric="decoded records/sec (RecordIO -> device byte-CSR), aggregate over GPUs",
+                     model="RecordIO decode (4M x 512 B records, 1/64 multi-part) -> HBM byte-CSR",
+                     dtype="raw bytes (u64 offsets)"),
+}
+
 
 def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--rows", type=int, default=10_000_000)
+    ap.add_argument("--format", default="libsvm", choices=sorted(FORMATS),
+                    help="libsvm (the BASELINE headline), libfm, csv or recordio")
+    ap.add_argument("--rows", type=int, default=0, help="0: the format's default size")
     ap.add_argument("--data-dir", default=os.environ.get("DMLC_BENCH_DIR", "/tmp/dmlc_bench"))
     ap.add_argument("--chunk-mb", type=int, default=64)
     ap.add_argument("--read-threads", type=int, default=0, help="0: auto")
@@ -58,13 +81,16 @@ def parse_args():
                     help="stream: every step re-reads the text from the page cache over PCIe; "
                          "hbm: HBM epoch cache -- the warmup epoch keeps the text resident in "
                          "HBM and timed epochs parse it from there (kernel-bound)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.rows <= 0:
+        args.rows = FORMATS[args.format]["rows"]
+    return args
 
 
 def dataset_dir(args, world: int) -> str:
     # one copy per world size: the page cache of a part lives on the NUMA node
     # of the rank that wrote it, which must be the rank that reads it
-    return os.path.join(args.data_dir, f"libsvm_{args.rows}r_{NUM_PARTS}p_seed0_w{world}")
+    return os.path.join(args.data_dir, f"{args.format}_{args.rows}r_{NUM_PARTS}p_seed0_w{world}")
 
 
 def ensure_dataset(args, rank: int, world: int, barrier) -> str:
@@ -78,7 +104,7 @@ def ensure_dataset(args, rank: int, world: int, barrier) -> str:
 
     d = dataset_dir(args, world)
     if rank == 0 and os.path.isdir(args.data_dir):
-        prefix = f"libsvm_{args.rows}r_{NUM_PARTS}p_seed0"
+        prefix = f"{args.format}_"
         for name in os.listdir(args.data_dir):
             if name.startswith(prefix) and os.path.join(args.data_dir, name) != d:
                 shutil.rmtree(os.path.join(args.data_dir, name), ignore_errors=True)
@@ -89,13 +115,13 @@ def ensure_dataset(args, rank: int, world: int, barrier) -> str:
     for p in range(NUM_PARTS):
         if p * world // NUM_PARTS != rank:
             continue
-        path = os.path.join(d, f"part-{p:05d}.libsvm")
+        path = os.path.join(d, f"part-{p:05d}.{args.format}")
         done = path + ".done"
         if os.path.exists(done):
             continue
         b, e = p * per, min(args.rows, (p + 1) * per)
         tmp = path + f".tmp{rank}"
-        write_synthetic(tmp, b, e, format="libsvm", seed=0, nthread=nthread)
+        write_synthetic(tmp, b, e, format=args.format, seed=0, nthread=nthread)
         os.replace(tmp, path)
         open(done, "w").close()
     barrier()
@@ -185,14 +211,28 @@ def main():
     read_threads = args.read_threads or max(4, min(16, len(os.sched_getaffinity(0))))
 
     local = {}  # this rank's own counters, gathered to rank 0 after timing
-    if use_gpu:
-        parser = data.GPUParser(ddir, rank, world, format="libsvm", chunk_mb=args.chunk_mb,
+    if args.mode == "hbm" and args.warmup < 1:
+        raise SystemExit("--mode hbm needs --warmup >= 1 (the warmup epoch fills the cache)")
+    if use_gpu and args.format == "recordio":
+        from dmlc_core_amd import io as dio
+
+        parser = dio.GPURecordIO(ddir, rank, world, chunk_mb=args.chunk_mb,
+                                 device_slots=args.device_slots, pinned_slots=args.pinned_slots,
+                                 zero_copy=args.zero_copy, device=local_rank,
+                                 hbm_cache=int(args.mode == "hbm"))
+
+        def step():
+            parser.before_first()
+            b = parser.read_all()
+            local["rows"], local["bytes"] = b["size"], parser.partition_bytes
+            return b["size"], b["bytes"], 0, parser.partition_bytes
+    elif use_gpu:
+        extra = {"label_column": 0} if args.format == "csv" else {}
+        parser = data.GPUParser(ddir, rank, world, format=args.format, chunk_mb=args.chunk_mb,
                                 read_threads=read_threads, pinned_slots=args.pinned_slots,
                                 device_slots=args.device_slots, device=local_rank,
                                 zero_copy=args.zero_copy,
-                                hbm_cache=int(args.mode == "hbm"))
-        if args.mode == "hbm" and args.warmup < 1:
-            raise SystemExit("--mode hbm needs --warmup >= 1 (the warmup epoch fills the cache)")
+                                hbm_cache=int(args.mode == "hbm"), **extra)
         csr = data.DeviceCSR()
 
         def step():
@@ -201,9 +241,25 @@ def main():
             parser.parse_all(csr)
             local["rows"], local["bytes"] = csr.rows, parser.partition_bytes
             return csr.rows, csr.nnz, csr.max_index, parser.partition_bytes
-    else:
+    elif args.format == "recordio":
+        from dmlc_core_amd import io as dio
+
         def step():
-            p = data.Parser(ddir + "?format=libsvm", rank, world, "libsvm")
+            split = dio.InputSplit(ddir, rank, world, "recordio")
+            n = nbytes = 0
+            while True:
+                rec = split.next_record()
+                if rec is None:
+                    break
+                n += 1
+                nbytes += len(rec)
+            local["rows"], local["bytes"] = n, nbytes
+            return n, nbytes, 0, nbytes
+    else:
+        uri = ddir + f"?format={args.format}" + ("&label_column=0" if args.format == "csv" else "")
+
+        def step():
+            p = data.Parser(uri, rank, world, args.format)
             rows, nnz, _ = p.drain()
             local["rows"], local["bytes"] = rows, p.bytes_read()
             return rows, nnz, 0, p.bytes_read()
@@ -265,41 +321,45 @@ def main():
     (rows, nnz, nbytes), max_index = totals
     ms = elapsed / max(1, args.steps) * 1e3
     value = rows * args.steps / elapsed
+    fmt = FORMATS[args.format]
     if rank == 0:
+        ingest = ("HBM epoch cache (input resident in HBM after the warmup epoch)"
+                  if use_gpu and args.mode == "hbm" else
+                  "zero-copy mmap+hipHostRegister DMA" if use_gpu and parser.stats().get("zero_copy")
+                  else "parallel pread -> pinned ring -> hipMemcpyAsync" if use_gpu else "CPU")
         out = {
-            "metric": "parsed rows/sec (LibSVM->CSR in device memory), aggregate over GPUs",
+            "metric": fmt["metric"],
             "value": round(value, 1),
-            "unit": "rows/s",
+            "unit": "records/s" if args.format == "recordio" else "rows/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 3),
             "higher_is_better": True,
             "scaling": "strong",
-            "vs_baseline": round(value / BASELINE_ROWS_PER_SEC, 3),
-            "dtype": "fp32 values / u32 indices (text parse, no matmul)",
-            "data": "synthetic (deterministic LibSVM, 20-60 nnz/row, 16 part files)",
+            "vs_baseline": round(value / fmt["baseline"], 3),
+            "dtype": fmt["dtype"],
+            "data": f"synthetic (deterministic {args.format}, 16 part files)",
             "config": {
-                "model": "LibSVM tokenize -> device CSR RowBlock (synthetic 10M-row sparse file)",
+                "model": fmt["model"],
                 "global_batch": int(rows),
                 "seq_len": None,
                 "parallelism": f"dp{world} (InputSplit byte-range shards, RCCL NumCol all-reduce)",
+                "format": args.format,
                 "rows": int(rows),
-                "nnz": int(nnz),
+                "nnz" if args.format != "recordio" else "payload_bytes": int(nnz),
                 "num_col": max_index + 1,
                 "input_bytes": int(nbytes),
                 "chunk_mb": args.chunk_mb,
                 "read_threads": read_threads,
                 "device": "gpu" if use_gpu else "cpu",
                 "numa_node_rank0": numa.get("numa_node", -1),
-                "ingest": ("HBM epoch cache (text resident in HBM after the warmup epoch)"
-                           if use_gpu and args.mode == "hbm" else
-                           "zero-copy mmap+hipHostRegister DMA" if use_gpu and parser.stats().get("zero_copy")
-                           else "parallel pread -> pinned ring -> hipMemcpyAsync"),
+                "ingest": ingest,
             },
             "per_gpu_rows_per_sec": round(value / max(1, world), 1),
             "input_GBps": round(nbytes * args.steps / elapsed / 1e9, 3),
             "mode": args.mode,
+            "baseline_value": fmt["baseline"],
         }
         out["per_rank"] = per_rank
         if use_gpu:

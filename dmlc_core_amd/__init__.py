@@ -19,7 +19,9 @@ spawning its ranks) never maps ``libamdhip64`` -- only the ranks it starts do.
 from __future__ import annotations
 
 import importlib
+import importlib.abc
 import os
+import sys
 
 __version__ = "0.1.0"
 
@@ -42,6 +44,23 @@ def _load_native():
         raise ImportError(
             "dmlc_core_amd native extension is not built; run `make -j8` in the repo root "
             f"({err})") from err
+
+
+class _TorchBeforeNative(importlib.abc.MetaPathFinder):
+    """Whichever way the extension is imported (``from dmlc_core_amd._dmlc
+    import X`` bypasses the package ``__getattr__``), torch is loaded first."""
+
+    def find_spec(self, fullname, path, target=None):  # noqa: D401
+        if fullname == __name__ + "._dmlc" and "torch" not in sys.modules:
+            try:
+                import torch  # noqa: F401
+            except ImportError:  # pragma: no cover
+                pass
+        return None  # the regular finders load the module
+
+
+if not any(isinstance(f, _TorchBeforeNative) for f in sys.meta_path):
+    sys.meta_path.insert(0, _TorchBeforeNative())
 
 
 def __getattr__(name):

@@ -34,7 +34,11 @@ class GPURecordIO:
     >>> t = r.to_torch(batch)           # {"offset": int64? u64 tensor, "data": u8 tensor}
 
     Streaming: ``for offsets, data in r.iter_host(): ...`` (one chunk at a time).
-    Config keys (also ``?k=v`` on the uri): chunk_mb, chunk_bytes, device, zero_copy.
+    Config keys (also ``?k=v`` on the uri): chunk_mb, chunk_bytes, device,
+    zero_copy, device_slots, pinned_slots, hbm_cache (epochs after the first
+    decode from an HBM-resident copy), replay_chunk_mb, and for indexed
+    RecordIO ``index=<index file>``, ``shuffle``, ``seed`` -- the epoch order of
+    the CPU ``indexed_recordio`` InputSplit, gathered on the device.
     """
 
     def __init__(self, uri: str, part: int = 0, nparts: int = 1, **config):

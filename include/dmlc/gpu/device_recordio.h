@@ -27,13 +27,40 @@ namespace dmlc {
 namespace gpu {
 
 struct DeviceRecordIOConfig {
-  /*! \brief bytes per chunk (a record must fit in one chunk) */
+  /*! \brief bytes per chunk / batch (< 4 GiB; a record longer than this gets a chunk of its own) */
   size_t chunk_bytes{64UL << 20};
   /*! \brief HIP device (-1 = current) */
   int device{-1};
   /*! \brief -1 auto (mmap + hipHostRegister, fall back to pinned staging), 0 off, 1 required */
   int zero_copy{-1};
-  /*! \brief apply `?k=v` overrides: chunk_mb, chunk_bytes, device, zero_copy */
+  /*! \brief chunks in flight on the device (H2D of later chunks overlaps the decode) */
+  int device_slots{3};
+  /*! \brief pinned host slots of the reader thread (staging path) */
+  int pinned_slots{3};
+  /*!
+   * \brief keep the partition's bytes resident in HBM after the first epoch
+   *  and decode later epochs from there (adjacent chunks merged up to
+   *  replay_chunk_bytes)
+   */
+  bool hbm_cache{false};
+  size_t replay_chunk_bytes{1UL << 30};
+  /*!
+   * \brief indexed RecordIO (reference "indexed_recordio" InputSplit): the
+   *  index file ("key offset" lines); shards by record count; with shuffle,
+   *  every epoch visits the shard's records in the std::mt19937(111 + seed)
+   *  order of the CPU IndexedRecordIOSplitter.  The shard is read into HBM
+   *  once and each batch is gathered on the device (LaunchRecordIOGather).
+   */
+  std::string index_uri;
+  bool shuffle{false};
+  int seed{0};
+  /*! \brief busy-poll budget (us) of a metadata wait before sleeping (src/gpu/host_wait.h) */
+  double wait_spin_us{50};
+  /*!
+   * \brief apply `?k=v` overrides: chunk_mb, chunk_bytes, device, zero_copy,
+   *  device_slots, pinned_slots, hbm_cache, replay_chunk_mb, index, shuffle,
+   *  seed, wait_spin_us
+   */
   void Update(const std::map<std::string, std::string>& args);
 };
 
@@ -46,11 +73,16 @@ struct DeviceRecordBatch {
 };
 
 struct DeviceRecordIOStats {
+  /*! \brief input bytes decoded (records with their headers) */
   size_t bytes{0};
   size_t chunks{0};
   size_t records{0};
   bool zero_copy{false};
+  /*! \brief host seconds waiting for the reader thread / for device results */
+  double wait_reader_sec{0};
   double wait_gpu_sec{0};
+  /*! \brief chunks decoded from the HBM-resident copy (hbm_cache / indexed) */
+  size_t replayed_chunks{0};
 };
 
 class DeviceRecordIOReader {

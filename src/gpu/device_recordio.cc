@@ -2,19 +2,33 @@
  * \file src/gpu/device_recordio.cc
  * \brief DeviceRecordIOReader (see dmlc/gpu/device_recordio.h).
  *
- * Per chunk, in stream order:
- *   copy stream    : wait(parsed[d]) -> H2D(text[d]) -> record(copied[d])
- *   compute stream : wait(copied[d]) -> K7a count+scan -> [host: nrec]
- *                    -> K7b emit -> K7c lengths -> K3 scan -> [host: bytes, err]
- *                    -> K7d gather -> record(parsed[d])
- * The H2D of the next chunks is queued before the current chunk is decoded.
+ * Sources of device-resident chunks ("pieces"), all starting at a record head:
+ *  - sequential, zero-copy: mmap + hipHostRegister'ed partition cut at record
+ *    heads (ZeroCopySource), one H2D per piece;
+ *  - sequential, staging: a reader thread fills pinned slots with
+ *    RecordIOSplitter chunks (ThreadedIter), one H2D per slot;
+ *  - HBM replay (hbm_cache): the first epoch's pieces stay in an arena,
+ *    later epochs decode straight from it (adjacent pieces merged);
+ *  - indexed: the shard's bytes are read into HBM once; every batch is
+ *    gathered on the device from the epoch order of the CPU
+ *    IndexedRecordIOSplitter (shuffled with std::mt19937(111 + seed)).
+ * Per piece, in stream order (device_slots pieces in flight):
+ *   copy stream    : wait(parsed[d]) -> H2D / gather (piece d) -> record(copied[d])
+ *   compute stream : wait(copied[d]) -> R1 count -> C2 scan -> [host: sizes]
+ *                    -> R2 fill -> C4 finish -> [host: error bits] -> record(parsed[d])
+ * The two host waits poll a flag the publishing kernel raises in mapped
+ * pinned memory (spin, then short sleeps: host_wait.h), no stream
+ * synchronisation and no device-to-host copies.
  */
 #include <dmlc/fault.h>
 #include <dmlc/gpu/device_recordio.h>
 #include <dmlc/gpu/hip_utils.h>
 #include <dmlc/logging.h>
+#include <dmlc/threadediter.h>
 #include <dmlc/timer.h>
 
+#include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -24,6 +38,7 @@
 #include "../io/filesys.h"
 #include "../io/recordio_split.h"
 #include "../io/uri_spec.h"
+#include "./host_wait.h"
 #include "./kernels.h"
 #include "./zero_copy_source.h"
 
@@ -31,26 +46,71 @@ namespace dmlc {
 namespace gpu {
 
 void DeviceRecordIOConfig::Update(const std::map<std::string, std::string>& args) {
+  auto mb = [](const std::string& v) { return static_cast<size_t>(std::atof(v.c_str()) * (1 << 20)); };
+  auto flag = [](const std::string& v) { return v != "0" && v != "false" && !v.empty(); };
   for (const auto& kv : args) {
-    if (kv.first == "chunk_mb") {
-      chunk_bytes = static_cast<size_t>(std::atof(kv.second.c_str()) * (1 << 20));
-    } else if (kv.first == "chunk_bytes") {
-      chunk_bytes = std::strtoull(kv.second.c_str(), nullptr, 10);
-    } else if (kv.first == "device") {
-      device = std::atoi(kv.second.c_str());
-    } else if (kv.first == "zero_copy") {
-      const std::string& v = kv.second;
-      zero_copy = (v == "auto" || v == "-1") ? -1 : ((v == "0" || v == "false") ? 0 : 1);
+    const std::string& k = kv.first;
+    const std::string& v = kv.second;
+    if (k == "chunk_mb") {
+      chunk_bytes = mb(v);
+    } else if (k == "chunk_bytes") {
+      chunk_bytes = std::strtoull(v.c_str(), nullptr, 10);
+    } else if (k == "device") {
+      device = std::atoi(v.c_str());
+    } else if (k == "zero_copy") {
+      zero_copy = (v == "auto" || v == "-1") ? -1 : (flag(v) ? 1 : 0);
+    } else if (k == "device_slots") {
+      device_slots = std::atoi(v.c_str());
+    } else if (k == "pinned_slots") {
+      pinned_slots = std::atoi(v.c_str());
+    } else if (k == "hbm_cache") {
+      hbm_cache = flag(v);
+    } else if (k == "replay_chunk_mb") {
+      replay_chunk_bytes = mb(v);
+    } else if (k == "index") {
+      index_uri = v;
+    } else if (k == "shuffle") {
+      shuffle = flag(v);
+    } else if (k == "seed") {
+      seed = std::atoi(v.c_str());
+    } else if (k == "wait_spin_us") {
+      wait_spin_us = std::atof(v.c_str());
     }
   }
   chunk_bytes = (chunk_bytes + 4095) & ~size_t(4095);
   CHECK_GE(chunk_bytes, 4096U);
-  CHECK_LT(chunk_bytes, size_t(1) << 34) << "chunk_bytes must be < 16 GiB (u32 word positions)";
+  // per-chunk output bytes and record counts are scanned as 32-bit halves
+  CHECK_LT(chunk_bytes, size_t(1) << 32) << "chunk_bytes must be < 4 GiB";
+  CHECK_LT(replay_chunk_bytes, size_t(1) << 32) << "replay_chunk_bytes must be < 4 GiB";
+  CHECK_GE(device_slots, 1);
+  CHECK_GE(pinned_slots, 1);
 }
 
 namespace {
 
-constexpr int kSlots = 2;
+/*! \brief a chunk read by the reader thread into pinned memory */
+struct HostSlot {
+  PinnedBuffer buf;
+  size_t size{0};
+};
+
+/*! \brief a device slot: a chunk's bytes (or the extents of a gathered batch) */
+struct DevSlot {
+  DeviceBuffer text;
+  Event copied, parsed;
+  bool used{false};
+  // indexed batches: extents in pinned memory and on the device
+  PinnedBuffer h_ext;
+  DeviceBuffer d_ext;
+};
+
+/*! \brief a device-resident chunk ready to decode once `slot`'s copy is done */
+struct Piece {
+  const uint32_t* words;
+  size_t bytes;
+  int slot;          // device slot (-1: HBM arena)
+  HostSlot* host;    // pinned slot to recycle after the copy (staging path)
+};
 
 class DeviceRecordIOImpl : public DeviceRecordIOReader {
  public:
@@ -59,47 +119,71 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
       : cfg_(cfg) {
     if (cfg_.device >= 0) SetDevice(cfg_.device);
     io::URI path(uri.c_str());
-    split_.reset(new io::RecordIOSplitter(io::FileSystem::GetInstance(path), uri.c_str(), part,
-                                          nparts));
+    io::FileSystem* fs = io::FileSystem::GetInstance(path);
+    for (int d = 0; d < cfg_.device_slots; ++d) slots_.emplace_back(new DevSlot());
+    hmap_.Reserve(sizeof(ChunkMeta), /*mapped=*/true);
+    std::memset(hmap_.get(), 0, sizeof(ChunkMeta));
+    meta_.Reserve(sizeof(ChunkMeta));
+    if (!cfg_.index_uri.empty()) {
+      indexed_.reset(new io::IndexedRecordIOSplitter(fs, uri.c_str(), cfg_.index_uri.c_str(), part,
+                                                     nparts, 1, cfg_.shuffle, cfg_.seed));
+      return;
+    }
+    split_.reset(new io::RecordIOSplitter(fs, uri.c_str(), part, nparts));
     if (cfg_.zero_copy != 0) {
       zc_.reset(new ZeroCopySource(ZeroCopySource::Cut::kRecordIO));
-      zc_->SetDrain([this]() { (void)hipStreamSynchronize(copy_.get()); });
+      zc_->SetDrain([this]() { copy_.Synchronize(); });
       if (!zc_->Init(split_.get(), cfg_.chunk_bytes)) {
         CHECK_NE(cfg_.zero_copy, 1) << "zero_copy=1 but mmap/hipHostRegister failed";
         zc_.reset();
       }
     }
     stats_.zero_copy = zc_ != nullptr;
-    if (zc_ == nullptr) split_->HintChunkSize(cfg_.chunk_bytes);
-    for (int d = 0; d < kSlots; ++d) {
-      slots_[d].text.Reserve(cfg_.chunk_bytes + 16);
-      if (zc_ == nullptr) slots_[d].staging.Reserve(cfg_.chunk_bytes + 16);
-    }
-    host_.Reserve(4 * sizeof(uint64_t));
-    scratch_.Reserve(3 * sizeof(uint64_t));
+    if (zc_ == nullptr) StartReader();
+    if (cfg_.hbm_cache) caching_ = true;
   }
+
   ~DeviceRecordIOImpl() override {
     (void)hipStreamSynchronize(copy_.get());
     (void)hipStreamSynchronize(compute_.get());
+    for (auto& p : ready_) {
+      if (p.host != nullptr) iter_.Recycle(&p.host);
+    }
+    ready_.clear();
+    iter_.Destroy();
   }
 
   void BeforeFirst() override {
-    DrainInflight();
+    Drain();
+    exhausted_ = false;
+    resident_rows_ = resident_bytes_ = 0;
+    if (indexed_ != nullptr) {
+      indexed_->BeforeFirst();  // the next epoch's order (re-shuffled)
+      epoch_pos_ = 0;
+      return;
+    }
+    if (cache_complete_) {
+      replay_ = true;
+      replay_idx_ = 0;
+      return;
+    }
+    // a partial first pass cannot complete the cache: start it over
+    if (cfg_.hbm_cache) {
+      cached_.clear();
+      arena_fill_ = 0;
+      caching_ = true;
+    }
     if (zc_ != nullptr) {
       zc_->Reset();
     } else {
-      split_->BeforeFirst();
+      iter_.BeforeFirst();
     }
-    exhausted_ = false;
-    resident_rows_ = resident_bytes_ = 0;
   }
 
   bool Next() override {
-    FillPipeline();
-    if (inflight_.empty()) return false;
-    const int d = inflight_.front();
-    inflight_.pop_front();
-    ProcessOne(d, false);
+    Piece p;
+    if (!NextPiece(&p)) return false;
+    Decode(p, false);
     return true;
   }
   const DeviceRecordBatch& Value() const override { return batch_; }
@@ -108,14 +192,9 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
     resident_rows_ = resident_bytes_ = 0;
     res_off_.Grow(sizeof(uint64_t), 0, compute_.get());
     DMLC_HIP_CHECK(hipMemsetAsync(res_off_.get<uint64_t>(), 0, sizeof(uint64_t), compute_.get()));
-    for (;;) {
-      FillPipeline();
-      if (inflight_.empty()) break;
-      const int d = inflight_.front();
-      inflight_.pop_front();
-      ProcessOne(d, true);
-    }
-    DMLC_HIP_CHECK(hipStreamSynchronize(compute_.get()));
+    Piece p;
+    while (NextPiece(&p)) Decode(p, true);
+    compute_.Synchronize();
     resident_.size = resident_rows_;
     resident_.bytes = resident_bytes_;
     resident_.offset = res_off_.get<uint64_t>();
@@ -124,6 +203,7 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
   }
 
   size_t PartitionBytes() const override {
+    if (indexed_ != nullptr) return IndexedBytes();
     if (zc_ != nullptr) return zc_->PartitionBytes();
     return split_->offset_end() - split_->offset_begin();
   }
@@ -131,134 +211,274 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
   hipStream_t stream() const override { return compute_.get(); }
 
  private:
-  struct Slot {
-    DeviceBuffer text;
-    PinnedBuffer staging;
-    Event copied, parsed;
-    size_t size{0};
-    bool used{false};
-  };
+  // ------------------------------------------------------------ sources
+  void StartReader() {
+    const size_t cap = cfg_.chunk_bytes;
+    io::RecordIOSplitter* split = split_.get();
+    split->HintChunkSize(cap);
+    iter_.set_max_capacity(static_cast<size_t>(cfg_.pinned_slots));
+    iter_.Init(
+        [split, cap](HostSlot** dptr) {
+          InputSplit::Blob blob;
+          if (!split->NextChunk(&blob)) return false;
+          if (*dptr == nullptr) *dptr = new HostSlot();
+          HostSlot* s = *dptr;
+          s->buf.Reserve(std::max(cap, blob.size) + 16);  // grows for a record longer than cap
+          std::memcpy(s->buf.get<char>(), blob.dptr, blob.size);
+          s->size = blob.size;
+          return true;
+        },
+        [split]() { split->BeforeFirst(); });
+  }
 
-  /*! \brief queue H2D copies of the next chunks into free device slots */
+  size_t IndexedBytes() const {
+    const size_t n = indexed_->NumRecords();
+    if (n == 0) return 0;
+    const size_t first = indexed_->FirstRecord();
+    const auto& last = indexed_->Record(first + n - 1);
+    return last.first + last.second - indexed_->Record(first).first;
+  }
+
+  /*! \brief the shard's bytes into HBM (once): records at arena + (offset - base) */
+  void LoadIndexedArena() {
+    if (arena_loaded_) return;
+    const size_t total = IndexedBytes();
+    const size_t base = indexed_->NumRecords() ? indexed_->Record(indexed_->FirstRecord()).first : 0;
+    arena_.Reserve(total + 16);
+    PinnedBuffer stage(std::min<size_t>(std::max<size_t>(total, 1), 64UL << 20));
+    for (size_t off = 0; off < total;) {
+      const size_t n = std::min(stage.bytes(), total - off);
+      indexed_->ReadBytes(base + off, n, stage.get<char>());
+      DMLC_HIP_CHECK(hipMemcpyAsync(arena_.get<char>() + off, stage.get(), n, hipMemcpyHostToDevice,
+                                    copy_.get()));
+      copy_.Synchronize();  // the stage is reused
+      off += n;
+    }
+    arena_base_ = base;
+    arena_loaded_ = true;
+  }
+
+  DevSlot& TakeSlot(int* d) {
+    *d = next_slot_;
+    next_slot_ = (next_slot_ + 1) % cfg_.device_slots;
+    return *slots_[*d];
+  }
+
+  /*! \brief the device slot `s` must hold `bytes` (+ pad); waits until no stream uses it */
+  void FitSlot(DevSlot* s, size_t bytes) {
+    if (bytes + 16 <= s->text.bytes()) return;
+    if (s->used) s->parsed.Synchronize();
+    s->text.Reserve(bytes + 16);
+  }
+
+  /*! \brief queue the next pieces until device_slots are in flight */
   void FillPipeline() {
-    while (!exhausted_ && static_cast<int>(inflight_.size()) < kSlots) {
+    while (!exhausted_ && static_cast<int>(ready_.size()) + busy_ < cfg_.device_slots) {
       DMLC_FAULT_POINT("recordio");
-      const int d = next_slot_;
-      Slot& s = slots_[d];
-      const char* src = nullptr;
-      size_t n = 0;
-      if (zc_ != nullptr) {
-        ZeroCopySource::Piece piece;
-        if (!zc_->Next(&piece)) {
-          exhausted_ = true;
-          break;
+      Piece p{nullptr, 0, -1, nullptr};
+      if (!(indexed_ != nullptr ? GatherBatch(&p) : (replay_ ? ReplayPiece(&p) : ReadPiece(&p)))) {
+        exhausted_ = true;
+        if (caching_) {
+          caching_ = false;
+          cache_complete_ = true;
         }
-        src = piece.ptr;
-        n = piece.size;
-      } else {
-        InputSplit::Blob blob;
-        if (!split_->NextChunk(&blob)) {
-          exhausted_ = true;
-          break;
-        }
-        if (blob.size + 16 > s.text.bytes() || blob.size + 16 > s.staging.bytes()) {
-          // the split's chunks can exceed the hint: grow this slot once both
-          // streams no longer touch it
-          DMLC_HIP_CHECK(hipStreamSynchronize(copy_.get()));
-          DMLC_HIP_CHECK(hipStreamSynchronize(compute_.get()));
-          s.text.Reserve(blob.size + 16);
-          s.staging.Reserve(blob.size + 16);
-        }
-        if (s.used) s.copied.Synchronize();  // staging[d] free again
-        std::memcpy(s.staging.get<char>(), blob.dptr, blob.size);
-        src = s.staging.get<char>();
-        n = blob.size;
+        break;
       }
-      CHECK_EQ(n % 4, 0U) << "RecordIO chunk not 4-byte aligned";
-      if (n + 16 > s.text.bytes()) {
-        // a zero-copy piece holding one record longer than chunk_bytes
-        DMLC_HIP_CHECK(hipStreamSynchronize(copy_.get()));
-        DMLC_HIP_CHECK(hipStreamSynchronize(compute_.get()));
-        s.text.Reserve(n + 16);
-      }
-      if (s.used) DMLC_HIP_CHECK(hipStreamWaitEvent(copy_.get(), s.parsed.get(), 0));
-      DMLC_HIP_CHECK(hipMemcpyAsync(s.text.get<char>(), src, n, hipMemcpyHostToDevice, copy_.get()));
-      s.copied.Record(copy_.get());
-      s.size = n;
-      s.used = true;
-      inflight_.push_back(d);
-      next_slot_ = (next_slot_ + 1) % kSlots;
-      stats_.bytes += n;
+      ready_.push_back(p);
     }
   }
 
-  void DrainInflight() {
-    inflight_.clear();
-    DMLC_HIP_CHECK(hipStreamSynchronize(copy_.get()));
-    DMLC_HIP_CHECK(hipStreamSynchronize(compute_.get()));
+  bool ReadPiece(Piece* p) {
+    const char* src = nullptr;
+    size_t n = 0;
+    HostSlot* host = nullptr;
+    if (zc_ != nullptr) {
+      ZeroCopySource::Piece zp;
+      if (!zc_->Next(&zp)) return false;
+      src = zp.ptr;
+      n = zp.size;
+    } else {
+      const double t0 = GetTime();
+      if (!iter_.Next(&host)) return false;
+      stats_.wait_reader_sec += GetTime() - t0;
+      src = host->buf.get<char>();
+      n = host->size;
+    }
+    CHECK_EQ(n % 4, 0U) << "RecordIO chunk not 4-byte aligned";
+    int d;
+    DevSlot& s = TakeSlot(&d);
+    char* dst;
+    if (caching_) {
+      // first pass of an hbm_cache epoch: the chunk lands in its arena place
+      if (arena_.bytes() == 0) arena_.Reserve(PartitionBytes() + 16);
+      CHECK_LE(arena_fill_ + n, PartitionBytes()) << "RecordIO HBM cache overflow";
+      dst = arena_.get<char>() + arena_fill_;
+      cached_.push_back({arena_fill_, n});
+      arena_fill_ += n;
+    } else {
+      FitSlot(&s, n);
+      dst = s.text.get<char>();
+    }
+    if (s.used) DMLC_HIP_CHECK(hipStreamWaitEvent(copy_.get(), s.parsed.get(), 0));
+    DMLC_HIP_CHECK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, copy_.get()));
+    s.copied.Record(copy_.get());
+    s.used = true;
+    *p = Piece{reinterpret_cast<const uint32_t*>(dst), n, d, host};
+    return true;
   }
 
-  void SyncCompute() {
-    double t0 = GetTime();
-    DMLC_HIP_CHECK(hipStreamSynchronize(compute_.get()));
+  bool ReplayPiece(Piece* p) {
+    if (replay_idx_ >= cached_.size()) return false;
+    size_t off = cached_[replay_idx_].first, n = cached_[replay_idx_].second;
+    ++replay_idx_;
+    // adjacent cached chunks decode as one (fewer launches and host waits)
+    while (replay_idx_ < cached_.size() && cached_[replay_idx_].first == off + n &&
+           n + cached_[replay_idx_].second <= cfg_.replay_chunk_bytes) {
+      n += cached_[replay_idx_++].second;
+    }
+    *p = Piece{reinterpret_cast<const uint32_t*>(arena_.get<char>() + off), n, -1, nullptr};
+    stats_.replayed_chunks += 1;
+    return true;
+  }
+
+  /*! \brief the next batch of the epoch order, gathered from the HBM shard into a slot */
+  bool GatherBatch(Piece* p) {
+    const size_t nrec = indexed_->NumRecords();
+    if (epoch_pos_ >= nrec) return false;
+    LoadIndexedArena();
+    // records of the epoch order until the batch holds chunk_bytes (at least one)
+    std::vector<uint64_t>& so = tmp_src_;
+    std::vector<uint32_t>& ln = tmp_len_;
+    std::vector<uint64_t>& dof = tmp_dst_;
+    so.clear();
+    ln.clear();
+    dof.clear();
+    size_t total = 0;
+    while (epoch_pos_ < nrec) {
+      const auto& r = indexed_->Record(indexed_->EpochRecord(epoch_pos_));
+      if (!so.empty() && total + r.second > cfg_.chunk_bytes) break;
+      CHECK_EQ(r.second % 4, 0U) << "indexed RecordIO: record size not a multiple of 4";
+      so.push_back(r.first - arena_base_);
+      ln.push_back(static_cast<uint32_t>(r.second));
+      dof.push_back(total);
+      total += r.second;
+      ++epoch_pos_;
+    }
+    const size_t k = so.size();
+    int d;
+    DevSlot& s = TakeSlot(&d);
+    FitSlot(&s, total);
+    const size_t ext_bytes = k * (2 * sizeof(uint64_t) + sizeof(uint32_t));
+    if (s.used) s.copied.Synchronize();  // the previous extents of this slot were consumed
+    s.h_ext.Reserve(ext_bytes);
+    s.d_ext.Reserve(ext_bytes);
+    char* h = s.h_ext.get<char>();
+    std::memcpy(h, so.data(), k * 8);
+    std::memcpy(h + k * 8, dof.data(), k * 8);
+    std::memcpy(h + k * 16, ln.data(), k * 4);
+    if (s.used) DMLC_HIP_CHECK(hipStreamWaitEvent(copy_.get(), s.parsed.get(), 0));
+    DMLC_HIP_CHECK(hipMemcpyAsync(s.d_ext.get(), h, ext_bytes, hipMemcpyHostToDevice, copy_.get()));
+    const char* dx = s.d_ext.get<char>();
+    LaunchRecordIOGather(arena_.get<uint8_t>(), reinterpret_cast<const uint64_t*>(dx),
+                         reinterpret_cast<const uint32_t*>(dx + k * 16),
+                         reinterpret_cast<const uint64_t*>(dx + k * 8), k, s.text.get<uint8_t>(),
+                         copy_.get());
+    s.copied.Record(copy_.get());
+    s.used = true;
+    *p = Piece{s.text.get<uint32_t>(), total, d, nullptr};
+    stats_.replayed_chunks += 1;
+    return true;
+  }
+
+  bool NextPiece(Piece* p) {
+    FillPipeline();
+    if (ready_.empty()) return false;
+    *p = ready_.front();
+    ready_.pop_front();
+    return true;
+  }
+
+  void Drain() {
+    copy_.Synchronize();
+    compute_.Synchronize();
+    for (auto& p : ready_) {
+      if (p.host != nullptr) iter_.Recycle(&p.host);
+    }
+    ready_.clear();
+    busy_ = 0;
+  }
+
+  // ------------------------------------------------------------ decode
+  ChunkMeta WaitMeta() {
+    const double t0 = GetTime();
+    ChunkMeta* hm = hmap_.get<ChunkMeta>();
+    volatile unsigned* flag = &hm->pad;
+    if (!WaitHostFlag(flag, cfg_.wait_spin_us, 0.05, &waits_)) compute_.Synchronize();
+    std::atomic_thread_fence(std::memory_order_acquire);
+    ChunkMeta m;
+    std::memcpy(&m, const_cast<const ChunkMeta*>(hm), sizeof(m));
+    *flag = 0;  // re-armed before the next publishing kernel
     stats_.wait_gpu_sec += GetTime() - t0;
+    return m;
   }
 
-  void ProcessOne(int d, bool resident) {
-    Slot& s = slots_[d];
-    hipStream_t st = compute_.get();
-    DMLC_HIP_CHECK(hipStreamWaitEvent(st, s.copied.get(), 0));
-    const uint32_t* words = s.text.get<uint32_t>();
-    const size_t nwords = s.size / 4;
-    const size_t tiles = RecordIOTiles(nwords);
-    tiles_.Reserve((tiles + 1) * sizeof(uint64_t));
-    partials_.Reserve((ScanPartials(std::max<size_t>(tiles, 1)) + 1) * sizeof(uint64_t));
-    uint64_t* dev = scratch_.get<uint64_t>();  // [0] nrec, [1] err
-    DMLC_HIP_CHECK(hipMemsetAsync(dev, 0, 2 * sizeof(uint64_t), st));
-    LaunchRecordIOCount(words, nwords, tiles_.get<uint64_t>(), partials_.get<uint64_t>(), dev, st);
-    DMLC_HIP_CHECK(hipMemcpyAsync(host_.get<uint64_t>(), dev, sizeof(uint64_t),
-                                  hipMemcpyDeviceToHost, st));
-    SyncCompute();
-    const size_t nrec = host_.get<uint64_t>()[0];
-    head_.Reserve(std::max<size_t>(nrec, 1) * sizeof(uint32_t));
-    len_.Reserve((nrec + 1) * sizeof(uint64_t));
-    partials_.Reserve((ScanPartials(std::max<size_t>(nrec, 1)) + 1) * sizeof(uint64_t));
-    uint64_t* rec_len = len_.get<uint64_t>();
-    uint32_t* err = reinterpret_cast<uint32_t*>(dev + 1);
-    LaunchRecordIOEmit(words, nwords, tiles_.get<uint64_t>(), head_.get<uint32_t>(), st);
-    LaunchRecordIOLengths(words, nwords, head_.get<uint32_t>(), nrec, rec_len, err, st);
-    if (nrec > 0) {
-      LaunchScanU64(rec_len, nrec, partials_.get<uint64_t>(), rec_len + nrec, st);
-    } else {
-      DMLC_HIP_CHECK(hipMemsetAsync(rec_len, 0, sizeof(uint64_t), st));
-    }
-    DMLC_HIP_CHECK(hipMemcpyAsync(host_.get<uint64_t>() + 1, rec_len + nrec, sizeof(uint64_t),
-                                  hipMemcpyDeviceToHost, st));
-    DMLC_HIP_CHECK(hipMemcpyAsync(host_.get<uint64_t>() + 2, dev + 1, sizeof(uint64_t),
-                                  hipMemcpyDeviceToHost, st));
-    SyncCompute();
-    const size_t bytes = host_.get<uint64_t>()[1];
-    const uint32_t e = static_cast<uint32_t>(host_.get<uint64_t>()[2]);
+  static void CheckErrors(unsigned e) {
     CHECK_EQ(e & kRecErrTruncated, 0U) << "RecordIO: a record runs past its chunk (corrupt file?)";
-    CHECK_EQ(e & kRecErrBadPart, 0U) << "RecordIO: malformed multi-part record";
-    if (!resident) {
-      out_.Reserve(std::max<size_t>(bytes, 1));
-      LaunchRecordIOGather(words, nwords, head_.get<uint32_t>(), nrec, rec_len, out_.get<uint8_t>(),
-                           st);
-      batch_.size = nrec;
-      batch_.bytes = bytes;
-      batch_.offset = rec_len;
-      batch_.data = out_.get<uint8_t>();
+    CHECK_EQ(e & kRecErrBadPart, 0U) << "RecordIO: malformed record (bad multi-part chain or header)";
+  }
+
+  void Decode(Piece p, bool resident) {
+    ScopedRange range("recordio_chunk");
+    busy_ = 1;
+    hipStream_t st = compute_.get();
+    if (p.slot >= 0) DMLC_HIP_CHECK(hipStreamWaitEvent(st, slots_[p.slot]->copied.get(), 0));
+    const size_t nwords = p.bytes / 4;
+    const size_t tiles = RecordIOTiles(nwords);
+    tcounts_.Reserve(TileScratchWords(tiles) * sizeof(uint64_t));
+    tflags_.Reserve(TileScratchWords(tiles) * sizeof(uint32_t));
+    partials_.Reserve(TileScratchSlots(tiles) * sizeof(MetaPartial));
+    ChunkMeta* dmeta = meta_.get<ChunkMeta>();
+    ChunkMeta* hm = hmap_.get<ChunkMeta>();
+    LaunchRecordIOTileCount(p.words, nwords, tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(), st);
+    LaunchTileScanRaw(tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(), tiles, dmeta, hm, st);
+    const ChunkMeta sizes = WaitMeta();
+    // the copy of this piece is complete: its pinned slot goes back to the reader
+    if (p.host != nullptr) iter_.Recycle(&p.host);
+    FillPipeline();  // keep PCIe busy while this piece decodes
+    CheckErrors(sizes.flags);
+    const size_t nrec = sizes.nrows, nbytes = sizes.nnz;
+    uint64_t* off;
+    uint8_t* dat;
+    uint64_t rec_base = 0, byte_base = 0;
+    if (resident) {
+      GrowResident(nrec, nbytes);
+      off = res_off_.get<uint64_t>();
+      dat = res_data_.get<uint8_t>();
+      rec_base = resident_rows_;
+      byte_base = resident_bytes_;
     } else {
-      GrowResident(nrec, bytes);
-      LaunchOffsetRebase(rec_len, nrec, 0, resident_bytes_,
-                         res_off_.get<uint64_t>() + resident_rows_, st);
-      LaunchRecordIOGather(words, nwords, head_.get<uint32_t>(), nrec, rec_len,
-                           res_data_.get<uint8_t>() + resident_bytes_, st);
-      resident_rows_ += nrec;
-      resident_bytes_ += bytes;
+      out_off_.Reserve((nrec + 1) * sizeof(uint64_t));
+      out_data_.Reserve(std::max<size_t>(nbytes, 1));
+      off = out_off_.get<uint64_t>();
+      dat = out_data_.get<uint8_t>();
     }
-    s.parsed.Record(st);
+    LaunchRecordIOTileFill(p.words, nwords, tcounts_.get<uint64_t>(), off, rec_base, dat, byte_base,
+                           partials_.get<MetaPartial>(), st);
+    LaunchTileFinish(partials_.get<MetaPartial>(), tiles, dmeta, hm, off, rec_base, byte_base, st);
+    const ChunkMeta done = WaitMeta();
+    if (p.slot >= 0) slots_[p.slot]->parsed.Record(st);
+    busy_ = 0;
+    CheckErrors(done.flags);
+    if (resident) {
+      resident_rows_ += nrec;
+      resident_bytes_ += nbytes;
+    } else {
+      batch_.size = nrec;
+      batch_.bytes = nbytes;
+      batch_.offset = off;
+      batch_.data = dat;
+    }
+    stats_.bytes += p.bytes;
     stats_.chunks += 1;
     stats_.records += nrec;
   }
@@ -266,8 +486,7 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
   void GrowResident(size_t nrec, size_t bytes) {
     const size_t need_off = (resident_rows_ + nrec + 1) * sizeof(uint64_t);
     if (need_off > res_off_.bytes()) {
-      res_off_.Grow(need_off + need_off / 2, (resident_rows_ + 1) * sizeof(uint64_t),
-                    compute_.get());
+      res_off_.Grow(need_off + need_off / 2, (resident_rows_ + 1) * sizeof(uint64_t), compute_.get());
     }
     const size_t need_data = resident_bytes_ + bytes;
     if (need_data > res_data_.bytes()) {
@@ -277,15 +496,27 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
 
   DeviceRecordIOConfig cfg_;
   std::unique_ptr<io::RecordIOSplitter> split_;
+  std::unique_ptr<io::IndexedRecordIOSplitter> indexed_;
   std::unique_ptr<ZeroCopySource> zc_;
+  ThreadedIter<HostSlot> iter_;
   Stream copy_, compute_;
-  Slot slots_[kSlots];
-  std::deque<int> inflight_;
+  std::vector<std::unique_ptr<DevSlot>> slots_;
+  std::deque<Piece> ready_;
   int next_slot_{0};
+  int busy_{0};
   bool exhausted_{false};
-  DeviceBuffer tiles_, partials_, head_, len_, out_, scratch_;
-  DeviceBuffer res_off_, res_data_;
-  PinnedBuffer host_;
+  // HBM arena: the hbm_cache copy (sequential) or the indexed shard
+  DeviceBuffer arena_;
+  size_t arena_fill_{0}, arena_base_{0}, replay_idx_{0}, epoch_pos_{0};
+  std::vector<std::pair<size_t, size_t>> cached_;
+  bool caching_{false}, cache_complete_{false}, replay_{false}, arena_loaded_{false};
+  std::vector<uint64_t> tmp_src_, tmp_dst_;
+  std::vector<uint32_t> tmp_len_;
+  // decode scratch and outputs
+  DeviceBuffer tcounts_, tflags_, partials_, meta_;
+  PinnedBuffer hmap_;
+  HostWaitStats waits_;
+  DeviceBuffer out_off_, out_data_, res_off_, res_data_;
   size_t resident_rows_{0}, resident_bytes_{0};
   DeviceRecordBatch batch_, resident_;
   DeviceRecordIOStats stats_;

@@ -8,7 +8,8 @@
  *   K3 offsets scan      LaunchScanU64            (scan_kernels.hip)
  *   K4 per-line fill     LaunchTextFill           (text_kernels.hip)
  *   K5 CSV / K6 LibFM    same launchers, TextFormat::kCSV / kLibFM
- *   K7 recordio decode   LaunchRecordIOIndex / LaunchRecordIOGather (recordio_kernels.hip)
+ *   K7 recordio decode   LaunchRecordIOTileCount / LaunchRecordIOTileFill, LaunchRecordIOGather
+ *                        (recordio_kernels.hip)
  *   K8 max reduce        fused into K4 (wave max + one atomicMax per wave)
  *   K9 fp8 pack / hash   LaunchHashedDenseFP8     (feature_kernels.hip)
  *   K10 csr concat       LaunchCSRAppend          (feature_kernels.hip)
@@ -194,36 +195,52 @@ void LaunchTileHashed(const char* text, size_t nbytes, TextFormat format,
                       uint32_t seed, bool fp8, void* out, float* labels, MetaPartial* partials,
                       ChunkMeta* meta, ChunkMeta* host_meta, hipStream_t stream);
 
+/*!
+ * \brief C2 alone over caller-filled per-tile u64 counts (hi 32 bits: items,
+ *  lo 32 bits: bytes): exclusive scan in place, meta->nrows = items,
+ *  meta->nnz = bytes, OR of tile_flags into meta->flags, published to
+ *  host_meta.  Scratch sizes as for LaunchTileCountScan (TileScratchWords).
+ */
+void LaunchTileScanRaw(uint64_t* tile_counts, uint32_t* tile_flags, size_t ntiles,
+                       ChunkMeta* meta, ChunkMeta* host_meta, hipStream_t stream);
+/*!
+ * \brief C4 alone: fold nslots MetaPartial slots into meta (max / or), write
+ *  offset[row_base + meta->nrows] = nnz_base + meta->nnz (offset may be null)
+ *  and publish meta to host_meta.  partials needs TileScratchSlots(nslots).
+ */
+void LaunchTileFinish(MetaPartial* partials, size_t nslots, ChunkMeta* meta, ChunkMeta* host_meta,
+                      uint64_t* offset, uint64_t row_base, uint64_t nnz_base, hipStream_t stream);
+
 // ----------------------------- RecordIO (K7) -----------------------------
 /*! \brief error bits reported by the RecordIO kernels */
 constexpr uint32_t kRecErrTruncated = 1;   // a part runs past the chunk end
 constexpr uint32_t kRecErrBadPart = 2;     // continuation part without its head
-/*! \brief u64 tile counters needed for `nwords` words */
+/*! \brief 2048-word tiles of a chunk of `nwords` words (scan scratch: TileScratchWords) */
 size_t RecordIOTiles(size_t nwords);
 /*!
- * \brief K7a: count record heads (aligned magic whose lrec has cflag 0/1) per
- *  4096-word tile and exclusive-scan the tile counts in place;
- *  *nrec receives the number of records.  partials >= ScanPartials(tiles)+1.
+ * \brief R1: per tile (record heads << 32 | output bytes) and error bits
+ *  (kRecErr*); scan them with LaunchTileScanRaw.  The chunk must start at a
+ *  record head and be < 4 GiB.
  */
-void LaunchRecordIOCount(const uint32_t* words, size_t nwords, uint64_t* tile_counts,
-                         uint64_t* partials, uint64_t* nrec, hipStream_t stream);
-/*! \brief K7b: compacted, ordered word positions of the record heads */
-void LaunchRecordIOEmit(const uint32_t* words, size_t nwords, const uint64_t* tile_counts,
-                        uint32_t* head_pos, hipStream_t stream);
+void LaunchRecordIOTileCount(const uint32_t* words, size_t nwords, uint64_t* tile_counts,
+                             uint32_t* tile_flags, hipStream_t stream);
 /*!
- * \brief K7c: payload bytes of every record, following multi-part chains
- *  (continuation parts add their length plus the re-inserted 4-byte magic);
- *  error bits are OR-ed into *err.
+ * \brief R2: decode every record of the chunk: record r (chunk-relative) gets
+ *  offset[rec_base + r] = byte_base + its output position and its payload
+ *  (multi-part records reassembled, escaped magic words re-inserted) at
+ *  data + that position.  tile_prefix: the scanned R1 counts; partials: one
+ *  MetaPartial per tile (error bits), folded by LaunchTileFinish, which also
+ *  writes the closing offset.
  */
-void LaunchRecordIOLengths(const uint32_t* words, size_t nwords, const uint32_t* head_pos,
-                           size_t nrec, uint64_t* rec_len, uint32_t* err, hipStream_t stream);
+void LaunchRecordIOTileFill(const uint32_t* words, size_t nwords, const uint64_t* tile_prefix,
+                            uint64_t* offset, uint64_t rec_base, uint8_t* data, uint64_t byte_base,
+                            MetaPartial* partials, hipStream_t stream);
 /*!
- * \brief K7d: gather payloads contiguously to out + rec_off[i] (exclusive
- *  scan of rec_len), re-inserting the escaped magic between parts.
+ * \brief R3: gather nrec whole records (src + src_off[k], len[k] bytes, 4-byte
+ *  multiples) to dst + dst_off[k]
  */
-void LaunchRecordIOGather(const uint32_t* words, size_t nwords, const uint32_t* head_pos,
-                          size_t nrec, const uint64_t* rec_off, uint8_t* out,
-                          hipStream_t stream);
+void LaunchRecordIOGather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len,
+                          const uint64_t* dst_off, size_t nrec, uint8_t* dst, hipStream_t stream);
 
 // --------------------------- features (K9-K11) ---------------------------
 /*!

@@ -242,7 +242,7 @@ constexpr int kScanPer = 8;
 __global__ __launch_bounds__(kScanThreads) void k_tile_scan(uint64_t* __restrict__ counts,
                                                             const uint32_t* __restrict__ flags,
                                                             size_t ntiles, ChunkMeta* meta,
-                                                            ChunkMeta* host_meta) {
+                                                            ChunkMeta* host_meta, int raw) {
   __shared__ uint64_t swave[kScanThreads / 64];
   __shared__ uint32_t sflag[kScanThreads / 64];
   const int wid = threadIdx.x / dev::kWave;
@@ -285,9 +285,10 @@ __global__ __launch_bounds__(kScanThreads) void k_tile_scan(uint64_t* __restrict
     uint32_t f = 0;
     for (int w = 0; w < kScanThreads / 64; ++w) f |= sflag[w];
     const uint64_t lines = carry >> 32, toks = carry & 0xffffffffull;
+    // text: (lines << 32 | tokens); raw (RecordIO): (records << 32 | bytes)
     meta->nlines = lines;
     meta->nrows = lines;
-    meta->nnz = toks - lines;
+    meta->nnz = raw ? toks : toks - lines;
     meta->max_index = 0;
     meta->max_field = 0;
     meta->flags = f;
@@ -1271,6 +1272,27 @@ void LaunchFinish(MetaPartial* partials, size_t ntiles, ChunkMeta* meta, ChunkMe
 
 size_t TileCount(size_t nbytes) { return (nbytes + kTileBytes - 1) / kTileBytes; }
 
+namespace {
+void TileScan(uint64_t* tile_counts, uint32_t* tile_flags, size_t ntiles, ChunkMeta* meta,
+              ChunkMeta* host_meta, int raw, hipStream_t stream) {
+  if (ntiles <= kTwoLevelTiles) {
+    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kScanThreads), 0, stream, tile_counts,
+                       tile_flags, ntiles, meta, host_meta, raw);
+    return;
+  }
+  // block totals / flags live past the tiles (TileScratchWords reserves them)
+  const size_t nblk = (ntiles + kScanBlockTiles - 1) / kScanBlockTiles;
+  uint64_t* bsum = tile_counts + ntiles;
+  uint32_t* bflag = tile_flags + ntiles;
+  hipLaunchKernelGGL(k_tile_scan_local, dim3(nblk), dim3(kScanThreads), 0, stream, tile_counts,
+                     tile_flags, ntiles, bsum, bflag);
+  hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kScanThreads), 0, stream, bsum, bflag, nblk, meta,
+                     host_meta, raw);
+  hipLaunchKernelGGL(k_tile_scan_add, dim3((ntiles + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                     stream, tile_counts, ntiles, bsum);
+}
+}  // namespace
+
 void LaunchTileCountScan(const char* text, size_t nbytes, uint64_t* tile_counts,
                          uint32_t* tile_flags, ChunkMeta* meta, ChunkMeta* host_meta,
                          hipStream_t stream) {
@@ -1281,21 +1303,17 @@ void LaunchTileCountScan(const char* text, size_t nbytes, uint64_t* tile_counts,
                        stream, reinterpret_cast<const uint8_t*>(text), nbytes, ntiles, tile_counts,
                        tile_flags);
   }
-  if (ntiles <= kTwoLevelTiles) {
-    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kScanThreads), 0, stream, tile_counts,
-                       tile_flags, ntiles, meta, host_meta);
-    return;
-  }
-  // block totals / flags live past the tiles (TileScratchWords reserves them)
-  const size_t nblk = (ntiles + kScanBlockTiles - 1) / kScanBlockTiles;
-  uint64_t* bsum = tile_counts + ntiles;
-  uint32_t* bflag = tile_flags + ntiles;
-  hipLaunchKernelGGL(k_tile_scan_local, dim3(nblk), dim3(kScanThreads), 0, stream, tile_counts,
-                     tile_flags, ntiles, bsum, bflag);
-  hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kScanThreads), 0, stream, bsum, bflag, nblk, meta,
-                     host_meta);
-  hipLaunchKernelGGL(k_tile_scan_add, dim3((ntiles + kThreads - 1) / kThreads), dim3(kThreads), 0,
-                     stream, tile_counts, ntiles, bsum);
+  TileScan(tile_counts, tile_flags, ntiles, meta, host_meta, 0, stream);
+}
+
+void LaunchTileScanRaw(uint64_t* tile_counts, uint32_t* tile_flags, size_t ntiles,
+                       ChunkMeta* meta, ChunkMeta* host_meta, hipStream_t stream) {
+  TileScan(tile_counts, tile_flags, ntiles, meta, host_meta, 1, stream);
+}
+
+void LaunchTileFinish(MetaPartial* partials, size_t nslots, ChunkMeta* meta, ChunkMeta* host_meta,
+                      uint64_t* offset, uint64_t row_base, uint64_t nnz_base, hipStream_t stream) {
+  LaunchFinish(partials, nslots, meta, host_meta, offset, row_base, nnz_base, stream);
 }
 
 size_t TileScratchWords(size_t ntiles) {

@@ -139,6 +139,30 @@ void IndexedRecordIOSplitter::BeforeFirst() {
   InputSplitBase::BeforeFirst();
 }
 
+void IndexedRecordIOSplitter::ReadBytes(size_t offset, size_t n, char* dst) {
+  size_t cur = offset, done = 0;
+  while (done < n) {
+    // the file holding byte `cur`, then as much of [cur, offset + n) as it has
+    const size_t fp = static_cast<size_t>(
+        std::upper_bound(file_offset_.begin(), file_offset_.end(), cur) - file_offset_.begin() - 1);
+    CHECK_LT(fp, files_.size()) << "RecordIO byte range beyond the data";
+    if (fs_ == nullptr || fp != file_ptr_) {
+      delete fs_;
+      file_ptr_ = fp;
+      fs_ = filesys_->OpenForRead(files_[fp].path);
+    }
+    fs_->Seek(cur - file_offset_[fp]);
+    const size_t can = std::min(n - done, file_offset_[fp + 1] - cur);
+    for (size_t got = 0; got < can;) {
+      const size_t k = fs_->Read(dst + done + got, can - got);
+      CHECK(k != 0) << "unexpected end of RecordIO file";
+      got += k;
+    }
+    done += can;
+    cur += can;
+  }
+}
+
 bool IndexedRecordIOSplitter::LoadRecords(Chunk* chunk, const std::vector<size_t>& ids) {
   size_t total = 0;
   for (size_t id : ids) total += index_[id].second;
@@ -146,38 +170,14 @@ bool IndexedRecordIOSplitter::LoadRecords(Chunk* chunk, const std::vector<size_t
   chunk->data.resize(total / sizeof(uint32_t) + 2);
   char* dst = reinterpret_cast<char*>(chunk->data.data());
   size_t pos = 0;
-  // coalesce consecutive records into one read
-  size_t i = 0;
-  while (i < ids.size()) {
+  // coalesce records that are adjacent in the file into one read
+  for (size_t i = 0; i < ids.size();) {
     size_t j = i + 1;
-    size_t off = index_[ids[i]].first, len = index_[ids[i]].second;
-    while (j < ids.size() && index_[ids[j]].first == off + len) {
-      len += index_[ids[j]].second;
-      ++j;
-    }
-    // locate the file and read [off, off+len), possibly across files
-    size_t remaining = len, cur = off;
-    while (remaining != 0) {
-      const size_t fp = static_cast<size_t>(
-          std::upper_bound(file_offset_.begin(), file_offset_.end(), cur) -
-          file_offset_.begin() - 1);
-      if (fs_ == nullptr || fp != file_ptr_) {
-        delete fs_;
-        file_ptr_ = fp;
-        fs_ = filesys_->OpenForRead(files_[fp].path);
-      }
-      fs_->Seek(cur - file_offset_[fp]);
-      const size_t can = std::min(remaining, file_offset_[fp + 1] - cur);
-      size_t got = 0;
-      while (got < can) {
-        const size_t n = fs_->Read(dst + pos + got, can - got);
-        CHECK(n != 0) << "unexpected end of RecordIO file";
-        got += n;
-      }
-      pos += can;
-      cur += can;
-      remaining -= can;
-    }
+    const size_t off = index_[ids[i]].first;
+    size_t len = index_[ids[i]].second;
+    while (j < ids.size() && index_[ids[j]].first == off + len) len += index_[ids[j++]].second;
+    ReadBytes(off, len, dst + pos);
+    pos += len;
     i = j;
   }
   chunk->begin = dst;

@@ -61,6 +61,20 @@ class IndexedRecordIOSplitter : public RecordIOSplitterBase {
   void SetBatchSize(size_t batch_size) { batch_size_ = batch_size; }
   /*! \brief number of records in this part */
   size_t NumRecords() const { return index_end_ - index_begin_; }
+  /*! \brief (file offset, size) of record i (global index, sorted by offset) */
+  const std::pair<size_t, size_t>& Record(size_t i) const { return index_[i]; }
+  /*! \brief global index of this part's first record */
+  size_t FirstRecord() const { return index_begin_; }
+  /*!
+   * \brief this epoch's k-th record (global index): the shuffled order drawn
+   *  by the last BeforeFirst, or the sequential one -- the order NextRecord /
+   *  NextChunk deliver (the GPU reader gathers batches in it)
+   */
+  size_t EpochRecord(size_t k) const {
+    return shuffle_ ? permutation_[k] : index_begin_ + k;
+  }
+  /*! \brief bytes [offset, offset + n) of the concatenated input files */
+  void ReadBytes(size_t offset, size_t n, char* dst);
 
  private:
   static const int kRandMagic = 111;

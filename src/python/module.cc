@@ -550,7 +550,9 @@ class PyDeviceRecordIO {
     d["chunks"] = s.chunks;
     d["records"] = s.records;
     d["zero_copy"] = s.zero_copy;
+    d["wait_reader_sec"] = s.wait_reader_sec;
     d["wait_gpu_sec"] = s.wait_gpu_sec;
+    d["replayed_chunks"] = s.replayed_chunks;
     return d;
   }
   uintptr_t Stream() const { return reinterpret_cast<uintptr_t>(reader_->stream()); }

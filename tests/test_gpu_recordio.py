@@ -97,3 +97,103 @@ def test_gpu_recordio_multi_file(tmp_path):
             r.read_all()
             got += io.split_records(*r.resident_to_host())
         assert got == allrecs
+
+
+def _write_indexed(path, idx, recs):
+    w = io.RecordIOWriter(str(path))
+    with open(idx, "w") as f:
+        for k, r in enumerate(recs):
+            f.write(f"{k}\t{w.tell()}\n")
+            w.write(r)
+    w.close()
+
+
+def _cpu_indexed_epochs(path, idx, part, nparts, shuffle, seed, epochs):
+    s = io.InputSplit(str(path), part, nparts, "indexed_recordio", index_uri=str(idx),
+                      shuffle=shuffle, seed=seed, batch_size=7)
+    out = []
+    for e in range(epochs):
+        if e:
+            s.before_first()
+        ep = []
+        while True:
+            r = s.next_record()
+            if r is None:
+                break
+            ep.append(r)
+        out.append(ep)
+    return out
+
+
+@pytest.mark.parametrize("shuffle", [False, True])
+def test_gpu_indexed_recordio_epoch_order_matches_cpu(tmp_path, shuffle):
+    """Shuffled epochs on the GPU (shard resident in HBM, batches gathered on
+    the device) visit records in exactly the CPU IndexedRecordIOSplitter's
+    mt19937(111 + seed) order, epoch after epoch."""
+    p, idx = tmp_path / "i.rec", tmp_path / "i.idx"
+    recs = _records(1500, 5, max_len=400)
+    _write_indexed(p, idx, recs)
+    for nparts in (1, 3):
+        for part in range(nparts):
+            cpu = _cpu_indexed_epochs(p, idx, part, nparts, shuffle, 7, 3)
+            r = io.GPURecordIO(str(p), part, nparts, index=str(idx), shuffle=int(shuffle), seed=7,
+                               chunk_bytes=32 * 1024)
+            for e in range(3):
+                if e:
+                    r.before_first()
+                r.read_all()
+                got = io.split_records(*r.resident_to_host())
+                assert got == cpu[e], (part, e)
+            if shuffle and len(cpu[0]) > 2:
+                assert cpu[0] != cpu[1]  # a new order every epoch
+            # streaming batches follow the same order
+            r.before_first()
+            streamed = []
+            for off, data in r.iter_host():
+                streamed += io.split_records(off, data)
+            assert streamed == cpu_next_epoch(p, idx, part, nparts, shuffle, 7, 4)
+
+
+def cpu_next_epoch(p, idx, part, nparts, shuffle, seed, epoch_count):
+    return _cpu_indexed_epochs(p, idx, part, nparts, shuffle, seed, epoch_count)[-1]
+
+
+@pytest.mark.parametrize("zero_copy", [0, 1])
+def test_gpu_recordio_hbm_cache_replay(tmp_path, zero_copy):
+    """hbm_cache: the first epoch leaves the shard resident; later epochs decode
+    from HBM (merged chunks) and equal the CPU reader."""
+    p = tmp_path / "h.rec"
+    recs = _records(2500, 9)
+    _write(p, recs)
+    r = io.GPURecordIO(str(p), 0, 1, chunk_bytes=16 * 1024, hbm_cache=1, zero_copy=zero_copy,
+                       device_slots=4)
+    for e in range(3):
+        if e:
+            r.before_first()
+        r.read_all()
+        assert io.split_records(*r.resident_to_host()) == recs, e
+    assert r.stats()["replayed_chunks"] > 0
+    # streaming from the cache too
+    r.before_first()
+    got = []
+    for off, data in r.iter_host():
+        got += io.split_records(off, data)
+    assert got == recs
+
+
+def test_gpu_recordio_rejects_corrupt_chain(tmp_path):
+    p = tmp_path / "c.rec"
+    recs = [b"x" * 40, bytes(MAGIC) * 3 + b"tail!", b"y" * 12]
+    _write(p, recs)
+    raw = bytearray(open(p, "rb").read())
+    # flip the cflag of the first continuation part to "whole record"
+    pos = raw.find(MAGIC, 48)
+    while pos >= 0 and ((int.from_bytes(raw[pos + 4:pos + 8], "little") >> 29) not in (2, 3)):
+        pos = raw.find(MAGIC, pos + 4)
+    assert pos > 0
+    lrec = int.from_bytes(raw[pos + 4:pos + 8], "little") & ((1 << 29) - 1)
+    raw[pos + 4:pos + 8] = lrec.to_bytes(4, "little")
+    open(p, "wb").write(bytes(raw))
+    r = io.GPURecordIO(str(p), zero_copy=0)
+    with pytest.raises(Exception, match="malformed record"):
+        r.read_all()
