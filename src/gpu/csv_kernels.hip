@@ -1,0 +1,447 @@
+/*!
+ * \file src/gpu/csv_kernels.hip
+ * \brief K5 fast path: CSV -> CSR on the tile pipeline (count -> two-level
+ *  scan -> fill -> finish, sizes via mapped pinned memory), lane per field.
+ *
+ * Reference loop: CSVParser::ParseBlock (`src/data/csv_parser.h:64-104`):
+ * every delimiter-separated field of a line is StrToFloat'ed after skipping
+ * leading blanks; the label (and weight) column leave the feature list and
+ * the remaining columns are numbered 0, 1, 2, ...; blank lines are no rows.
+ *
+ * A wave owns the rows that START in its 8 KiB tile and walks the text in
+ * 1 KiB steps, 16 bytes per lane, until the first row start of the next tile
+ * (at most 4 KiB past its own; longer rows send the chunk to the exact
+ * kernels).  Per step every lane turns its 16 bytes into field-start and
+ * row-start masks; a segmented wave scan (reset at row starts) gives every
+ * field its column, a packed wave scan its field / row / excluded-column
+ * ordinals.  The column tells what a field is (label, weight, feature
+ * `column - excluded columns before it`), the ordinals where it goes:
+ *   S1 k_csv_tile_count : (rows << 32 | entries) per tile + irregular flag,
+ *                         straight from global memory (no LDS);
+ *   C2 (tile_kernels.hip, raw scan), then
+ *   S2 k_csv_tile_fill  : the same walk over a two-step LDS ring (one step
+ *                         prefetched, so a number's 16-byte window never
+ *                         leaves LDS); the step's fields are listed in LDS and
+ *                         decoded 64 per round with the register-window
+ *                         decoder (token_decode.h; empty fields are 0, other
+ *                         shapes go through strtonum.h's StrToFloat from
+ *                         global memory); row starts write the row pointer,
+ *                         a row's last field settles a missing label / weight;
+ *   C4 (tile_kernels.hip) folds max index / flags and closes the offsets.
+ */
+#include <hip/hip_runtime.h>
+
+#include "../data/strtonum.h"
+#include "./device_common.h"
+#include "./kernels.h"
+#include "./token_decode.h"
+
+namespace dmlc {
+namespace gpu {
+namespace {
+
+using namespace dev;  // NOLINT(build/namespaces)
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+constexpr uint32_t kStep = 1024;
+constexpr uint32_t kExt = 4096;
+constexpr uint32_t kTileSteps = static_cast<uint32_t>(kTileBytes) / kStep;
+constexpr uint32_t kMaxSteps = (static_cast<uint32_t>(kTileBytes) + kExt) / kStep;
+constexpr uint32_t kListCap = 512;     // fields per step (avg field >= 2 bytes)
+constexpr uint32_t kRingVecs = 2 * kStep / 16 + 2;  // two steps + a mirror of slot 0's head
+
+struct CsvCfg {
+  int label_col;
+  int weight_col;   // -1, or a column other than label_col
+  int has_weight;   // weight_column >= 0 (every row gets a weight)
+  uint32_t delim;
+};
+
+/*! \brief 16-bit mask of the bytes of g equal to the byte in c4 (exact SWAR test) */
+__device__ __forceinline__ uint32_t eq16(uint4 g, uint32_t c4) {
+  auto z = [c4](uint32_t x) {
+    const uint32_t y = x ^ c4;
+    const uint32_t h = ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u;
+    return (((h >> 7) & 0x01010101u) * 0x01020408u) >> 24;  // byte k -> bit k
+  };
+  return z(g.x) | (z(g.y) << 4) | (z(g.z) << 8) | (z(g.w) << 12);
+}
+
+/*! \brief 16-bit mask of bytes < 0x20 other than \t \n \r */
+__device__ __forceinline__ uint32_t ctl16(uint4 g) {
+  auto z = [](uint32_t x) {
+    const uint32_t h = ~(((x & 0x7F7F7F7Fu) + 0x60606060u) | x) & 0x80808080u;
+    return (((h >> 7) & 0x01010101u) * 0x01020408u) >> 24;
+  };
+  const uint32_t lt20 = z(g.x) | (z(g.y) << 4) | (z(g.z) << 8) | (z(g.w) << 12);
+  return lt20 & ~(eq16(g, 0x09090909u) | eq16(g, 0x0A0A0A0Au) | eq16(g, 0x0D0D0D0Du));
+}
+
+/*! \brief 16 bytes of the chunk at pos, zero past its end (the buffer is 16-byte padded) */
+__device__ __forceinline__ uint4 load16_clip(const uint8_t* __restrict__ text, size_t pos, size_t n) {
+  const uint4 v = *reinterpret_cast<const uint4*>(text + (pos < n ? pos : 0));
+  const uint32_t keep = pos < n ? static_cast<uint32_t>(n - pos < 16 ? n - pos : 16) : 0u;
+  const uint64_t m_lo = keep >= 8 ? ~0ull : ((1ull << (8 * keep)) - 1ull);
+  const uint64_t m_hi = keep >= 16 ? ~0ull : (keep <= 8 ? 0ull : ((1ull << (8 * (keep - 8))) - 1ull));
+  return make_uint4(v.x & static_cast<uint32_t>(m_lo), v.y & static_cast<uint32_t>(m_lo >> 32),
+                    v.z & static_cast<uint32_t>(m_hi), v.w & static_cast<uint32_t>(m_hi >> 32));
+}
+
+/*! \brief wave-uniform state of a tile walk */
+struct Walk {
+  uint32_t carry_eol, carry_delim;  // last byte of the previous step
+  uint32_t col_carry;               // fields since the last row start
+  uint32_t rows, fields, excl;      // owned so far
+  bool started, done, bad;
+};
+
+/*! \brief one lane's 16 bytes of a step after the wave scans */
+struct Slice {
+  uint32_t fm, lm;  // owned field starts / row starts (bit k = byte k)
+  uint32_t col0;    // column of the first field when no row start precedes it in the slice
+  uint64_t before;  // packed fields | rows << 21 | excluded << 42 of the earlier lanes
+  uint64_t total;   // the same for the whole step
+};
+
+__device__ __forceinline__ bool excluded(uint32_t col, const CsvCfg& cfg) {
+  return static_cast<int>(col) == cfg.label_col || static_cast<int>(col) == cfg.weight_col;
+}
+
+/*!
+ * \brief masks, ownership and scans of step `s` (g: the lane's 16 bytes at
+ *  tile offset s * kStep + 16 * lane; nrem: chunk bytes from the tile start,
+ *  capped at 4 GiB).  Updates the walk state (all lanes see the same values).
+ */
+__device__ __forceinline__ Slice step_slice(uint4 g, uint32_t s, uint32_t nrem, const CsvCfg& cfg,
+                                            bool count_excl, Walk* w, int lane) {
+  const uint32_t p = s * kStep + 16u * lane;
+  const uint32_t z = eq16(g, 0u);
+  const uint32_t e = eq16(g, 0x0A0A0A0Au) | eq16(g, 0x0D0D0D0Du) | z;  // NUL: past the chunk
+  const uint32_t d = eq16(g, cfg.delim * 0x01010101u);
+  // control bytes, and NULs inside the chunk, are text to the reference
+  const uint32_t inside = p >= nrem ? 0u : (nrem - p >= 16 ? 0xFFFFu : (1u << (nrem - p)) - 1u);
+  const bool bad = ((ctl16(g) | z) & inside) != 0;
+  const uint32_t last_e = (e >> 15) & 1u, last_d = (d >> 15) & 1u;
+  const uint32_t up_e = __shfl_up(last_e, 1, kWave);
+  const uint32_t up_d = __shfl_up(last_d, 1, kWave);
+  const uint32_t pe = lane == 0 ? w->carry_eol : up_e;
+  const uint32_t pd = lane == 0 ? w->carry_delim : up_d;
+  uint32_t lm = ~e & ((e << 1) | pe) & 0xFFFFu;
+  uint32_t fm = lm | (((d << 1) | pd) & 0xFFFFu);
+  w->carry_eol = __shfl(last_e, kWave - 1, kWave);
+  w->carry_delim = __shfl(last_d, kWave - 1, kWave);
+  // ownership: from the first row start in the tile to the first one after it
+  uint32_t own = 0xFFFFu;
+  const uint64_t any_ls = __ballot(lm != 0);
+  const int first_lane = any_ls != 0 ? __builtin_ctzll(any_ls) : 0;
+  const uint32_t first_lm = __shfl(lm, first_lane, kWave);
+  const uint32_t first_bit = first_lm & (0u - first_lm);
+  if (s < kTileSteps) {
+    if (!w->started) {
+      if (any_ls == 0) {
+        own = 0;
+      } else {
+        own = lane < first_lane ? 0u : (lane == first_lane ? (~(first_bit - 1u) & 0xFFFFu) : 0xFFFFu);
+        w->started = true;
+      }
+    }
+    if (s + 1 == kTileSteps && !w->started) w->done = true;  // no row starts in this tile
+  } else {
+    if (!w->started) {
+      own = 0;
+      w->done = true;
+    } else if (any_ls != 0) {
+      own = lane < first_lane ? 0xFFFFu : (lane == first_lane ? first_bit - 1u : 0u);
+      w->done = true;  // the next tile's first row
+    }
+  }
+  if (s * kStep + kStep >= nrem) w->done = true;  // the chunk ends in this step
+  fm &= own;
+  lm &= own;
+  w->bad |= __any(bad && own != 0);
+  // column of the lane's first field: segmented scan, reset at row starts
+  uint32_t x;
+  if (lm != 0) {
+    const uint32_t hi = 31u - __builtin_clz(lm);
+    x = static_cast<uint32_t>(__popc(fm >> hi)) | 0x80000000u;
+  } else {
+    x = static_cast<uint32_t>(__popc(fm));
+  }
+#pragma unroll
+  for (int dd = 1; dd < kWave; dd <<= 1) {
+    const uint32_t y = __shfl_up(x, dd, kWave);
+    if (lane >= dd && !(x & 0x80000000u)) x = (x + (y & 0x7FFFFFFFu)) | (y & 0x80000000u);
+  }
+  const uint32_t prev = __shfl_up(x, 1, kWave);
+  const uint32_t last = __shfl(x, kWave - 1, kWave);
+  Slice o;
+  o.fm = fm;
+  o.lm = lm;
+  o.col0 = lane == 0 ? w->col_carry
+                     : (prev & 0x7FFFFFFFu) + ((prev & 0x80000000u) ? 0u : w->col_carry);
+  w->col_carry = (last & 0x7FFFFFFFu) + ((last & 0x80000000u) ? 0u : w->col_carry);
+  // excluded columns among the lane's fields
+  uint32_t nx = 0;
+  if (count_excl) {
+    uint32_t col = o.col0;
+    for (uint32_t m = fm; m != 0; m &= m - 1) {
+      const uint32_t b = static_cast<uint32_t>(__builtin_ctz(m));
+      if ((lm >> b) & 1u) col = 0;
+      nx += excluded(col, cfg) ? 1u : 0u;
+      ++col;
+    }
+  }
+  const uint64_t packed = static_cast<uint64_t>(__popc(fm)) |
+                          (static_cast<uint64_t>(__popc(lm)) << 21) |
+                          (static_cast<uint64_t>(nx) << 42);
+  o.before = wave_excl_scan(packed, &o.total);
+  return o;
+}
+
+__device__ __forceinline__ uint32_t f21(uint64_t v, int k) {
+  return static_cast<uint32_t>((v >> (21 * k)) & 0x1FFFFFull);
+}
+
+__global__ __launch_bounds__(kThreads) void k_csv_tile_count(const uint8_t* __restrict__ text,
+                                                             size_t n, size_t ntiles, CsvCfg cfg,
+                                                             uint64_t* __restrict__ counts,
+                                                             uint32_t* __restrict__ flags) {
+  const int lane = lane_id();
+  const size_t tile = static_cast<size_t>(blockIdx.x) * kWaves + threadIdx.x / kWave;
+  if (tile >= ntiles) return;  // whole waves leave; nothing below synchronises waves
+  const size_t tile0 = tile * kTileBytes;
+  const uint32_t nrem = static_cast<uint32_t>(n - tile0 < 0xFFFFFFFFull ? n - tile0 : 0xFFFFFFFFull);
+  Walk w{};
+  w.carry_eol = 1u;
+  if (tile0 != 0) {
+    const uint32_t c = text[tile0 - 1];
+    w.carry_eol = (c == '\n' || c == '\r') ? 1u : 0u;
+  }
+  const bool count_excl = cfg.label_col >= 0 || cfg.weight_col >= 0;
+  bool over = false;
+  uint4 g = load16_clip(text, tile0 + 16u * lane, n);
+  for (uint32_t s = 0; s < kMaxSteps; ++s) {
+    const uint4 nxt = load16_clip(text, tile0 + (s + 1) * kStep + 16u * lane, n);  // prefetch
+    const Slice sl = step_slice(g, s, nrem, cfg, count_excl, &w, lane);
+    over |= f21(sl.total, 0) > kListCap;
+    w.fields += f21(sl.total, 0);
+    w.rows += f21(sl.total, 1);
+    w.excl += f21(sl.total, 2);
+    if (w.done) break;
+    g = nxt;
+  }
+  // rows run past the extension while the chunk goes on: exact kernels
+  const bool irregular = w.bad || over || (!w.done && tile0 + kTileBytes + kExt < n);
+  if (lane == 0) {
+    counts[tile] = (static_cast<uint64_t>(w.rows) << 32) | (w.fields - w.excl);
+    flags[tile] = irregular ? kFlagIrregular : 0u;
+  }
+}
+
+/*! \brief StrToFloat of the field at global position q (the generic path) */
+__device__ __noinline__ float generic_field(const char* q, const char* end, char delim,
+                                            bool* last) {
+  const char* fe = q;
+  while (fe != end && *fe != delim && *fe != '\n' && *fe != '\r') ++fe;
+  *last = fe == end || *fe != delim;
+  while (q != fe && data::isspace(*q)) ++q;
+  return data::StrToFloat(q, fe, nullptr);
+}
+
+template <typename IndexType>
+__global__ __launch_bounds__(kThreads) void k_csv_tile_fill(const uint8_t* __restrict__ text,
+                                                            size_t n, size_t ntiles, CsvCfg cfg,
+                                                            const uint64_t* __restrict__ prefix,
+                                                            FillTarget<IndexType> out,
+                                                            MetaPartial* __restrict__ partials) {
+  __shared__ uint4 s_ring[kWaves][kRingVecs];
+  __shared__ uint2 s_list[kWaves][kListCap];
+  const int lane = lane_id();
+  const int wave = threadIdx.x / kWave;
+  const size_t tile = static_cast<size_t>(blockIdx.x) * kWaves + wave;
+  if (tile >= ntiles) return;
+  uint4* ring = s_ring[wave];
+  uint2* list = s_list[wave];
+  const size_t tile0 = tile * kTileBytes;
+  const uint32_t nrem = static_cast<uint32_t>(n - tile0 < 0xFFFFFFFFull ? n - tile0 : 0xFFFFFFFFull);
+  const uint64_t pre = prefix[tile];
+  const uint64_t R = out.row_base + (pre >> 32);          // the tile's first row
+  const uint64_t C = out.nnz_base + (pre & 0xffffffffull);  // and first entry
+  Walk w{};
+  w.carry_eol = 1u;
+  if (tile0 != 0) {
+    const uint32_t c = text[tile0 - 1];
+    w.carry_eol = (c == '\n' || c == '\r') ? 1u : 0u;
+  }
+  const bool count_excl = cfg.label_col >= 0 || cfg.weight_col >= 0;
+  const uint32_t delim = cfg.delim;
+  uint64_t mx = 0;
+  bool irregular = false, any_value = false;
+  // slot 0 <- step 0 (+ mirror of its head past slot 1)
+  {
+    const uint4 v = load16_clip(text, tile0 + 16u * lane, n);
+    ring[lane] = v;
+    if (lane < 2) ring[2 * kStep / 16 + lane] = v;
+  }
+  for (uint32_t s = 0; s < kMaxSteps; ++s) {
+    const uint32_t slot = (s & 1u) * (kStep / 16);
+    // prefetch step s + 1 into the other slot (its head mirrored when that is slot 0)
+    if (s + 1 < kMaxSteps) {
+      const uint4 v = load16_clip(text, tile0 + (s + 1) * kStep + 16u * lane, n);
+      const uint32_t nslot = ((s + 1) & 1u) * (kStep / 16);
+      ring[nslot + lane] = v;
+      if (nslot == 0 && lane < 2) ring[2 * kStep / 16 + lane] = v;
+    }
+    wave_sync();
+    const Slice sl = step_slice(ring[slot + lane], s, nrem, cfg, count_excl, &w, lane);
+    // list the lane's fields: x = ring byte | row in tile << 16, y = column | entry in tile << 16
+    {
+      uint32_t col = sl.col0;
+      uint32_t at = f21(sl.before, 0);
+      uint32_t row = w.rows + f21(sl.before, 1);  // rows started before this lane, this tile
+      uint32_t ent = (w.fields + f21(sl.before, 0)) - (w.excl + f21(sl.before, 2));
+      for (uint32_t m = sl.fm; m != 0; m &= m - 1) {
+        const uint32_t b = static_cast<uint32_t>(__builtin_ctz(m));
+        if ((sl.lm >> b) & 1u) {
+          col = 0;
+          ++row;
+        }
+        if (at < kListCap) {
+          list[at] = make_uint2((slot * 16u + 16u * lane + b) | ((row - 1u) << 16),
+                                col | (ent << 16));
+        }
+        ++at;
+        ent += excluded(col, cfg) ? 0u : 1u;
+        ++col;
+      }
+    }
+    const uint32_t nf = f21(sl.total, 0);
+    w.fields += nf;
+    w.rows += f21(sl.total, 1);
+    w.excl += f21(sl.total, 2);
+    irregular |= nf > kListCap;
+    wave_sync();
+    const uint32_t nlist = nf < kListCap ? nf : kListCap;
+    for (uint32_t r0 = 0; r0 < nlist; r0 += kWave) {
+      const uint32_t k = r0 + lane;
+      if (k < nlist) {
+        const uint2 en = list[k];
+        const uint32_t off = en.x & 0xFFFFu;
+        const uint32_t row_t = en.x >> 16;
+        const uint32_t col = en.y & 0xFFFFu;
+        const uint32_t ent = en.y >> 16;
+        const uint32_t c0 = reinterpret_cast<const uint8_t*>(ring)[off];
+        float v;
+        bool last;
+        if (c0 == delim || c0 == '\n' || c0 == '\r' || c0 == 0) {
+          v = 0.0f;  // empty field
+          last = c0 != delim;
+        } else {
+          const tok::Num x = tok::parse_num(ring, off);
+          const bool t_eol = x.term == '\n' || x.term == '\r' || x.term == 0;
+          if (x.ok_float && (x.term == delim || t_eol)) {
+            v = x.fval;
+            last = t_eol;
+          } else {
+            const size_t gpos = tile0 + s * kStep + (off - slot * 16u);
+            v = generic_field(reinterpret_cast<const char*>(text) + gpos,
+                              reinterpret_cast<const char*>(text) + n, static_cast<char>(delim),
+                              &last);
+          }
+        }
+        const uint64_t row = R + row_t;
+        const uint64_t e = C + ent;
+        if (row >= out.row_limit) {
+          irregular = true;
+        } else {
+          if (static_cast<int>(col) == cfg.label_col) {
+            out.label[row] = v;
+          } else if (static_cast<int>(col) == cfg.weight_col) {
+            out.weight[row] = v;
+          } else if (e < out.nnz_limit) {
+            uint32_t idx = col;
+            idx -= (cfg.label_col >= 0 && col > static_cast<uint32_t>(cfg.label_col)) ? 1u : 0u;
+            idx -= (cfg.weight_col >= 0 && col > static_cast<uint32_t>(cfg.weight_col)) ? 1u : 0u;
+            out.index[e] = static_cast<IndexType>(idx);
+            out.value[e] = v;
+            mx = idx > mx ? idx : mx;
+            any_value = true;
+          } else {
+            irregular = true;
+          }
+          if (col == 0) {
+            out.offset[row] = e;
+            if (cfg.label_col < 0) out.label[row] = 0.0f;
+          }
+          if (last) {
+            // a short row: no label / weight field
+            if (cfg.label_col >= 0 && col < static_cast<uint32_t>(cfg.label_col)) out.label[row] = 0.0f;
+            if (cfg.has_weight && (cfg.weight_col < 0 || col < static_cast<uint32_t>(cfg.weight_col))) {
+              out.weight[row] = 1.0f;
+            }
+          }
+        }
+      }
+    }
+    if (w.done) break;
+    wave_sync();  // the next prefetch overwrites this step's slot
+  }
+  unsigned fl = 0;
+  if (irregular || w.bad) fl |= kFlagIrregular;
+  if (any_value) fl |= kFlagValue;
+  if (cfg.has_weight) fl |= kFlagWeight;
+  const unsigned long long m = wave_max(static_cast<unsigned long long>(mx));
+  fl = wave_or(fl);
+  if (lane == 0) {
+    MetaPartial p;
+    p.max_index = m;
+    p.max_field = 0;
+    p.flags = fl;
+    p.pad = 0;
+    partials[tile] = p;
+  }
+}
+
+CsvCfg MakeCfg(int label_column, int weight_column, char delimiter) {
+  CsvCfg c;
+  c.label_col = label_column < 0 ? -1 : label_column;
+  // weight_column == label_column: the label takes the column (the reference
+  // tests it first), rows still get weight 1.0
+  c.weight_col = (weight_column < 0 || weight_column == label_column) ? -1 : weight_column;
+  c.has_weight = weight_column >= 0 ? 1 : 0;
+  c.delim = static_cast<uint8_t>(delimiter);
+  return c;
+}
+
+}  // namespace
+
+void LaunchCsvTileCount(const char* text, size_t nbytes, int label_column, int weight_column,
+                        char delimiter, uint64_t* tile_counts, uint32_t* tile_flags,
+                        hipStream_t stream) {
+  const size_t ntiles = TileCount(nbytes);
+  if (ntiles == 0) return;
+  hipLaunchKernelGGL(k_csv_tile_count, dim3((ntiles + kWaves - 1) / kWaves), dim3(kThreads), 0,
+                     stream, reinterpret_cast<const uint8_t*>(text), nbytes, ntiles,
+                     MakeCfg(label_column, weight_column, delimiter), tile_counts, tile_flags);
+}
+
+template <typename IndexType>
+void LaunchCsvTileFill(const char* text, size_t nbytes, int label_column, int weight_column,
+                       char delimiter, const uint64_t* tile_prefix, const FillTarget<IndexType>& out,
+                       MetaPartial* partials, hipStream_t stream) {
+  const size_t ntiles = TileCount(nbytes);
+  if (ntiles == 0) return;
+  hipLaunchKernelGGL((k_csv_tile_fill<IndexType>), dim3((ntiles + kWaves - 1) / kWaves),
+                     dim3(kThreads), 0, stream, reinterpret_cast<const uint8_t*>(text), nbytes,
+                     ntiles, MakeCfg(label_column, weight_column, delimiter), tile_prefix, out,
+                     partials);
+}
+
+template void LaunchCsvTileFill<uint32_t>(const char*, size_t, int, int, char, const uint64_t*,
+                                          const FillTarget<uint32_t>&, MetaPartial*, hipStream_t);
+template void LaunchCsvTileFill<uint64_t>(const char*, size_t, int, int, char, const uint64_t*,
+                                          const FillTarget<uint64_t>&, MetaPartial*, hipStream_t);
+
+}  // namespace gpu
+}  // namespace dmlc

@@ -133,6 +133,9 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     } else {
       LOG(FATAL) << "DeviceParser: unsupported format " << cfg_.format;
     }
+    CHECK(tcfg_.format != TextFormat::kCSV || cfg_.label_column < 0 ||
+          cfg_.label_column != cfg_.weight_column)
+        << "label_column and weight_column must differ";
     tcfg_.label_column = cfg_.label_column;
     tcfg_.weight_column = cfg_.weight_column;
     tcfg_.delimiter = cfg_.delimiter;
@@ -533,6 +536,41 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     }
   }
 
+  /*!
+   * \brief CSV on the tile pipeline (csv_kernels.hip): lane-per-row count ->
+   *  raw scan -> fill -> finish, both size read-outs through mapped pinned
+   *  memory; false when the chunk must take the exact path (rows longer than
+   *  the tile extension, control bytes).
+   */
+  bool CsvFastParse(const char* text, size_t nbytes, DeviceCSR<IndexType>* out, size_t row_base,
+                    size_t nnz_base, ChunkPlan* plan) {
+    hipStream_t s = compute_->get();
+    ChunkMeta* dmeta = meta_.get<ChunkMeta>();
+    ChunkMeta* hm = hmap_.get<ChunkMeta>();
+    const size_t ntiles = TileCount(nbytes);
+    LaunchCsvTileCount(text, nbytes, tcfg_.label_column, tcfg_.weight_column, tcfg_.delimiter,
+                       tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(), s);
+    LaunchTileScanRaw(tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(), ntiles, dmeta, hm, s);
+    const ChunkMeta sizes = WaitMapped(hm);
+    AfterFirstSync();
+    if (sizes.flags & kFlagIrregular) return false;
+    plan->nlines = sizes.nrows;
+    plan->nrows = sizes.nrows;
+    plan->nnz = sizes.nnz;
+    const bool need_weight = tcfg_.weight_column >= 0;
+    FillTarget<IndexType> tgt = PrepareOutput(out, row_base, nnz_base, *plan, need_weight, nbytes);
+    LaunchCsvTileFill<IndexType>(text, nbytes, tcfg_.label_column, tcfg_.weight_column,
+                                 tcfg_.delimiter, tcounts_.get<uint64_t>(), tgt,
+                                 slots_.get<MetaPartial>(), s);
+    LaunchTileFinish(slots_.get<MetaPartial>(), ntiles, dmeta, hm, tgt.offset, row_base, nnz_base,
+                     s);
+    const ChunkMeta m = WaitMapped(hm);
+    CHECK(!(m.flags & kFlagIrregular))
+        << "internal error: CSV fill pass disagreed with the count pass";
+    Accumulate(m);
+    return true;
+  }
+
   /*! \brief exact wave-per-line parse (any input) */
   void ExactParse(const char* text, size_t nbytes, DeviceCSR<IndexType>* out, size_t row_base,
                   size_t nnz_base, ChunkPlan* plan, bool first_sync_done) {
@@ -632,16 +670,15 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     const size_t row_base = append ? out->rows_ : 0;
     const size_t nnz_base = append ? out->nnz_ : 0;
     ChunkPlan plan;
-    const bool token_format = tcfg_.format != TextFormat::kCSV;
+    const bool csv = tcfg_.format == TextFormat::kCSV;
     const bool more = WithNextChunk([&](const char* text, size_t nbytes) {
       bool done = false;
-      if (token_format && cfg_.fast_path) {
-        done = FastParse(text, nbytes, out, row_base, nnz_base, &plan);
+      if (cfg_.fast_path) {
+        done = csv ? CsvFastParse(text, nbytes, out, row_base, nnz_base, &plan)
+                   : FastParse(text, nbytes, out, row_base, nnz_base, &plan);
         if (!done) stats_.exact_chunks += 1;
       }
-      if (!done) {
-        ExactParse(text, nbytes, out, row_base, nnz_base, &plan, token_format && cfg_.fast_path);
-      }
+      if (!done) ExactParse(text, nbytes, out, row_base, nnz_base, &plan, cfg_.fast_path);
     });
     if (!more) return false;
     out->rows_ = row_base + plan.nrows;

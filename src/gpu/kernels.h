@@ -211,6 +211,25 @@ void LaunchTileScanRaw(uint64_t* tile_counts, uint32_t* tile_flags, size_t ntile
 void LaunchTileFinish(MetaPartial* partials, size_t nslots, ChunkMeta* meta, ChunkMeta* host_meta,
                       uint64_t* offset, uint64_t row_base, uint64_t nnz_base, hipStream_t stream);
 
+// ------------------------- CSV on the tile pipeline -------------------------
+/*!
+ * \brief S1: per 8 KiB tile (rows starting in it << 32 | their entries) and
+ *  kFlagIrregular (a row running > 4 KiB past its tile, control bytes); scan
+ *  them with LaunchTileScanRaw.  tile_counts / tile_flags: TileScratchWords.
+ */
+void LaunchCsvTileCount(const char* text, size_t nbytes, int label_column, int weight_column,
+                        char delimiter, uint64_t* tile_counts, uint32_t* tile_flags,
+                        hipStream_t stream);
+/*!
+ * \brief S2: every row of a regular chunk into out (index / value / label /
+ *  weight / offset) from the scanned S1 prefixes; one MetaPartial per tile
+ *  (max index, kFlagValue / kFlagWeight), folded by LaunchTileFinish.
+ */
+template <typename IndexType>
+void LaunchCsvTileFill(const char* text, size_t nbytes, int label_column, int weight_column,
+                       char delimiter, const uint64_t* tile_prefix, const FillTarget<IndexType>& out,
+                       MetaPartial* partials, hipStream_t stream);
+
 // ----------------------------- RecordIO (K7) -----------------------------
 /*! \brief error bits reported by the RecordIO kernels */
 constexpr uint32_t kRecErrTruncated = 1;   // a part runs past the chunk end

@@ -279,7 +279,10 @@ __device__ void walk_line(const uint8_t* __restrict__ text, uint32_t b, uint32_t
   uint32_t tok_base = 0, rank_base = 0;
   bool prev_sep = true;     // byte before the line start behaves as a separator
   bool prev_delim = false;  // CSV: previous byte was the delimiter
-  for (uint32_t pstart = wbase; pstart < e; pstart += kPiece) {
+  // CSV: a line ending in the delimiter has an empty field at e, which can be
+  // the first byte of one more piece
+  const uint32_t stop = (F == TextFormat::kCSV && text[e - 1] == static_cast<uint8_t>(delim)) ? e + 1 : e;
+  for (uint32_t pstart = wbase; pstart < stop; pstart += kPiece) {
     const uint32_t pos = pstart + 16 * lane;
     // token starts of this lane's 16 bytes
     uint32_t starts;
@@ -288,7 +291,9 @@ __device__ void walk_line(const uint8_t* __restrict__ text, uint32_t b, uint32_t
       const uint32_t up_delim = __shfl_up(mcur.delim, 1, dev::kWave);
       if constexpr (F == TextFormat::kCSV) {
         const uint32_t pd = lane == 0 ? (prev_delim ? 1u : 0u) : ((up_delim >> 15) & 1u);
-        starts = ~mcur.eol & ~(mcur.sep & ~mcur.delim) & ((mcur.delim << 1) | pd);
+        // every byte after a delimiter starts a field -- also the line end
+        // after a trailing delimiter (an empty last field, csv_parser.h)
+        starts = (mcur.delim << 1) | pd;
         if (b >= pos && b < pos + 16) starts |= 1u << (b - pos);
         starts &= 0xFFFFu;
       } else {

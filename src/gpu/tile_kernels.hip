@@ -647,7 +647,7 @@ __device__ __noinline__ void generic_token(const uint8_t* __restrict__ text, siz
  */
 constexpr int kFillWaves = kThreads / 64;
 #ifndef DMLC_FILL_WAVES
-#define DMLC_FILL_WAVES 8
+#define DMLC_FILL_WAVES 4  // measured best (profiles/r03_fill_ablation)
 #endif
 constexpr uint32_t kStepBytes = 2048;
 constexpr int kSteps = static_cast<int>(kTileBytes / kStepBytes);
@@ -732,7 +732,8 @@ __device__ __forceinline__ uint32_t round_slot(int lane) {
 }
 
 template <TextFormat F, typename IndexType>
-__global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(const uint8_t* __restrict__ text, size_t n,
+__global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
+    const uint8_t* __restrict__ text, size_t n,
                                                         size_t ntiles,
                                                         const uint64_t* __restrict__ prefix,
                                                         FillTarget<IndexType> out,

@@ -150,6 +150,56 @@ def test_csv_gpu_equals_cpu(tmp_path, label_column):
     np.testing.assert_array_equal(g["value"], c["value"])
 
 
+CSV_FIELDS = ["1", "0.5", "-2", "+3.75", ".25", "5.", "", " 7", "  -1.5", "1e3", "2.5E-2",
+              "1.5.3", "3x", "123456789.5", "-", "+.5", "12345678", "1234567", "0.1234567",
+              "9.87654321", "x", "4 ", "\t8"]
+
+
+@pytest.mark.parametrize("delim", [",", "\t"])
+@pytest.mark.parametrize("label_column,weight_column", [(-1, -1), (0, -1), (2, 0), (1, 3), (0, 5)])
+def test_csv_shape_fuzz_matches_cpu(tmp_path, delim, label_column, weight_column):
+    """CSV tile path (lane per row) vs the CPU parser: every field shape the
+    register-window decoder takes and many it hands to StrToFloat (blanks,
+    junk, exponents, long digit runs, empty fields), short rows that lack the
+    label / weight column, CRLF, blank lines, no final newline; plus rows over
+    the 4 KiB tile extension, which send their chunk to the exact kernels."""
+    rng = np.random.default_rng(40 + label_column * 7 + weight_column)
+    fields = [f for f in CSV_FIELDS if delim not in f]
+    lines = []
+    for r in range(4000):
+        n = int(rng.integers(1, 40))
+        lines.append(delim.join(fields[int(rng.integers(len(fields)))] for _ in range(n)))
+        if rng.random() < 0.02:
+            lines.append("")
+    p = str(tmp_path / "f.csv")
+    with open(p, "w", newline="") as f:
+        f.write("\r\n".join(lines[:100]) + "\n" + "\n".join(lines[100:]))
+    q = f"?label_column={label_column}&weight_column={weight_column}"
+    if delim != ",":
+        q += "&delimiter=\t"
+    cfg = dict(label_column=label_column, weight_column=weight_column, delimiter=delim)
+    c = cpu_rows(p + q, "csv")
+    for chunk in (8192, 64 * 1024, 1 << 20):
+        gp = data.GPUParser(p + q, format="csv", chunk_bytes=chunk, **cfg)
+        g = pyref.concat_blocks([gp.parse_all().to_host()])
+        for k in ("label", "weight", "offset", "index", "value"):
+            np.testing.assert_array_equal(g[k], c[k], err_msg=f"{k} chunk={chunk}")
+        assert gp.stats()["exact_chunks"] == 0
+    # wide rows (> 4 KiB past their tile): exact kernels for those chunks
+    wide = str(tmp_path / "wide.csv")
+    with open(wide, "w") as f:
+        f.write("\n".join(lines[:500]) + "\n")
+        f.write(delim.join(["1.25"] * 3000) + "\n")
+        f.write("\n".join(lines[500:1500]))
+    gp = data.GPUParser(wide + q, format="csv", chunk_bytes=32 * 1024, **cfg)
+    g = pyref.concat_blocks([gp.parse_all().to_host()])
+    c = cpu_rows(wide + q, "csv")
+    for k in ("label", "weight", "offset", "index", "value"):
+        np.testing.assert_array_equal(g[k], c[k], err_msg=k)
+    st = gp.stats()
+    assert 0 < st["exact_chunks"] < st["chunks"]
+
+
 def test_index64_gpu(tmp_path):
     p = str(tmp_path / "b.libsvm")
     with open(p, "w") as f:
