@@ -34,29 +34,6 @@ class SparseLogReg(torch.nn.Module):
             logits, label, weight=w, reduction="mean")
 
 
-class _FP8Linear(torch.autograd.Function):
-    """y = x8 @ w with x8 OCP fp8 e4m3 (scale sx) and w quantised to fp8 per
-    tensor, on the MFMA fp8 path (torch._scaled_mm -> hipBLASLt); the weight
-    gradient is computed in bf16 (fp8 forward / bf16 backward)."""
-
-    @staticmethod
-    def forward(ctx, x8, sx, w):
-        amax = w.detach().abs().max().clamp(min=1e-12).float()
-        sw = (amax / 448.0).reshape(())
-        w8 = (w.detach() / sw).to(torch.float8_e4m3fn)
-        y = torch._scaled_mm(x8, w8.t().contiguous().t(), scale_a=sx, scale_b=sw,
-                             out_dtype=torch.float32)
-        ctx.save_for_backward(x8, sx)
-        return y
-
-    @staticmethod
-    def backward(ctx, gy):
-        x8, sx = ctx.saved_tensors
-        xb = x8.to(torch.bfloat16) * sx.to(torch.bfloat16)
-        gw = (xb.t() @ gy.to(torch.bfloat16)).float()
-        return None, None, gw
-
-
 def fp8_gemm_available(device=None) -> bool:
     """True when torch._scaled_mm runs OCP fp8 e4m3 GEMMs on this device."""
     if not torch.cuda.is_available():
@@ -71,48 +48,95 @@ def fp8_gemm_available(device=None) -> bool:
         return False
 
 
+class _HashedFMFunction(torch.autograd.Function):
+    """HashedFM forward / backward as two HIP kernels over the fp8 batch
+    (src/gpu/fm_kernels.hip): F1 reads the batch once and writes y and xV,
+    F2 reads it once more and writes per-block partials of G^T X and
+    (X^2)^T g, summed here; no fp32 / bf16 copy of the batch exists."""
+
+    @staticmethod
+    def forward(ctx, x8, sx: float, w, v, bias):
+        rows, dim = x8.shape
+        dev = x8.device
+        wt = torch.cat([w, v], dim=1).detach().t().contiguous().to(torch.bfloat16)
+        q = (v.detach().float() ** 2).sum(1).contiguous()
+        b = bias.detach().float().contiguous()
+        y = torch.empty(rows, dtype=torch.float32, device=dev)
+        xv = torch.empty((rows, v.shape[1]), dtype=torch.float32, device=dev)
+        _dmlc().fm_forward(x8.data_ptr(), rows, dim, wt.data_ptr(), q.data_ptr(), b.data_ptr(),
+                           float(sx), y.data_ptr(), xv.data_ptr(), _num_cus(dev), _stream())
+        ctx.save_for_backward(x8, xv, v.detach())
+        ctx.sx = float(sx)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x8, xv, v = ctx.saved_tensors
+        rows, dim = x8.shape
+        g = gy.detach().float().contiguous()
+        nblk = max(1, min(2 * _num_cus(x8.device), (rows + 31) // 32))
+        part = torch.empty((nblk, v.shape[1] + 2, dim), dtype=torch.float32, device=x8.device)
+        _dmlc().fm_backward(x8.data_ptr(), rows, dim, g.data_ptr(), xv.data_ptr(), nblk,
+                            part.data_ptr(), _stream())
+        z = part.sum(0)
+        sx = ctx.sx
+        gw = (sx * z[0]).unsqueeze(1)
+        gv = sx * z[1:1 + v.shape[1]].t() - v * (sx * sx * z[-1]).unsqueeze(1)
+        return None, None, gw, gv, g.sum().reshape(1)
+
+
+def _dmlc():
+    from .. import _dmlc as ext
+    return ext
+
+
+def _stream() -> int:
+    return int(torch.cuda.current_stream().cuda_stream)
+
+
+_CUS = {}
+
+
+def _num_cus(dev) -> int:
+    i = dev.index if dev.index is not None else torch.cuda.current_device()
+    if i not in _CUS:
+        _CUS[i] = torch.cuda.get_device_properties(i).multi_processor_count
+    return _CUS[i]
+
+
 class HashedFM(torch.nn.Module):
     """Factorisation machine on hashed fp8 features (BASELINE config 5).
 
     Input: the ``[rows, dim]`` float8_e4m3fn batch of
     ``GPUParser.parse_all_hashed`` (fused tokenize -> hash -> fp8 kernel) or of
     :func:`~dmlc_core_amd.ops.hashed_dense`, with its quantisation ``scale``.
-    ``y = b + x.w + 1/2 sum_f ((x V)_f^2 - (x^2 V^2)_f)``: the linear term and
-    ``x V`` share ONE fp8 GEMM on the MFMA fp8 path (``torch._scaled_mm`` ->
-    hipBLASLt, ``[w | V]`` quantised per tensor, N padded to 16); the
-    ``x^2 V^2`` term is a bf16 GEMM.  Where the fp8 GEMM is unavailable the
-    first term falls back to bf16 (``self.gemm`` tells which ran).
+    ``y = b + x.w + 1/2 sum_f ((x V)_f^2 - (x^2 V^2)_f)``; the last term is
+    ``x^2 . q`` with ``q = rowsum(V^2)``.  On a GPU (rank 16, dim a multiple of
+    128) forward and backward are the bf16-MFMA kernels of
+    ``src/gpu/fm_kernels.hip``, each reading the fp8 batch once; elsewhere the
+    fp32 formula runs on the dequantised batch (``self.gemm`` tells which).
     """
 
     def __init__(self, dim: int = 1024, rank: int = 16, seed: int = 0):
         super().__init__()
         if dim % 16 != 0:
-            raise ValueError("dim must be a multiple of 16 (fp8 GEMM tiles)")
+            raise ValueError("dim must be a multiple of 16")
         self.dim, self.rank, self.seed = int(dim), int(rank), int(seed)
         self.bias = torch.nn.Parameter(torch.zeros(1))
         self.w = torch.nn.Parameter(torch.zeros(dim, 1))
         self.v = torch.nn.Parameter(torch.randn(dim, rank) * 0.01)
         self.gemm = None
 
-    def forward(self, x8: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
-        sx = torch.tensor(1.0 / scale, dtype=torch.float32, device=x8.device)
-        wv = torch.cat([self.w, self.v], dim=1)
-        n = wv.shape[1]
-        pad = (-n) % 16
-        wvp = torch.nn.functional.pad(wv, (0, pad))
-        if self.gemm is None:
-            self.gemm = "fp8" if fp8_gemm_available(x8.device) else "bf16"
-        if self.gemm == "fp8":
-            y = _FP8Linear.apply(x8, sx, wvp)[:, :n]
-        else:
-            xb = x8.to(torch.bfloat16) * sx.to(torch.bfloat16)
-            y = (xb @ wvp.to(torch.bfloat16)).float()[:, :n]
-        lin = y[:, 0] + self.bias
-        xv = y[:, 1:]
-        x2 = (x8.to(torch.float32) * sx) ** 2
-        x2v2 = (x2.to(torch.bfloat16) @ (self.v ** 2).to(torch.bfloat16)).float()
-        return lin + 0.5 * (xv ** 2 - x2v2).sum(-1)
+    def _native(self, x8: torch.Tensor) -> bool:
+        return (x8.is_cuda and x8.dtype == torch.float8_e4m3fn and self.rank == 16
+                and self.dim % 128 == 0 and self.dim <= 2048)
 
+    def forward(self, x8: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
+        if self._native(x8):
+            self.gemm = "hip_mfma_bf16"
+            return _HashedFMFunction.apply(x8.contiguous(), 1.0 / scale, self.w, self.v, self.bias)
+        self.gemm = "torch_fp32"
+        return self.reference(x8.float() / scale, self.w, self.v, self.bias)
     @staticmethod
     def reference(x: torch.Tensor, w, v, bias) -> torch.Tensor:
         """fp32 reference of the same model on dequantised features."""

@@ -1,0 +1,297 @@
+/*!
+ * \file src/gpu/fm_kernels.hip
+ * \brief HashedFM (BASELINE config 5) forward / backward on the fp8 hashed
+ *  batch, bf16 MFMA on gfx950, the batch read once per pass.
+ *
+ * Model: y_r = b + s x_r.w + 1/2 (sum_f (s x_r.V_f)^2 - s^2 x_r^2.q),
+ * q_n = sum_f V_nf^2 (the x^2 V^2 term summed over f is one dot product with
+ * q), x = fp8 e4m3 codes, s = 1 / quantisation scale.
+ *
+ * F1 k_fm_fwd: a wave takes 32 rows; per 128-feature block each lane loads
+ *   64 contiguous bytes of its row (lanes l and l+32 the two halves of a
+ *   128-byte line) and feeds them, 8 at a time, as the A fragment of
+ *   v_mfma_f32_32x32x16_bf16 against B = [w | V] (bf16, LDS-resident,
+ *   columns 17..31 zero).  The K order inside a block is permuted the same way
+ *   for A and B, so no data moves between lanes.  x^2.q accumulates on the
+ *   VALU from the same converted registers.  The epilogue reduces (xV)^2 over
+ *   the 16 V lanes with xor-shuffles and writes y and xV (kept for F2).
+ * F2 k_fm_bwd: with g = dL/dy and G_r = [g_r, g_r xV_r] (17 columns),
+ *   Z = G^T X (summed over rows) and t = (x^2)^T g give every gradient:
+ *   dw = s Z_0, dV_nf = s Z_{1+f,n} - V_nf s^2 t_n.  Rows are the reduction
+ *   index, so X must arrive with rows along K: an identity MFMA turns each
+ *   32 x 32 X tile into an accumulator with features on lanes and rows in
+ *   registers, which is exactly the B operand of the next MFMA (G^T from LDS
+ *   in the matching permuted row order).  Eight waves share one G tile; each
+ *   keeps 128 features of Z in 64 accumulator registers and writes one
+ *   partial per workgroup (summed by the caller).
+ */
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "./device_common.h"
+#include "./kernels.h"
+
+namespace dmlc {
+namespace gpu {
+namespace {
+
+using namespace dev;  // NOLINT(build/namespaces)
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kFwdThreads = 256;
+constexpr int kBwdThreads = 512;  // 8 waves x 128 features = 1024 features per workgroup
+constexpr int kBwdWaveFeatures = 128;
+
+/*! \brief two dwords of fp8 e4m3 codes -> 8 floats (exact) */
+__device__ __forceinline__ void fp8x8(uint32_t lo, uint32_t hi, float f[8]) {
+  const f32x2 a = __builtin_amdgcn_cvt_pk_f32_fp8(static_cast<int>(lo), false);
+  const f32x2 b = __builtin_amdgcn_cvt_pk_f32_fp8(static_cast<int>(lo), true);
+  const f32x2 c = __builtin_amdgcn_cvt_pk_f32_fp8(static_cast<int>(hi), false);
+  const f32x2 d = __builtin_amdgcn_cvt_pk_f32_fp8(static_cast<int>(hi), true);
+  f[0] = a[0];
+  f[1] = a[1];
+  f[2] = b[0];
+  f[3] = b[1];
+  f[4] = c[0];
+  f[5] = c[1];
+  f[6] = d[0];
+  f[7] = d[1];
+}
+
+__device__ __forceinline__ bf16x8 to_bf16x8(const float f[8]) {
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = static_cast<__bf16>(f[j]);
+  return v;
+}
+
+__device__ __forceinline__ uint32_t word(const uint4 (&v)[4], int i) {
+  const uint4 q = v[i >> 2];
+  const int k = i & 3;
+  return k == 0 ? q.x : (k == 1 ? q.y : (k == 2 ? q.z : q.w));
+}
+
+__device__ __forceinline__ void load64(const uint8_t* p, bool valid, uint4 (&v)[4]) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = valid ? q[i] : make_uint4(0, 0, 0, 0);
+}
+
+/*!
+ * F1.  LDS: [w | V]^T as bf16 [17][dim + 8] (the pad spreads the 17 B-lanes
+ * over bank quads) then q as f32 [dim].
+ */
+__global__ __launch_bounds__(kFwdThreads) void k_fm_fwd(const uint8_t* __restrict__ x,
+                                                        int64_t rows, int dim,
+                                                        const __bf16* __restrict__ wt,
+                                                        const float* __restrict__ q,
+                                                        const float* __restrict__ bias, float sx,
+                                                        float* __restrict__ y,
+                                                        float* __restrict__ xv) {
+  extern __shared__ uint4 smem[];
+  const int ldw = dim + 8;
+  __bf16* s_wt = reinterpret_cast<__bf16*>(smem);
+  float* s_q = reinterpret_cast<float*>(s_wt + kFmCols * ldw);
+  for (int i = threadIdx.x; i < kFmCols * dim / 8; i += kFwdThreads) {
+    const int c = i / (dim / 8), k8 = i % (dim / 8);
+    *reinterpret_cast<uint4*>(s_wt + c * ldw + 8 * k8) =
+        reinterpret_cast<const uint4*>(wt + static_cast<size_t>(c) * dim)[k8];
+  }
+  for (int i = threadIdx.x; i < dim / 4; i += kFwdThreads) {
+    reinterpret_cast<float4*>(s_q)[i] = reinterpret_cast<const float4*>(q)[i];
+  }
+  __syncthreads();
+  const int lane = lane_id();
+  const int h = lane >> 5, col = lane & 31;
+  const int waves = kFwdThreads / kWave;
+  const int64_t ntiles = (rows + 31) / 32;
+  const float b0 = *bias;
+  const int nblk = dim / 128;
+  const bf16x8 zero8 = {};
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * waves + threadIdx.x / kWave; t < ntiles;
+       t += static_cast<int64_t>(gridDim.x) * waves) {
+    const int64_t row = t * 32 + col;  // the row of this lane's A fragment
+    const bool valid = row < rows;
+    const uint8_t* xr = x + (valid ? row : 0) * dim + 64 * h;
+    f32x16 acc = {};
+    float x2q = 0.0f;
+    uint4 cur[4], nxt[4];
+    load64(xr, valid, cur);
+    for (int kb = 0; kb < nblk; ++kb) {
+      if (kb + 1 < nblk) load64(xr + 128 * (kb + 1), valid, nxt);
+      const int kbase = 128 * kb + 64 * h;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float f[8];
+        fp8x8(word(cur, 2 * i), word(cur, 2 * i + 1), f);
+        const float4 q0 = *reinterpret_cast<const float4*>(s_q + kbase + 8 * i);
+        const float4 q1 = *reinterpret_cast<const float4*>(s_q + kbase + 8 * i + 4);
+        x2q += f[0] * f[0] * q0.x + f[1] * f[1] * q0.y + f[2] * f[2] * q0.z + f[3] * f[3] * q0.w +
+               f[4] * f[4] * q1.x + f[5] * f[5] * q1.y + f[6] * f[6] * q1.z + f[7] * f[7] * q1.w;
+        const bf16x8 b = col < kFmCols
+                             ? *reinterpret_cast<const bf16x8*>(s_wt + col * ldw + kbase + 8 * i)
+                             : zero8;
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(to_bf16x8(f), b, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) cur[i] = nxt[i];
+    }
+    // lanes r and r + 32 hold the two halves of row r's x^2.q
+    x2q += __shfl_xor(x2q, 32, kWave);
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int m = (reg & 3) + 8 * (reg >> 2) + 4 * h;  // accumulator row (C/D map)
+      const float v = acc[reg];
+      float sq = (col >= 1 && col <= kFmRank) ? v * v : 0.0f;
+#pragma unroll
+      for (int d = 1; d < 32; d <<= 1) sq += __shfl_xor(sq, d, kWave);
+      const float lin = __shfl(v, h * 32, kWave);
+      const float xq = __shfl(x2q, m, kWave);
+      const int64_t r = t * 32 + m;
+      if (r < rows) {
+        if (col == 0) {
+          y[r] = b0 + sx * lin + 0.5f * sx * sx * (sq - xq);
+        } else if (col <= kFmRank) {
+          xv[r * kFmRank + (col - 1)] = sx * v;
+        }
+      }
+    }
+  }
+}
+
+/*!
+ * F2.  Workgroup = 8 waves over rows [blockIdx.x * rows_per_block, ...) and
+ * features [1024 * blockIdx.y, + 1024); wave w takes 128 of them.  Writes
+ * part[blockIdx.x][c][n] for c < 17 (Z) and c = 17 (t), n < dim.
+ */
+__global__ __launch_bounds__(kBwdThreads) void k_fm_bwd(const uint8_t* __restrict__ x,
+                                                        int64_t rows, int dim,
+                                                        const float* __restrict__ g,
+                                                        const float* __restrict__ xv,
+                                                        int64_t rows_per_block,
+                                                        float* __restrict__ part) {
+  __shared__ __bf16 s_gt[32][32 + 8];  // G^T [column][row], columns 17..31 zero
+  __shared__ float s_g[32];
+  const int lane = lane_id();
+  const int h = lane >> 5, n = lane & 31;
+  const int wave = threadIdx.x / kWave;
+  const int fbase = 1024 * blockIdx.y + kBwdWaveFeatures * wave;
+  const bool active = fbase < dim;
+  for (int i = threadIdx.x; i < 32 * 40; i += kBwdThreads) (&s_gt[0][0])[i] = static_cast<__bf16>(0.0f);
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  const int64_t r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
+  // identity B fragments: element j of step s is 1 for column n's (h, s, j)
+  bf16x8 eye[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool one = h == (n >> 4) && s == ((n >> 3) & 1) && j == (n & 7);
+      eye[s][j] = static_cast<__bf16>(one ? 1.0f : 0.0f);
+    }
+  }
+  f32x16 acc[4] = {};
+  float tacc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int64_t t0 = r0; t0 < r1; t0 += 32) {
+    __syncthreads();  // the previous tile's G is consumed
+    if (threadIdx.x < 256) {
+      const int row = threadIdx.x >> 3, part_id = threadIdx.x & 7;
+      const int64_t r = t0 + row;
+      const bool ok = r < r1;
+      const float gv = ok ? g[r] : 0.0f;
+      const float2 v = ok ? *reinterpret_cast<const float2*>(xv + r * kFmRank + 2 * part_id)
+                          : make_float2(0.0f, 0.0f);
+      s_gt[1 + 2 * part_id][row] = static_cast<__bf16>(gv * v.x);
+      s_gt[2 + 2 * part_id][row] = static_cast<__bf16>(gv * v.y);
+      if (part_id == 0) {
+        s_gt[0][row] = static_cast<__bf16>(gv);
+        s_g[row] = gv;
+      }
+    }
+    __syncthreads();
+    if (!active) continue;
+    const int64_t r = t0 + n;  // the row of this lane's X fragment
+    const bool ok = r < r1;
+    uint4 xw[4];
+    load64(x + (ok ? r : 0) * dim + fbase + 64 * h, ok, xw);
+    // G^T fragments: element j of step s = row 16 s + 8 (j >> 2) + 4 h + (j & 3)
+    bf16x8 ga[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ga[s][j] = s_gt[n][16 * s + 8 * (j >> 2) + 4 * h + (j & 3)];
+    }
+    float gr[16];
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) gr[reg] = s_g[(reg & 3) + 8 * (reg >> 2) + 4 * h];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      // T: this block's 32 x 32 X tile, features on lanes, rows in registers
+      f32x16 tt = {};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float f[8];
+        fp8x8(word(xw, 2 * (2 * b + s)), word(xw, 2 * (2 * b + s) + 1), f);
+        tt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(to_bf16x8(f), eye[s], tt, 0, 0, 0);
+      }
+      float ta = 0.0f;
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) ta += tt[reg] * tt[reg] * gr[reg];
+      tacc[b] += ta;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 tb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) tb[j] = static_cast<__bf16>(tt[8 * s + j]);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[s], tb, acc[b], 0, 0, 0);
+      }
+    }
+  }
+  if (!active) return;
+  float* out = part + static_cast<size_t>(blockIdx.x) * (kFmCols + 1) * dim;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    // column n of block b <-> feature 64 (n >> 4) + 16 b + 8 ((n >> 3) & 1) + (n & 7)
+    const int feat = fbase + 64 * (n >> 4) + 16 * b + 8 * ((n >> 3) & 1) + (n & 7);
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int c = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (c < kFmCols) out[static_cast<size_t>(c) * dim + feat] = acc[b][reg];
+    }
+    const float tt = tacc[b] + __shfl_xor(tacc[b], 32, kWave);
+    if (h == 0) out[static_cast<size_t>(kFmCols) * dim + feat] = tt;
+  }
+}
+
+}  // namespace
+
+size_t FmForwardSharedBytes(int dim) {
+  return static_cast<size_t>(kFmCols) * (dim + 8) * sizeof(__bf16) + static_cast<size_t>(dim) * 4;
+}
+
+void LaunchFmForward(const uint8_t* x, int64_t rows, int dim, const void* wt_bf16, const float* q,
+                     const float* bias, float sx, float* y, float* xv, int num_cus,
+                     hipStream_t stream) {
+  if (rows == 0) return;
+  const int64_t ntiles = (rows + 31) / 32;
+  const int64_t want = (ntiles + kFwdThreads / kWave - 1) / (kFwdThreads / kWave);
+  const int64_t cap = static_cast<int64_t>(num_cus) * 4;  // persistent: LDS [w | V] loaded once per CU slot
+  const int grid = static_cast<int>(want < cap ? want : cap);
+  hipLaunchKernelGGL(k_fm_fwd, dim3(grid), dim3(kFwdThreads), FmForwardSharedBytes(dim), stream, x,
+                     rows, dim, reinterpret_cast<const __bf16*>(wt_bf16), q, bias, sx, y, xv);
+}
+
+void LaunchFmBackward(const uint8_t* x, int64_t rows, int dim, const float* g, const float* xv,
+                      int nblocks, float* part, hipStream_t stream) {
+  if (rows == 0 || nblocks == 0) return;
+  const int64_t per = (((rows + nblocks - 1) / nblocks) + 31) / 32 * 32;
+  hipLaunchKernelGGL(k_fm_bwd, dim3(nblocks, (dim + 1023) / 1024), dim3(kBwdThreads), 0, stream, x,
+                     rows, dim, g, xv, per, part);
+}
+
+}  // namespace gpu
+}  // namespace dmlc

@@ -297,6 +297,28 @@ void LaunchCSRSpMV(const uint64_t* offset, const IndexType* index, const float* 
 template <typename IndexType>
 void LaunchCSRSpMVT(const uint64_t* offset, const IndexType* index, const float* value,
                     size_t nrows, const float* d, float* g, hipStream_t stream);
+// ------------------------ HashedFM (fm_kernels.hip) ------------------------
+/*! \brief factor rank of the HIP HashedFM kernels and the [w | V] column count */
+constexpr int kFmRank = 16;
+constexpr int kFmCols = kFmRank + 1;
+/*! \brief dynamic LDS of LaunchFmForward for `dim` features */
+size_t FmForwardSharedBytes(int dim);
+/*!
+ * \brief F1: y[r] = bias + sx x_r.w + 1/2 (|sx x_r V|^2 - sx^2 x_r^2.q) and
+ *  xv[r] = sx x_r V for the fp8 e4m3 batch x [rows x dim]; wt_bf16 = [w | V]^T
+ *  as bf16 [17 x dim], q[n] = sum_f V_nf^2.  dim: multiple of 128, <= 2048.
+ */
+void LaunchFmForward(const uint8_t* x, int64_t rows, int dim, const void* wt_bf16, const float* q,
+                     const float* bias, float sx, float* y, float* xv, int num_cus,
+                     hipStream_t stream);
+/*!
+ * \brief F2: per-block partials part[nblocks][18][dim] of Z = G^T x (G_r =
+ *  [g_r, g_r xv_r], rows 0..16) and t = (x^2)^T g (row 17); the caller sums
+ *  over blocks.  dim: multiple of 128.
+ */
+void LaunchFmBackward(const uint8_t* x, int64_t rows, int dim, const float* g, const float* xv,
+                      int nblocks, float* part, hipStream_t stream);
+
 /*! \brief K10: dst_offset[i] = src_offset[i] - src_base + dst_base for i<=nrows */
 void LaunchOffsetRebase(const uint64_t* src_offset, size_t nrows, uint64_t src_base,
                         uint64_t dst_base, uint64_t* dst_offset, hipStream_t stream);

@@ -678,6 +678,31 @@ PYBIND11_MODULE(_dmlc, m) {
   // ---- HIP feature kernels on raw device pointers (torch tensors' data_ptr) ----
   auto stream_of = [](uintptr_t s) { return reinterpret_cast<hipStream_t>(s); };
   m.def(
+      "fm_forward",
+      [stream_of](uintptr_t x, int64_t rows, int dim, uintptr_t wt, uintptr_t q, uintptr_t bias,
+                  float sx, uintptr_t y, uintptr_t xv, int num_cus, uintptr_t stream) {
+        CHECK(dim > 0 && dim % 128 == 0 && dim <= 2048)
+            << "HashedFM kernels need dim a multiple of 128, <= 2048 (got " << dim << ")";
+        gpu::LaunchFmForward(reinterpret_cast<const uint8_t*>(x), rows, dim,
+                             reinterpret_cast<const void*>(wt), reinterpret_cast<const float*>(q),
+                             reinterpret_cast<const float*>(bias), sx, reinterpret_cast<float*>(y),
+                             reinterpret_cast<float*>(xv), num_cus, stream_of(stream));
+      },
+      py::arg("x"), py::arg("rows"), py::arg("dim"), py::arg("wt"), py::arg("q"), py::arg("bias"),
+      py::arg("sx"), py::arg("y"), py::arg("xv"), py::arg("num_cus"), py::arg("stream"));
+  m.def(
+      "fm_backward",
+      [stream_of](uintptr_t x, int64_t rows, int dim, uintptr_t g, uintptr_t xv, int nblocks,
+                  uintptr_t part, uintptr_t stream) {
+        CHECK(dim > 0 && dim % 128 == 0) << "HashedFM kernels need dim a multiple of 128";
+        gpu::LaunchFmBackward(reinterpret_cast<const uint8_t*>(x), rows, dim,
+                              reinterpret_cast<const float*>(g), reinterpret_cast<const float*>(xv),
+                              nblocks, reinterpret_cast<float*>(part), stream_of(stream));
+      },
+      py::arg("x"), py::arg("rows"), py::arg("dim"), py::arg("g"), py::arg("xv"),
+      py::arg("nblocks"), py::arg("part"), py::arg("stream"));
+  m.attr("fm_rank") = gpu::kFmRank;
+  m.def(
       "spmv",
       [stream_of](uintptr_t offset, uintptr_t index, uintptr_t value, size_t nrows, uintptr_t w,
                   float bias, uintptr_t y, uintptr_t stream, bool index64) {

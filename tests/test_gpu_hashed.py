@@ -103,8 +103,8 @@ def test_hashed_fm_on_fused_fp8_batch(dataset):
     x = b["x"].float() / scale
     ref = HashedFM.reference(x, model.w.detach(), model.v.detach(), model.bias.detach())
     err = (y.detach() - ref).abs().max().item() / (ref.abs().max().item() + 1e-6)
-    assert model.gemm in ("fp8", "bf16")
-    assert err < 0.05, (err, model.gemm)  # fp8 weights + bf16 interaction term
+    assert model.gemm == "hip_mfma_bf16"
+    assert err < 0.05, (err, model.gemm)  # bf16 [w | V] operand
     loss = torch.nn.functional.binary_cross_entropy_with_logits(y, b["label"].clamp(0, 1))
     loss.backward()
     assert model.w.grad is not None and torch.isfinite(model.w.grad).all()
@@ -148,3 +148,39 @@ def test_hashed_strategies_agree(dataset, dim):
                                    rtol=1e-6, atol=1e-6)
     with pytest.raises(ValueError):
         data.GPUParser(p, format=fmt).parse_all_hashed(dim, strategy="nope")
+
+
+@pytest.mark.parametrize("dim,rows", [(128, 37), (512, 1000), (1024, 4133)])
+def test_fm_kernels_match_fp32(dim, rows):
+    """F1 / F2 (bf16 MFMA over the fp8 batch) against fp32 autograd of the same
+    model: x is exact in bf16, [w | V] is rounded to bf16 for the x.[w | V]
+    product (the kernel's operand), x^2.q and the epilogue stay f32; the
+    backward's G = [g, g xV] operand is bf16, hence the looser gradient bound."""
+    torch.manual_seed(dim + rows)
+    dev = "cuda"
+    x8 = (torch.randn(rows, dim, device=dev) * 2).to(torch.float8_e4m3fn)
+    x8[:, ::7] = 0  # sparse-ish, like a hashed batch
+    scale = 0.5
+    model = HashedFM(dim=dim, rank=16).to(dev)
+    with torch.no_grad():
+        model.w.normal_(0, 0.05)
+        model.v.normal_(0, 0.05)
+        model.bias.fill_(0.3)
+    r = torch.randn(rows, device=dev)
+    y = model(x8, scale=scale)
+    assert model.gemm == "hip_mfma_bf16"
+    (y * r).sum().backward()
+    x = x8.float() / scale
+    w = model.w.detach().clone().requires_grad_(True)
+    v = model.v.detach().clone().requires_grad_(True)
+    b = model.bias.detach().clone().requires_grad_(True)
+    wb = w.detach().to(torch.bfloat16).float() + (w - w.detach())  # bf16 values, fp32 grads
+    vb = v.detach().to(torch.bfloat16).float() + (v - v.detach())
+    xv = x @ vb
+    ref = b + (x @ wb).squeeze(-1) + 0.5 * ((xv ** 2).sum(-1) - (x ** 2) @ (v ** 2).sum(1))
+    (ref * r).sum().backward()
+    tol = ref.detach().abs().max().item()
+    assert (y.detach() - ref.detach()).abs().max().item() <= 1e-4 * tol + 1e-5
+    for got, want in ((model.w.grad, w.grad), (model.v.grad, v.grad), (model.bias.grad, b.grad)):
+        err = (got - want).abs().max().item() / (want.abs().max().item() + 1e-6)
+        assert err < 2e-2, err
