@@ -4,7 +4,7 @@
 #                      dmlc_core_amd/_dmlc*.so      (pybind11 module)
 #   make test-bin   -> build/dmlc_unittest           (C++ unit tests, no GPU needed)
 #   make tools      -> build/dmlc_gen, build/dmlc_bench_cpu, build/dmlc_recordio_dist,
-#                      build/dmlc_fs, build/dmlc_recordio
+#                      build/dmlc_fs, build/dmlc_recordio, build/dmlc_objserver
 #
 # Host code: g++ -std=c++17 -O3 -fopenmp -ffp-contract=off (bit-exact parsing).
 # Device code: hipcc --offload-arch=gfx950 (CDNA4 only; no other targets).
@@ -120,8 +120,13 @@ $(BUILD)/dmlc_gpu_api_check: tools/dmlc_gpu_api_check.cc $(LIB) $(HEADERS)
 	$(CXX) $(CXXFLAGS_BASE) $< -o $@ -L$(LIBDIR) -ldmlc -Wl,-rpath,$(abspath $(LIBDIR)) \
 	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64
 
+# loopback S3 / HTTP object server (sendfile) for the remote-reader benchmarks
+$(BUILD)/dmlc_objserver: tools/dmlc_objserver.cc
+	@mkdir -p $(BUILD)
+	$(CXX) -std=c++17 -O2 -Wall -pthread $< -o $@
+
 tools: $(BUILD)/dmlc_parameter_example $(BUILD)/dmlc_gen $(BUILD)/dmlc_bench_cpu $(BUILD)/dmlc_recordio_dist $(BUILD)/dmlc_fs \
-  $(BUILD)/dmlc_recordio $(BUILD)/dmlc_gpu_api_check
+  $(BUILD)/dmlc_recordio $(BUILD)/dmlc_gpu_api_check $(BUILD)/dmlc_objserver
 
 clean:
 	rm -rf $(BUILD) $(LIB) $(PYMOD)

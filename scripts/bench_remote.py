@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""BASELINE config 4 throughput: s3:// (and http://) objects -> parallel ranged
+GETs -> pinned-host ring -> HIP tile parser -> CSR in HBM, on one GPU.
+
+The objects are served over loopback by tools/dmlc_objserver (sendfile from
+the page cache, so the server is not the bound); the same files parsed from
+local disk give the reference point.  Each configuration runs one warm epoch
+and then --epochs timed epochs of GPUParser.parse_all; the parser's ring
+statistics split the time into waiting for the reader (wait_reader_sec: the
+network / storage side is the bound) and waiting for the GPU (wait_gpu_sec).
+Prints one JSON object.
+
+usage: python scripts/bench_remote.py [--rows N] [--files F] [--epochs E]
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=2_000_000)
+    ap.add_argument("--files", type=int, default=8)
+    ap.add_argument("--epochs", type=int, default=3)
+    ap.add_argument("--threads", default="8,16,32", help="read_threads values for s3://")
+    ap.add_argument("--data", default="/tmp/dmlc_remote_bench")
+    args = ap.parse_args()
+
+    import torch
+
+    from dmlc_core_amd import data
+
+    bucket = os.path.join(args.data, "bench", "train")
+    os.makedirs(bucket, exist_ok=True)
+    per = args.rows // args.files
+    for i in range(args.files):
+        f = os.path.join(bucket, f"part-{i:03d}.libsvm")
+        if not os.path.exists(f):
+            data.write_synthetic(f + ".tmp", i * per, (i + 1) * per, format="libsvm", seed=3,
+                                 nthread=16)
+            os.replace(f + ".tmp", f)
+    nbytes = sum(os.path.getsize(os.path.join(bucket, x)) for x in os.listdir(bucket))
+    srv = subprocess.Popen([os.path.join(ROOT, "build", "dmlc_objserver"), "--root", args.data],
+                           stdout=subprocess.PIPE, text=True)
+    try:
+        port = int(srv.stdout.readline().split()[1])
+        os.environ.update({"S3_ENDPOINT": f"http://127.0.0.1:{port}", "S3_ACCESS_KEY_ID": "bench",
+                           "S3_SECRET_ACCESS_KEY": "bench", "S3_REGION": "us-east-1"})
+        runs = [("local", bucket + "/", 8)]
+        runs += [("s3", "s3://bench/train/", int(t)) for t in args.threads.split(",") if t]
+        runs.append(("http_one_file", f"http://127.0.0.1:{port}/bench/train/part-000.libsvm", 16))
+        out = {"rows": args.rows, "files": args.files, "bytes": nbytes, "epochs": args.epochs,
+               "server": "tools/dmlc_objserver (loopback, sendfile)", "runs": []}
+        for name, uri, threads in runs:
+            gp = data.GPUParser(uri, format="libsvm", read_threads=threads)
+            csr = data.DeviceCSR()
+            gp.parse_all(csr)  # warm epoch: page cache, pinned ring, output reserve
+            torch.cuda.synchronize()
+            s0 = gp.stats()
+            t0 = time.perf_counter()
+            rows = 0
+            for _ in range(args.epochs):
+                gp.before_first()
+                csr.clear()
+                gp.parse_all(csr)
+                rows += csr.rows
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            s1 = gp.stats()
+            part = nbytes if name != "http_one_file" else os.path.getsize(
+                os.path.join(bucket, "part-000.libsvm"))
+            rec = {"name": name, "uri": uri, "read_threads": threads,
+                   "sec_per_epoch": round(dt / args.epochs, 4),
+                   "rows_per_sec": round(rows / dt, 1),
+                   "GBps": round(part * args.epochs / dt / 1e9, 3),
+                   "wait_reader_sec_per_epoch": round((s1["wait_reader_sec"] - s0["wait_reader_sec"]) / args.epochs, 4),
+                   "wait_gpu_sec_per_epoch": round((s1["wait_gpu_sec"] - s0["wait_gpu_sec"]) / args.epochs, 4),
+                   "zero_copy": s1.get("zero_copy")}
+            out["runs"].append(rec)
+            print(json.dumps(rec), file=sys.stderr, flush=True)
+        print(json.dumps(out), flush=True)
+    finally:
+        srv.kill()
+        srv.wait()
+
+
+if __name__ == "__main__":
+    main()
