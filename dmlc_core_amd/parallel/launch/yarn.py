@@ -13,6 +13,10 @@ Two ways to reach a cluster:
   ApplicationMaster's policy to the containers the service reports
   (`yarn_am.py`): a memory-limit kill aborts the job, other failures are
   retried by YARN up to DMLC_MAX_ATTEMPT, and more than that aborts.
+  ``--files`` / ``--archives`` (and auto-cached command files) are uploaded
+  through the WebHDFS backend to ``$DMLC_YARN_STAGING/<job>/`` and localised
+  in the spec (`stage_files`), as the reference Client does with -file /
+  -archive.
 """
 from __future__ import annotations
 
@@ -66,15 +70,74 @@ _MEMORY_KILL = ("beyond physical memory", "beyond virtual memory",
                 "exceeding allocated physical", "exceeding allocated virtual")
 
 
-def service_spec(args, envs: Dict[str, object], name: str) -> dict:
+def staging_root(args) -> Optional[str]:
+    """Where -file / -archive payloads are staged for the service containers:
+    ``$DMLC_YARN_STAGING`` (any writable dmlc URI, e.g.
+    ``webhdfs://nn:9870/user/me/.dmlc``), else ``--hdfs-tempdir`` on the
+    WebHDFS endpoint ``$DMLC_WEBHDFS_ENDPOINT``."""
+    root = os.environ.get("DMLC_YARN_STAGING", "")
+    if root:
+        return root.rstrip("/")
+    ep = os.environ.get("DMLC_WEBHDFS_ENDPOINT", "")
+    if ep:
+        ep = ep.split("://", 1)[-1].rstrip("/")
+        return f"webhdfs://{ep}/{args.hdfs_tempdir.strip('/')}"
+    return None
+
+
+def _cluster_path(uri: str) -> str:
+    """webhdfs://host:port/a/b -> /a/b (the path YARN resolves on its default FS)."""
+    if "://" not in uri:
+        return uri
+    rest = uri.split("://", 1)[1]
+    return "/" + rest.split("/", 1)[1] if "/" in rest else "/"
+
+
+def stage_files(args, name: str, upload: bool = True) -> List[dict]:
+    """Ship the job's files like the reference Client (`Client.java:122-160`:
+    copy every -file / -archive into the job's HDFS temp dir and localise it
+    in each container): upload them through the native filesystem layer (the
+    WebHDFS backend, no JVM) under ``<staging>/<name>/`` and return the YARN
+    Services ``configuration.files`` entries -- STATIC for files, ARCHIVE
+    (unpacked into a directory of the same name) for archives."""
+    fset, _ = get_cache_file_set(args)
+    items = [(f, "STATIC") for f in sorted(fset)] + [(a, "ARCHIVE") for a in args.archives]
+    if not items:
+        return []
+    root = staging_root(args)
+    if root is None:
+        raise SystemExit("YARN services submission ships files through HDFS: set DMLC_YARN_STAGING "
+                         "(e.g. webhdfs://namenode:9870/user/<me>/.dmlc) or DMLC_WEBHDFS_ENDPOINT")
+    entries = []
+    for local, kind in items:
+        base = os.path.basename(local.rstrip("/"))
+        dst = f"{root}/{name}/{base}"
+        if upload:
+            from ... import io as dio
+            out = dio.Stream(dst, "w")
+            with open(local, "rb") as f:
+                while True:
+                    buf = f.read(16 << 20)
+                    if not buf:
+                        break
+                    out.write(buf)
+            out.close()
+        entries.append({"type": kind, "src_file": _cluster_path(dst), "dest_file": base})
+    return entries
+
+
+def service_spec(args, envs: Dict[str, object], name: str,
+                 files: Optional[List[dict]] = None) -> dict:
     """YARN Services spec: a `worker` (and `server`) component, one container
-    per task, restart on failure up to DMLC_MAX_ATTEMPT - 1 times."""
+    per task, restart on failure up to DMLC_MAX_ATTEMPT - 1 times; `files`
+    (from `stage_files`) are localised into every container."""
     _, cmd = get_cache_file_set(args)
     max_attempt = int(os.environ.get("DMLC_MAX_ATTEMPT", "3"))
     env = {k: str(v) for k, v in envs.items()}
     env.update({k: str(v) for k, v in user_envs(args).items()})
     env.update({"DMLC_JOB_CLUSTER": "yarn", "DMLC_NUM_WORKER": str(args.num_workers),
-                "DMLC_NUM_SERVER": str(args.num_servers)})
+                "DMLC_NUM_SERVER": str(args.num_servers),
+                "DMLC_JOB_ARCHIVES": ":".join(os.path.basename(a) for a in args.archives)})
     comps = []
     for role, n, cores, mem in (("worker", args.num_workers, args.worker_cores, args.worker_memory),
                                 ("server", args.num_servers, args.server_cores, args.server_memory)):
@@ -88,7 +151,8 @@ def service_spec(args, envs: Dict[str, object], name: str) -> dict:
             "resource": res, "restart_policy": "ON_FAILURE",
             "configuration": {
                 "env": dict(env, DMLC_ROLE=role),
-                "properties": {"yarn.service.container-failure.retry.max": str(max_attempt - 1)}},
+                "properties": {"yarn.service.container-failure.retry.max": str(max_attempt - 1)},
+                "files": [dict(f) for f in (files or [])]},
         })
     return {"name": name, "version": "1.0", "queue": args.queue, "components": comps}
 
@@ -188,9 +252,12 @@ def submit(args):
 def submit_service(args, rm: str):
     """JVM-free path: the tracker runs here, tasks run in YARN service containers."""
     name = (args.jobname or "dmlc") + f"-{os.getpid()}"
+    staged: List[dict] = []
 
     def launch(nworker, nserver, envs):
-        spec = service_spec(args, envs, name)
+        if not staged:
+            staged.extend(stage_files(args, name, upload=not args.dry_run))
+        spec = service_spec(args, envs, name, staged)
         if args.dry_run:
             print(json.dumps(spec, indent=1, sort_keys=True))
             return

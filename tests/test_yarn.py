@@ -182,3 +182,63 @@ def test_submit_dry_run_uses_services_api_without_jar(monkeypatch, capsys):
     spec = json.loads(capsys.readouterr().out)
     assert {c["name"] for c in spec["components"]} == {"worker", "server"}
     assert spec["queue"] == "default"
+
+
+def test_service_stages_files_and_archives_through_webhdfs(rm, tmp_path, monkeypatch):
+    """-file / -archive shipping (reference Client.java:122-160) on the
+    Services path: payloads go through the native WebHDFS backend (namenode
+    redirect -> datanode, no body to the namenode) into the staging dir, and
+    every component localises them (STATIC files, ARCHIVE unpacked)."""
+    import tarfile
+
+    import mock_remote
+    mock_remote.WebHdfsHandler.store = {}
+    mock_remote.WebHdfsHandler.namenode_bodies = 0
+    srv = mock_remote.serve(mock_remote.WebHdfsHandler)
+    try:
+        addr = f"127.0.0.1:{srv.server_address[1]}"
+        monkeypatch.setenv("DMLC_YARN_STAGING", f"webhdfs://{addr}/user/alice/.dmlc/")
+        script = tmp_path / "train_job.py"
+        script.write_text("print('hi')\n")
+        blob = tmp_path / "vocab.bin"
+        blob.write_bytes(bytes(range(256)) * 4096)
+        (tmp_path / "env").mkdir()
+        (tmp_path / "env" / "cfg.txt").write_text("x=1\n")
+        arc = tmp_path / "env.tar.gz"
+        with tarfile.open(arc, "w:gz") as t:
+            t.add(tmp_path / "env", arcname="env")
+        args = get_opts(["--cluster", "yarn", "--num-workers", "2", "--files", str(blob),
+                         "--archives", str(arc), "python", str(script), "--epochs", "3"])
+        entries = yarn.stage_files(args, "job-7")
+        job = yarn.YarnServiceJob(rm, "job-7")
+        job.submit(yarn.service_spec(args, {}, "job-7", entries))
+        store = mock_remote.WebHdfsHandler.store
+        base = "/user/alice/.dmlc/job-7/"
+        assert store[base + "train_job.py"] == script.read_bytes()
+        assert store[base + "vocab.bin"] == blob.read_bytes()
+        assert store[base + "env.tar.gz"] == arc.read_bytes()
+        assert mock_remote.WebHdfsHandler.namenode_bodies == 0
+        comp = _RM.services["job-7"]["components"][0]
+        files = {f["dest_file"]: f for f in comp["configuration"]["files"]}
+        assert files["train_job.py"] == {"type": "STATIC", "src_file": base + "train_job.py",
+                                         "dest_file": "train_job.py"}
+        assert files["vocab.bin"]["type"] == "STATIC"
+        assert files["env.tar.gz"] == {"type": "ARCHIVE", "src_file": base + "env.tar.gz",
+                                       "dest_file": "env.tar.gz"}
+        assert comp["launch_command"] == "python ./train_job.py --epochs 3"
+        assert comp["configuration"]["env"]["DMLC_JOB_ARCHIVES"] == "env.tar.gz"
+    finally:
+        srv.shutdown()
+
+
+def test_service_staging_requires_a_target(monkeypatch, tmp_path):
+    monkeypatch.delenv("DMLC_YARN_STAGING", raising=False)
+    monkeypatch.delenv("DMLC_WEBHDFS_ENDPOINT", raising=False)
+    f = tmp_path / "a.txt"
+    f.write_text("1")
+    args = get_opts(["--cluster", "yarn", "--num-workers", "1", "--files", str(f), "true"])
+    with pytest.raises(SystemExit, match="DMLC_YARN_STAGING"):
+        yarn.stage_files(args, "j")
+    monkeypatch.setenv("DMLC_WEBHDFS_ENDPOINT", "http://nn:9870")
+    assert yarn.staging_root(args) == "webhdfs://nn:9870/tmp"
+    assert yarn.stage_files(args, "j", upload=False)[0]["src_file"] == "/tmp/j/a.txt"
