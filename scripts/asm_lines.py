@@ -23,7 +23,8 @@ for l in s[start:end]:
     t = l.strip()
     if l.startswith("\t") and not t.startswith((".", ";")):
         op = t.split()[0]
-        k = "V" if op.startswith("v_") else "S" if op.startswith("s_") else "D" if op.startswith("ds_") else "M"
+        k = ("V" if op.startswith("v_") else "S" if op.startswith("s_")
+             else "D" if op.startswith("ds_") else "M")
         tot[cur] += 1
         kinds[cur][k] += 1
 src = {}

@@ -13,7 +13,8 @@ c = collections.Counter(x.split()[0] for x in ins)
 print(s[start][:120])
 print("static instructions", len(ins))
 print("VALU", sum(v for k, v in c.items() if k.startswith("v_")),
-      "SALU", sum(v for k, v in c.items() if k.startswith("s_") and not k.startswith(("s_waitcnt", "s_cbranch", "s_branch"))),
+      "SALU", sum(v for k, v in c.items()
+                  if k.startswith("s_") and not k.startswith(("s_waitcnt", "s_cbranch", "s_branch"))),
       "DS", sum(v for k, v in c.items() if k.startswith("ds_")),
       "VMEM", sum(v for k, v in c.items() if k.startswith(("global_", "buffer_", "flat_"))),
       "branches", sum(v for k, v in c.items() if "branch" in k))

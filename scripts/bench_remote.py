@@ -79,8 +79,10 @@ def main():
                    "sec_per_epoch": round(dt / args.epochs, 4),
                    "rows_per_sec": round(rows / dt, 1),
                    "GBps": round(part * args.epochs / dt / 1e9, 3),
-                   "wait_reader_sec_per_epoch": round((s1["wait_reader_sec"] - s0["wait_reader_sec"]) / args.epochs, 4),
-                   "wait_gpu_sec_per_epoch": round((s1["wait_gpu_sec"] - s0["wait_gpu_sec"]) / args.epochs, 4),
+                   "wait_reader_sec_per_epoch": round(
+                       (s1["wait_reader_sec"] - s0["wait_reader_sec"]) / args.epochs, 4),
+                   "wait_gpu_sec_per_epoch": round(
+                       (s1["wait_gpu_sec"] - s0["wait_gpu_sec"]) / args.epochs, 4),
                    "zero_copy": s1.get("zero_copy")}
             out["runs"].append(rec)
             print(json.dumps(rec), file=sys.stderr, flush=True)

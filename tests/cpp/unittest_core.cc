@@ -428,7 +428,8 @@ TEST(Parameter, UpdateOptionalBoolAndDocs) {
   // optional<int> with enums: "None" empties it and prints back as None
   p.Init(std::map<std::string, std::string>{{"name", "a"}, {"maybe", "None"}, {"flag", " FALSE"}});
   EXPECT_FALSE(p.maybe.has_value());
-  EXPECT_EQ(p.__DICT__()["maybe"], "None");
+  const auto dict = p.__DICT__();  // the EXPECT macros bind references: keep the map alive
+  EXPECT_EQ(dict.at("maybe"), "None");
   EXPECT_FALSE(*p.flag);
   // trailing garbage after a number is an error; trailing blanks are not
   EXPECT_THROW(p.Init(std::map<std::string, std::string>{{"name", "a"}, {"nthread", "3x"}}),

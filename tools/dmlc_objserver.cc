@@ -187,16 +187,22 @@ bool Serve(int fd, const std::string& method, const std::string& target,
     const std::string spec = r->second.substr(6);
     const size_t dash = spec.find('-');
     b = std::strtoull(spec.substr(0, dash).c_str(), nullptr, 10);
-    if (dash + 1 < spec.size()) e = std::min<uint64_t>(e, std::strtoull(spec.c_str() + dash + 1, nullptr, 10));
+    if (dash + 1 < spec.size()) {
+      e = std::min<uint64_t>(e, std::strtoull(spec.c_str() + dash + 1, nullptr, 10));
+    }
     ranged = true;
     if (b >= size) {
       ::close(f);
-      return Reply(fd, 416, "Range Not Satisfiable", "", {"Content-Range: bytes */" + std::to_string(size)}, head);
+      return Reply(fd, 416, "Range Not Satisfiable", "",
+                   {"Content-Range: bytes */" + std::to_string(size)}, head);
     }
   }
   const uint64_t len = size == 0 ? 0 : e - b + 1;
   std::string h = ranged ? "HTTP/1.1 206 Partial Content\r\n" : "HTTP/1.1 200 OK\r\n";
-  if (ranged) h += "Content-Range: bytes " + std::to_string(b) + "-" + std::to_string(e) + "/" + std::to_string(size) + "\r\n";
+  if (ranged) {
+    h += "Content-Range: bytes " + std::to_string(b) + "-" + std::to_string(e) + "/" +
+         std::to_string(size) + "\r\n";
+  }
   h += "Accept-Ranges: bytes\r\nContent-Length: " + std::to_string(len) + "\r\n\r\n";
   bool ok = SendAll(fd, h.data(), h.size());
   if (ok && !head) {
