@@ -16,7 +16,7 @@ import torch
 
 from .. import _dmlc
 
-__all__ = ["spmv", "spmv_t", "hashed_dense", "SpMVFunction", "csr_spmv"]
+__all__ = ["spmv", "spmv_t", "hashed_dense", "SpMVFunction", "csr_spmv", "transpose"]
 
 
 def _ptr(t) -> int:
@@ -84,25 +84,65 @@ def hashed_dense(csr: Dict, dim: int, seed: int = 0, fp8: bool = True,
     return out
 
 
+def transpose(csr: Dict, num_features: int) -> Dict:
+    """The CSR's transpose (CSC / inverted index) on the device, as a
+    CSR-shaped dict whose rows are the features: ``offset`` int64
+    [num_features + 1], ``index`` int32 row ids, ``value`` (or None).
+
+    Built once with a stable device sort of the feature ids, it turns the
+    gradient X^T d into a gather SpMV (K11 over the transpose): every output
+    is summed on chip and written once, instead of one memory-side f32
+    atomic per nonzero, which runs ~17x below the contiguous atomic rate when
+    64 lanes hit 64 different rows (MI355X_MICROARCH.md, Global float
+    atomics).  Feature ids must be < 2^31."""
+    _check(csr)
+    offset, index, value = csr["offset"], csr["index"], csr.get("value")
+    nrows, nnz, dev = offset.numel() - 1, index.numel(), index.device
+    off = offset.view(torch.int64) if offset.dtype != torch.int64 else offset
+    counts = off[1:] - off[:-1]
+    rows = torch.repeat_interleave(torch.arange(nrows, dtype=torch.int32, device=dev), counts,
+                                   output_size=nnz)
+    key = index.view(torch.int32) if index.element_size() == 4 else index.view(torch.int64)
+    skey, perm = torch.sort(key, stable=True)
+    bounds = torch.arange(num_features + 1, dtype=skey.dtype, device=dev)
+    col_ptr = torch.searchsorted(skey, bounds).to(torch.int64)
+    return {"offset": col_ptr.contiguous(), "index": rows[perm].contiguous(),
+            "value": value[perm].contiguous() if value is not None else None}
+
+
 class SpMVFunction(torch.autograd.Function):
-    """Autograd wrapper: forward = spmv, backward d/dw = spmv_t."""
+    """Autograd wrapper: forward = spmv, backward d/dw = X^T g -- a gather
+    SpMV over the cached transpose (``csr['transpose']``, built on the first
+    backward) when ``grad == "transpose"``, else the f32-atomic spmv_t."""
 
     @staticmethod
-    def forward(ctx, w, bias, csr_tuple):
+    def forward(ctx, w, bias, csr_tuple, holder, grad):
         offset, index, value = csr_tuple
-        csr = {"offset": offset, "index": index, "value": value}
-        ctx.csr = csr
+        ctx.csr = {"offset": offset, "index": index, "value": value}
+        ctx.holder, ctx.grad = holder, grad
         ctx.num_features = w.numel()
-        return spmv(csr, w, 0.0) + bias
+        return spmv(ctx.csr, w, 0.0) + bias
 
     @staticmethod
     def backward(ctx, grad_out):
         grad_out = grad_out.contiguous().float()
-        gw = spmv_t(ctx.csr, grad_out, ctx.num_features)
+        if ctx.grad == "transpose":
+            t = ctx.holder.get("transpose")
+            if t is None or t["offset"].numel() != ctx.num_features + 1:
+                t = transpose(ctx.csr, ctx.num_features)
+                ctx.holder["transpose"] = t
+            gw = spmv(t, grad_out, 0.0)
+        else:
+            gw = spmv_t(ctx.csr, grad_out, ctx.num_features)
         gb = grad_out.sum().reshape(1)
-        return gw, gb, None
+        return gw, gb, None, None, None
 
 
-def csr_spmv(csr: Dict, w: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
-    """Differentiable y = X w + b for a device CSR batch."""
-    return SpMVFunction.apply(w, bias, (csr["offset"], csr["index"], csr.get("value")))
+def csr_spmv(csr: Dict, w: torch.Tensor, bias: torch.Tensor, grad: str = "transpose") -> torch.Tensor:
+    """Differentiable y = X w + b for a device CSR batch.  grad="transpose"
+    caches the CSR's transpose in ``csr['transpose']`` (one device sort) and
+    computes X^T g as a gather SpMV; grad="atomic" scatters with f32 atomics
+    (no extra memory, ~10x slower on a 10 M x 1 M batch)."""
+    if grad not in ("transpose", "atomic"):
+        raise ValueError(f"grad must be 'transpose' or 'atomic', got {grad!r}")
+    return SpMVFunction.apply(w, bias, (csr["offset"], csr["index"], csr.get("value")), csr, grad)
