@@ -646,13 +646,15 @@ __device__ __noinline__ void generic_token(const uint8_t* __restrict__ text, siz
  *  from global memory (bit-identical by construction).
  */
 constexpr int kFillWaves = kThreads / 64;
+constexpr uint32_t kDecodeCarry = 64;  // tokens a step may leave for the next one's rounds
 #ifndef DMLC_FILL_WAVES
 #define DMLC_FILL_WAVES 4  // measured best (profiles/r03_fill_ablation)
 #endif
 constexpr uint32_t kStepBytes = 2048;
 constexpr int kSteps = static_cast<int>(kTileBytes / kStepBytes);
-constexpr uint32_t kStageVecs = (kStepBytes + 64) / 16;   // a step + 64 B of the next
-constexpr uint32_t kListCap = kStepBytes / 2;              // tokens of a step, at most
+constexpr uint32_t kSlotBytes = kStepBytes + 64;           // a step + 64 B of the next
+constexpr uint32_t kStageVecs = 2 * kSlotBytes / 16;       // two slots: step s and s - 1
+constexpr uint32_t kListCap = kDecodeCarry + kStepBytes / 2;  // carried + a step's tokens
 
 /*!
  * \brief the 16 B at chunk offset pos, bytes at or past n zeroed (the
@@ -672,19 +674,21 @@ __device__ __forceinline__ uint4 load16_clip(const uint8_t* __restrict__ text, s
 
 /*!
  * \brief append the token starts of one lane's 16 B slice to the wave's list
- *  (`at` = its first list position; `line0` = line starts of the step before
- *  this slice).  An entry is  offset (11 bits) | line start (bit 11) | line
- *  ordinal in the step, this token's line included (bits 12..23), so a round
- *  can take the entries in any lane order.  The first two starts are written
- *  unconditionally -- a lane with fewer writes a private dummy slot past
- *  kListCap -- so the common case has no per-lane loop; slices with more
- *  starts (tokens shorter than 8 B) take the loop.
+ *  (`at` = its first list position; `line0` = line starts of the tile before
+ *  this slice).  An entry is  staging offset (13 bits: slot * kSlotBytes +
+ *  byte in the step) | line start (bit 13) | line ordinal in the tile, this
+ *  token's line included (bits 14..26), so a round can take the entries in
+ *  any lane order and a token can be decoded a step after it was listed.
+ *  The first two starts are written unconditionally -- a lane with fewer
+ *  writes a private dummy slot past kListCap -- so the common case has no
+ *  per-lane loop; slices with more starts (tokens shorter than 8 B) take the
+ *  loop.
  */
 __device__ __forceinline__ uint32_t list_entry(uint32_t tm_bit_j, uint32_t lm, uint32_t base,
                                                uint32_t line0) {
   const uint32_t j = tm_bit_j;
   const uint32_t upto = lm & ((2u << j) - 1u);  // line starts up to byte j of the slice
-  return (base + j) | (((lm >> j) & 1u) << 11) | ((line0 + __popc(upto)) << 12);
+  return (base + j) | (((lm >> j) & 1u) << 13) | ((line0 + __popc(upto)) << 14);
 }
 
 __device__ __forceinline__ void list_slice(uint32_t* sl, uint32_t tm, uint32_t lm, uint32_t at,
@@ -772,8 +776,9 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
   float* const wgt_at = out.weight != nullptr ? out.weight + R - 1 : nullptr;
   uint64_t* const qid_at = out.qid != nullptr ? out.qid + R - 1 : nullptr;
 
-  uint32_t tok_i = 0;  // tokens of this tile before the current step
+  uint32_t tok0 = 0;   // tile token ordinal of list position 0
   uint32_t lcnt = 0;   // line starts of this tile so far
+  uint32_t carry = 0;  // list entries left for the next step's rounds (listed, not decoded)
   uint64_t mx_index = 0, mx_field = 0;
   bool any_value = false, any_weight = false, irregular = false, neg = false, need_w = false;
 
@@ -791,10 +796,13 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
       if (!last) nb = load16_clip(text, nxt + 1024 + lane * 16, n);
     }
     if (last && lane >= 4) na = make_uint4(0, 0, 0, 0);
-    // ---- 2. stage the step (+ the next 64 B) and list its tokens
-    st[lane] = a;
-    st[64 + lane] = b;
-    if (lane < 4) st[128 + lane] = na;
+    // ---- 2. stage the step (+ the next 64 B) in slot s & 1 -- the other slot
+    // still holds step s - 1 for the tokens carried from it -- and list its tokens
+    const uint32_t sbase = (static_cast<uint32_t>(s) & 1u) * kSlotBytes;
+    uint4* const ss = st + sbase / 16;
+    ss[lane] = a;
+    ss[64 + lane] = b;
+    if (lane < 4) ss[128 + lane] = na;
     const size_t pos_a = tile0 + s * kStepBytes + lane * 16;
     const uint32_t left_a = __shfl_up(a.w >> 24, 1, dev::kWave);
     const uint32_t pc_a = lane == 0 ? carry_pc : left_a;
@@ -818,21 +826,27 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
     const uint32_t ntok = ntok_a + static_cast<uint32_t>((tot >> 16) & 0xFFFFu);
     const uint32_t nline_a = static_cast<uint32_t>((tot >> 32) & 0xFFFFu);
     const uint32_t nline = nline_a + static_cast<uint32_t>(tot >> 48);
-    list_slice(sl, tm_a, lm_a, static_cast<uint32_t>(before & 0xFFFFu), lane * 16,
-               static_cast<uint32_t>((before >> 32) & 0xFFFFu), lane);
-    list_slice(sl, tm_b, lm_b, ntok_a + static_cast<uint32_t>((before >> 16) & 0xFFFFu),
-               1024 + lane * 16, nline_a + static_cast<uint32_t>(before >> 48), lane);
+    list_slice(sl, tm_a, lm_a, carry + static_cast<uint32_t>(before & 0xFFFFu), sbase + lane * 16,
+               lcnt + static_cast<uint32_t>((before >> 32) & 0xFFFFu), lane);
+    list_slice(sl, tm_b, lm_b, carry + ntok_a + static_cast<uint32_t>((before >> 16) & 0xFFFFu),
+               sbase + 1024 + lane * 16, lcnt + nline_a + static_cast<uint32_t>(before >> 48), lane);
     dev::wave_sync();  // the staged text and the list are visible to every lane
 
-    // ---- 3. decode 64 listed tokens per round
-    for (uint32_t r0 = 0; r0 < (exp_mode == 3 ? 0u : ntok); r0 += dev::kWave) {
+    // ---- 3. decode 64 listed tokens per round.  Only whole rounds run: the
+    // rest of this step's tokens (< 64) wait for the next step's rounds, so a
+    // step does not pay a mostly idle last round; every older token is
+    // decoded now (its slot is restaged next step), and the last step takes all
+    const uint32_t total = carry + ntok;
+    const uint32_t rest = total % dev::kWave < ntok ? total % dev::kWave : ntok;
+    const uint32_t ndec = (last || exp_mode == 3) ? (exp_mode == 3 ? 0u : total) : total - rest;
+    for (uint32_t r0 = 0; r0 < ndec; r0 += dev::kWave) {
       const uint32_t li = r0 + slot;
-      const bool active = li < ntok;
+      const bool active = li < ndec;
       const uint32_t e = active ? sl[li] : 0u;
-      const bool is_label = active && ((e >> 11) & 1u) != 0;
-      const uint32_t off = e & 0x7FFu;  // 0 in idle lanes: they decode harmless bytes
-      const uint32_t lc = lcnt + (e >> 12);
-      const uint32_t i = tok_i + li;
+      const bool is_label = active && ((e >> 13) & 1u) != 0;
+      const uint32_t off = e & 0x1FFFu;  // 0 in idle lanes: they decode harmless bytes
+      const uint32_t lc = e >> 14;
+      const uint32_t i = tok0 + li;
       tok::Token t;
       t.u0_hi = t.u1_hi = 0;
       t.u1 = 0;
@@ -848,7 +862,12 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
         ok = tok::decode<F>(st, off, is_label, &t);
       }
       if (active & !ok) {
-        generic_token<F, IndexType>(text, n, tile0 + s * kStepBytes + off, is_label, &t, &bad);
+        // the step a slot holds: s, or s - 1 for a carried token
+        const uint32_t in_slot = off >= kSlotBytes ? 1u : 0u;
+        const int step = in_slot == (static_cast<uint32_t>(s) & 1u) ? s : s - 1;
+        generic_token<F, IndexType>(text, n, tile0 + static_cast<size_t>(step) * kStepBytes + off -
+                                                 in_slot * kSlotBytes,
+                                    is_label, &t, &bad);
       }
       const int32_t rel = static_cast<int32_t>(i) - static_cast<int32_t>(lc);
       const bool row_ok = static_cast<int64_t>(lc) - 1 < row_room;
@@ -889,7 +908,13 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
       }
       neg |= active && bad;
     }
-    tok_i += ntok;
+    // the undecoded rest moves to the front of the list (all lanes read before any writes)
+    const uint32_t left = exp_mode == 3 ? 0u : total - ndec;  // mode 3 decodes nothing
+    const uint32_t moved = lane < static_cast<int>(left) ? sl[ndec + lane] : 0u;
+    dev::wave_sync();
+    if (lane < static_cast<int>(left)) sl[lane] = moved;
+    tok0 += ndec;
+    carry = left;
     lcnt += nline;
     a = na;
     b = nb;
