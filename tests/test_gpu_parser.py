@@ -401,3 +401,20 @@ def test_two_level_scan_and_finish_on_large_chunks(tmp_path):
         256, seed=1, fp8=False, strategy="fused")
     np.testing.assert_allclose(big["x"].cpu().numpy(), small["x"].cpu().numpy(), rtol=1e-6, atol=1e-6)
     np.testing.assert_array_equal(big["label"].cpu().numpy(), c["label"])
+
+
+def test_replay_chunk_limit_is_enforced(tmp_path):
+    """Merged HBM-replay chunks must stay below the 32-bit offsets of the tile
+    scan and the exact path's line starts: an over-large replay_chunk_mb is
+    rejected up front, for text and for RecordIO."""
+    from dmlc_core_amd import io
+    p = str(tmp_path / "s.libsvm")
+    data.write_synthetic(p, 0, 100, seed=1)
+    with pytest.raises(Exception, match="replay_chunk_bytes"):
+        data.GPUParser(p, hbm_cache=1, replay_chunk_mb=4096)
+    r = str(tmp_path / "s.rec")
+    w = io.RecordIOWriter(r)
+    w.write(b"abc")
+    w.close()
+    with pytest.raises(Exception, match="replay_chunk_bytes"):
+        io.GPURecordIO(r, hbm_cache=1, replay_chunk_mb=8192)
