@@ -956,6 +956,7 @@ constexpr int kHashSegs = (static_cast<int>(kTileBytes) + kHashExt) / 4096;
 constexpr int kHashRows = 4;                              // rows built per LDS round
 constexpr unsigned kHashOffBits = 14;                     // staged offset < 12288
 constexpr uint32_t kHashMaxTok = 3072;  // listed tokens per tile (more: exact kernel)
+constexpr uint32_t kHashMaxRows = 1024;  // owned rows per tile on the wave-per-row path
 
 template <TextFormat F, typename IndexType, bool kFP8>
 __global__ __launch_bounds__(kThreads) void k_tile_hash(const uint8_t* __restrict__ text, size_t n,
@@ -968,6 +969,7 @@ __global__ __launch_bounds__(kThreads) void k_tile_hash(const uint8_t* __restric
   __shared__ uint32_t s_tok[kHashMaxTok];
   __shared__ uint32_t s_scan[4];
   __shared__ uint32_t s_end;  // staged offset where the owned region ends
+  __shared__ uint16_t s_row_first[kHashMaxRows + 1];  // list index of each owned row's label
   extern __shared__ __attribute__((aligned(16))) float s_rows[];
   const uint8_t* lds = reinterpret_cast<const uint8_t*>(s_text);
   const size_t tile0 = static_cast<size_t>(blockIdx.x) * kTileBytes;
@@ -1106,6 +1108,11 @@ __global__ __launch_bounds__(kThreads) void k_tile_hash(const uint8_t* __restric
       const uint32_t i = threadIdx.x + k * kThreads;
       vals[k] = 0.0f;
       if (i < ntok) {
+        const uint32_t e = s_tok[i];
+        const uint32_t lc = (e >> kHashOffBits) & 0x1FFFu;
+        if ((e >> 31) != 0 && lc != 0 && lc <= kHashMaxRows && (e & ((1u << kHashOffBits) - 1)) < lim) {
+          s_row_first[lc - 1] = static_cast<uint16_t>(i);  // row lc - 1 starts at its label
+        }
         uint32_t res;
         decode(i, &res, &vals[k]);
         s_tok[i] = res;  // same lane reads and rewrites entry i
@@ -1118,7 +1125,57 @@ __global__ __launch_bounds__(kThreads) void k_tile_hash(const uint8_t* __restric
       if (i < ntok) s_val[i] = vals[k];
     }
   }
-  for (uint32_t r0 = 0; r0 < nlines_tile && !irregular; r0 += kHashRows) {
+  // one row (f32 in LDS at src) -> out row `row`: fp8 (16 columns per lane
+  // and store) or f32
+  auto write_row = [&](uint64_t row, const float* src, int lane) {
+    if constexpr (kFP8) {
+      uint4* o = reinterpret_cast<uint4*>(static_cast<uint8_t*>(out) + row * dim);
+      for (int c = lane * 16; c < dim; c += dev::kWave * 16) {
+        const float4* f = reinterpret_cast<const float4*>(src + c);
+        uint32_t w[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 x = f[q];
+          int pk = __builtin_amdgcn_cvt_pk_fp8_f32(x.x * scale, x.y * scale, 0, false);
+          pk = __builtin_amdgcn_cvt_pk_fp8_f32(x.z * scale, x.w * scale, pk, true);
+          w[q] = static_cast<uint32_t>(pk);
+        }
+        o[c / 16] = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+    } else {
+      float4* o = reinterpret_cast<float4*>(static_cast<float*>(out) + row * dim);
+      for (int c = lane * 4; c < dim; c += dev::kWave * 4) {
+        o[c / 4] = *reinterpret_cast<const float4*>(src + c);
+      }
+    }
+  };
+  const bool by_row = one_pass && !irregular && nlines_tile <= kHashMaxRows;
+  if (by_row) {
+    // every owned token was decoded once; rows are contiguous in the list
+    // (text order), row r spanning [s_row_first[r], s_row_first[r + 1]).
+    // Each wave builds whole rows in its own LDS row (no workgroup barrier
+    // per row group, no re-scan of the tile's tokens per group)
+    if (threadIdx.x == 0) s_row_first[nlines_tile] = static_cast<uint16_t>(ntok);
+    __syncthreads();
+    const int w = threadIdx.x / dev::kWave;
+    const int lane = dev::lane_id();
+    float* mine = rows + static_cast<size_t>(w) * dim;
+    for (uint32_t r = w; r < nlines_tile; r += kThreads / dev::kWave) {
+      for (int c = lane * 4; c < dim; c += dev::kWave * 4) {
+        *reinterpret_cast<float4*>(mine + c) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      }
+      dev::wave_sync();
+      const uint32_t lo = s_row_first[r], hi = s_row_first[r + 1];
+      for (uint32_t i = lo + lane; i < hi; i += dev::kWave) {
+        const uint32_t res = s_tok[i];
+        if (res != kNone && (res >> 12) == r) atomicAdd(&mine[res & 0xFFFu], s_val[i]);
+      }
+      dev::wave_sync();
+      write_row(row_base + line_base + r, mine, lane);
+      dev::wave_sync();  // the row is read out before the next one is zeroed
+    }
+  }
+  for (uint32_t r0 = 0; r0 < nlines_tile && !irregular && !by_row; r0 += kHashRows) {
     for (int c = threadIdx.x; c < kHashRows * dim; c += kThreads) rows[c] = 0.0f;
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < ntok; i += kThreads) {
@@ -1144,31 +1201,7 @@ __global__ __launch_bounds__(kThreads) void k_tile_hash(const uint8_t* __restric
                                                                            : kHashRows;
     // wave w writes row w of the round: 16 columns per lane -> one 16 B store
     const uint32_t j = threadIdx.x / dev::kWave;
-    if (j < nr) {
-      const uint64_t row = row_base + line_base + r0 + j;
-      const float* src = rows + j * dim;
-      const int lane = dev::lane_id();
-      if constexpr (kFP8) {
-        uint4* o = reinterpret_cast<uint4*>(static_cast<uint8_t*>(out) + row * dim);
-        for (int c = lane * 16; c < dim; c += dev::kWave * 16) {
-          const float4* f = reinterpret_cast<const float4*>(src + c);
-          uint32_t w[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float4 x = f[q];
-            int pk = __builtin_amdgcn_cvt_pk_fp8_f32(x.x * scale, x.y * scale, 0, false);
-            pk = __builtin_amdgcn_cvt_pk_fp8_f32(x.z * scale, x.w * scale, pk, true);
-            w[q] = static_cast<uint32_t>(pk);
-          }
-          o[c / 16] = make_uint4(w[0], w[1], w[2], w[3]);
-        }
-      } else {
-        float4* o = reinterpret_cast<float4*>(static_cast<float*>(out) + row * dim);
-        for (int c = lane * 4; c < dim; c += dev::kWave * 4) {
-          o[c / 4] = *reinterpret_cast<const float4*>(src + c);
-        }
-      }
-    }
+    if (j < nr) write_row(row_base + line_base + r0 + j, rows + j * dim, dev::lane_id());
     __syncthreads();
   }
   unsigned fl = 0;
