@@ -13,8 +13,8 @@ from typing import Dict, Iterator, Optional
 
 from .. import _dmlc
 
-__all__ = ["Parser", "RowBlockIter", "GPUParser", "DeviceCSR", "csr_to_torch", "iter_blocks",
-           "write_synthetic", "to_sparse_csr", "GPUBlockDataset"]
+__all__ = ["Parser", "RowBlockIter", "GPUParser", "ShuffledGPUParser", "DeviceCSR", "csr_to_torch",
+           "iter_blocks", "write_synthetic", "to_sparse_csr", "GPUBlockDataset"]
 
 write_synthetic = _dmlc.write_synthetic
 
@@ -165,6 +165,95 @@ class GPUParser:
     @property
     def partition_bytes(self) -> int:
         return self._p.partition_bytes()
+
+
+class ShuffledGPUParser:
+    """GPU counterpart of ``InputSplitShuffle`` (reference
+    ``include/dmlc/input_split_shuffle.h``): the rank's shard is cut into
+    ``num_shuffle_parts`` sub-shards, visited each epoch in the order the CPU
+    split uses (``std::mt19937(666 + part + nparts + num_shuffle_parts +
+    seed)``, reshuffled by ``before_first``).  Sub-shard ``i`` is partition
+    ``part * num_shuffle_parts + i`` of ``nparts * num_shuffle_parts`` and is
+    parsed by a :class:`GPUParser` created when it is reached (one at a time,
+    so the pinned ring and device slots exist once).  Same ``parse_all`` /
+    ``next`` / ``value_*`` surface as GPUParser; rows come out in the CPU
+    split's record order.
+    """
+
+    def __init__(self, uri: str, part: int = 0, nparts: int = 1, num_shuffle_parts: int = 2,
+                 shuffle_seed: int = 0, format: str = "libsvm", index64: bool = False,  # noqa: A002
+                 **config):
+        if num_shuffle_parts < 1:
+            raise ValueError("num_shuffle_parts must be >= 1")
+        self.uri, self.part, self.nparts = uri, int(part), int(nparts)
+        self.k, self.seed = int(num_shuffle_parts), int(shuffle_seed)
+        self.format, self.index64, self._config = format, index64, dict(config)
+        self._epoch = 0
+        self._order = self._order_of(0)
+        self._pos = 0
+        self._cur = None
+        self._done_stats: Dict[str, float] = {}
+
+    def _order_of(self, epoch: int):
+        return list(_dmlc.shuffle_parts_order(self.part, self.nparts, self.k, self.seed, epoch))
+
+    @property
+    def order(self):
+        """sub-shard visiting order of the current epoch"""
+        return list(self._order)
+
+    def _open(self, sub: int) -> "GPUParser":
+        return GPUParser(self.uri, self.part * self.k + sub, self.nparts * self.k, format=self.format,
+                         index64=self.index64, **self._config)
+
+    def _close(self):
+        if self._cur is not None:
+            for key, v in self._cur.stats().items():
+                if isinstance(v, (int, float)) and not isinstance(v, bool):
+                    self._done_stats[key] = self._done_stats.get(key, 0) + v
+            self._cur = None
+
+    def parse_all(self, out=None):
+        """Parse the rest of this epoch into ``out`` (a DeviceCSR, appended)."""
+        if out is None:
+            out = DeviceCSR(self.index64)
+        if self._cur is not None:  # finish a sub-shard that next() started
+            self._cur.parse_all(out)
+            self._close()
+            self._pos += 1
+        while self._pos < self.k:
+            self._cur = self._open(self._order[self._pos])
+            self._cur.parse_all(out)
+            self._close()
+            self._pos += 1
+        return out
+
+    def next(self) -> bool:
+        while self._pos < self.k:
+            if self._cur is None:
+                self._cur = self._open(self._order[self._pos])
+            if self._cur.next():
+                return True
+            self._close()
+            self._pos += 1
+        return False
+
+    def value_to_host(self) -> Dict:
+        return self._cur.value_to_host()
+
+    def value_torch(self) -> Dict:
+        return self._cur.value_torch()
+
+    def before_first(self) -> None:
+        """Start the next epoch with a new visiting order."""
+        self._close()
+        self._epoch += 1
+        self._order = self._order_of(self._epoch)
+        self._pos = 0
+
+    def stats(self) -> Dict:
+        """Counters summed over the sub-shard parsers closed so far."""
+        return dict(self._done_stats)
 
 
 def csr_to_torch(csr) -> Dict[str, Optional["object"]]:

@@ -26,6 +26,22 @@ class InputSplitShuffle : public InputSplit {
    * \param num_shuffle_parts sub-shards per rank (>1 to shuffle)
    * \param shuffle_seed seed of the visiting order
    */
+  /*!
+   * \brief the sub-shard visiting order of epoch `epoch` (0 = the order after
+   *  construction, k = after k BeforeFirst calls) of a split created with the
+   *  same arguments -- for readers that visit the sub-shards themselves (the
+   *  GPU parser's shuffled mode)
+   */
+  static std::vector<unsigned> VisitOrder(unsigned part_index, unsigned num_parts,
+                                          unsigned num_shuffle_parts, int shuffle_seed,
+                                          unsigned epoch) {
+    std::vector<unsigned> order(num_shuffle_parts);
+    for (unsigned i = 0; i < num_shuffle_parts; ++i) order[i] = i;
+    if (num_shuffle_parts <= 1) return order;
+    std::mt19937 rnd(kRandMagic_ + part_index + num_parts + num_shuffle_parts + shuffle_seed);
+    for (unsigned e = 0; e <= epoch; ++e) std::shuffle(order.begin(), order.end(), rnd);
+    return order;
+  }
   static InputSplit* Create(const char* uri, unsigned part_index, unsigned num_parts,
                             const char* type, unsigned num_shuffle_parts,
                             int shuffle_seed) {

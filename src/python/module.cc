@@ -702,6 +702,9 @@ PYBIND11_MODULE(_dmlc, m) {
       py::arg("x"), py::arg("rows"), py::arg("dim"), py::arg("g"), py::arg("xv"),
       py::arg("nblocks"), py::arg("part"), py::arg("stream"));
   m.attr("fm_rank") = gpu::kFmRank;
+  m.def("shuffle_parts_order", &InputSplitShuffle::VisitOrder, py::arg("part"), py::arg("nparts"),
+        py::arg("num_shuffle_parts"), py::arg("seed"), py::arg("epoch"),
+        "sub-shard visiting order of InputSplitShuffle in a given epoch");
   m.def(
       "spmv",
       [stream_of](uintptr_t offset, uintptr_t index, uintptr_t value, size_t nrows, uintptr_t w,

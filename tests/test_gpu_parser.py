@@ -418,3 +418,43 @@ def test_replay_chunk_limit_is_enforced(tmp_path):
     w.close()
     with pytest.raises(Exception, match="replay_chunk_bytes"):
         io.GPURecordIO(r, hbm_cache=1, replay_chunk_mb=8192)
+
+
+@pytest.mark.parametrize("nparts", [1, 2])
+def test_shuffled_gpu_parser_follows_input_split_shuffle(tmp_path, nparts):
+    """ShuffledGPUParser visits the sub-shards in InputSplitShuffle's per-epoch
+    order: each epoch's CSR (parse_all and streaming next) equals the CPU
+    parser's rows of the sub-shards in that order."""
+    from dmlc_core_amd import _dmlc
+    d = tmp_path / "s"
+    d.mkdir()
+    for i in range(3):
+        data.write_synthetic(str(d / f"p{i}.libsvm"), i * 1500, (i + 1) * 1500, seed=23)
+    uri, k, seed = str(d), 4, 9
+    for part in range(nparts):
+        sp = data.ShuffledGPUParser(uri, part, nparts, num_shuffle_parts=k, shuffle_seed=seed,
+                                    chunk_bytes=64 * 1024)
+        orders = []
+        for epoch in range(3):
+            if epoch:
+                sp.before_first()
+            order = list(_dmlc.shuffle_parts_order(part, nparts, k, seed, epoch))
+            assert sp.order == order
+            orders.append(order)
+            want = cpu_rows_parts(uri, [part * k + s for s in order], nparts * k)
+            if epoch < 2:
+                got = pyref.concat_blocks([sp.parse_all().to_host()])
+            else:
+                blocks = []
+                while sp.next():
+                    blocks.append(sp.value_to_host())
+                got = pyref.concat_blocks(blocks)
+            assert_same(got, want)
+        assert len({tuple(o) for o in orders}) > 1  # the order changes between epochs
+
+
+def cpu_rows_parts(uri, parts, nparts):
+    blocks = []
+    for p in parts:
+        blocks.extend(data.iter_blocks(uri, p, nparts, type="libsvm"))
+    return pyref.concat_blocks(blocks)

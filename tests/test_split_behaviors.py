@@ -93,3 +93,32 @@ def test_partition_reader_grows_for_a_record_longer_than_its_buffer(tmp_path):
         chunks.append(c)
     assert b"".join(chunks).split(b"\n")[:-1] == lines
     assert max(len(c) for c in chunks) > 4096
+
+
+def test_shuffle_parts_order_matches_input_split_shuffle(tmp_path):
+    """_dmlc.shuffle_parts_order (used by the GPU ShuffledGPUParser) is the
+    visiting order of InputSplitShuffle: the split's records in epochs 0 and 1
+    are the sub-shards' records concatenated in that order."""
+    from dmlc_core_amd import _dmlc, io
+    d = tmp_path / "sh"
+    d.mkdir()
+    for i in range(3):
+        (d / f"p{i}.txt").write_text("".join(f"{i}-{k}\n" for k in range(400)))
+    uri = str(d)
+    for part, nparts, k, seed in ((0, 1, 4, 3), (1, 2, 3, 0)):
+        split = io.InputSplit(uri, part, nparts, "text", num_shuffle_parts=k, seed=seed)
+        for epoch in range(2):
+            if epoch:
+                split.before_first()
+            got = []
+            while True:
+                r = split.next_record()
+                if r is None:
+                    break
+                got.append(r.rstrip(b"\0\r\n"))
+            order = _dmlc.shuffle_parts_order(part, nparts, k, seed, epoch)
+            assert sorted(order) == list(range(k))
+            want = []
+            for sub in order:
+                want += [r.rstrip(b"\0\r\n") for r in io.iter_records(uri, part * k + sub, nparts * k)]
+            assert got == want, (part, epoch, order)
