@@ -55,6 +55,7 @@ struct CsvCfg {
   int label_col;
   int weight_col;   // -1, or a column other than label_col
   int has_weight;   // weight_column >= 0 (every row gets a weight)
+  int zero_excl;    // label / weight columns equal to 0 (excluded field per row)
   uint32_t delim;
 };
 
@@ -108,13 +109,20 @@ __device__ __forceinline__ bool excluded(uint32_t col, const CsvCfg& cfg) {
   return static_cast<int>(col) == cfg.label_col || static_cast<int>(col) == cfg.weight_col;
 }
 
+constexpr int kExclNone = 0;  // no label / weight column
+constexpr int kExclRows = 1;  // label / weight only in column 0: counted per row
+constexpr int kExclCols = 2;  // columns needed (per-field column numbers)
+
+__device__ __forceinline__ void col_scan(const CsvCfg& cfg, bool count, int lane, Walk* w,
+                                         Slice* o, uint32_t* nx);
+
 /*!
  * \brief masks, ownership and scans of step `s` (g: the lane's 16 bytes at
  *  tile offset s * kStep + 16 * lane; nrem: chunk bytes from the tile start,
  *  capped at 4 GiB).  Updates the walk state (all lanes see the same values).
  */
 __device__ __forceinline__ Slice step_slice(uint4 g, uint32_t s, uint32_t nrem, const CsvCfg& cfg,
-                                            bool count_excl, Walk* w, int lane) {
+                                            int excl_mode, Walk* w, int lane) {
   const uint32_t p = s * kStep + 16u * lane;
   const uint32_t z = eq16(g, 0u);
   const uint32_t e = eq16(g, 0x0A0A0A0Au) | eq16(g, 0x0D0D0D0Du) | z;  // NUL: past the chunk
@@ -160,7 +168,30 @@ __device__ __forceinline__ Slice step_slice(uint4 g, uint32_t s, uint32_t nrem, 
   fm &= own;
   lm &= own;
   w->bad |= __any(bad && own != 0);
-  // column of the lane's first field: segmented scan, reset at row starts
+  Slice o;
+  o.fm = fm;
+  o.lm = lm;
+  uint32_t nx = 0;  // excluded columns among the lane's fields
+  if (excl_mode != kExclCols) {
+    // label / weight only in column 0 (or none): one excluded field per row,
+    // no columns needed (the count pass of the common `label_column=0`)
+    nx = static_cast<uint32_t>(__popc(lm)) * static_cast<uint32_t>(cfg.zero_excl);
+    o.col0 = 0;
+  } else {
+    col_scan(cfg, true, lane, w, &o, &nx);
+  }
+  const uint64_t packed = static_cast<uint64_t>(__popc(fm)) |
+                          (static_cast<uint64_t>(__popc(lm)) << 21) |
+                          (static_cast<uint64_t>(nx) << 42);
+  o.before = wave_excl_scan(packed, &o.total);
+  return o;
+}
+
+/*! \brief column of each lane's first field (segmented scan, reset at row
+ *  starts) and, with count, the excluded columns among its fields */
+__device__ __forceinline__ void col_scan(const CsvCfg& cfg, bool count, int lane, Walk* w,
+                                         Slice* o, uint32_t* nx) {
+  const uint32_t fm = o->fm, lm = o->lm;
   uint32_t x;
   if (lm != 0) {
     const uint32_t hi = 31u - __builtin_clz(lm);
@@ -175,28 +206,18 @@ __device__ __forceinline__ Slice step_slice(uint4 g, uint32_t s, uint32_t nrem, 
   }
   const uint32_t prev = __shfl_up(x, 1, kWave);
   const uint32_t last = __shfl(x, kWave - 1, kWave);
-  Slice o;
-  o.fm = fm;
-  o.lm = lm;
-  o.col0 = lane == 0 ? w->col_carry
-                     : (prev & 0x7FFFFFFFu) + ((prev & 0x80000000u) ? 0u : w->col_carry);
+  o->col0 = lane == 0 ? w->col_carry
+                      : (prev & 0x7FFFFFFFu) + ((prev & 0x80000000u) ? 0u : w->col_carry);
   w->col_carry = (last & 0x7FFFFFFFu) + ((last & 0x80000000u) ? 0u : w->col_carry);
-  // excluded columns among the lane's fields
-  uint32_t nx = 0;
-  if (count_excl) {
-    uint32_t col = o.col0;
+  if (count) {
+    uint32_t col = o->col0;
     for (uint32_t m = fm; m != 0; m &= m - 1) {
       const uint32_t b = static_cast<uint32_t>(__builtin_ctz(m));
       if ((lm >> b) & 1u) col = 0;
-      nx += excluded(col, cfg) ? 1u : 0u;
+      *nx += excluded(col, cfg) ? 1u : 0u;
       ++col;
     }
   }
-  const uint64_t packed = static_cast<uint64_t>(__popc(fm)) |
-                          (static_cast<uint64_t>(__popc(lm)) << 21) |
-                          (static_cast<uint64_t>(nx) << 42);
-  o.before = wave_excl_scan(packed, &o.total);
-  return o;
 }
 
 __device__ __forceinline__ uint32_t f21(uint64_t v, int k) {
@@ -218,12 +239,13 @@ __global__ __launch_bounds__(kThreads) void k_csv_tile_count(const uint8_t* __re
     const uint32_t c = text[tile0 - 1];
     w.carry_eol = (c == '\n' || c == '\r') ? 1u : 0u;
   }
-  const bool count_excl = cfg.label_col >= 0 || cfg.weight_col >= 0;
+  const int excl_mode = (cfg.label_col > 0 || cfg.weight_col > 0) ? kExclCols
+                        : (cfg.zero_excl != 0 ? kExclRows : kExclNone);
   bool over = false;
   uint4 g = load16_clip(text, tile0 + 16u * lane, n);
   for (uint32_t s = 0; s < kMaxSteps; ++s) {
     const uint4 nxt = load16_clip(text, tile0 + (s + 1) * kStep + 16u * lane, n);  // prefetch
-    const Slice sl = step_slice(g, s, nrem, cfg, count_excl, &w, lane);
+    const Slice sl = step_slice(g, s, nrem, cfg, excl_mode, &w, lane);
     over |= f21(sl.total, 0) > kListCap;
     w.fields += f21(sl.total, 0);
     w.rows += f21(sl.total, 1);
@@ -274,7 +296,6 @@ __global__ __launch_bounds__(kThreads) void k_csv_tile_fill(const uint8_t* __res
     const uint32_t c = text[tile0 - 1];
     w.carry_eol = (c == '\n' || c == '\r') ? 1u : 0u;
   }
-  const bool count_excl = cfg.label_col >= 0 || cfg.weight_col >= 0;
   const uint32_t delim = cfg.delim;
   uint64_t mx = 0;
   bool irregular = false, any_value = false;
@@ -294,7 +315,8 @@ __global__ __launch_bounds__(kThreads) void k_csv_tile_fill(const uint8_t* __res
       if (nslot == 0 && lane < 2) ring[2 * kStep / 16 + lane] = v;
     }
     wave_sync();
-    const Slice sl = step_slice(ring[slot + lane], s, nrem, cfg, count_excl, &w, lane);
+    // the fill lists every field with its column: always the column scan
+    const Slice sl = step_slice(ring[slot + lane], s, nrem, cfg, kExclCols, &w, lane);
     // list the lane's fields: x = ring byte | row in tile << 16, y = column | entry in tile << 16
     {
       uint32_t col = sl.col0;
@@ -410,6 +432,7 @@ CsvCfg MakeCfg(int label_column, int weight_column, char delimiter) {
   // tests it first), rows still get weight 1.0
   c.weight_col = (weight_column < 0 || weight_column == label_column) ? -1 : weight_column;
   c.has_weight = weight_column >= 0 ? 1 : 0;
+  c.zero_excl = (c.label_col == 0 ? 1 : 0) + (c.weight_col == 0 ? 1 : 0);
   c.delim = static_cast<uint8_t>(delimiter);
   return c;
 }
