@@ -17,10 +17,10 @@ __all__ = ["SparseLogReg", "HashedFM", "fp8_gemm_available"]
 class SparseLogReg(torch.nn.Module):
     """Sparse logistic regression: p(y=1|x) = sigmoid(x . w + b)."""
 
-    def __init__(self, num_features: int, grad: str = "transpose"):
+    def __init__(self, num_features: int, grad: str = "auto"):
         super().__init__()
         self.num_features = int(num_features)
-        self.grad = grad  # X^T g: "transpose" (cached inverted index) or "atomic"
+        self.grad = grad  # X^T g: "auto" / "transpose" (cached inverted index) / "atomic"
         self.weight = torch.nn.Parameter(torch.zeros(self.num_features, dtype=torch.float32))
         self.bias = torch.nn.Parameter(torch.zeros(1, dtype=torch.float32))
 

@@ -106,3 +106,32 @@ def test_transpose_and_gather_gradient_match(csr_t):
         grads[mode] = m.weight.grad.clone()
     assert "transpose" in t  # cached for the next step
     torch.testing.assert_close(grads["transpose"], grads["atomic"], rtol=1e-4, atol=1e-6)
+
+
+def test_transpose_of_a_row_slice_and_auto_mode(csr_t):
+    """A batch that is a row slice of a larger CSR (offsets not starting at 0,
+    full index / value arrays -- examples/train_sparse_logreg.py) transposes to
+    the slice's own entries; grad="auto" uses atomics on a dict's first
+    backward and the cached transpose from the second on."""
+    import torch
+    from dmlc_core_amd.models import SparseLogReg
+    t, csr = csr_t
+    nfeat = int(csr.max_index) + 1
+    x = dense_ref(t, nfeat)
+    b, e = 1000, 1700
+    batch = {"offset": t["offset"][b:e + 1], "index": t["index"], "value": t["value"]}
+    d = torch.randn(e - b, device="cuda")
+    g = ops.spmv(ops.transpose(batch, nfeat), d, 0.0)
+    torch.testing.assert_close(g.cpu(), x[b:e].t() @ d.cpu(), rtol=1e-4, atol=1e-4)
+    m = SparseLogReg(nfeat).cuda()  # grad="auto"
+    holder = {"offset": t["offset"][b:e + 1], "index": t["index"], "value": t["value"],
+              "label": t["label"][b:e]}
+    grads = []
+    for _ in range(3):
+        m.zero_grad()
+        m.loss(holder).backward()
+        grads.append(m.weight.grad.clone())
+        if _ == 0:
+            assert "transpose" not in holder
+    assert "transpose" in holder
+    torch.testing.assert_close(grads[1], grads[0], rtol=1e-4, atol=1e-6)
