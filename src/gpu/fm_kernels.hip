@@ -196,28 +196,44 @@ __global__ __launch_bounds__(kBwdThreads) void k_fm_bwd(const uint8_t* __restric
   }
   f32x16 acc[4] = {};
   float tacc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  // the next tile's X fragment and G inputs are loaded while this tile computes
+  const int grow = threadIdx.x >> 3, gpart = threadIdx.x & 7;  // G producer (threads < 256)
+  auto load_g = [&](int64_t t, float* gv, float2* v) {
+    const int64_t r = t + grow;
+    const bool ok = threadIdx.x < 256 && r < r1;
+    *gv = ok ? g[r] : 0.0f;
+    *v = ok ? *reinterpret_cast<const float2*>(xv + r * kFmRank + 2 * gpart) : make_float2(0.0f, 0.0f);
+  };
+  auto load_x = [&](int64_t t, uint4 (&w)[4]) {
+    const int64_t r = t + n;  // the row of this lane's X fragment
+    const bool ok = active && r < r1;
+    load64(x + (ok ? r : 0) * dim + fbase + 64 * h, ok, w);
+  };
+  float gv_n = 0.0f;
+  float2 v_n = make_float2(0.0f, 0.0f);
+  uint4 xw[4], xw_n[4];
+  if (r0 < r1) {
+    load_g(r0, &gv_n, &v_n);
+    load_x(r0, xw_n);
+  }
   for (int64_t t0 = r0; t0 < r1; t0 += 32) {
     __syncthreads();  // the previous tile's G is consumed
     if (threadIdx.x < 256) {
-      const int row = threadIdx.x >> 3, part_id = threadIdx.x & 7;
-      const int64_t r = t0 + row;
-      const bool ok = r < r1;
-      const float gv = ok ? g[r] : 0.0f;
-      const float2 v = ok ? *reinterpret_cast<const float2*>(xv + r * kFmRank + 2 * part_id)
-                          : make_float2(0.0f, 0.0f);
-      s_gt[1 + 2 * part_id][row] = static_cast<__bf16>(gv * v.x);
-      s_gt[2 + 2 * part_id][row] = static_cast<__bf16>(gv * v.y);
-      if (part_id == 0) {
-        s_gt[0][row] = static_cast<__bf16>(gv);
-        s_g[row] = gv;
+      s_gt[1 + 2 * gpart][grow] = static_cast<__bf16>(gv_n * v_n.x);
+      s_gt[2 + 2 * gpart][grow] = static_cast<__bf16>(gv_n * v_n.y);
+      if (gpart == 0) {
+        s_gt[0][grow] = static_cast<__bf16>(gv_n);
+        s_g[grow] = gv_n;
       }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xw[i] = xw_n[i];
+    if (t0 + 32 < r1) {
+      load_g(t0 + 32, &gv_n, &v_n);
+      load_x(t0 + 32, xw_n);
     }
     __syncthreads();
     if (!active) continue;
-    const int64_t r = t0 + n;  // the row of this lane's X fragment
-    const bool ok = r < r1;
-    uint4 xw[4];
-    load64(x + (ok ? r : 0) * dim + fbase + 64 * h, ok, xw);
     // G^T fragments: element j of step s = row 16 s + 8 (j >> 2) + 4 h + (j & 3)
     bf16x8 ga[2];
 #pragma unroll
