@@ -169,12 +169,15 @@ __device__ __forceinline__ bool count16(uint4 v, uint32_t pc, size_t pos, size_t
     *toks += __popc(tm);
     *lines += __popc(lm);
     bad |= (lm & ~tm) != 0;  // a line that starts with a blank
-    uint32_t t = tm;
-    while (t != 0) {  // token starts must be [0-9+-.]
-      const int j = (__ffs(t) - 1) >> 3;
-      t &= t - 1;
-      bad |= !num_start((x >> (8 * j)) & 0xFFu);
-    }
+    // token starts must be [0-9+-.]: SWAR byte tests, no per-token loop
+    const uint32_t y = x ^ 0x30303030u;
+    const uint32_t digit = ~(((y & 0x7F7F7F7Fu) + 0x76767676u) | y) & 0x80808080u;  // y < 10
+    auto eqb = [x](uint32_t c4) {
+      const uint32_t z = x ^ c4;
+      return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u;
+    };
+    const uint32_t num_ok = digit | eqb(0x2B2B2B2Bu) | eqb(0x2D2D2D2Du) | eqb(0x2E2E2E2Eu);
+    bad |= (tm & ~num_ok) != 0;
     uint32_t c = lt20 & valid;
     while (c != 0) {  // control bytes other than \t \n \r
       const int j = (__ffs(c) - 1) >> 3;
