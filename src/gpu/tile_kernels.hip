@@ -1,7 +1,7 @@
 /*!
  * \file src/gpu/tile_kernels.hip
  * \brief LDS-staged tile parser: the LibSVM / LibFM fast path in three launches
- *  and one host read-back of the chunk sizes.
+ *  and one host wait (mapped pinned memory) for the chunk sizes.
  *
  *  Every row of a regular chunk is one line whose first byte starts its label
  *  token, so with L(p) = line starts at or before byte p and T(p) = tokens
@@ -10,22 +10,25 @@
  *      nnz(feature token k of line l) = k - l - 1
  *  No per-line or per-token index arrays are materialised.
  *
- *  C1 k_tile_count (grid = tiles of 8 KiB): SWAR byte masks of 16 B per lane,
- *     per tile (line starts << 32 | token starts) and an irregular bit (a line
- *     that starts with a blank, a token that does not start with [0-9+-.]:
- *     qid tokens, digit-less tokens, label-less lines).  Reads the chunk once.
+ *  C1 k_tile_count (one wave per 8 KiB tile): SWAR byte masks of 16 B per
+ *     lane, per tile (line starts << 32 | token starts) and an irregular bit (a
+ *     line that starts with a blank, a token that does not start with
+ *     [0-9+-.], control bytes other than \t \n \r); the token-start test
+ *     is byte-parallel (no per-token loop).  Reads the chunk once.
  *  C2 k_tile_scan  (one 1024-lane workgroup): exclusive scan of the tile
- *     counts, OR of the flags; writes nlines / nrows / nnz / flags to the
- *     ChunkMeta the host reads back (the single blocking read per chunk).
- *  C3 k_tile_fill  (grid = tiles): stage the tile in LDS with coalesced 16 B
- *     loads, recompute the masks from the same registers, workgroup-scan them
- *     and compact (tile offset, line ordinal, label bit) of every token into an
- *     LDS list; then lane i parses token i straight from the LDS tile with
- *     strtonum.h's ParsePair / ParseTriple (bit-identical to the CPU parser)
- *     over a separator-bounded byte iterator, and stores index / value /
- *     label / offset directly.  Only a tile's last token, which may continue
- *     into the next tile, is read from global memory.
- *     K8 (max index / field, flags) is a per-workgroup slot.
+ *     counts, OR of the flags; nlines / nrows / nnz / flags go to the
+ *     ChunkMeta and to mapped pinned memory the host polls (no D2H copy).
+ *  C3 k_tile_fill  (one wave per tile, no workgroup barrier): streams the tile
+ *     in 2 KiB steps through two LDS slots (step s and s - 1) with the next
+ *     step prefetched in registers, lists every token (staging offset, line
+ *     start bit, tile line ordinal) in a wave-private LDS list, and decodes
+ *     whole 64-token rounds only -- a step's remainder waits for the next
+ *     step's rounds.  Lane i decodes token i from two aligned ds_read_b128 in
+ *     registers (token_decode.h: integer fields with parse_int, values with
+ *     parse_num; anything else through strtonum.h's ParsePair / ParseTriple
+ *     from global memory, bit-identical to the CPU parser) and stores index /
+ *     value / label / offset directly.  K8 (max index / field, flags) is a
+ *     per-wave slot.
  *  (C2 and C4 become two-level -- many workgroups, then one -- above 8192
  *  tiles, i.e. for the 1 GiB passes over HBM-resident text.)
  *  C4 k_tile_finish (one workgroup): fold the slots into the ChunkMeta and
@@ -178,8 +181,10 @@ __device__ __forceinline__ bool count16(uint4 v, uint32_t pc, size_t pos, size_t
     };
     const uint32_t num_ok = digit | eqb(0x2B2B2B2Bu) | eqb(0x2D2D2D2Du) | eqb(0x2E2E2E2Eu);
     bad |= (tm & ~num_ok) != 0;
+    // control bytes other than \t \n \r: rare (line ends), a short loop is cheaper
+    // than three more byte tests per word (measured: 88.5 vs 103.5 us per call)
     uint32_t c = lt20 & valid;
-    while (c != 0) {  // control bytes other than \t \n \r
+    while (c != 0) {
       const int j = (__ffs(c) - 1) >> 3;
       c &= c - 1;
       bad |= !((0x2600u >> ((x >> (8 * j)) & 0xFFu)) & 1u);
