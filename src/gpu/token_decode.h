@@ -39,17 +39,14 @@ namespace gpu {
 namespace tok {
 
 /*! \brief 16 bytes starting at byte `a` of a 16-byte-aligned LDS buffer
- *  (the buffer must hold 32 bytes from a & ~15) */
+ *  (the buffer must hold 32 bytes from a & ~15): the five dwords covering
+ *  them, read one by one, funnel-shifted into place.  LDS issue is cheap in
+ *  the (VALU-bound) decode rounds; two aligned ds_read_b128 plus the 15
+ *  selects of the dword window cost more VALU issue. */
 __device__ __forceinline__ uint4 ext16(const uint4* lds, uint32_t a) {
-  const uint4 x = lds[a >> 4];
-  const uint4 y = lds[(a >> 4) + 1];
-  const uint32_t q = (a >> 2) & 3u, r = a & 3u;
-  // words q .. q+4 of (x, y)
-  const uint32_t w0 = q == 0 ? x.x : (q == 1 ? x.y : (q == 2 ? x.z : x.w));
-  const uint32_t w1 = q == 0 ? x.y : (q == 1 ? x.z : (q == 2 ? x.w : y.x));
-  const uint32_t w2 = q == 0 ? x.z : (q == 1 ? x.w : (q == 2 ? y.x : y.y));
-  const uint32_t w3 = q == 0 ? x.w : (q == 1 ? y.x : (q == 2 ? y.y : y.z));
-  const uint32_t w4 = q == 0 ? y.x : (q == 1 ? y.y : (q == 2 ? y.z : y.w));
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(lds) + (a >> 2);
+  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+  const uint32_t r = a & 3u;
   return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, r), __builtin_amdgcn_alignbyte(w2, w1, r),
                     __builtin_amdgcn_alignbyte(w3, w2, r), __builtin_amdgcn_alignbyte(w4, w3, r));
 }
