@@ -72,8 +72,10 @@ __device__ __forceinline__ uint32_t lead_digits(uint32_t g, uint32_t* val) {
   const uint32_t k = static_cast<uint32_t>(__builtin_ctzg(bad, 32)) >> 3;
   // k digits right-aligned (a 64-bit shift: k = 0 shifts them all out)
   const uint32_t x = static_cast<uint32_t>((static_cast<uint64_t>(lo4) << (8u * (4u - k))));
-  const uint32_t t = ((x << 3) + (x << 1) + (x >> 8)) & 0x00FF00FFu;  // x * 10 without v_mul_lo
-  *val = (t & 0xFFu) * 100u + (t >> 16);
+  // digit pairs by byte dot products (v_dot4_u32_u8), then pair0 * 100 + pair1
+  const uint32_t p0 = __builtin_amdgcn_udot4(x, 0x0000010Au, 0u, false);
+  const uint32_t p1 = __builtin_amdgcn_udot4(x, 0x010A0000u, 0u, false);
+  *val = __umul24(p0, 100u) + p1;
   return k;
 }
 
