@@ -261,14 +261,21 @@ __global__ __launch_bounds__(kThreads) void k_csv_tile_count(const uint8_t* __re
   }
 }
 
-/*! \brief StrToFloat of the field at global position q (the generic path) */
-__device__ __noinline__ float generic_field(const char* q, const char* end, char delim,
-                                            bool* last) {
+/*! \brief StrToFloat of the field at global position q (the generic path);
+ *  returned by value -- an out-pointer into the caller's frame would put it on
+ *  the stack (a scratch store + load per field round) */
+struct GenericField {
+  float v;
+  bool last;
+};
+__device__ __noinline__ GenericField generic_field(const char* q, const char* end, char delim) {
   const char* fe = q;
   while (fe != end && *fe != delim && *fe != '\n' && *fe != '\r') ++fe;
-  *last = fe == end || *fe != delim;
+  GenericField r;
+  r.last = fe == end || *fe != delim;
   while (q != fe && data::isspace(*q)) ++q;
-  return data::StrToFloat(q, fe, nullptr);
+  r.v = data::StrToFloat(q, fe, nullptr);
+  return r;
 }
 
 template <typename IndexType>
@@ -367,9 +374,11 @@ __global__ __launch_bounds__(kThreads) void k_csv_tile_fill(const uint8_t* __res
             last = t_eol;
           } else {
             const size_t gpos = tile0 + s * kStep + (off - slot * 16u);
-            v = generic_field(reinterpret_cast<const char*>(text) + gpos,
-                              reinterpret_cast<const char*>(text) + n, static_cast<char>(delim),
-                              &last);
+            const GenericField g = generic_field(reinterpret_cast<const char*>(text) + gpos,
+                                                 reinterpret_cast<const char*>(text) + n,
+                                                 static_cast<char>(delim));
+            v = g.v;
+            last = g.last;
           }
         }
         const uint64_t row = R + row_t;

@@ -132,9 +132,10 @@ __global__ __launch_bounds__(kThreads) void k_hashed_dense(
           *reinterpret_cast<uint4*>(static_cast<uint8_t*>(out) + r * dim + c) =
               make_uint4(w[0], w[1], w[2], w[3]);
         } else {
+          // rebuilt per element: a plain float4 array copy here went through scratch
           float4* o = reinterpret_cast<float4*>(static_cast<float*>(out) + r * dim + c);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] = x[q];
+          for (int q = 0; q < 4; ++q) o[q] = make_float4(x[q].x, x[q].y, x[q].z, x[q].w);
         }
       }
     } else if constexpr (kFP8) {

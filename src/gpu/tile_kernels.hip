@@ -608,9 +608,19 @@ __device__ __forceinline__ bool fast_token(const uint8_t* lds, uint32_t off, boo
  *  Out of line: it is rare, and inlined it would raise the register
  *  allocation of the whole fill kernel.
  */
+struct GenericResult {
+  tok::Token t;
+  bool bad;
+};
+
 template <TextFormat F, typename IndexType>
-__device__ __noinline__ void generic_token(const uint8_t* __restrict__ text, size_t n, size_t gpos,
-                                           bool is_label, tok::Token* t, bool* bad) {
+__device__ __noinline__ GenericResult generic_token(const uint8_t* __restrict__ text, size_t n,
+                                                    size_t gpos, bool is_label) {
+  GenericResult res;
+  tok::Token* const t = &res.t;
+  bool* const bad = &res.bad;
+  t->u0 = t->u1 = t->u0_hi = t->u1_hi = 0;
+  t->f0 = t->f1 = 0.0f;
   const uint8_t* lim = text + n;
   auto beg = sep_begin(text + gpos, lim);
   auto end = sep_end(lim);
@@ -635,6 +645,7 @@ __device__ __noinline__ void generic_token(const uint8_t* __restrict__ text, siz
     t->u1_hi = static_cast<uint32_t>(static_cast<uint64_t>(idx) >> 32);
     t->f0 = f0;
   }
+  return res;
 }
 
 /*!
@@ -873,9 +884,13 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
         // the step a slot holds: s, or s - 1 for a carried token
         const uint32_t in_slot = off >= kSlotBytes ? 1u : 0u;
         const int step = in_slot == (static_cast<uint32_t>(s) & 1u) ? s : s - 1;
-        generic_token<F, IndexType>(text, n, tile0 + static_cast<size_t>(step) * kStepBytes + off -
-                                                 in_slot * kSlotBytes,
-                                    is_label, &t, &bad);
+        // by value: result pointers into this frame would put t / bad on the
+        // stack, with a scratch store + load (and a vmcnt(0) wait) every round
+        const GenericResult g = generic_token<F, IndexType>(
+            text, n, tile0 + static_cast<size_t>(step) * kStepBytes + off - in_slot * kSlotBytes,
+            is_label);
+        t = g.t;
+        bad = g.bad;
       }
       const int32_t rel = static_cast<int32_t>(i) - static_cast<int32_t>(lc);
       const bool row_ok = static_cast<int64_t>(lc) - 1 < row_room;
