@@ -12,9 +12,10 @@
  *
  *  C1 k_tile_count (one wave per 8 KiB tile): SWAR byte masks of 16 B per
  *     lane, per tile (line starts << 32 | token starts) and an irregular bit (a
- *     line that starts with a blank, a token that does not start with
- *     [0-9+-.], control bytes other than \t \n \r); the token-start test
- *     is byte-parallel (no per-token loop).  Reads the chunk once.
+ *     line that starts with a blank, control bytes other than \t \n \r).
+ *     Reads the chunk once.  A token that does not start with [0-9+-.] never
+ *     passes the fill's register-window decoder; the fill (and the fused hash
+ *     kernel) flags it irregular on that fallback path, at no fast-path cost.
  *  C2 k_tile_scan  (one 1024-lane workgroup): exclusive scan of the tile
  *     counts, OR of the flags; nlines / nrows / nnz / flags go to the
  *     ChunkMeta and to mapped pinned memory the host polls (no D2H copy).
@@ -36,6 +37,8 @@
  *  Traffic per chunk: text read twice (C1, C3) + the CSR written once.
  */
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 
 #include "../data/strtonum.h"
 #include "./device_common.h"
@@ -145,11 +148,13 @@ __device__ __forceinline__ uint32_t prev_byte(const uint8_t* __restrict__ text, 
  *  masks (bit 7 of byte j), popcounted without gathering, plus the irregular
  *  checks of lane_masks<true>.  pc: the byte before the 16.
  */
+template <bool kFull>
 __device__ __forceinline__ bool count16(uint4 v, uint32_t pc, size_t pos, size_t n,
                                         uint32_t* lines, uint32_t* toks) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  // bytes at or past n are "separators" (no starts there)
-  const size_t room = pos >= n ? 0 : (n - pos < 16 ? n - pos : 16);
+  // bytes at or past n are "separators" (no starts there); kFull: the whole
+  // tile lies before n (every tile but a chunk's last), no per-word masks
+  const size_t room = kFull ? 16 : (pos >= n ? 0 : (n - pos < 16 ? n - pos : 16));
   uint32_t prev_sep = (pc <= 0x20u) ? 0x80u : 0u;  // sep bit of the byte before, at bit 7
   uint32_t prev_eol = (pc == '\n' || pc == '\r') ? 0x80u : 0u;
   bool bad = false;
@@ -172,15 +177,9 @@ __device__ __forceinline__ bool count16(uint4 v, uint32_t pc, size_t pos, size_t
     *toks += __popc(tm);
     *lines += __popc(lm);
     bad |= (lm & ~tm) != 0;  // a line that starts with a blank
-    // token starts must be [0-9+-.]: SWAR byte tests, no per-token loop
-    const uint32_t y = x ^ 0x30303030u;
-    const uint32_t digit = ~(((y & 0x7F7F7F7Fu) + 0x76767676u) | y) & 0x80808080u;  // y < 10
-    auto eqb = [x](uint32_t c4) {
-      const uint32_t z = x ^ c4;
-      return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u;
-    };
-    const uint32_t num_ok = digit | eqb(0x2B2B2B2Bu) | eqb(0x2D2D2D2Du) | eqb(0x2E2E2E2Eu);
-    bad |= (tm & ~num_ok) != 0;
+    // (token starts outside [0-9+-.] are flagged by the fill / hash kernels:
+    // such a token never passes the register-window decoder, so the check
+    // costs nothing on the fast path -- here it was ~40% of the count's VALU)
     // control bytes other than \t \n \r: rare (line ends), a short loop is cheaper
     // than three more byte tests per word (measured: 88.5 vs 103.5 us per call)
     uint32_t c = lt20 & valid;
@@ -215,12 +214,20 @@ __global__ __launch_bounds__(kThreads) void k_tile_count(const uint8_t* __restri
   const uint32_t first = base == 0 ? static_cast<uint32_t>('\n') : text[base - 1];
   uint32_t lines = 0, toks = 0;
   bool bad = false;
+  auto count_tile = [&](auto full) {
 #pragma unroll
-  for (int j = 0; j < kCountLoads; ++j) {
-    const uint32_t left = __shfl_up(v[j].w >> 24, 1, dev::kWave);
-    const uint32_t wrap = j == 0 ? first : __shfl(v[j - 1].w >> 24, dev::kWave - 1, dev::kWave);
-    const uint32_t pc = lane == 0 ? wrap : left;
-    bad |= count16(v[j], pc, base + j * 1024 + lane * 16, n, &lines, &toks);
+    for (int j = 0; j < kCountLoads; ++j) {
+      const uint32_t left = __shfl_up(v[j].w >> 24, 1, dev::kWave);
+      const uint32_t wrap = j == 0 ? first : __shfl(v[j - 1].w >> 24, dev::kWave - 1, dev::kWave);
+      const uint32_t pc = lane == 0 ? wrap : left;
+      bad |= count16<decltype(full)::value>(v[j], pc, base + j * 1024 + lane * 16, n, &lines,
+                                            &toks);
+    }
+  };
+  if (base + kTileBytes <= n) {  // wave-uniform: every tile but a chunk's last
+    count_tile(std::true_type{});
+  } else {
+    count_tile(std::false_type{});
   }
   lines = dev::wave_sum(lines);
   toks = dev::wave_sum(toks);
@@ -886,11 +893,13 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
         const int step = in_slot == (static_cast<uint32_t>(s) & 1u) ? s : s - 1;
         // by value: result pointers into this frame would put t / bad on the
         // stack, with a scratch store + load (and a vmcnt(0) wait) every round
-        const GenericResult g = generic_token<F, IndexType>(
-            text, n, tile0 + static_cast<size_t>(step) * kStepBytes + off - in_slot * kSlotBytes,
-            is_label);
+        const size_t gpos =
+            tile0 + static_cast<size_t>(step) * kStepBytes + off - in_slot * kSlotBytes;
+        const GenericResult g = generic_token<F, IndexType>(text, n, gpos, is_label);
         t = g.t;
         bad = g.bad;
+        // qid:, comments, junk: the exact kernels own the reference semantics
+        irregular |= !num_start(text[gpos]);
       }
       const int32_t rel = static_cast<int32_t>(i) - static_cast<int32_t>(lc);
       const bool row_ok = static_cast<int64_t>(lc) - 1 < row_room;
@@ -1076,6 +1085,7 @@ __global__ __launch_bounds__(kThreads) void k_tile_hash(const uint8_t* __restric
   constexpr int kPerLane = 4;  // tokens per lane held in registers (ntok <= 1024)
   float vals[kPerLane];
   const bool one_pass = ntok <= static_cast<uint32_t>(kPerLane * kThreads);
+  bool bad_start = false;
   auto decode = [&](uint32_t i, uint32_t* res, float* sval) {
     *res = kNone;
     const uint32_t e = s_tok[i];
@@ -1088,6 +1098,10 @@ __global__ __launch_bounds__(kThreads) void k_tile_hash(const uint8_t* __restric
     float f0 = 0.0f, f1 = 0.0f;
     bool bad = false;
     if (!fast_token<F>(lds, off, is_label, &r, &u0, &u1, &f0, &f1)) {
+      // a token start outside [0-9+-.] never passes fast_token: the exact
+      // kernels own those (k_tile_count no longer checks token starts)
+      // (per lane: `irregular` steers workgroup barriers and must stay uniform)
+      if (!num_start(lds[off])) bad_start = true;
       const uint8_t* l = lds + lim;
       auto b = sep_begin(lds + off, l);
       auto en = sep_end(l);
@@ -1228,7 +1242,7 @@ __global__ __launch_bounds__(kThreads) void k_tile_hash(const uint8_t* __restric
     __syncthreads();
   }
   unsigned fl = 0;
-  if (irregular) fl |= kFlagIrregular;
+  if (irregular || bad_start) fl |= kFlagIrregular;
   if (neg) fl |= kFlagNegIndex;
   dev::block_store_partial(0ull, 0ull, fl, partials);
 }

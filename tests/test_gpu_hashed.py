@@ -133,6 +133,29 @@ def test_fused_tile_kernel_long_lines_fall_back(tmp_path):
     np.testing.assert_allclose(fused["x"].cpu().numpy(), k9.cpu().numpy(), rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("fmt,junk", [("libsvm", "0 junk 3:1\n1 qid:4 5:1\n"),
+                                      ("libfm", "1 x:2:1 1:3:0.5\n0 #c 2:2:1\n")])
+def test_fused_tile_kernel_bad_token_starts_fall_back(tmp_path, fmt, junk):
+    """Token starts outside [0-9+-.] are flagged by the fused kernel itself
+    (the count pass no longer checks them): the chunk takes the exact per-line
+    kernel and the batch equals the all-exact run."""
+    p = str(tmp_path / f"j.{fmt}")
+    data.write_synthetic(p, 0, 600, format=fmt, seed=4)
+    with open(p, "a") as f:
+        f.write(junk)
+    data.write_synthetic(str(tmp_path / "t"), 600, 1200, format=fmt, seed=4)
+    with open(p, "a") as f:
+        f.write(open(str(tmp_path / "t")).read())
+    g = data.GPUParser(p, format=fmt, chunk_bytes=32 * 1024)
+    fused = g.parse_all_hashed(256, seed=2, fp8=False, strategy="fused")
+    assert 0 < g.stats()["exact_chunks"] < g.stats()["chunks"]
+    exact = data.GPUParser(p, format=fmt, chunk_bytes=32 * 1024, fast_path=0).parse_all_hashed(
+        256, seed=2, fp8=False, strategy="fused")
+    np.testing.assert_array_equal(fused["label"].cpu().numpy(), exact["label"].cpu().numpy())
+    np.testing.assert_allclose(fused["x"].cpu().numpy(), exact["x"].cpu().numpy(), rtol=1e-6,
+                               atol=1e-6)
+
+
 @pytest.mark.parametrize("dim", [256, 1024])
 def test_hashed_strategies_agree(dataset, dim):
     """auto / csr / fused return the same batch (f32: exact up to the order of

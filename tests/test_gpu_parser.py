@@ -70,21 +70,24 @@ def test_zero_copy_and_pinned_ring_agree(tmp_path, zero_copy):
     assert gp.stats()["zero_copy"] == bool(zero_copy)
 
 
-def test_irregular_chunks_fall_back(tmp_path):
+@pytest.mark.parametrize("fmt,junk", [("libsvm", "1 qid:9 1:1 2:2\n0 junk 3:1\n"),
+                                      ("libfm", "1 x:1:1 2:2:2\n0 #c 3:3:1\n")])
+def test_irregular_chunks_fall_back(tmp_path, fmt, junk):
     # qid tokens and digit-less tokens are not handled by the token-parallel
-    # path: those chunks must be re-parsed exactly, the rest stay fast
-    p = str(tmp_path / "m.libsvm")
-    data.write_synthetic(p, 0, 2000, format="libsvm", seed=5)
+    # path (the fill flags them on its fallback decode): those chunks must be
+    # re-parsed exactly, the rest stay fast
+    p = str(tmp_path / f"m.{fmt}")
+    data.write_synthetic(p, 0, 2000, format=fmt, seed=5)
     with open(p, "a") as f:
-        f.write("1 qid:9 1:1 2:2\n0 junk 3:1\n")
-    data.write_synthetic(str(tmp_path / "tail.libsvm"), 2000, 4000, seed=5)
+        f.write(junk)
+    data.write_synthetic(str(tmp_path / "tail"), 2000, 4000, format=fmt, seed=5)
     with open(p, "a") as f:
-        f.write(open(str(tmp_path / "tail.libsvm")).read())
-    gp = data.GPUParser(p, chunk_bytes=64 * 1024)
+        f.write(open(str(tmp_path / "tail")).read())
+    gp = data.GPUParser(p, format=fmt, chunk_bytes=64 * 1024)
     csr = gp.parse_all()
     st = gp.stats()
     assert 0 < st["exact_chunks"] < st["chunks"]
-    assert_same(pyref.concat_blocks([csr.to_host()]), cpu_rows(p, "libsvm"))
+    assert_same(pyref.concat_blocks([csr.to_host()]), cpu_rows(p, fmt), field=fmt == "libfm")
 
 
 def test_libsvm_gpu_edge_cases(tmp_path):
