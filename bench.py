@@ -265,11 +265,12 @@ def main():
             return rows, nnz, 0, p.bytes_read()
 
     def global_counts(rows, nnz, max_index, nbytes):
+        if dist is None:  # one rank: the totals are its own (no device round trip)
+            return [float(rows), float(nnz), float(nbytes)], int(max_index)
         t = torch.tensor([rows, nnz, nbytes], dtype=torch.float64, device=dev)
         m = torch.tensor([max_index], dtype=torch.float64, device=dev)
-        if dist is not None:
-            dist.all_reduce(t)
-            dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
         return t.tolist(), int(m.item())
 
     for _ in range(args.warmup):

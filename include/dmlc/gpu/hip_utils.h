@@ -135,6 +135,10 @@ class DeviceBuffer {
     return static_cast<T*>(ptr_);
   }
   size_t bytes() const { return bytes_; }
+  void swap(DeviceBuffer& o) noexcept {
+    std::swap(ptr_, o.ptr_);
+    std::swap(bytes_, o.bytes_);
+  }
 
  private:
   void* ptr_{nullptr};
@@ -173,6 +177,10 @@ class PinnedBuffer {
     return static_cast<T*>(ptr_);
   }
   size_t bytes() const { return bytes_; }
+  void swap(PinnedBuffer& o) noexcept {
+    std::swap(ptr_, o.ptr_);
+    std::swap(bytes_, o.bytes_);
+  }
 
  private:
   void* ptr_{nullptr};

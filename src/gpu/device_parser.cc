@@ -162,6 +162,13 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     hmeta_.Reserve(2 * sizeof(ChunkMeta));
     hmap_.Reserve(sizeof(ChunkMeta), /*mapped=*/true);
     std::memset(hmap_.get(), 0, sizeof(ChunkMeta));  // WaitMapped polls its pad word
+    if (cfg_.hbm_cache) {
+      // second C1/C2 scratch set: the next resident chunk's count + scan is
+      // queued behind the current fill (PrelaunchCount)
+      meta_next_.Reserve(2 * sizeof(ChunkMeta));
+      hmap_next_.Reserve(sizeof(ChunkMeta), /*mapped=*/true);
+      std::memset(hmap_next_.get(), 0, sizeof(ChunkMeta));
+    }
     slots_.Reserve(std::max<size_t>(kMaxPartialBlocks, TileScratchSlots(TileCount(cfg_.chunk_bytes))) *
                    sizeof(MetaPartial));
     iter_.set_max_capacity(static_cast<size_t>(cfg_.pinned_slots));
@@ -402,6 +409,10 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   void DrainInflight() {
     copy_->Synchronize();
     compute_->Synchronize();
+    if (pre_.valid) {  // finished (stream synchronised): re-arm its flag
+      static_cast<ChunkMeta*>(hmap_next_.get())->pad = 0;
+      pre_.valid = false;
+    }
     while (!inflight_.empty()) {
       if (inflight_.front().slot != nullptr) iter_.Recycle(&inflight_.front().slot);
       inflight_.pop_front();
@@ -505,10 +516,21 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   bool FastParse(const char* text, size_t nbytes, DeviceCSR<IndexType>* out, size_t row_base,
                  size_t nnz_base, ChunkPlan* plan) {
     hipStream_t s = compute_->get();
+    if (pre_.valid && pre_.text == text && pre_.nbytes == nbytes) {
+      // this chunk's C1 + C2 were queued behind the previous fill: take over
+      // their scratch set (its sizes are published, or about to be, in hmap_next_)
+      tcounts_.swap(tcounts_next_);
+      tflags_.swap(tflags_next_);
+      meta_.swap(meta_next_);
+      hmap_.swap(hmap_next_);
+      pre_.valid = false;
+    } else {
+      DropPrelaunch();
+      LaunchTileCountScan(text, nbytes, tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(),
+                          meta_.get<ChunkMeta>(), hmap_.get<ChunkMeta>(), s);
+    }
     ChunkMeta* dmeta = meta_.get<ChunkMeta>();
     ChunkMeta* hm = hmap_.get<ChunkMeta>();
-    LaunchTileCountScan(text, nbytes, tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(), dmeta, hm,
-                        s);
     const ChunkMeta sizes = WaitMapped(hm);
     AfterFirstSync();
     if (sizes.flags & kFlagIrregular) return false;
@@ -520,6 +542,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       FillTarget<IndexType> tgt = PrepareOutput(out, row_base, nnz_base, *plan, need_weight, nbytes);
       LaunchTileFill<IndexType>(text, nbytes, tcfg_.format, tcounts_.get<uint64_t>(), tgt,
                                 slots_.get<MetaPartial>(), dmeta, hm, s);
+      PrelaunchCount();
       ChunkMeta m = WaitMapped(hm);
       if (m.flags & kFlagIrregular) return false;
       if ((m.flags & kFlagNeedWeight) && !need_weight) {
@@ -611,6 +634,37 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     acc_max_index_ = std::max<uint64_t>(acc_max_index_, m.max_index);
     acc_max_field_ = std::max<uint64_t>(acc_max_field_, m.max_field);
     acc_flags_ |= m.flags;
+  }
+
+  /*!
+   * \brief ParseAll over HBM-resident text: queue the next chunk's count +
+   *  scan (C1 + C2) into the second scratch set right behind the current
+   *  fill, so the GPU does not idle while the host reads the fill's result
+   *  and turns around (~20-50 us per chunk in the trace).  The next FastParse
+   *  adopts the set when its chunk is the one prelaunched.
+   */
+  void PrelaunchCount() {
+    if (!(replay_ && merge_replay_) || pre_.valid || inflight_.empty()) {
+      return;
+    }
+    const Inflight& nx = inflight_.front();
+    if (nx.d >= 0) return;  // not resident (its copy would have to be waited for)
+    const size_t tiles = TileCount(nx.size);
+    tcounts_next_.Reserve(TileScratchWords(tiles) * sizeof(uint64_t));
+    tflags_next_.Reserve(TileScratchWords(tiles) * sizeof(uint32_t));
+    LaunchTileCountScan(nx.text, nx.size, tcounts_next_.get<uint64_t>(),
+                        tflags_next_.get<uint32_t>(), meta_next_.get<ChunkMeta>(),
+                        hmap_next_.get<ChunkMeta>(), compute_->get());
+    pre_.valid = true;
+    pre_.text = nx.text;
+    pre_.nbytes = nx.size;
+  }
+
+  /*! \brief retire a prelaunched count nobody will adopt (its flag re-armed) */
+  void DropPrelaunch() {
+    if (!pre_.valid) return;
+    (void)WaitMapped(hmap_next_.get<ChunkMeta>());
+    pre_.valid = false;
   }
 
   /*! \brief the H2D of the current chunk is complete: recycle and keep PCIe busy */
@@ -787,6 +841,14 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   DeviceBuffer tiles_, lines_, info_, partials_, meta_;
   /*! \brief tile parser scratch: per-tile counts (scanned in place) and flags */
   DeviceBuffer tcounts_, tflags_;
+  // the prelaunched next chunk's C1 + C2 scratch (hbm_cache ParseAll only)
+  DeviceBuffer tcounts_next_, tflags_next_, meta_next_;
+  PinnedBuffer hmap_next_;
+  struct Prelaunch {
+    bool valid{false};
+    const char* text{nullptr};
+    size_t nbytes{0};
+  } pre_;
   /*! \brief per-workgroup reduction slots (MetaPartial) */
   DeviceBuffer slots_;
   PinnedBuffer hmeta_;

@@ -286,6 +286,34 @@ def test_hbm_epoch_cache_replay_and_resume(tmp_path, zero_copy):
     assert_same(pyref.concat_blocks(head + again), c)
 
 
+@pytest.mark.parametrize("replay_mb", [0.0625, 0.25])
+def test_hbm_replay_prelaunched_counts(tmp_path, replay_mb):
+    """Replayed ParseAll queues the next resident chunk's count + scan behind
+    the current fill (a second scratch set).  Many merged chunks, a weight
+    column first seen late (the fill re-runs its chunk), an irregular chunk
+    in the middle (exact fallback) and a resume in between: every epoch equals
+    the CPU parser."""
+    d = tmp_path / "c"
+    d.mkdir()
+    for i in range(3):
+        data.write_synthetic(str(d / f"p{i}.libsvm"), i * 1500, (i + 1) * 1500, seed=37,
+                             weight_every=5 if i == 2 else 0)
+    with open(d / "p1.libsvm", "a") as f:
+        f.write("1 qid:3 4:1\n")
+    c = cpu_rows(str(d), "libsvm")
+    gp = data.GPUParser(str(d), chunk_bytes=32 * 1024, hbm_cache=1, replay_chunk_mb=replay_mb)
+    csr = data.DeviceCSR()
+    for epoch in range(3):
+        gp.before_first()
+        csr.clear()
+        gp.parse_all(csr)
+        assert_same(pyref.concat_blocks([csr.to_host()]), c)
+        if epoch == 1:
+            gp.before_first()
+            assert gp.next()  # a partial streaming pass between two replays
+    assert gp.stats()["exact_chunks"] > 0
+
+
 def test_weight_column_first_seen_in_a_late_chunk(tmp_path):
     """The tile fill learns about weights only when it meets one: the column
     is allocated then (earlier rows 1.0) and that chunk is written again."""
