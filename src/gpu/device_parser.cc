@@ -513,22 +513,41 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
    *  take the exact path.  One blocking read-back (the chunk's sizes) before
    *  the fill, one for the maxima / flags after it.
    */
-  bool FastParse(const char* text, size_t nbytes, DeviceCSR<IndexType>* out, size_t row_base,
-                 size_t nnz_base, ChunkPlan* plan) {
+  /*! \brief the tile pipeline's count + scan (LibSVM / LibFM C1 + C2, or CSV S1 + scan) */
+  void LaunchCountScan(const char* text, size_t nbytes, uint64_t* counts, uint32_t* flags,
+                       ChunkMeta* dmeta, ChunkMeta* hm) {
     hipStream_t s = compute_->get();
+    if (tcfg_.format == TextFormat::kCSV) {
+      LaunchCsvTileCount(text, nbytes, tcfg_.label_column, tcfg_.weight_column, tcfg_.delimiter,
+                         counts, flags, s);
+      LaunchTileScanRaw(counts, flags, TileCount(nbytes), dmeta, hm, s);
+    } else {
+      LaunchTileCountScan(text, nbytes, counts, flags, dmeta, hm, s);
+    }
+  }
+
+  /*! \brief count + scan of this chunk into the current scratch set: adopt the
+   *  prelaunched set when it holds this chunk, else launch them now */
+  void CountScanCurrent(const char* text, size_t nbytes) {
     if (pre_.valid && pre_.text == text && pre_.nbytes == nbytes) {
-      // this chunk's C1 + C2 were queued behind the previous fill: take over
-      // their scratch set (its sizes are published, or about to be, in hmap_next_)
+      // queued behind the previous fill: take over that scratch set (its sizes
+      // are published, or about to be, in hmap_next_)
       tcounts_.swap(tcounts_next_);
       tflags_.swap(tflags_next_);
       meta_.swap(meta_next_);
       hmap_.swap(hmap_next_);
       pre_.valid = false;
-    } else {
-      DropPrelaunch();
-      LaunchTileCountScan(text, nbytes, tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(),
-                          meta_.get<ChunkMeta>(), hmap_.get<ChunkMeta>(), s);
+      return;
     }
+    DropPrelaunch();
+    LaunchCountScan(text, nbytes, tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(),
+                    meta_.get<ChunkMeta>(), hmap_.get<ChunkMeta>());
+  }
+
+  bool FastParse(const char* text, size_t nbytes, DeviceCSR<IndexType>* out, size_t row_base,
+                 size_t nnz_base, ChunkPlan* plan) {
+    hipStream_t s = compute_->get();
+    CountScanCurrent(text, nbytes);
     ChunkMeta* dmeta = meta_.get<ChunkMeta>();
     ChunkMeta* hm = hmap_.get<ChunkMeta>();
     const ChunkMeta sizes = WaitMapped(hm);
@@ -568,12 +587,10 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   bool CsvFastParse(const char* text, size_t nbytes, DeviceCSR<IndexType>* out, size_t row_base,
                     size_t nnz_base, ChunkPlan* plan) {
     hipStream_t s = compute_->get();
+    const size_t ntiles = TileCount(nbytes);
+    CountScanCurrent(text, nbytes);
     ChunkMeta* dmeta = meta_.get<ChunkMeta>();
     ChunkMeta* hm = hmap_.get<ChunkMeta>();
-    const size_t ntiles = TileCount(nbytes);
-    LaunchCsvTileCount(text, nbytes, tcfg_.label_column, tcfg_.weight_column, tcfg_.delimiter,
-                       tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(), s);
-    LaunchTileScanRaw(tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(), ntiles, dmeta, hm, s);
     const ChunkMeta sizes = WaitMapped(hm);
     AfterFirstSync();
     if (sizes.flags & kFlagIrregular) return false;
@@ -587,6 +604,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
                                  slots_.get<MetaPartial>(), s);
     LaunchTileFinish(slots_.get<MetaPartial>(), ntiles, dmeta, hm, tgt.offset, row_base, nnz_base,
                      s);
+    PrelaunchCount();
     const ChunkMeta m = WaitMapped(hm);
     CHECK(!(m.flags & kFlagIrregular))
         << "internal error: CSV fill pass disagreed with the count pass";
@@ -652,9 +670,8 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     const size_t tiles = TileCount(nx.size);
     tcounts_next_.Reserve(TileScratchWords(tiles) * sizeof(uint64_t));
     tflags_next_.Reserve(TileScratchWords(tiles) * sizeof(uint32_t));
-    LaunchTileCountScan(nx.text, nx.size, tcounts_next_.get<uint64_t>(),
-                        tflags_next_.get<uint32_t>(), meta_next_.get<ChunkMeta>(),
-                        hmap_next_.get<ChunkMeta>(), compute_->get());
+    LaunchCountScan(nx.text, nx.size, tcounts_next_.get<uint64_t>(), tflags_next_.get<uint32_t>(),
+                    meta_next_.get<ChunkMeta>(), hmap_next_.get<ChunkMeta>());
     pre_.valid = true;
     pre_.text = nx.text;
     pre_.nbytes = nx.size;

@@ -11,7 +11,8 @@
  *  an 8-GPU node, on the NUMA nodes whose cores also run the pread / window
  *  registration threads.  So: spin (with `pause`) for `spin_us`, then poll
  *  with short sleeps (timer slack lowered to 1 us for this thread, so a
- *  20 us sleep costs ~20 us, not the default 50 us slack), and give up after
+ *  5 us nap costs ~5-7 us, not the default 50 us slack: the wake-up latency
+ *  sits between a kernel finishing and the next launch), and give up after
  *  `bound_s` so a kernel that never publishes surfaces through the caller's
  *  stream synchronise instead of hanging here.
  */
@@ -60,7 +61,7 @@ inline bool WaitHostFlag(const volatile unsigned* flag, double spin_us, double b
     (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // 1 us
     slack_set = true;
   }
-  const struct timespec nap = {0, 20000};  // 20 us
+  const struct timespec nap = {0, 5000};  // 5 us
   for (;;) {
     if (*flag != 0) {
       ++st->slept;
