@@ -88,9 +88,10 @@ class GPUParser:
         return out
 
     #: widest dim at which the fused kernel beats tile CSR + K9 on MI355X
-    #: (profiles/r02_session5: 1.35x at dim 128-256, 0.88x at dim 1024, where
-    #: the per-tile LDS row buffers cost more than writing the CSR once)
-    FUSED_HASH_MAX_DIM = 512
+    #: (profiles/r03_hashed_prelaunch: 1.15x at dim 128, 1.03x at 256, 0.95x
+    #: at 512, 0.65-0.9x at 1024 -- the tile fill got faster in round 3, and
+    #: above 256 the per-wave LDS row buffers cost more than writing the CSR)
+    FUSED_HASH_MAX_DIM = 256
 
     def parse_all_hashed(self, dim: int, seed: int = 0, fp8: bool = True, scale: float = 1.0,
                          strategy: str = "auto"):

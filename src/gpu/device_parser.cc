@@ -782,9 +782,9 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       if (cfg_.fast_path && dim % 16 == 0) {
         // tile parser: C1 + C2 sizes, then the fused tile kernel builds the
         // rows of the lines each workgroup owns
+        CountScanCurrent(text, nbytes);  // may adopt a prelaunched count + scan
+        dmeta = meta_.get<ChunkMeta>();
         ChunkMeta* hm = hmap_.get<ChunkMeta>();
-        LaunchTileCountScan(text, nbytes, tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(), dmeta,
-                            hm, s);
         const ChunkMeta sizes = WaitMapped(hm);
         AfterFirstSync();
         if (!(sizes.flags & kFlagIrregular)) {
@@ -793,6 +793,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
                                       out->rows, dim, scale, seed, fp8, out->x.get(),
                                       out->label.get<float>(), slots_.get<MetaPartial>(), dmeta,
                                       hm, s);
+          PrelaunchCount();
           const ChunkMeta m = WaitMapped(hm);
           CHECK(!(m.flags & kFlagNegIndex)) << "negative feature index in " << cfg_.format
                                             << " input";
