@@ -792,8 +792,14 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
   // position C + (i - lcnt); its row is R + lcnt - 1 (as k_tile_scan defines)
   const uint64_t C = out.nnz_base + tok_base - line_base;
   const uint64_t R = out.row_base + line_base;
-  const int64_t nnz_room = static_cast<int64_t>(out.nnz_limit) - static_cast<int64_t>(C);
-  const int64_t row_room = static_cast<int64_t>(out.row_limit) - static_cast<int64_t>(R);
+  // rooms clamped to int32 (a tile's ordinals are < 2^13): 32-bit compares per token
+  auto clamp32 = [](int64_t v) {
+    return static_cast<int32_t>(v > INT32_MAX ? INT32_MAX : (v < INT32_MIN ? INT32_MIN : v));
+  };
+  const int32_t nnz_room =
+      clamp32(static_cast<int64_t>(out.nnz_limit) - static_cast<int64_t>(C));
+  const int32_t row_room =
+      clamp32(static_cast<int64_t>(out.row_limit) - static_cast<int64_t>(R));
   IndexType* const idx_at = out.index + C;
   float* const val_at = out.value + C;
   IndexType* const fld_at = out.field != nullptr ? out.field + C : nullptr;
@@ -805,7 +811,9 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
   uint32_t tok0 = 0;   // tile token ordinal of list position 0
   uint32_t lcnt = 0;   // line starts of this tile so far
   uint32_t carry = 0;  // list entries left for the next step's rounds (listed, not decoded)
-  uint64_t mx_index = 0, mx_field = 0;
+  // maxima in the index width (32-bit compares for u32 indices)
+  using MaxT = typename std::conditional<sizeof(IndexType) == 4, uint32_t, uint64_t>::type;
+  MaxT mx_index = 0, mx_field = 0;
   bool any_value = false, any_weight = false, irregular = false, neg = false, need_w = false;
 
 #pragma unroll 1
@@ -902,7 +910,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
         irregular |= !num_start(text[gpos]);
       }
       const int32_t rel = static_cast<int32_t>(i) - static_cast<int32_t>(lc);
-      const bool row_ok = static_cast<int64_t>(lc) - 1 < row_room;
+      const bool row_ok = static_cast<int32_t>(lc) - 1 < row_room;
       const bool nnz_ok = rel < nnz_room;
       bool field_ok = true;
       if (F == TextFormat::kLibFM) field_ok = is_label || t.r >= 2;
@@ -923,7 +931,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
           val_at[rel] = t.r == 2 ? t.f0 : 1.0f;
         }
         any_value |= feat && t.r == 2;
-        const uint64_t iu = static_cast<uint64_t>(static_cast<IndexType>(u0));
+        const MaxT iu = static_cast<MaxT>(static_cast<IndexType>(u0));
         mx_index = feat && iu > mx_index ? iu : mx_index;
       } else {
         const uint64_t u1 = (static_cast<uint64_t>(t.u1_hi) << 32) | t.u1;
@@ -933,8 +941,8 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
           val_at[rel] = t.r == 3 ? t.f0 : 1.0f;
         }
         any_value |= feat && t.r == 3;
-        const uint64_t iu = static_cast<uint64_t>(static_cast<IndexType>(u1));
-        const uint64_t fu = static_cast<uint64_t>(static_cast<IndexType>(u0));
+        const MaxT iu = static_cast<MaxT>(static_cast<IndexType>(u1));
+        const MaxT fu = static_cast<MaxT>(static_cast<IndexType>(u0));
         mx_index = feat && iu > mx_index ? iu : mx_index;
         mx_field = feat && fu > mx_field ? fu : mx_field;
       }
