@@ -97,15 +97,16 @@ __device__ __forceinline__ bool num_start(uint32_t c) {
  *  control byte other than \t \n \r, a line starting with a blank, a token
  *  starting outside [0-9+-.]).
  */
-template <bool kCheck>
+template <bool kCheck, bool kFull = false>
 __device__ __forceinline__ bool lane_masks(uint4 v, uint32_t pc, size_t pos, size_t n,
                                            uint32_t* lm, uint32_t* tm) {
   uint32_t sep, eol, ctl;
   classify16(v, &sep, &eol, &ctl);
   const uint32_t prev_eol = (pc == '\n' || pc == '\r') ? 1u : 0u;
   const uint32_t prev_sep = (prev_eol || pc == ' ' || pc == '\t') ? 1u : 0u;
-  uint32_t valid = 0xFFFFu;
-  if (pos >= n) {
+  uint32_t valid = 0xFFFFu;  // kFull: all 16 bytes are before n (no 64-bit compares)
+  if (kFull) {
+  } else if (pos >= n) {
     valid = 0;
   } else if (n - pos < 16) {
     valid = (1u << (n - pos)) - 1u;
@@ -847,8 +848,13 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
     const uint32_t pc_b = lane == 0 ? last_a : left_b;
     carry_pc = __shfl(b.w >> 24, dev::kWave - 1, dev::kWave);
     uint32_t lm_a, tm_a, lm_b, tm_b;
-    (void)lane_masks<false>(a, pc_a, pos_a, n, &lm_a, &tm_a);
-    (void)lane_masks<false>(b, pc_b, pos_a + 1024, n, &lm_b, &tm_b);
+    if (tile0 + static_cast<size_t>(s + 1) * kStepBytes <= n) {  // wave-uniform: a full step
+      (void)lane_masks<false, true>(a, pc_a, pos_a, n, &lm_a, &tm_a);
+      (void)lane_masks<false, true>(b, pc_b, pos_a + 1024, n, &lm_b, &tm_b);
+    } else {
+      (void)lane_masks<false>(a, pc_a, pos_a, n, &lm_a, &tm_a);
+      (void)lane_masks<false>(b, pc_b, pos_a + 1024, n, &lm_b, &tm_b);
+    }
     // one 64-bit scan of four 16-bit counts: tokens / lines of both slices
     const uint64_t cnt = static_cast<uint64_t>(__popc(tm_a)) |
                          (static_cast<uint64_t>(__popc(tm_b)) << 16) |
