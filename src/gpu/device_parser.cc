@@ -163,8 +163,10 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     hmap_.Reserve(sizeof(ChunkMeta), /*mapped=*/true);
     std::memset(hmap_.get(), 0, sizeof(ChunkMeta));  // WaitMapped polls its pad word
     if (cfg_.hbm_cache) {
-      // second C1/C2 scratch set: the next resident chunk's count + scan is
-      // queued behind the current fill (PrelaunchCount)
+      // second C1/C2 scratch set: the next resident chunk's count + scan runs
+      // on its own stream, concurrently with the current fill (PrelaunchCount)
+      count_stream_.reset(new Stream());
+      pre_done_.reset(new Event());
       meta_next_.Reserve(2 * sizeof(ChunkMeta));
       hmap_next_.Reserve(sizeof(ChunkMeta), /*mapped=*/true);
       std::memset(hmap_next_.get(), 0, sizeof(ChunkMeta));
@@ -193,6 +195,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     // destructors never throw, so errors are ignored here
     if (copy_) (void)hipStreamSynchronize(copy_->get());
     if (compute_) (void)hipStreamSynchronize(compute_->get());
+    if (count_stream_) (void)hipStreamSynchronize(count_stream_->get());
     for (auto& f : inflight_) {
       if (f.slot != nullptr) iter_.Recycle(&f.slot);
     }
@@ -409,10 +412,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   void DrainInflight() {
     copy_->Synchronize();
     compute_->Synchronize();
-    if (pre_.valid) {  // finished (stream synchronised): re-arm its flag
-      static_cast<ChunkMeta*>(hmap_next_.get())->pad = 0;
-      pre_.valid = false;
-    }
+    DropPrelaunch();
     while (!inflight_.empty()) {
       if (inflight_.front().slot != nullptr) iter_.Recycle(&inflight_.front().slot);
       inflight_.pop_front();
@@ -435,7 +435,10 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     // publishes (a fault) still surfaces through the sync
     volatile unsigned* flag = &hm->pad;
     const bool seen = WaitHostFlag(flag, cfg_.wait_spin_us, 0.05, &wait_stats_);
-    if (!seen) compute_->Synchronize();
+    if (!seen) {
+      compute_->Synchronize();
+      if (count_stream_) count_stream_->Synchronize();
+    }
     std::atomic_thread_fence(std::memory_order_acquire);
     stats_.wait_gpu_sec += GetTime() - t0;
     stats_.waits_spun = wait_stats_.spun;
@@ -515,8 +518,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
    */
   /*! \brief the tile pipeline's count + scan (LibSVM / LibFM C1 + C2, or CSV S1 + scan) */
   void LaunchCountScan(const char* text, size_t nbytes, uint64_t* counts, uint32_t* flags,
-                       ChunkMeta* dmeta, ChunkMeta* hm) {
-    hipStream_t s = compute_->get();
+                       ChunkMeta* dmeta, ChunkMeta* hm, hipStream_t s) {
     if (tcfg_.format == TextFormat::kCSV) {
       LaunchCsvTileCount(text, nbytes, tcfg_.label_column, tcfg_.weight_column, tcfg_.delimiter,
                          counts, flags, s);
@@ -537,11 +539,13 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       meta_.swap(meta_next_);
       hmap_.swap(hmap_next_);
       pre_.valid = false;
+      // the fill reads the tile prefix the other stream wrote
+      DMLC_HIP_CHECK(hipStreamWaitEvent(compute_->get(), pre_done_->get(), 0));
       return;
     }
     DropPrelaunch();
     LaunchCountScan(text, nbytes, tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(),
-                    meta_.get<ChunkMeta>(), hmap_.get<ChunkMeta>());
+                    meta_.get<ChunkMeta>(), hmap_.get<ChunkMeta>(), compute_->get());
   }
 
   bool FastParse(const char* text, size_t nbytes, DeviceCSR<IndexType>* out, size_t row_base,
@@ -670,8 +674,12 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     const size_t tiles = TileCount(nx.size);
     tcounts_next_.Reserve(TileScratchWords(tiles) * sizeof(uint64_t));
     tflags_next_.Reserve(TileScratchWords(tiles) * sizeof(uint32_t));
+    // its own stream: count + scan (HBM- and VALU-light next to the fill)
+    // overlap the current fill instead of queueing behind it.  The set it
+    // writes was last used by the chunk before the current one, which is done.
     LaunchCountScan(nx.text, nx.size, tcounts_next_.get<uint64_t>(), tflags_next_.get<uint32_t>(),
-                    meta_next_.get<ChunkMeta>(), hmap_next_.get<ChunkMeta>());
+                    meta_next_.get<ChunkMeta>(), hmap_next_.get<ChunkMeta>(), count_stream_->get());
+    pre_done_->Record(count_stream_->get());
     pre_.valid = true;
     pre_.text = nx.text;
     pre_.nbytes = nx.size;
@@ -680,7 +688,8 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   /*! \brief retire a prelaunched count nobody will adopt (its flag re-armed) */
   void DropPrelaunch() {
     if (!pre_.valid) return;
-    (void)WaitMapped(hmap_next_.get<ChunkMeta>());
+    count_stream_->Synchronize();
+    static_cast<ChunkMeta*>(hmap_next_.get())->pad = 0;
     pre_.valid = false;
   }
 
@@ -862,6 +871,8 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   // the prelaunched next chunk's C1 + C2 scratch (hbm_cache ParseAll only)
   DeviceBuffer tcounts_next_, tflags_next_, meta_next_;
   PinnedBuffer hmap_next_;
+  std::unique_ptr<Stream> count_stream_;  // prelaunched counts (hbm_cache only)
+  std::unique_ptr<Event> pre_done_;
   struct Prelaunch {
     bool valid{false};
     const char* text{nullptr};
