@@ -124,6 +124,11 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
     hmap_.Reserve(sizeof(ChunkMeta), /*mapped=*/true);
     std::memset(hmap_.get(), 0, sizeof(ChunkMeta));
     meta_.Reserve(sizeof(ChunkMeta));
+    // second R1 + scan scratch set: the next replayed piece's count runs on
+    // count_ while the current piece's fill runs (PrelaunchCount)
+    hmap_next_.Reserve(sizeof(ChunkMeta), /*mapped=*/true);
+    std::memset(hmap_next_.get(), 0, sizeof(ChunkMeta));
+    meta_next_.Reserve(sizeof(ChunkMeta));
     if (!cfg_.index_uri.empty()) {
       indexed_.reset(new io::IndexedRecordIOSplitter(fs, uri.c_str(), cfg_.index_uri.c_str(), part,
                                                      nparts, 1, cfg_.shuffle, cfg_.seed));
@@ -146,6 +151,7 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
   ~DeviceRecordIOImpl() override {
     (void)hipStreamSynchronize(copy_.get());
     (void)hipStreamSynchronize(compute_.get());
+    (void)hipStreamSynchronize(count_.get());
     for (auto& p : ready_) {
       if (p.host != nullptr) iter_.Recycle(&p.host);
     }
@@ -401,6 +407,7 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
   void Drain() {
     copy_.Synchronize();
     compute_.Synchronize();
+    DropPrelaunch();
     for (auto& p : ready_) {
       if (p.host != nullptr) iter_.Recycle(&p.host);
     }
@@ -413,7 +420,10 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
     const double t0 = GetTime();
     ChunkMeta* hm = hmap_.get<ChunkMeta>();
     volatile unsigned* flag = &hm->pad;
-    if (!WaitHostFlag(flag, cfg_.wait_spin_us, 0.05, &waits_)) compute_.Synchronize();
+    if (!WaitHostFlag(flag, cfg_.wait_spin_us, 0.05, &waits_)) {
+      compute_.Synchronize();
+      count_.Synchronize();
+    }
     std::atomic_thread_fence(std::memory_order_acquire);
     ChunkMeta m;
     std::memcpy(&m, const_cast<const ChunkMeta*>(hm), sizeof(m));
@@ -434,13 +444,27 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
     if (p.slot >= 0) DMLC_HIP_CHECK(hipStreamWaitEvent(st, slots_[p.slot]->copied.get(), 0));
     const size_t nwords = p.bytes / 4;
     const size_t tiles = RecordIOTiles(nwords);
-    tcounts_.Reserve(TileScratchWords(tiles) * sizeof(uint64_t));
-    tflags_.Reserve(TileScratchWords(tiles) * sizeof(uint32_t));
+    if (pre_.valid && pre_.words == p.words && pre_.bytes == p.bytes) {
+      // R1 + scan of this piece ran on count_ beside the previous fill: adopt
+      // that scratch set; the fill waits for the scan that wrote its prefix
+      tcounts_.swap(tcounts_next_);
+      tflags_.swap(tflags_next_);
+      meta_.swap(meta_next_);
+      hmap_.swap(hmap_next_);
+      pre_.valid = false;
+      DMLC_HIP_CHECK(hipStreamWaitEvent(st, pre_done_.get(), 0));
+    } else {
+      DropPrelaunch();
+      tcounts_.Reserve(TileScratchWords(tiles) * sizeof(uint64_t));
+      tflags_.Reserve(TileScratchWords(tiles) * sizeof(uint32_t));
+      LaunchRecordIOTileCount(p.words, nwords, tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(),
+                              st);
+      LaunchTileScanRaw(tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(), tiles,
+                        meta_.get<ChunkMeta>(), hmap_.get<ChunkMeta>(), st);
+    }
     partials_.Reserve(TileScratchSlots(tiles) * sizeof(MetaPartial));
     ChunkMeta* dmeta = meta_.get<ChunkMeta>();
     ChunkMeta* hm = hmap_.get<ChunkMeta>();
-    LaunchRecordIOTileCount(p.words, nwords, tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(), st);
-    LaunchTileScanRaw(tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(), tiles, dmeta, hm, st);
     const ChunkMeta sizes = WaitMeta();
     // the copy of this piece is complete: its pinned slot goes back to the reader
     if (p.host != nullptr) iter_.Recycle(&p.host);
@@ -465,6 +489,7 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
     LaunchRecordIOTileFill(p.words, nwords, tcounts_.get<uint64_t>(), off, rec_base, dat, byte_base,
                            partials_.get<MetaPartial>(), st);
     LaunchTileFinish(partials_.get<MetaPartial>(), tiles, dmeta, hm, off, rec_base, byte_base, st);
+    if (resident) PrelaunchCount();
     const ChunkMeta done = WaitMeta();
     if (p.slot >= 0) slots_[p.slot]->parsed.Record(st);
     busy_ = 0;
@@ -483,6 +508,38 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
     stats_.records += nrec;
   }
 
+  /*!
+   * \brief ReadAll over the HBM cache: start the next replayed piece's R1 +
+   *  scan on count_ (second scratch set) so it overlaps the current fill
+   *  instead of following the host's turnaround; the set it writes was last
+   *  used by the piece before the current one, which is complete.
+   */
+  void PrelaunchCount() {
+    if (!replay_ || indexed_ != nullptr || pre_.valid || ready_.empty()) return;
+    const Piece& nx = ready_.front();
+    if (nx.slot >= 0 || nx.host != nullptr) return;  // not an arena-resident piece
+    const size_t nwords = nx.bytes / 4;
+    const size_t tiles = RecordIOTiles(nwords);
+    tcounts_next_.Reserve(TileScratchWords(tiles) * sizeof(uint64_t));
+    tflags_next_.Reserve(TileScratchWords(tiles) * sizeof(uint32_t));
+    LaunchRecordIOTileCount(nx.words, nwords, tcounts_next_.get<uint64_t>(),
+                            tflags_next_.get<uint32_t>(), count_.get());
+    LaunchTileScanRaw(tcounts_next_.get<uint64_t>(), tflags_next_.get<uint32_t>(), tiles,
+                      meta_next_.get<ChunkMeta>(), hmap_next_.get<ChunkMeta>(), count_.get());
+    pre_done_.Record(count_.get());
+    pre_.valid = true;
+    pre_.words = nx.words;
+    pre_.bytes = nx.bytes;
+  }
+
+  /*! \brief retire a prelaunched count nobody adopts (its flag re-armed) */
+  void DropPrelaunch() {
+    if (!pre_.valid) return;
+    count_.Synchronize();
+    hmap_next_.get<ChunkMeta>()->pad = 0;
+    pre_.valid = false;
+  }
+
   void GrowResident(size_t nrec, size_t bytes) {
     const size_t need_off = (resident_rows_ + nrec + 1) * sizeof(uint64_t);
     if (need_off > res_off_.bytes()) {
@@ -499,7 +556,8 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
   std::unique_ptr<io::IndexedRecordIOSplitter> indexed_;
   std::unique_ptr<ZeroCopySource> zc_;
   ThreadedIter<HostSlot> iter_;
-  Stream copy_, compute_;
+  Stream copy_, compute_, count_;
+  Event pre_done_;
   std::vector<std::unique_ptr<DevSlot>> slots_;
   std::deque<Piece> ready_;
   int next_slot_{0};
@@ -515,6 +573,14 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
   // decode scratch and outputs
   DeviceBuffer tcounts_, tflags_, partials_, meta_;
   PinnedBuffer hmap_;
+  // the prelaunched next piece's R1 + scan scratch (ReadAll over the HBM cache)
+  DeviceBuffer tcounts_next_, tflags_next_, meta_next_;
+  PinnedBuffer hmap_next_;
+  struct Prelaunch {
+    bool valid{false};
+    const uint32_t* words{nullptr};
+    size_t bytes{0};
+  } pre_;
   HostWaitStats waits_;
   DeviceBuffer out_off_, out_data_, res_off_, res_data_;
   size_t resident_rows_{0}, resident_bytes_{0};

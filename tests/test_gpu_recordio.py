@@ -181,6 +181,27 @@ def test_gpu_recordio_hbm_cache_replay(tmp_path, zero_copy):
     assert got == recs
 
 
+@pytest.mark.parametrize("replay_mb", [0.03, 0.1])
+def test_gpu_recordio_replay_prelaunched_counts(tmp_path, replay_mb):
+    """read_all over the HBM cache runs the next piece's count + scan on a
+    second stream beside the current fill: many small merged pieces, epochs
+    with a streaming pass in between, every epoch equal to the CPU reader."""
+    p = tmp_path / "q.rec"
+    recs = _records(3000, 11)
+    _write(p, recs)
+    r = io.GPURecordIO(str(p), 0, 1, chunk_bytes=16 * 1024, hbm_cache=1, device_slots=3,
+                       replay_chunk_mb=replay_mb)
+    for e in range(4):
+        if e:
+            r.before_first()
+        r.read_all()
+        assert io.split_records(*r.resident_to_host()) == recs, e
+        if e == 1:
+            r.before_first()
+            assert next(r.iter_host(), None) is not None  # a partial streaming pass
+    assert r.stats()["replayed_chunks"] > 4
+
+
 def test_gpu_recordio_rejects_corrupt_chain(tmp_path):
     p = tmp_path / "c.rec"
     recs = [b"x" * 40, bytes(MAGIC) * 3 + b"tail!", b"y" * 12]
