@@ -345,7 +345,9 @@ def main():
                 "model": fmt["model"],
                 "global_batch": int(rows),
                 "seq_len": None,
-                "parallelism": f"dp{world} (InputSplit byte-range shards, RCCL NumCol all-reduce)",
+                "parallelism": (f"dp{world} (InputSplit byte-range shards, "
+                                + ("RCCL" if use_gpu else "gloo") + " NumCol all-reduce)"
+                                if world > 1 else "dp1 (one InputSplit shard, no collective)"),
                 "format": args.format,
                 "rows": int(rows),
                 "nnz" if args.format != "recordio" else "payload_bytes": int(nnz),

@@ -114,6 +114,14 @@ def transpose(csr: Dict, num_features: int) -> Dict:
             "value": value[perm].contiguous() if value is not None else None}
 
 
+def _source_key(csr: Dict, num_features: int):
+    """identity of the tensors a cached transpose was built from: storage,
+    size and in-place version of offset / index / value"""
+    def one(t):
+        return None if t is None else (int(t.data_ptr()), t.numel(), t._version)
+    return (num_features, one(csr["offset"]), one(csr["index"]), one(csr.get("value")))
+
+
 class SpMVFunction(torch.autograd.Function):
     """Autograd wrapper: forward = spmv, backward d/dw = X^T g -- a gather
     SpMV over the transpose cached in ``csr['transpose']``, or the f32-atomic
@@ -133,15 +141,20 @@ class SpMVFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_out):
         grad_out = grad_out.contiguous().float()
+        key = _source_key(ctx.csr, ctx.num_features)
         t = ctx.holder.get("transpose")
-        if t is not None and t["offset"].numel() != ctx.num_features + 1:
-            t = None
+        if t is not None and ctx.holder.get("_transpose_key") != key:
+            t = None  # the dict now holds other tensors (or they were written in place)
         if t is None and ctx.grad != "atomic":
             uses = ctx.holder.get("_backward_calls", 0) + 1
+            if ctx.holder.get("_calls_key") != key:
+                uses = 1
             ctx.holder["_backward_calls"] = uses
+            ctx.holder["_calls_key"] = key
             if ctx.grad == "transpose" or uses >= 2:
                 t = transpose(ctx.csr, ctx.num_features)
                 ctx.holder["transpose"] = t
+                ctx.holder["_transpose_key"] = key
         if t is not None and ctx.grad != "atomic":
             gw = spmv(t, grad_out, 0.0)
         else:

@@ -80,6 +80,7 @@ class CSVParser : public TextParserBase<IndexType, DType> {
       ++column;
       if (fe == le) break;
       p = fe + 1;
+      if (p == le) break;  // a trailing delimiter opens no empty field (reference :83-96)
     }
     out->label.push_back(static_cast<DType>(label));
     // a weight column gives every row a weight (1.0 when the row is short)

@@ -136,7 +136,9 @@ __device__ __forceinline__ Slice step_slice(uint4 g, uint32_t s, uint32_t nrem, 
   const uint32_t pe = lane == 0 ? w->carry_eol : up_e;
   const uint32_t pd = lane == 0 ? w->carry_delim : up_d;
   uint32_t lm = ~e & ((e << 1) | pe) & 0xFFFFu;
-  uint32_t fm = lm | (((d << 1) | pd) & 0xFFFFu);
+  // a delimiter opens a field unless the line (or the chunk) ends right after
+  // it: no empty last field for a trailing delimiter (reference csv_parser.h:83-96)
+  uint32_t fm = lm | (((d << 1) | pd) & ~e & 0xFFFFu);
   w->carry_eol = __shfl(last_e, kWave - 1, kWave);
   w->carry_delim = __shfl(last_d, kWave - 1, kWave);
   // ownership: from the first row start in the tile to the first one after it
@@ -272,7 +274,8 @@ __device__ __noinline__ GenericField generic_field(const char* q, const char* en
   const char* fe = q;
   while (fe != end && *fe != delim && *fe != '\n' && *fe != '\r') ++fe;
   GenericField r;
-  r.last = fe == end || *fe != delim;
+  // the row's last field: EOL / chunk end, or a trailing delimiter before them
+  r.last = fe == end || *fe != delim || fe + 1 == end || fe[1] == '\n' || fe[1] == '\r';
   while (q != fe && data::isspace(*q)) ++q;
   r.v = data::StrToFloat(q, fe, nullptr);
   return r;
@@ -360,18 +363,25 @@ __global__ __launch_bounds__(kThreads) void k_csv_tile_fill(const uint8_t* __res
         const uint32_t row_t = en.x >> 16;
         const uint32_t col = en.y & 0xFFFFu;
         const uint32_t ent = en.y >> 16;
-        const uint32_t c0 = reinterpret_cast<const uint8_t*>(ring)[off];
+        const uint8_t* rb = reinterpret_cast<const uint8_t*>(ring);
+        const uint32_t c0 = rb[off];
+        // a field ended by a delimiter is still the row's last one when the
+        // line ends right after that delimiter (no empty trailing field)
+        auto eol_at = [&](uint32_t o) {
+          const uint32_t c = rb[o];
+          return c == '\n' || c == '\r' || c == 0;
+        };
         float v;
         bool last;
         if (c0 == delim || c0 == '\n' || c0 == '\r' || c0 == 0) {
           v = 0.0f;  // empty field
-          last = c0 != delim;
+          last = c0 != delim || eol_at(off + 1);
         } else {
           const tok::Num x = tok::parse_num(ring, off);
           const bool t_eol = x.term == '\n' || x.term == '\r' || x.term == 0;
           if (x.ok_float && (x.term == delim || t_eol)) {
             v = x.fval;
-            last = t_eol;
+            last = t_eol || eol_at(x.end + 1);
           } else {
             const size_t gpos = tile0 + s * kStep + (off - slot * 16u);
             const GenericField g = generic_field(reinterpret_cast<const char*>(text) + gpos,

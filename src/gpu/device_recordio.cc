@@ -199,7 +199,9 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
     res_off_.Grow(sizeof(uint64_t), 0, compute_.get());
     DMLC_HIP_CHECK(hipMemsetAsync(res_off_.get<uint64_t>(), 0, sizeof(uint64_t), compute_.get()));
     Piece p;
+    merge_replay_ = true;  // resident decode: adjacent cached chunks may merge
     while (NextPiece(&p)) Decode(p, true);
+    merge_replay_ = false;
     compute_.Synchronize();
     resident_.size = resident_rows_;
     resident_.bytes = resident_bytes_;
@@ -337,8 +339,9 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
     if (replay_idx_ >= cached_.size()) return false;
     size_t off = cached_[replay_idx_].first, n = cached_[replay_idx_].second;
     ++replay_idx_;
-    // adjacent cached chunks decode as one (fewer launches and host waits)
-    while (replay_idx_ < cached_.size() && cached_[replay_idx_].first == off + n &&
+    // ReadAll: adjacent cached chunks decode as one (fewer launches and host
+    // waits); Next() keeps the first epoch's batch boundaries (<= chunk_bytes)
+    while (merge_replay_ && replay_idx_ < cached_.size() && cached_[replay_idx_].first == off + n &&
            n + cached_[replay_idx_].second <= cfg_.replay_chunk_bytes) {
       n += cached_[replay_idx_++].second;
     }
@@ -568,6 +571,7 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
   size_t arena_fill_{0}, arena_base_{0}, replay_idx_{0}, epoch_pos_{0};
   std::vector<std::pair<size_t, size_t>> cached_;
   bool caching_{false}, cache_complete_{false}, replay_{false}, arena_loaded_{false};
+  bool merge_replay_{false};  // inside ReadAll: ReplayPiece may merge cached chunks
   std::vector<uint64_t> tmp_src_, tmp_dst_;
   std::vector<uint32_t> tmp_len_;
   // decode scratch and outputs

@@ -56,11 +56,16 @@ inline bool WaitHostFlag(const volatile unsigned* flag, double spin_us, double b
     CpuRelax();
     if ((i & 63u) == 63u && GetTime() >= spin_end) break;
   }
-  static thread_local bool slack_set = false;
-  if (!slack_set) {
-    (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // 1 us
-    slack_set = true;
-  }
+  // a tight timer slack for the sleep phase only: the caller's thread (often
+  // the training loop) gets its own slack back before we return
+  const int old_slack = prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);
+  (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // 1 us
+  struct Restore {
+    int v;
+    ~Restore() {
+      if (v > 0) (void)prctl(PR_SET_TIMERSLACK, static_cast<unsigned long>(v), 0, 0, 0);
+    }
+  } restore{old_slack};
   const struct timespec nap = {0, 5000};  // 5 us
   for (;;) {
     if (*flag != 0) {

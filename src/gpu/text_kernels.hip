@@ -279,10 +279,7 @@ __device__ void walk_line(const uint8_t* __restrict__ text, uint32_t b, uint32_t
   uint32_t tok_base = 0, rank_base = 0;
   bool prev_sep = true;     // byte before the line start behaves as a separator
   bool prev_delim = false;  // CSV: previous byte was the delimiter
-  // CSV: a line ending in the delimiter has an empty field at e, which can be
-  // the first byte of one more piece
-  const uint32_t stop = (F == TextFormat::kCSV && text[e - 1] == static_cast<uint8_t>(delim)) ? e + 1 : e;
-  for (uint32_t pstart = wbase; pstart < stop; pstart += kPiece) {
+  for (uint32_t pstart = wbase; pstart < e; pstart += kPiece) {
     const uint32_t pos = pstart + 16 * lane;
     // token starts of this lane's 16 bytes
     uint32_t starts;
@@ -291,11 +288,13 @@ __device__ void walk_line(const uint8_t* __restrict__ text, uint32_t b, uint32_t
       const uint32_t up_delim = __shfl_up(mcur.delim, 1, dev::kWave);
       if constexpr (F == TextFormat::kCSV) {
         const uint32_t pd = lane == 0 ? (prev_delim ? 1u : 0u) : ((up_delim >> 15) & 1u);
-        // every byte after a delimiter starts a field -- also the line end
-        // after a trailing delimiter (an empty last field, csv_parser.h)
+        // every byte after a delimiter starts a field, up to the line end: a
+        // trailing delimiter opens no empty last field (reference
+        // csv_parser.h:83-96 stops when p reaches lend after the delimiter)
         starts = (mcur.delim << 1) | pd;
         if (b >= pos && b < pos + 16) starts |= 1u << (b - pos);
-        starts &= 0xFFFFu;
+        const uint32_t room = e > pos ? (e - pos < 16 ? e - pos : 16u) : 0u;
+        starts &= room >= 16 ? 0xFFFFu : ((1u << room) - 1u);
       } else {
         const uint32_t ps = lane == 0 ? (prev_sep ? 1u : 0u) : ((up_sep >> 15) & 1u);
         starts = ~mcur.sep & ((mcur.sep << 1) | ps) & 0xFFFFu;

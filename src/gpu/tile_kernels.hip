@@ -768,8 +768,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
                                                         size_t ntiles,
                                                         const uint64_t* __restrict__ prefix,
                                                         FillTarget<IndexType> out,
-                                                        MetaPartial* __restrict__ partials,
-                                                        int exp_mode) {
+                                                        MetaPartial* __restrict__ partials) {
   __shared__ uint4 s_text[kFillWaves][kStageVecs];
   __shared__ uint32_t s_list[kFillWaves][kListCap + 64];  // + a dummy slot per lane
   const int wave = threadIdx.x / dev::kWave;
@@ -878,7 +877,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
     // decoded now (its slot is restaged next step), and the last step takes all
     const uint32_t total = carry + ntok;
     const uint32_t rest = total % dev::kWave < ntok ? total % dev::kWave : ntok;
-    const uint32_t ndec = (last || exp_mode == 3) ? (exp_mode == 3 ? 0u : total) : total - rest;
+    const uint32_t ndec = last ? total : total - rest;
     for (uint32_t r0 = 0; r0 < ndec; r0 += dev::kWave) {
       const uint32_t li = r0 + slot;
       const bool active = li < ndec;
@@ -891,16 +890,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
       t.u0_hi = t.u1_hi = 0;
       t.u1 = 0;
       bool bad = false;
-      bool ok;
-      if (exp_mode >= 1) {
-        t.u0 = off;
-        t.f0 = 1.0f;
-        t.f1 = 0.0f;
-        t.r = 1;
-        ok = true;
-      } else {
-        ok = tok::decode<F>(st, off, is_label, &t);
-      }
+      const bool ok = tok::decode<F>(st, off, is_label, &t);
       if (active & !ok) {
         // the step a slot holds: s, or s - 1 for a carried token
         const uint32_t in_slot = off >= kSlotBytes ? 1u : 0u;
@@ -921,7 +911,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
       bool field_ok = true;
       if (F == TextFormat::kLibFM) field_ok = is_label || t.r >= 2;
       irregular |= active & (is_label ? !row_ok : (!nnz_ok | !field_ok));
-      if (active & is_label & row_ok & (exp_mode != 2)) {
+      if (active & is_label & row_ok) {
         lab_at[lc] = t.f0;
         off_at[lc] = C + 1 + (static_cast<int64_t>(i) - static_cast<int64_t>(lc));
         if (wgt_at != nullptr) wgt_at[lc] = t.r == 2 ? t.f1 : 1.0f;
@@ -929,7 +919,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
       }
       need_w |= active & is_label & (wgt_at == nullptr) & (t.r == 2);
       any_weight |= active & is_label & (t.r == 2);
-      const bool feat = active & !is_label & nnz_ok & field_ok & (exp_mode != 2);
+      const bool feat = active & !is_label & nnz_ok & field_ok;
       const uint64_t u0 = (static_cast<uint64_t>(t.u0_hi) << 32) | t.u0;
       if constexpr (F == TextFormat::kLibSVM) {
         if (feat) {
@@ -955,7 +945,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
       neg |= active && bad;
     }
     // the undecoded rest moves to the front of the list (all lanes read before any writes)
-    const uint32_t left = exp_mode == 3 ? 0u : total - ndec;  // mode 3 decodes nothing
+    const uint32_t left = total - ndec;
     const uint32_t moved = lane < static_cast<int>(left) ? sl[ndec + lane] : 0u;
     dev::wave_sync();
     if (lane < static_cast<int>(left)) sl[lane] = moved;
@@ -1441,13 +1431,12 @@ void LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
   const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
   if (ntiles != 0) {
     const dim3 grid(static_cast<unsigned>((ntiles + kFillWaves - 1) / kFillWaves));
-    static const int exp_mode = getenv("DMLC_FILL_EXP") ? atoi(getenv("DMLC_FILL_EXP")) : 0;
     if (format == TextFormat::kLibFM) {
       hipLaunchKernelGGL((k_tile_fill<TextFormat::kLibFM, IndexType>), grid, dim3(kThreads), 0,
-                         stream, t, nbytes, ntiles, tile_prefix, out, partials, exp_mode);
+                         stream, t, nbytes, ntiles, tile_prefix, out, partials);
     } else {
       hipLaunchKernelGGL((k_tile_fill<TextFormat::kLibSVM, IndexType>), grid, dim3(kThreads), 0,
-                         stream, t, nbytes, ntiles, tile_prefix, out, partials, exp_mode);
+                         stream, t, nbytes, ntiles, tile_prefix, out, partials);
     }
   }
   LaunchFinish(partials, ntiles, meta, host_meta, out.offset, out.row_base, out.nnz_base, stream);

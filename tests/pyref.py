@@ -169,6 +169,10 @@ def parse_csv(text: str, label_column=-1, delim=","):
     rows = []
     for line in _lines(text):
         fields = line.split(delim)
+        # reference csv_parser.h:83-96: after skipping a delimiter the loop stops
+        # when p reaches the line end, so a trailing delimiter adds no field
+        if len(fields) > 1 and fields[-1] == "":
+            fields.pop()
         lab = 0.0
         feats = []
         for c, f in enumerate(fields):

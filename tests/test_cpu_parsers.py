@@ -135,6 +135,23 @@ def test_csv_matches_oracle(tmp_path, label_column):
     np.testing.assert_array_equal(got["index"], np.array(idx, np.uint64))
 
 
+# trailing delimiters, derived by hand from the reference loop
+# (csv_parser.h:83-96: parse, skip to ',', step over it, stop at the line end)
+CSV_TRAILING = "1,2,\n3,,\n,\n4,5\n6,\n"
+CSV_TRAILING_ROWS = [[1.0, 2.0], [3.0, 0.0], [0.0], [4.0, 5.0], [6.0]]
+
+
+def test_csv_trailing_delimiter_matches_reference(tmp_path):
+    p = write(str(tmp_path / "t.csv"), CSV_TRAILING)
+    got = pyref.concat_blocks(list(data.iter_blocks(p, type="csv")))
+    np.testing.assert_array_equal(got["offset"], np.cumsum([0] + [len(r) for r in CSV_TRAILING_ROWS]))
+    np.testing.assert_array_equal(got["value"], np.array(sum(CSV_TRAILING_ROWS, []), np.float32))
+    assert [r[1] for r in pyref.parse_csv(CSV_TRAILING)] == CSV_TRAILING_ROWS
+    # label column 1 of '6,' is missing: label 0
+    got = pyref.concat_blocks(list(data.iter_blocks(p + "?label_column=1", type="csv")))
+    np.testing.assert_array_equal(got["label"], np.array([2, 0, 0, 5, 0], np.float32))
+
+
 def test_csv_auto_format(tmp_path):
     p = write(str(tmp_path / "a.csv"), "1,2\n3,4\n")
     got = pyref.concat_blocks(list(data.iter_blocks(p + "?format=csv&label_column=0", type="auto")))

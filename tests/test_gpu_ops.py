@@ -135,3 +135,38 @@ def test_transpose_of_a_row_slice_and_auto_mode(csr_t):
             assert "transpose" not in holder
     assert "transpose" in holder
     torch.testing.assert_close(grads[1], grads[0], rtol=1e-4, atol=1e-6)
+
+
+def test_cached_transpose_follows_the_dict_tensors(csr_t):
+    """A dict refilled with another batch's tensors (csr.update(next_batch))
+    must not reuse the transpose of the previous tensors: every backward
+    equals the atomic gradient of the tensors the dict holds now."""
+    import torch
+    from dmlc_core_amd.models import SparseLogReg
+    t, csr = csr_t
+    nfeat = int(csr.max_index) + 1
+    m = SparseLogReg(nfeat, grad="transpose").cuda()
+    ref = SparseLogReg(nfeat, grad="atomic").cuda()
+    with torch.no_grad():
+        m.weight.copy_(torch.linspace(-1, 1, nfeat, device="cuda"))
+        ref.weight.copy_(m.weight)
+    holder = {}
+    for b, e in ((0, 900), (900, 2000), (300, 1300)):
+        batch = {"offset": t["offset"][b:e + 1].clone(), "index": t["index"], "value": t["value"],
+                 "label": t["label"][b:e].clone()}
+        holder.update(batch)
+        m.zero_grad()
+        ref.zero_grad()
+        m.loss(holder).backward()
+        ref.loss(batch).backward()
+        torch.testing.assert_close(m.weight.grad, ref.weight.grad, rtol=1e-4, atol=1e-6)
+    # an in-place rewrite of the values invalidates it too
+    holder["value"] = t["value"].clone()
+    m.zero_grad()
+    m.loss(holder).backward()
+    holder["value"].mul_(2.0)
+    m.zero_grad()
+    ref.zero_grad()
+    m.loss(holder).backward()
+    ref.loss({k: holder[k] for k in ("offset", "index", "value", "label")}).backward()
+    torch.testing.assert_close(m.weight.grad, ref.weight.grad, rtol=1e-4, atol=1e-6)

@@ -138,6 +138,26 @@ def test_libfm_gpu_equals_cpu(tmp_path):
     assert_same(g, c, field=True)
 
 
+@pytest.mark.parametrize("fast_path", [1, 0])
+@pytest.mark.parametrize("label_column", [-1, 1])
+def test_csv_trailing_delimiter_matches_reference(tmp_path, fast_path, label_column):
+    """a line ending in the delimiter has no empty last field (reference
+    csv_parser.h:83-96), on the tile path and on the exact per-line kernels"""
+    from test_cpu_parsers import CSV_TRAILING, CSV_TRAILING_ROWS
+    p = str(tmp_path / "t.csv")
+    with open(p, "w") as f:
+        f.write(CSV_TRAILING * 50)
+    rows = CSV_TRAILING_ROWS * 50
+    g = gpu_rows(p, "csv", label_column=label_column, fast_path=fast_path)
+    if label_column < 0:
+        np.testing.assert_array_equal(g["offset"], np.cumsum([0] + [len(r) for r in rows]))
+        np.testing.assert_array_equal(g["value"], np.array(sum(rows, []), np.float32))
+    else:
+        lab = [r[1] if len(r) > 1 else 0.0 for r in rows]
+        np.testing.assert_array_equal(g["label"], np.array(lab, np.float32))
+    assert_same(g, cpu_rows(p + f"?label_column={label_column}", "csv"))
+
+
 @pytest.mark.parametrize("label_column", [-1, 0, 3])
 def test_csv_gpu_equals_cpu(tmp_path, label_column):
     p = str(tmp_path / "s.csv")

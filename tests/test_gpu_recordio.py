@@ -173,10 +173,12 @@ def test_gpu_recordio_hbm_cache_replay(tmp_path, zero_copy):
         r.read_all()
         assert io.split_records(*r.resident_to_host()) == recs, e
     assert r.stats()["replayed_chunks"] > 0
-    # streaming from the cache too
+    # streaming from the cache too, with the first epoch's batch sizes (the
+    # resident read_all merges cached chunks; Next() must not)
     r.before_first()
     got = []
     for off, data in r.iter_host():
+        assert len(data) <= 16 * 1024 + 1024, len(data)
         got += io.split_records(off, data)
     assert got == recs
 

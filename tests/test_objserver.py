@@ -72,3 +72,27 @@ def test_ranged_reads_match_file(server):
     s = io.Stream("s3://bk/text/part-2.txt", "r")
     data = s.read(1 << 30)
     assert data == (root / "bk" / "text" / "part-2.txt").read_bytes()
+
+
+def test_range_edge_cases(server):
+    """suffix ranges return the last N bytes (as S3); a reversed range is 416"""
+    import http.client
+    port, root, _ = server
+    body = (root / "bk" / "text" / "part-1.txt").read_bytes()
+
+    def get(rng):
+        c = http.client.HTTPConnection("127.0.0.1", port, timeout=10)
+        c.request("GET", "/bk/text/part-1.txt", headers={"Range": rng})
+        r = c.getresponse()
+        out = (r.status, r.getheader("Content-Length"), r.read())
+        c.close()
+        return out
+
+    st, ln, data = get("bytes=-500")
+    assert st == 206 and data == body[-500:] and int(ln) == 500
+    st, _, data = get("bytes=-%d" % (len(body) + 10))
+    assert st == 206 and data == body
+    st, _, data = get("bytes=10-19")
+    assert st == 206 and data == body[10:20]
+    st, _, _ = get("bytes=100-50")
+    assert st == 416

@@ -186,12 +186,22 @@ bool Serve(int fd, const std::string& method, const std::string& target,
   if (r != hdr.end() && r->second.compare(0, 6, "bytes=") == 0) {
     const std::string spec = r->second.substr(6);
     const size_t dash = spec.find('-');
-    b = std::strtoull(spec.substr(0, dash).c_str(), nullptr, 10);
-    if (dash + 1 < spec.size()) {
-      e = std::min<uint64_t>(e, std::strtoull(spec.c_str() + dash + 1, nullptr, 10));
+    bool bad = dash == std::string::npos;
+    if (!bad && dash == 0) {
+      // suffix range bytes=-N: the last N bytes (as S3)
+      const uint64_t want = std::strtoull(spec.c_str() + 1, nullptr, 10);
+      bad = want == 0;
+      b = size - std::min<uint64_t>(want, size);
+    } else if (!bad) {
+      b = std::strtoull(spec.substr(0, dash).c_str(), nullptr, 10);
+      if (dash + 1 < spec.size()) {
+        const uint64_t last = std::strtoull(spec.c_str() + dash + 1, nullptr, 10);
+        bad = last < b;
+        e = std::min<uint64_t>(e, last);
+      }
     }
     ranged = true;
-    if (b >= size) {
+    if (bad || b >= size) {
       ::close(f);
       return Reply(fd, 416, "Range Not Satisfiable", "",
                    {"Content-Range: bytes */" + std::to_string(size)}, head);
