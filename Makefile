@@ -34,6 +34,7 @@ CPU_SRCS := src/logging.cc src/fault.cc src/io.cc src/recordio.cc src/data.cc sr
   src/io/shard_reader.cc src/io/http.cc src/io/s3_filesys.cc src/io/azure_filesys.cc \
   src/io/hdfs_filesys.cc \
   src/gpu/runtime.cc src/gpu/device_parser.cc src/gpu/device_recordio.cc src/gpu/device_row_iter.cc \
+  src/gpu/device_page_cache.cc \
   src/dist/tracker_client.cc src/dist/communicator.cc
 HIP_SRCS := $(wildcard src/gpu/*.hip)
 

@@ -77,10 +77,12 @@ def parse_args():
     ap.add_argument("--device", choices=["auto", "gpu", "cpu"], default="auto")
     ap.add_argument("--zero-copy", default="auto", choices=["auto", "0", "1"],
                     help="mmap + hipHostRegister the shard (DMA from page cache)")
-    ap.add_argument("--mode", default="stream", choices=["stream", "hbm"],
+    ap.add_argument("--mode", default="stream", choices=["stream", "hbm", "cache"],
                     help="stream: every step re-reads the text from the page cache over PCIe; "
                          "hbm: HBM epoch cache -- the warmup epoch keeps the text resident in "
-                         "HBM and timed epochs parse it from there (kernel-bound)")
+                         "HBM and timed epochs parse it from there (kernel-bound); "
+                         "cache: the `#cache` binary page file (DiskRowIter format, built once "
+                         "from a GPU parse) is DMA'd zero-copy into the device CSR every step")
     args = ap.parse_args()
     if args.rows <= 0:
         args.rows = FORMATS[args.format]["rows"]
@@ -226,6 +228,25 @@ def main():
             b = parser.read_all()
             local["rows"], local["bytes"] = b["size"], parser.partition_bytes
             return b["size"], b["bytes"], 0, parser.partition_bytes
+    elif use_gpu and args.mode == "cache":
+        extra = {"label_column": 0} if args.format == "csv" else {}
+        cache_path = os.path.join(ddir, f"rowblock_r{rank}of{world}.cache")
+        if not os.path.exists(cache_path):
+            build = data.GPUParser(ddir, rank, world, format=args.format, chunk_mb=args.chunk_mb,
+                                   read_threads=read_threads, device=local_rank,
+                                   zero_copy=args.zero_copy, **extra)
+            tmp = data.DeviceCSR()
+            build.parse_all(tmp)
+            data.write_page_cache(tmp, cache_path + ".tmp")
+            os.replace(cache_path + ".tmp", cache_path)
+            del build, tmp
+        parser = data.PageCache(cache_path, device=local_rank)
+        csr = data.DeviceCSR()
+
+        def step():
+            parser.load(csr)
+            local["rows"], local["bytes"] = csr.rows, parser.bytes
+            return csr.rows, csr.nnz, csr.max_index, parser.bytes
     elif use_gpu:
         extra = {"label_column": 0} if args.format == "csv" else {}
         parser = data.GPUParser(ddir, rank, world, format=args.format, chunk_mb=args.chunk_mb,
@@ -289,7 +310,7 @@ def main():
     sync()
     elapsed = time.perf_counter() - t0
     # per-rank view (rows, bytes, own time, host waits) gathered to every rank
-    st = parser.stats() if use_gpu else {}
+    st = parser.stats() if use_gpu and args.mode != "cache" else {}
     mine = torch.tensor([rank, local["rows"], local["bytes"], elapsed,
                          st.get("wait_reader_sec", 0.0), st.get("wait_gpu_sec", 0.0)],
                         dtype=torch.float64, device=dev)
@@ -326,6 +347,8 @@ def main():
     if rank == 0:
         ingest = ("HBM epoch cache (input resident in HBM after the warmup epoch)"
                   if use_gpu and args.mode == "hbm" else
+                  "#cache page file: zero-copy DMA of binary RowBlock pages (no parse)"
+                  if use_gpu and args.mode == "cache" else
                   "zero-copy mmap+hipHostRegister DMA" if use_gpu and parser.stats().get("zero_copy")
                   else "parallel pread -> pinned ring -> hipMemcpyAsync" if use_gpu else "CPU")
         out = {
@@ -365,7 +388,11 @@ def main():
             "baseline_value": fmt["baseline"],
         }
         out["per_rank"] = per_rank
-        if use_gpu:
+        if use_gpu and args.mode == "cache":
+            out["metric"] = fmt["metric"].replace("->CSR", " #cache pages->CSR")
+            out["cache"] = {"bytes": parser.bytes, "pages": len(parser.pages()),
+                            "zero_copy": parser.zero_copy}
+        elif use_gpu:
             out["parser_stats_last_rank0"] = parser.stats()
         print(json.dumps(out), flush=True)
     ddist.finalize()

@@ -14,7 +14,8 @@ from typing import Dict, Iterator, Optional
 from .. import _dmlc
 
 __all__ = ["Parser", "RowBlockIter", "GPUParser", "ShuffledGPUParser", "DeviceCSR", "csr_to_torch",
-           "iter_blocks", "write_synthetic", "to_sparse_csr", "GPUBlockDataset"]
+           "iter_blocks", "write_synthetic", "to_sparse_csr", "GPUBlockDataset", "PageCache",
+           "write_page_cache"]
 
 write_synthetic = _dmlc.write_synthetic
 
@@ -44,7 +45,8 @@ def Parser(uri: str, part: int = 0, nparts: int = 1, type: str = "auto",  # noqa
 def RowBlockIter(uri: str, part: int = 0, nparts: int = 1, type: str = "auto",  # noqa: N802,A002
                  index64: bool = False):
     """In-memory (or ``#cache`` paged) iterator, reference RowBlockIter<I>::Create;
-    ``?device=gpu`` parses the whole shard on the MI355X (DeviceRowIter)."""
+    ``?device=gpu`` parses the whole shard on the MI355X (DeviceRowIter), and
+    with ``#cachefile`` loads / builds the same binary page file DiskRowIter uses."""
     cls = _dmlc.RowBlockIter64 if index64 else _dmlc.RowBlockIter
     return cls(_host_blocks_uri(uri), part, nparts, type)
 
@@ -60,6 +62,21 @@ def iter_blocks(uri: str, part: int = 0, nparts: int = 1, type: str = "auto",  #
 def DeviceCSR(index64: bool = False):  # noqa: N802
     """Empty HBM-resident CSR container."""
     return _dmlc.DeviceCSR64() if index64 else _dmlc.DeviceCSR()
+
+
+def PageCache(path: str, device: int = -1, index64: bool = False):  # noqa: N802
+    """Open a ``#cache`` page file (DiskRowIter's binary RowBlock pages) for
+    zero-copy DMA into HBM: ``.load(csr)`` replaces a :func:`DeviceCSR`'s
+    contents with every page (no parse).  None when the file does not exist."""
+    cls = _dmlc.PageCache64 if index64 else _dmlc.PageCache
+    return cls.open(path, device)
+
+
+def write_page_cache(csr, path: str, page_mb: float = 64.0) -> int:
+    """Write a DeviceCSR as ``#cache`` pages (the CPU DiskRowIter's format and
+    64 MiB page rule: same bytes for the same shard).  Returns the page count."""
+    cls = _dmlc.PageCache64 if isinstance(csr, _dmlc.DeviceCSR64) else _dmlc.PageCache
+    return cls.write(csr, path, page_mb)
 
 
 class GPUParser:
@@ -87,40 +104,44 @@ class GPUParser:
         self._p.parse_all(out)
         return out
 
-    #: widest dim at which the fused kernel beats tile CSR + K9 on MI355X
-    #: (profiles/r03_hashed_prelaunch: 1.15x at dim 128, 1.03x at 256, 0.95x
-    #: at 512, 0.65-0.9x at 1024 -- the tile fill got faster in round 3, and
-    #: above 256 the per-wave LDS row buffers cost more than writing the CSR)
-    FUSED_HASH_MAX_DIM = 256
-
     def parse_all_hashed(self, dim: int, seed: int = 0, fp8: bool = True, scale: float = 1.0,
-                         strategy: str = "auto"):
+                         strategy: str = "auto", out: Optional[Dict] = None):
         """Rest of the partition as a hashed dense batch (BASELINE config 5).
         Returns ``{"x": [rows, dim] float8_e4m3fn (or float32), "label": [rows]
-        float32}`` as torch tensors on the device.
+        float32, "batch": handle}`` as torch tensors on the device.
 
-        ``strategy``: ``"fused"`` tokenises, hashes and packs with ONE kernel
-        per chunk (no CSR in between); ``"csr"`` parses to a device CSR and
-        runs :func:`dmlc_core_amd.ops.hashed_dense` (K9); ``"auto"`` takes the
-        faster of the two for ``dim`` (fused up to FUSED_HASH_MAX_DIM).  Both
-        compute the same hash."""
+        ``strategy``: ``"fused"`` (and ``"auto"``) tokenises, hashes and packs
+        with ONE wave-per-tile kernel per chunk (no CSR in between; the tile
+        parser's fast path when dim % 16 == 0, the exact per-line kernel
+        otherwise); ``"csr"`` parses to a device CSR and runs
+        :func:`dmlc_core_amd.ops.hashed_dense` (K9).  Both compute the same hash
+        and the same fp8 bytes.
+
+        ``out``: an earlier result of this call whose tensors are no longer
+        used; its HBM buffers are refilled in place (no multi-GB allocation
+        per epoch).  The earlier ``x`` / ``label`` tensors then alias the new
+        batch."""
         import torch
         import torch.utils.dlpack as tdl
 
         if strategy not in ("auto", "fused", "csr"):
             raise ValueError(f"strategy must be auto, fused or csr, not {strategy!r}")
-        if strategy == "csr" or (strategy == "auto" and dim > self.FUSED_HASH_MAX_DIM):
+        if strategy == "csr":
             from .. import ops
 
             t = csr_to_torch(self.parse_all())
             x = ops.hashed_dense(t, int(dim), seed=seed, fp8=fp8, scale=scale)
-            return {"x": x, "label": t["label"].clone()}  # the CSR buffers are released
+            return {"x": x, "label": t["label"].clone(), "batch": None}  # the CSR is released
 
-        d = self._p.parse_all_hashed(int(dim), float(scale), int(seed) & 0xFFFFFFFF, bool(fp8))
+        handle = out.get("batch") if isinstance(out, dict) else out
+        if handle is not None and torch.cuda.is_available():
+            # the refill must not overtake torch work still reading the old batch
+            torch.cuda.ExternalStream(self._p.stream()).wait_stream(torch.cuda.current_stream())
+        d = self._p.parse_all_hashed(int(dim), float(scale), int(seed) & 0xFFFFFFFF, bool(fp8), handle)
         x = tdl.from_dlpack(d["x"]).view(d["rows"], d["dim"])
         if fp8:
             x = x.view(torch.float8_e4m3fn)
-        return {"x": x, "label": tdl.from_dlpack(d["label"])}
+        return {"x": x, "label": tdl.from_dlpack(d["label"]), "batch": d["batch"]}
 
     def before_first(self):
         self._p.before_first()

@@ -44,9 +44,14 @@ def main():
         csr = two.parse_all()
         return ops.hashed_dense(data.csr_to_torch(csr), args.dim, seed=1, fp8=True, scale=0.5)
 
+    prev = {}
+
     def step_fused():
+        # the batch of the previous pass is refilled in place (out=)
         fused.before_first()
-        return fused.parse_all_hashed(args.dim, seed=1, fp8=True, scale=0.5, strategy="fused")["x"]
+        prev["b"] = fused.parse_all_hashed(args.dim, seed=1, fp8=True, scale=0.5, strategy="fused",
+                                           out=prev.get("b"))
+        return prev["b"]["x"]
 
     res = {}
     for name, fn in (("csr_then_k9", step_two), ("fused", step_fused)):
@@ -60,7 +65,7 @@ def main():
         res[name] = {"ms": round(dt * 1e3, 3), "rows_per_sec": round(x.shape[0] / dt, 1),
                      "text_GBps": round(nbytes / dt / 1e9, 2)}
     a = step_two().view(torch.uint8)
-    b = step_fused().view(torch.uint8)
+    b = step_fused().view(torch.uint8).clone()
     res["identical_fp8"] = bool(torch.equal(a, b))
     res["mismatch_frac"] = float((a != b).float().mean())
     model = HashedFM(dim=args.dim, rank=16).cuda()
@@ -86,8 +91,8 @@ def main():
         t = {}
         for name, fn in (("csr_then_k9", lambda: ops.hashed_dense(
                 data.csr_to_torch(two.parse_all()), d, seed=1, fp8=True, scale=0.5)),
-                         ("fused", lambda: fused.parse_all_hashed(d, seed=1, fp8=True, scale=0.5,
-                                                                  strategy="fused")["x"])):
+                         ("fused", lambda: prev.__setitem__("b", fused.parse_all_hashed(
+                             d, seed=1, fp8=True, scale=0.5, strategy="fused", out=prev.get("b"))))):
             (two if name == "csr_then_k9" else fused).before_first()
             fn()
             torch.cuda.synchronize()

@@ -9,7 +9,8 @@
  * entries (:150-158).
  * Differences: CSV is registered for uint64 as well and threaded (§7.4 #4);
  * `?device=gpu[:k]` routes both factories to the MI355X path
- * (src/gpu/device_row_iter.cc: GPUParser per chunk, DeviceRowIter whole shard);
+ * (src/gpu/device_row_iter.cc: GPUParser per chunk, DeviceRowIter whole shard,
+ * `#cache` through the same binary page file as DiskRowIter);
  * `?nthread=N` is honoured; RowBlockIter keeps `?k=v` args when a cache file
  * is used (the reference dropped them).
  */
@@ -97,7 +98,9 @@ inline RowBlockIter<IndexType>* CreateIter_(const char* uri_, unsigned part_inde
       ptype = it != spec.args.end() ? it->second : "libsvm";
     }
     CHECK(DeviceRoute<IndexType>::iter != nullptr) << "device=gpu: the GPU path is not built in";
-    return DeviceRoute<IndexType>::iter(spec.uri, spec.args, part_index, num_parts, ptype);
+    // `#cache` is honoured on this route too (DevicePageCache: same page file)
+    return DeviceRoute<IndexType>::iter(spec.uri, spec.args, part_index, num_parts, ptype,
+                                        spec.cache_file);
   }
   std::string parser_uri = uri_;
   const size_t hash = parser_uri.find('#');

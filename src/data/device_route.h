@@ -27,10 +27,12 @@ struct DeviceRoute {
   typedef Parser<IndexType>* (*ParserFn)(const std::string& uri,
                                          const std::map<std::string, std::string>& args,
                                          unsigned part, unsigned nparts, const std::string& type);
+  /*! cache_file: the `#cache` page file ("" for none), as DiskRowIter's */
   typedef RowBlockIter<IndexType>* (*IterFn)(const std::string& uri,
                                              const std::map<std::string, std::string>& args,
                                              unsigned part, unsigned nparts,
-                                             const std::string& type);
+                                             const std::string& type,
+                                             const std::string& cache_file);
   static ParserFn parser;
   static IterFn iter;
 };

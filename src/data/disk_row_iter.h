@@ -4,6 +4,9 @@
  * Parity: reference `src/data/disk_row_iter.h:29-139` — first use builds the
  * cache by flushing a RowBlockContainer every 64 MiB, later epochs stream the
  * pages back through a ThreadedIter; NumCol tracked over all pages.
+ * Difference: the 64 MiB test runs after every row, not after every parser
+ * block, so page boundaries do not depend on the parser's thread count (and
+ * match the GPU route's DevicePageCache byte for byte).
  */
 #ifndef DMLC_DATA_DISK_ROW_ITER_H_
 #define DMLC_DATA_DISK_ROW_ITER_H_
@@ -80,14 +83,21 @@ class DiskRowIter : public RowBlockIter<IndexType, DType> {
     std::unique_ptr<Stream> fo(Stream::Create(cache_file_.c_str(), "w"));
     RowBlockContainer<IndexType, DType> page;
     const double tstart = GetTime();
+    // the page-size test runs after every row (the reference tests after each
+    // parser block, whose size depends on the thread count): page boundaries
+    // are a function of the data alone, and the GPU route's DevicePageCache
+    // writes the same pages
     while (parser->Next()) {
-      page.Push(parser->Value());
-      if (page.MemCostBytes() >= kPageSize) {
-        page.Finalize();
-        page.Save(fo.get());
-        page.Clear();
-        VLOG(1) << (parser->BytesRead() >> 20UL) << "MB read, "
-                << (parser->BytesRead() >> 20UL) / (GetTime() - tstart) << " MB/sec";
+      const RowBlock<IndexType, DType> blk = parser->Value();
+      for (size_t i = 0; i < blk.size; ++i) {
+        page.Push(blk[i]);
+        if (page.MemCostBytes() >= kPageSize) {
+          page.Finalize();
+          page.Save(fo.get());
+          page.Clear();
+          VLOG(1) << (parser->BytesRead() >> 20UL) << "MB read, "
+                  << (parser->BytesRead() >> 20UL) / (GetTime() - tstart) << " MB/sec";
+        }
       }
     }
     if (page.Size() != 0) {

@@ -776,10 +776,22 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     CHECK(tcfg_.format != TextFormat::kCSV) << "hashed batches are built from LibSVM / LibFM";
     CHECK(dim > 0 && dim % 4 == 0 && dim <= 4096) << "dim must be a multiple of 4 in (0, 4096]";
     ScopedRange range("DeviceParser::ParseAllHashed");
+    if (out->row_cap != 0 && (out->dim != dim || out->fp8 != fp8 || out->device != device_)) {
+      *out = DeviceHashedBatch();  // a reused batch of another shape: reallocate
+    }
     out->device = device_;
     out->dim = dim;
     out->fp8 = fp8;
     out->rows = 0;
+    // the first chunk sizes the batch for the whole partition from its density
+    // (no doubling copies of a multi-GB batch); a reused batch usually fits already
+    auto reserve = [&](size_t chunk_rows, size_t nbytes) {
+      if (out->rows == 0) {
+        const double f = static_cast<double>(PartitionBytes()) / std::max<size_t>(nbytes, 1);
+        out->Reserve(static_cast<size_t>(chunk_rows * f * 1.02) + 1, compute_->get());
+      }
+      out->Reserve(out->rows + chunk_rows, compute_->get());
+    };
     hipStream_t s = compute_->get();
     merge_replay_ = true;  // resident text: parse adjacent cached chunks together
     struct Unmerge {
@@ -797,9 +809,9 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
         const ChunkMeta sizes = WaitMapped(hm);
         AfterFirstSync();
         if (!(sizes.flags & kFlagIrregular)) {
-          out->Reserve(out->rows + sizes.nrows, s);
+          reserve(sizes.nrows, nbytes);
           LaunchTileHashed<IndexType>(text, nbytes, tcfg_.format, tcounts_.get<uint64_t>(),
-                                      out->rows, dim, scale, seed, fp8, out->x.get(),
+                                      out->rows, sizes.nlines, dim, scale, seed, fp8, out->x.get(),
                                       out->label.get<float>(), slots_.get<MetaPartial>(), dmeta,
                                       hm, s);
           PrelaunchCount();
@@ -828,7 +840,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       LaunchScanU64(info_.get<uint64_t>(), nlines, partials_.get<uint64_t>(), total, s);
       LaunchMetaFromTotal(total, dmeta, s);
       const size_t nrows = ReadBack<ChunkMeta>(dmeta).nrows;
-      out->Reserve(out->rows + nrows, s);
+      reserve(nrows, nbytes);
       DMLC_HIP_CHECK(hipMemsetAsync(dmeta, 0, sizeof(ChunkMeta), s));
       LaunchTextHashed<IndexType>(text, nbytes, lines_.get<uint32_t>(), nlines, tcfg_.format,
                                   info_.get<uint64_t>(), out->rows, dim, scale, seed, fp8,

@@ -20,9 +20,13 @@
  *  DeviceRowIter<I>: the whole partition parsed into one HBM-resident CSR
  *                   (ParseAll), served as a single block (also when it is
  *                   empty), NumCol = max index + 1 (the reference's
- *                   BasicRowIter, src/data/basic_row_iter.h:35-48).
+ *                   BasicRowIter, src/data/basic_row_iter.h:35-48).  With
+ *                   `uri#cachefile` it is DiskRowIter's device twin: the
+ *                   page file is DMA'd into HBM when it exists, else built
+ *                   from the GPU parse (gpu/device_page_cache.h).
  */
 #include <dmlc/data.h>
+#include <dmlc/gpu/device_page_cache.h>
 #include <dmlc/gpu/device_parser.h>
 #include <dmlc/logging.h>
 
@@ -112,10 +116,25 @@ class GPUParser : public Parser<IndexType> {
 template <typename IndexType>
 class DeviceRowIter : public RowBlockIter<IndexType> {
  public:
-  DeviceRowIter(const std::string& uri, unsigned part, unsigned nparts, const RouteArgs& r) {
-    std::unique_ptr<gpu::DeviceParser<IndexType>> p(
-        gpu::DeviceParser<IndexType>::Create(uri, part, nparts, r.cfg));
-    p->ParseAll(&csr_);
+  DeviceRowIter(const std::string& uri, unsigned part, unsigned nparts, const RouteArgs& r,
+                const std::string& cache_file) {
+    const char* how = "parsed";
+    if (!cache_file.empty()) {
+      // DiskRowIter's protocol (reference src/data/disk_row_iter.h:94-141):
+      // load the page file when it exists, else build it from this parse
+      auto cache = gpu::DevicePageCache<IndexType>::Open(cache_file, r.cfg.device);
+      if (cache != nullptr) {
+        cache->Load(&csr_);
+        how = cache->zero_copy() ? "loaded (zero-copy DMA) from cache" : "loaded from cache";
+      } else {
+        Parse(uri, part, nparts, r);
+        const size_t pages = gpu::DevicePageCache<IndexType>::Write(csr_, cache_file);
+        LOG(INFO) << "DeviceRowIter: wrote " << pages << " cache pages to " << cache_file;
+        how = "parsed, cache built";
+      }
+    } else {
+      Parse(uri, part, nparts, r);
+    }
     const gpu::DeviceRowBlock<IndexType> d = csr_.View();
     num_col_ = static_cast<size_t>(d.max_index) + 1;
     if (r.to_host) {
@@ -124,8 +143,8 @@ class DeviceRowIter : public RowBlockIter<IndexType> {
     } else {
       block_ = DeviceView(d);
     }
-    LOG(INFO) << "DeviceRowIter: " << d.size << " rows, " << d.nnz << " entries resident in HBM"
-              << (r.to_host ? " (host copy served)" : "");
+    LOG(INFO) << "DeviceRowIter: " << d.size << " rows, " << d.nnz << " entries resident in HBM ("
+              << how << ")" << (r.to_host ? ", host copy served" : "");
   }
   void BeforeFirst() override { at_ = 0; }
   bool Next() override {
@@ -137,6 +156,11 @@ class DeviceRowIter : public RowBlockIter<IndexType> {
   size_t NumCol() const override { return num_col_; }
 
  private:
+  void Parse(const std::string& uri, unsigned part, unsigned nparts, const RouteArgs& r) {
+    std::unique_ptr<gpu::DeviceParser<IndexType>> p(
+        gpu::DeviceParser<IndexType>::Create(uri, part, nparts, r.cfg));
+    p->ParseAll(&csr_);
+  }
   gpu::DeviceCSR<IndexType> csr_;
   gpu::HostCSR<IndexType> host_;
   RowBlock<IndexType> block_;
@@ -157,8 +181,9 @@ template <typename IndexType>
 RowBlockIter<IndexType>* CreateDeviceRowIter(const std::string& uri,
                                              const std::map<std::string, std::string>& args,
                                              unsigned part, unsigned nparts,
-                                             const std::string& type) {
-  return new DeviceRowIter<IndexType>(uri, part, nparts, ParseRoute(args, type));
+                                             const std::string& type,
+                                             const std::string& cache_file) {
+  return new DeviceRowIter<IndexType>(uri, part, nparts, ParseRoute(args, type), cache_file);
 }
 
 namespace {

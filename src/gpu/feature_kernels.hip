@@ -170,6 +170,38 @@ void LaunchFill(float* p, size_t n, float v, hipStream_t stream) {
   hipLaunchKernelGGL(k_fill, dim3(GridFor(n, kThreads)), dim3(kThreads), 0, stream, p, n, v);
 }
 
+namespace {
+/*! \brief one row pointer per lane; its page by binary search of the (small,
+ *  L2-resident) page table */
+__global__ __launch_bounds__(kThreads) void k_page_rebase(uint64_t* __restrict__ offset,
+                                                          size_t nrows,
+                                                          const uint64_t* __restrict__ row_end,
+                                                          const uint64_t* __restrict__ nnz_base,
+                                                          int npages) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * kThreads;
+  for (size_t r = static_cast<size_t>(blockIdx.x) * kThreads + threadIdx.x; r < nrows;
+       r += stride) {
+    int lo = 0, hi = npages - 1;  // first page whose cumulative row end exceeds r
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (row_end[mid] > r) {
+        hi = mid;
+      } else {
+        lo = mid + 1;
+      }
+    }
+    offset[r + 1] += nnz_base[lo];
+  }
+}
+}  // namespace
+
+void LaunchPageRebase(uint64_t* offset, size_t nrows, const uint64_t* page_row_end,
+                      const uint64_t* page_nnz_base, int npages, hipStream_t stream) {
+  if (nrows == 0 || npages == 0) return;
+  hipLaunchKernelGGL(k_page_rebase, dim3(GridFor(nrows, kThreads)), dim3(kThreads), 0, stream,
+                     offset, nrows, page_row_end, page_nnz_base, npages);
+}
+
 void LaunchOffsetRebase(const uint64_t* src_offset, size_t nrows, uint64_t src_base,
                         uint64_t dst_base, uint64_t* dst_offset, hipStream_t stream) {
   hipLaunchKernelGGL(k_rebase, dim3(GridFor(nrows + 1, kThreads)), dim3(kThreads), 0, stream,

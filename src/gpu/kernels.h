@@ -183,17 +183,20 @@ void LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
 
 /*!
  * \brief fused tokenize -> hash -> dense rows on the tile parser (config 5):
- *  rows = the lines of a regular chunk (tile_prefix from LaunchTileCountScan),
- *  row row_base + line of a [rows x dim] fp8 (x scale) or f32 batch, labels
- *  alongside; no CSR is written.  Sets kFlagIrregular when a line runs more
- *  than 4 KiB past its tile (re-run the chunk with LaunchTextHashed), merges
- *  kFlagNegIndex.  dim: multiple of 16, <= 4096.
+ *  rows = the `nlines` lines of a regular chunk (tile_prefix from
+ *  LaunchTileCountScan), row row_base + line of a [rows x dim] fp8 (x scale)
+ *  or f32 batch, labels alongside; no CSR is written.  One wave per tile, the
+ *  lines that start in it (followed past the tile end, any length).  Sets
+ *  kFlagIrregular for tokens only the exact kernels parse (qid:, junk; re-run
+ *  the chunk with LaunchTextHashed), merges kFlagNegIndex.  dim: multiple of
+ *  16, <= 4096.
  */
 template <typename IndexType>
 void LaunchTileHashed(const char* text, size_t nbytes, TextFormat format,
-                      const uint64_t* tile_prefix, uint64_t row_base, int dim, float scale,
-                      uint32_t seed, bool fp8, void* out, float* labels, MetaPartial* partials,
-                      ChunkMeta* meta, ChunkMeta* host_meta, hipStream_t stream);
+                      const uint64_t* tile_prefix, uint64_t row_base, uint64_t nlines, int dim,
+                      float scale, uint32_t seed, bool fp8, void* out, float* labels,
+                      MetaPartial* partials, ChunkMeta* meta, ChunkMeta* host_meta,
+                      hipStream_t stream);
 
 /*!
  * \brief C2 alone over caller-filled per-tile u64 counts (hi 32 bits: items,
@@ -322,6 +325,13 @@ void LaunchFmBackward(const uint8_t* x, int64_t rows, int dim, const float* g, c
 /*! \brief K10: dst_offset[i] = src_offset[i] - src_base + dst_base for i<=nrows */
 void LaunchOffsetRebase(const uint64_t* src_offset, size_t nrows, uint64_t src_base,
                         uint64_t dst_base, uint64_t* dst_offset, hipStream_t stream);
+/*!
+ * \brief page-cache row pointers: offset[r + 1] (r < nrows) holds the
+ *  page-local end of row r; add its page's nnz base.  page_row_end[p] =
+ *  rows of pages 0..p (cumulative), page_nnz_base[p] = entries before page p.
+ */
+void LaunchPageRebase(uint64_t* offset, size_t nrows, const uint64_t* page_row_end,
+                      const uint64_t* page_nnz_base, int npages, hipStream_t stream);
 /*! \brief fill n floats with v */
 void LaunchFill(float* p, size_t n, float v, hipStream_t stream);
 

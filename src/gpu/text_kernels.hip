@@ -291,7 +291,8 @@ __device__ void walk_line(const uint8_t* __restrict__ text, uint32_t b, uint32_t
         // every byte after a delimiter starts a field, up to the line end: a
         // trailing delimiter opens no empty last field (reference
         // csv_parser.h:83-96 stops when p reaches lend after the delimiter)
-        starts = (mcur.delim << 1) | pd;
+        // (e is the next line's start: the EOL bytes lie inside [b, e))
+        starts = ((mcur.delim << 1) | pd) & ~mcur.eol;
         if (b >= pos && b < pos + 16) starts |= 1u << (b - pos);
         const uint32_t room = e > pos ? (e - pos < 16 ? e - pos : 16u) : 0u;
         starts &= room >= 16 ? 0xFFFFu : ((1u << room) - 1u);

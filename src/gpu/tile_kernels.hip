@@ -977,278 +977,283 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
 }
 
 /*!
- * \brief fused tokenize -> hash -> dense row (BASELINE config 5) on the tile
- *  parser: workgroup t OWNS the lines that start in tile t.  It stages the
- *  tile plus a 4 KiB extension (the rest of its last line) in LDS, compacts the
- *  tokens of its own lines, and builds kRows rows at a time in LDS (dim floats
- *  each, ds_add_f32 of +-value into bucket hash % dim), then writes each row
- *  once -- OCP fp8 e4m3 (v_cvt_pk_fp8_f32, 4 columns per 32-bit store) or
- *  f32 -- with its label.  No CSR is written.  A line running past the
- *  extension sets kFlagIrregular (the caller re-runs the chunk on the exact
- *  per-line kernel).
+ * \brief fused tokenize -> hash -> dense row (BASELINE config 5) on the fill
+ *  kernel's wave-autonomous pipeline.  Wave w OWNS the lines that start in its
+ *  8 KiB tile (`own` of them, from the C2 prefix -- no per-tile host data):
+ *   1. the tile streams through the two LDS slots in 2 KiB steps exactly as in
+ *      k_tile_fill (register prefetch, SWAR masks, DPP scan, wave-private token
+ *      list, 64-token decode rounds through tok::decode).  Only owned tokens
+ *      are listed: the head of the tile (the rest of the previous tile's last
+ *      line) and everything after the owned lines are masked out before the
+ *      scan, in the first / last step only (wave-uniform test);
+ *   2. the last owned line is followed past the tile end step by step until
+ *      the next line start (or the end of the text) -- no extension cap and
+ *      no fallback for long lines; steps after the first extension step
+ *      prefetch only the 64 B tail (lines > 2 KiB past the tile are rare);
+ *   3. every decoded feature adds +-value at bucket hash % dim of ONE f32 row
+ *      in the wave's LDS (ds_add_f32); when a round moves past a line, that row
+ *      is flushed: each lane reads its 16 columns, zeroes them, converts to
+ *      OCP fp8 e4m3 (v_cvt_pk_fp8_f32) and writes one 16 B store -- a whole
+ *      row per wave store, zero spans included, no separate memset pass.
+ *  The label token's lane writes the label.  No CSR, no per-row LDS buffers
+ *  per workgroup, no barrier.  Hash and bucket are K9's (dev::hash_u64), so
+ *  the fp8 bytes equal tile CSR + K9.  Reference token loop:
+ *  src/data/libfm_parser.h:36-93, libsvm_parser.h:36-99 (strtonum.h:266-303).
  */
-constexpr int kHashExt = 4096;                            // bytes staged past the tile
-constexpr int kHashSegs = (static_cast<int>(kTileBytes) + kHashExt) / 4096;
-constexpr int kHashRows = 4;                              // rows built per LDS round
-constexpr unsigned kHashOffBits = 14;                     // staged offset < 12288
-constexpr uint32_t kHashMaxTok = 3072;  // listed tokens per tile (more: exact kernel)
-constexpr uint32_t kHashMaxRows = 1024;  // owned rows per tile on the wave-per-row path
+struct HashTarget {
+  void* x;            // [row_limit, dim] fp8 bytes or f32
+  float* label;
+  uint64_t row_base;  // global row of the chunk's first line
+  uint64_t nlines;    // lines of the chunk (the C2 total)
+  int dim;
+  float scale;
+  uint32_t seed;
+};
+
+/*! \brief keep the token starts of a slice whose line ordinals are in [1, own];
+ *  L0 = ordinal at the slice start (line starts before it, this tile) */
+__device__ __forceinline__ uint32_t owned_tokens(uint32_t tm, uint32_t lm, uint32_t L0,
+                                                 uint32_t own) {
+  uint32_t m = tm;
+  if (L0 == 0) m &= lm != 0 ? ~((lm & (0u - lm)) - 1u) : 0u;  // from the first line start on
+  const uint32_t nl = static_cast<uint32_t>(__popc(lm));
+  if (L0 + nl > own) {
+    if (L0 > own) return 0u;
+    uint32_t x = lm;
+    for (uint32_t k = own - L0; k != 0; --k) x &= x - 1u;  // drop the starts still owned
+    m &= (x & (0u - x)) - 1u;  // bytes before the first line start past `own`
+  }
+  return m;
+}
 
 template <TextFormat F, typename IndexType, bool kFP8>
-__global__ __launch_bounds__(kThreads) void k_tile_hash(const uint8_t* __restrict__ text, size_t n,
-                                                        const uint64_t* __restrict__ prefix,
-                                                        uint64_t row_base, int dim, float scale,
-                                                        uint32_t seed, void* __restrict__ out,
-                                                        float* __restrict__ labels,
-                                                        MetaPartial* __restrict__ partials) {
-  __shared__ uint4 s_text[(kTileBytes + kHashExt) / 16 + 4];
-  __shared__ uint32_t s_tok[kHashMaxTok];
-  __shared__ uint32_t s_scan[4];
-  __shared__ uint32_t s_end;  // staged offset where the owned region ends
-  __shared__ uint16_t s_row_first[kHashMaxRows + 1];  // list index of each owned row's label
-  extern __shared__ __attribute__((aligned(16))) float s_rows[];
-  const uint8_t* lds = reinterpret_cast<const uint8_t*>(s_text);
-  const size_t tile0 = static_cast<size_t>(blockIdx.x) * kTileBytes;
-  const uint64_t line_base = prefix[blockIdx.x] >> 32;
-  const uint32_t staged_end = static_cast<uint32_t>(
-      n - tile0 < kTileBytes + kHashExt ? n - tile0 : kTileBytes + kHashExt);
-  if (threadIdx.x == 0) s_end = 0xFFFFFFFFu;
+__global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
+    const uint8_t* __restrict__ text, size_t n, size_t ntiles,
+    const uint64_t* __restrict__ prefix, HashTarget out, MetaPartial* __restrict__ partials) {
+  __shared__ uint4 s_text[kFillWaves][kStageVecs];
+  __shared__ uint32_t s_list[kFillWaves][kListCap + 64];
+  extern __shared__ __attribute__((aligned(16))) float s_hrow[];  // kFillWaves x dim
+  const int wave = threadIdx.x / dev::kWave;
+  const int lane = dev::lane_id();
+  const size_t tile = static_cast<size_t>(blockIdx.x) * kFillWaves + wave;
+  if (tile >= ntiles) return;  // whole waves leave; nothing below synchronises waves
+  uint4* const st = s_text[wave];
+  uint32_t* const sl = s_list[wave];
+  const int dim = out.dim;
+  float* const row = s_hrow + static_cast<size_t>(wave) * dim;
+  const uint32_t slot = round_slot(lane);
+  const size_t tile0 = tile * kTileBytes;
+  const uint64_t line_base = prefix[tile] >> 32;
+  const uint64_t line_next = tile + 1 < ntiles ? prefix[tile + 1] >> 32 : out.nlines;
+  const uint32_t own = static_cast<uint32_t>(line_next - line_base);
+  bool irregular = false, neg = false;
+  if (own != 0) {
+    const uint64_t R = out.row_base + line_base;  // global row of tile line ordinal 1
+    const bool pow2 = (dim & (dim - 1)) == 0;
+    const uint32_t dmask = static_cast<uint32_t>(dim - 1);
+    for (int c = lane * 4; c < dim; c += dev::kWave * 4) {
+      *reinterpret_cast<float4*>(row + c) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+    // one row out: read + zero this lane's columns, convert, one 16 B store
+    auto flush = [&](uint32_t lc) {
+      dev::wave_sync();  // the row's adds are done
+      const uint64_t g = R + lc - 1;
+      const bool ok = lc <= own;
+      if constexpr (kFP8) {
+        uint8_t* o = static_cast<uint8_t*>(out.x) + g * static_cast<uint64_t>(dim);
+        for (int c = lane * 16; c < dim; c += dev::kWave * 16) {
+          float4* r4 = reinterpret_cast<float4*>(row + c);
+          float4 x[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            x[q] = r4[q];
+            r4[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+          }
+          uint32_t w[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            int pk = __builtin_amdgcn_cvt_pk_fp8_f32(x[q].x * out.scale, x[q].y * out.scale, 0, false);
+            pk = __builtin_amdgcn_cvt_pk_fp8_f32(x[q].z * out.scale, x[q].w * out.scale, pk, true);
+            w[q] = static_cast<uint32_t>(pk);
+          }
+          if (ok) *reinterpret_cast<uint4*>(o + c) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+      } else {
+        float* o = static_cast<float*>(out.x) + g * static_cast<uint64_t>(dim);
+        for (int c = lane * 4; c < dim; c += dev::kWave * 4) {
+          float4* r4 = reinterpret_cast<float4*>(row + c);
+          const float4 x = *r4;
+          *r4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+          if (ok) *reinterpret_cast<float4*>(o + c) = make_float4(x.x, x.y, x.z, x.w);
+        }
+      }
+      dev::wave_sync();  // zeros land before the next row's adds
+    };
 
-  // ---- stage tile + extension; bytes at or past n are zero in LDS
-  uint4 v[kHashSegs];
-  uint32_t pc[kHashSegs];
-#pragma unroll
-  for (int s = 0; s < kHashSegs; ++s) {
-    const size_t pos = tile0 + s * 4096 + threadIdx.x * 16;
-    v[s] = load16(text, pos, n);
-    pc[s] = prev_byte(text, pos, v[s]);
-    if (pos < n && n - pos < 16) {  // the segment straddling n: clear its tail
-      uint32_t w[4] = {v[s].x, v[s].y, v[s].z, v[s].w};
-      const uint32_t keep = static_cast<uint32_t>(n - pos);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int lo = 4 * q;
-        if (static_cast<int>(keep) <= lo) {
-          w[q] = 0;
-        } else if (static_cast<int>(keep) < lo + 4) {
-          w[q] &= (1u << (8 * (keep - lo))) - 1u;
+    uint4 a = load16_clip(text, tile0 + lane * 16, n);
+    uint4 b = load16_clip(text, tile0 + 1024 + lane * 16, n);
+    uint32_t carry_pc = tile0 == 0 ? static_cast<uint32_t>('\n') : text[tile0 - 1];
+    uint32_t lcnt = 0;   // line starts seen so far (this tile's ordinals)
+    uint32_t carry = 0;  // list entries left for the next step's rounds
+    uint32_t open = 0;   // ordinal of the row being accumulated (0: none yet)
+    bool have_full = true;  // a / b hold the whole current step
+#pragma unroll 1
+    for (int s = 0;; ++s) {
+      const size_t cur = tile0 + static_cast<size_t>(s) * kStepBytes;
+      if (!have_full) {  // a line running > 2 KiB past the tile: load what was not prefetched
+        a = load16_clip(text, cur + lane * 16, n);
+        b = load16_clip(text, cur + 1024 + lane * 16, n);
+      }
+      // prefetch: the next step whole while it lies in the tile or is the first
+      // extension step, else only its first 64 B (this step's tail)
+      const size_t nxt = cur + kStepBytes;
+      const bool full_next = s + 1 <= kSteps;
+      uint4 na = make_uint4(0, 0, 0, 0), nb = make_uint4(0, 0, 0, 0);
+      if (full_next) {
+        if (nxt + kStepBytes <= n) {
+          na = *reinterpret_cast<const uint4*>(text + nxt + lane * 16);
+          nb = *reinterpret_cast<const uint4*>(text + nxt + 1024 + lane * 16);
+        } else {
+          na = load16_clip(text, nxt + lane * 16, n);
+          nb = load16_clip(text, nxt + 1024 + lane * 16, n);
         }
+      } else if (lane < 4) {
+        na = load16_clip(text, nxt + lane * 16, n);
       }
-      v[s] = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-    s_text[s * 256 + threadIdx.x] = v[s];
-  }
-  // ---- compact the tokens of the owned lines (line starts in the tile)
-  uint32_t carry = 0;
-  uint32_t nlines_tile = 0;
-#pragma unroll
-  for (int s = 0; s < kHashSegs; ++s) {
-    const size_t pos = tile0 + s * 4096 + threadIdx.x * 16;
-    uint32_t lm, tm;
-    (void)lane_masks<false>(v[s], pc[s], pos, n, &lm, &tm);
-    const bool ext = s * 4096 >= static_cast<int>(kTileBytes);
-    if (ext && lm != 0) atomicMin(&s_end, static_cast<uint32_t>(s * 4096 + threadIdx.x * 16 +
-                                                                 __ffs(lm) - 1));
-    const uint32_t mine = (static_cast<uint32_t>(__popc(lm)) << 16) | __popc(tm);
-    uint32_t tot;
-    const uint32_t before = dev::block_excl_scan_256<uint32_t>(mine, s_scan, &tot) + carry;
-    uint32_t line = before >> 16;
-    uint32_t tok = before & 0xffffu;
-    uint32_t all = lm | tm;
-    while (all != 0) {
-      const int j = __ffs(all) - 1;
-      all &= all - 1;
-      const uint32_t bit = 1u << j;
-      const uint32_t off = static_cast<uint32_t>(s * 4096 + threadIdx.x * 16 + j);
-      if (lm & bit) ++line;
-      if (tm & bit) {  // every token is listed; those at or past `end` are skipped later
-        const uint32_t label = (lm & bit) ? 1u : 0u;
-        if (tok < kHashMaxTok) s_tok[tok] = off | (line << kHashOffBits) | (label << 31);
-        ++tok;
-      }
-    }
-    carry += tot;
-    if (!ext) nlines_tile = carry >> 16;
-    __syncthreads();
-  }
-  const uint32_t end = s_end;  // first line start in the extension (barrier above)
-  const uint32_t ntok_all = carry & 0xffffu;
-  const uint32_t ntok = ntok_all < kHashMaxTok ? ntok_all : kHashMaxTok;
-  bool irregular = ntok_all > kHashMaxTok;  // very many tiny tokens: exact kernel
-  if (end == 0xFFFFFFFFu && staged_end == kTileBytes + kHashExt && tile0 + staged_end < n &&
-      nlines_tile != 0) {
-    irregular = true;  // the last owned line runs past the extension
-  }
-  const uint32_t lim = end == 0xFFFFFFFFu ? staged_end : end;
-  float* rows = s_rows;
-  bool neg = false;
-  // ---- decode every owned token ONCE: labels are written out, features
-  // become (row in tile << 12 | bucket) in s_tok and their signed value in a
-  // register, later spilled to LDS over the (no longer needed) text
-  constexpr uint32_t kNone = 0xFFFFFFFFu;
-  constexpr int kPerLane = 4;  // tokens per lane held in registers (ntok <= 1024)
-  float vals[kPerLane];
-  const bool one_pass = ntok <= static_cast<uint32_t>(kPerLane * kThreads);
-  bool bad_start = false;
-  auto decode = [&](uint32_t i, uint32_t* res, float* sval) {
-    *res = kNone;
-    const uint32_t e = s_tok[i];
-    const uint32_t off = e & ((1u << kHashOffBits) - 1);
-    const uint32_t lcnt = (e >> kHashOffBits) & 0x1FFFu;
-    if (off >= lim || lcnt == 0) return;  // outside the owned lines
-    const bool is_label = (e >> 31) & 1u;
-    int r = 0;
-    uint64_t u0 = 0, u1 = 0;
-    float f0 = 0.0f, f1 = 0.0f;
-    bool bad = false;
-    if (!fast_token<F>(lds, off, is_label, &r, &u0, &u1, &f0, &f1)) {
-      // a token start outside [0-9+-.] never passes fast_token: the exact
-      // kernels own those (k_tile_count no longer checks token starts)
-      // (per lane: `irregular` steers workgroup barriers and must stay uniform)
-      if (!num_start(lds[off])) bad_start = true;
-      const uint8_t* l = lds + lim;
-      auto b = sep_begin(lds + off, l);
-      auto en = sep_end(l);
-      if (is_label) {
-        r = data::ParsePair<float, float>(b, en, &f0, &f1, &bad);
-      } else if constexpr (F == TextFormat::kLibSVM) {
-        IndexType idx = 0;
-        r = data::ParsePair<IndexType, float>(b, en, &idx, &f0, &bad);
-        u0 = idx;
+      const uint32_t sbase = (static_cast<uint32_t>(s) & 1u) * kSlotBytes;
+      uint4* const ss = st + sbase / 16;
+      ss[lane] = a;
+      ss[64 + lane] = b;
+      if (lane < 4) ss[128 + lane] = na;
+      const size_t pos_a = cur + lane * 16;
+      const uint32_t left_a = __shfl_up(a.w >> 24, 1, dev::kWave);
+      const uint32_t pc_a = lane == 0 ? carry_pc : left_a;
+      const uint32_t left_b = __shfl_up(b.w >> 24, 1, dev::kWave);
+      const uint32_t last_a = __shfl(a.w >> 24, dev::kWave - 1, dev::kWave);
+      const uint32_t pc_b = lane == 0 ? last_a : left_b;
+      carry_pc = __shfl(b.w >> 24, dev::kWave - 1, dev::kWave);
+      uint32_t lm_a, tm_a, lm_b, tm_b;
+      if (nxt <= n) {  // wave-uniform: a full step
+        (void)lane_masks<false, true>(a, pc_a, pos_a, n, &lm_a, &tm_a);
+        (void)lane_masks<false, true>(b, pc_b, pos_a + 1024, n, &lm_b, &tm_b);
       } else {
-        IndexType fid = 0, idx = 0;
-        r = data::ParseTriple<IndexType, IndexType, float>(b, en, &fid, &idx, &f0, &bad);
-        u0 = fid;
-        u1 = idx;
+        (void)lane_masks<false>(a, pc_a, pos_a, n, &lm_a, &tm_a);
+        (void)lane_masks<false>(b, pc_b, pos_a + 1024, n, &lm_b, &tm_b);
       }
-    }
-    if (is_label) {
-      labels[row_base + line_base + lcnt - 1] = f0;
-      return;
-    }
-    uint64_t key;
-    float val;
-    if constexpr (F == TextFormat::kLibSVM) {
-      key = dev::hash_key(static_cast<uint64_t>(static_cast<IndexType>(u0)), 0, false);
-      val = r == 2 ? f0 : 1.0f;
-    } else {
-      if (r < 2) return;  // not a field:index token (the CPU parser skips it too)
-      key = dev::hash_key(static_cast<uint64_t>(static_cast<IndexType>(u1)),
-                          static_cast<uint64_t>(static_cast<IndexType>(u0)), true);
-      val = r == 3 ? f0 : 1.0f;
-    }
-    neg |= bad;
-    const uint32_t h = dev::hash_u64(key, seed);
-    *res = ((lcnt - 1) << 12) | (h % static_cast<uint32_t>(dim));
-    *sval = (h & 0x80000000u) ? -val : val;
-  };
-  float* s_val = reinterpret_cast<float*>(s_text);  // overlays the text after decoding
-  if (one_pass && !irregular) {
-#pragma unroll
-    for (int k = 0; k < kPerLane; ++k) {
-      const uint32_t i = threadIdx.x + k * kThreads;
-      vals[k] = 0.0f;
-      if (i < ntok) {
-        const uint32_t e = s_tok[i];
-        const uint32_t lc = (e >> kHashOffBits) & 0x1FFFu;
-        if ((e >> 31) != 0 && lc != 0 && lc <= kHashMaxRows && (e & ((1u << kHashOffBits) - 1)) < lim) {
-          s_row_first[lc - 1] = static_cast<uint16_t>(i);  // row lc - 1 starts at its label
-        }
-        uint32_t res;
-        decode(i, &res, &vals[k]);
-        s_tok[i] = res;  // same lane reads and rewrites entry i
+      uint64_t cnt = static_cast<uint64_t>(__popc(tm_a)) |
+                     (static_cast<uint64_t>(__popc(tm_b)) << 16) |
+                     (static_cast<uint64_t>(__popc(lm_a)) << 32) |
+                     (static_cast<uint64_t>(__popc(lm_b)) << 48);
+      uint64_t tot;
+      uint64_t before = dev::wave_excl_scan(cnt, &tot);
+      const uint32_t nline_a = static_cast<uint32_t>((tot >> 32) & 0xFFFFu);
+      const uint32_t nline = nline_a + static_cast<uint32_t>(tot >> 48);
+      const uint32_t la0 = lcnt + static_cast<uint32_t>((before >> 32) & 0xFFFFu);
+      const uint32_t lb0 = lcnt + nline_a + static_cast<uint32_t>(before >> 48);
+      if (lcnt == 0 || lcnt + nline > own) {
+        // wave-uniform (first / last step): drop tokens outside the owned lines
+        tm_a = owned_tokens(tm_a, lm_a, la0, own);
+        tm_b = owned_tokens(tm_b, lm_b, lb0, own);
+        cnt = static_cast<uint64_t>(__popc(tm_a)) | (static_cast<uint64_t>(__popc(tm_b)) << 16);
+        before = (before & ~0xFFFFFFFFull) | dev::wave_excl_scan(cnt, &tot);
       }
-    }
-    __syncthreads();  // every lane is done reading the text
-#pragma unroll
-    for (int k = 0; k < kPerLane; ++k) {
-      const uint32_t i = threadIdx.x + k * kThreads;
-      if (i < ntok) s_val[i] = vals[k];
-    }
-  }
-  // one row (f32 in LDS at src) -> out row `row`: fp8 (16 columns per lane
-  // and store) or f32
-  auto write_row = [&](uint64_t row, const float* src, int lane) {
-    if constexpr (kFP8) {
-      uint4* o = reinterpret_cast<uint4*>(static_cast<uint8_t*>(out) + row * dim);
-      for (int c = lane * 16; c < dim; c += dev::kWave * 16) {
-        const float4* f = reinterpret_cast<const float4*>(src + c);
-        uint32_t w[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 x = f[q];
-          int pk = __builtin_amdgcn_cvt_pk_fp8_f32(x.x * scale, x.y * scale, 0, false);
-          pk = __builtin_amdgcn_cvt_pk_fp8_f32(x.z * scale, x.w * scale, pk, true);
-          w[q] = static_cast<uint32_t>(pk);
-        }
-        o[c / 16] = make_uint4(w[0], w[1], w[2], w[3]);
-      }
-    } else {
-      float4* o = reinterpret_cast<float4*>(static_cast<float*>(out) + row * dim);
-      for (int c = lane * 4; c < dim; c += dev::kWave * 4) {
-        o[c / 4] = *reinterpret_cast<const float4*>(src + c);
-      }
-    }
-  };
-  const bool by_row = one_pass && !irregular && nlines_tile <= kHashMaxRows;
-  if (by_row) {
-    // every owned token was decoded once; rows are contiguous in the list
-    // (text order), row r spanning [s_row_first[r], s_row_first[r + 1]).
-    // Each wave builds whole rows in its own LDS row (no workgroup barrier
-    // per row group, no re-scan of the tile's tokens per group)
-    if (threadIdx.x == 0) s_row_first[nlines_tile] = static_cast<uint16_t>(ntok);
-    __syncthreads();
-    const int w = threadIdx.x / dev::kWave;
-    const int lane = dev::lane_id();
-    float* mine = rows + static_cast<size_t>(w) * dim;
-    for (uint32_t r = w; r < nlines_tile; r += kThreads / dev::kWave) {
-      for (int c = lane * 4; c < dim; c += dev::kWave * 4) {
-        *reinterpret_cast<float4*>(mine + c) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      }
+      const uint32_t ntok_a = static_cast<uint32_t>(tot & 0xFFFFu);
+      const uint32_t ntok = ntok_a + static_cast<uint32_t>((tot >> 16) & 0xFFFFu);
+      list_slice(sl, tm_a, lm_a, carry + static_cast<uint32_t>(before & 0xFFFFu), sbase + lane * 16,
+                 la0, lane);
+      list_slice(sl, tm_b, lm_b, carry + ntok_a + static_cast<uint32_t>((before >> 16) & 0xFFFFu),
+                 sbase + 1024 + lane * 16, lb0, lane);
       dev::wave_sync();
-      const uint32_t lo = s_row_first[r], hi = s_row_first[r + 1];
-      for (uint32_t i = lo + lane; i < hi; i += dev::kWave) {
-        const uint32_t res = s_tok[i];
-        if (res != kNone && (res >> 12) == r) atomicAdd(&mine[res & 0xFFFu], s_val[i]);
+      lcnt += nline;
+      const bool eol_end = carry_pc == '\n' || carry_pc == '\r';
+      const bool last = nxt >= n || lcnt > own || (s + 1 >= kSteps && lcnt == own && eol_end);
+
+      const uint32_t total = carry + ntok;
+      const uint32_t rest = total % dev::kWave < ntok ? total % dev::kWave : ntok;
+      const uint32_t ndec = last ? total : total - rest;
+      for (uint32_t r0 = 0; r0 < ndec; r0 += dev::kWave) {
+        const uint32_t li = r0 + slot;
+        const bool active = li < ndec;
+        const uint32_t e = active ? sl[li] : 0u;
+        const bool is_label = active && ((e >> 13) & 1u) != 0;
+        const uint32_t off = e & 0x1FFFu;
+        const uint32_t lc = e >> 14;
+        tok::Token t;
+        t.u0_hi = t.u1_hi = 0;
+        t.u1 = 0;
+        bool bad = false;
+        const bool ok = tok::decode<F>(st, off, is_label, &t);
+        if (active & !ok) {
+          const uint32_t in_slot = off >= kSlotBytes ? 1u : 0u;
+          const int step = in_slot == (static_cast<uint32_t>(s) & 1u) ? s : s - 1;
+          const size_t gpos =
+              tile0 + static_cast<size_t>(step) * kStepBytes + off - in_slot * kSlotBytes;
+          const GenericResult gr = generic_token<F, IndexType>(text, n, gpos, is_label);
+          t = gr.t;
+          bad = gr.bad;
+          irregular |= !num_start(text[gpos]);  // qid:, comments, junk: the exact kernels
+        }
+        if (active & is_label) out.label[R + lc - 1] = t.f0;
+        bool feat = active & !is_label;
+        uint64_t key;
+        float val;
+        const uint64_t u0 = (static_cast<uint64_t>(t.u0_hi) << 32) | t.u0;
+        if constexpr (F == TextFormat::kLibSVM) {
+          key = static_cast<uint64_t>(static_cast<IndexType>(u0));
+          val = t.r == 2 ? t.f0 : 1.0f;
+        } else {
+          const uint64_t u1 = (static_cast<uint64_t>(t.u1_hi) << 32) | t.u1;
+          feat &= t.r >= 2;  // not field:index: the CPU parser skips it too
+          key = dev::hash_key(static_cast<uint64_t>(static_cast<IndexType>(u1)),
+                              static_cast<uint64_t>(static_cast<IndexType>(u0)), true);
+          val = t.r == 3 ? t.f0 : 1.0f;
+        }
+        neg |= active && bad;
+        const uint32_t h = dev::hash_u64(key, out.seed);
+        uint32_t bucket;
+        if (pow2) {
+          bucket = h & dmask;
+        } else {
+          bucket = h % static_cast<uint32_t>(dim);
+        }
+        const float sv = (h & 0x80000000u) ? -val : val;
+        // the round's rows, in text order: list entries r0 .. r0 + 63
+        const uint32_t lo = sl[r0] >> 14;
+        const uint32_t hi = sl[r0 + dev::kWave - 1 < ndec ? r0 + dev::kWave - 1 : ndec - 1] >> 14;
+        for (uint32_t rr = lo; rr <= hi; ++rr) {
+          if (rr != open) {
+            if (open != 0) flush(open);
+            open = rr;
+          }
+          if (feat && lc == rr) atomicAdd(&row[bucket], sv);
+        }
       }
+      if (last) break;
+      // the undecoded rest moves to the front of the list (all lanes read before any writes)
+      const uint32_t left = total - ndec;
+      const uint32_t moved = lane < static_cast<int>(left) ? sl[ndec + lane] : 0u;
       dev::wave_sync();
-      write_row(row_base + line_base + r, mine, lane);
-      dev::wave_sync();  // the row is read out before the next one is zeroed
+      if (lane < static_cast<int>(left)) sl[lane] = moved;
+      carry = left;
+      a = na;
+      b = nb;
+      have_full = full_next;
+      dev::wave_sync();  // every lane is done with this step's text and list
     }
-  }
-  for (uint32_t r0 = 0; r0 < nlines_tile && !irregular && !by_row; r0 += kHashRows) {
-    for (int c = threadIdx.x; c < kHashRows * dim; c += kThreads) rows[c] = 0.0f;
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < ntok; i += kThreads) {
-      uint32_t res;
-      float sv = 0.0f;
-      if (one_pass) {
-        res = s_tok[i];
-        if (res == kNone) continue;
-        sv = s_val[i];
-      } else {
-        // many tiny tokens: decode again in every round (rare)
-        const uint32_t lcnt = (s_tok[i] >> kHashOffBits) & 0x1FFFu;
-        if (lcnt - 1 - r0 >= static_cast<uint32_t>(kHashRows)) continue;
-        decode(i, &res, &sv);
-        if (res == kNone) continue;
-      }
-      const uint32_t lr = (res >> 12) - r0;
-      if (lr >= static_cast<uint32_t>(kHashRows)) continue;
-      atomicAdd(&rows[lr * dim + (res & 0xFFFu)], sv);
-    }
-    __syncthreads();
-    const uint32_t nr = nlines_tile - r0 < static_cast<uint32_t>(kHashRows) ? nlines_tile - r0
-                                                                           : kHashRows;
-    // wave w writes row w of the round: 16 columns per lane -> one 16 B store
-    const uint32_t j = threadIdx.x / dev::kWave;
-    if (j < nr) write_row(row_base + line_base + r0 + j, rows + j * dim, dev::lane_id());
-    __syncthreads();
+    if (open != 0) flush(open);
   }
   unsigned fl = 0;
-  if (irregular || bad_start) fl |= kFlagIrregular;
+  if (irregular) fl |= kFlagIrregular;
   if (neg) fl |= kFlagNegIndex;
-  dev::block_store_partial(0ull, 0ull, fl, partials);
+  fl = dev::wave_or(fl);
+  if (lane == 0) {
+    MetaPartial p;
+    p.max_index = 0;
+    p.max_field = 0;
+    p.flags = fl;
+    p.pad = 0;
+    partials[tile] = p;
+  }
 }
 
 /*!
@@ -1444,17 +1449,19 @@ void LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
 
 template <typename IndexType>
 void LaunchTileHashed(const char* text, size_t nbytes, TextFormat format,
-                      const uint64_t* tile_prefix, uint64_t row_base, int dim, float scale,
-                      uint32_t seed, bool fp8, void* out, float* labels, MetaPartial* partials,
-                      ChunkMeta* meta, ChunkMeta* host_meta, hipStream_t stream) {
+                      const uint64_t* tile_prefix, uint64_t row_base, uint64_t nlines, int dim,
+                      float scale, uint32_t seed, bool fp8, void* out, float* labels,
+                      MetaPartial* partials, ChunkMeta* meta, ChunkMeta* host_meta,
+                      hipStream_t stream) {
   const size_t ntiles = TileCount(nbytes);
   const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
-  const size_t smem = static_cast<size_t>(kHashRows) * dim * sizeof(float);
+  const size_t smem = static_cast<size_t>(kFillWaves) * dim * sizeof(float);
+  HashTarget tgt{out, labels, row_base, nlines, dim, scale, seed};
   if (ntiles != 0) {
-#define DMLC_TILE_HASH(FMT, FP8)                                                               \
-  hipLaunchKernelGGL((k_tile_hash<FMT, IndexType, FP8>), dim3(ntiles), dim3(kThreads), smem,  \
-                     stream, t, nbytes, tile_prefix, row_base, dim, scale, seed, out, labels,  \
-                     partials)
+    const dim3 grid(static_cast<unsigned>((ntiles + kFillWaves - 1) / kFillWaves));
+#define DMLC_TILE_HASH(FMT, FP8)                                                              \
+  hipLaunchKernelGGL((k_tile_hash<FMT, IndexType, FP8>), grid, dim3(kThreads), smem, stream, t, \
+                     nbytes, ntiles, tile_prefix, tgt, partials)
     if (format == TextFormat::kLibFM) {
       if (fp8) {
         DMLC_TILE_HASH(TextFormat::kLibFM, true);
@@ -1474,11 +1481,11 @@ void LaunchTileHashed(const char* text, size_t nbytes, TextFormat format,
 }
 
 template void LaunchTileHashed<uint32_t>(const char*, size_t, TextFormat, const uint64_t*,
-                                         uint64_t, int, float, uint32_t, bool, void*, float*,
-                                         MetaPartial*, ChunkMeta*, ChunkMeta*, hipStream_t);
+                                         uint64_t, uint64_t, int, float, uint32_t, bool, void*,
+                                         float*, MetaPartial*, ChunkMeta*, ChunkMeta*, hipStream_t);
 template void LaunchTileHashed<uint64_t>(const char*, size_t, TextFormat, const uint64_t*,
-                                         uint64_t, int, float, uint32_t, bool, void*, float*,
-                                         MetaPartial*, ChunkMeta*, ChunkMeta*, hipStream_t);
+                                         uint64_t, uint64_t, int, float, uint32_t, bool, void*,
+                                         float*, MetaPartial*, ChunkMeta*, ChunkMeta*, hipStream_t);
 
 template void LaunchTileFill<uint32_t>(const char*, size_t, TextFormat, const uint64_t*,
                                        const FillTarget<uint32_t>&, MetaPartial*, ChunkMeta*,

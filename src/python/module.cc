@@ -12,6 +12,7 @@
 #include <dmlc/fault.h>
 #include <dmlc/dist/communicator.h>
 #include <dmlc/dist/tracker_client.h>
+#include <dmlc/gpu/device_page_cache.h>
 #include <dmlc/gpu/device_parser.h>
 #include <dmlc/gpu/device_recordio.h>
 #include <dmlc/gpu/hip_utils.h>
@@ -392,9 +393,13 @@ class PyDeviceParser {
     py::gil_scoped_release nogil;
     p_->ParseAll(out.csr_.get());
   }
-  /*! \brief fused tokenize -> hash -> fp8/f32 dense batch; DLPack capsules */
-  py::dict ParseAllHashed(int dim, float scale, uint32_t seed, bool fp8) {
-    auto batch = std::make_shared<gpu::DeviceHashedBatch>();
+  /*! \brief fused tokenize -> hash -> fp8/f32 dense batch; DLPack capsules.
+   *  out: the "batch" handle of an earlier result whose tensors the caller is
+   *  done with -- its HBM buffers are refilled instead of allocated again. */
+  py::dict ParseAllHashed(int dim, float scale, uint32_t seed, bool fp8, py::object out) {
+    std::shared_ptr<gpu::DeviceHashedBatch> batch;
+    if (!out.is_none()) batch = out.cast<std::shared_ptr<gpu::DeviceHashedBatch>>();
+    if (batch == nullptr) batch = std::make_shared<gpu::DeviceHashedBatch>();
     {
       py::gil_scoped_release nogil;
       p_->ParseAllHashed(batch.get(), dim, scale, seed, fp8);
@@ -410,6 +415,7 @@ class PyDeviceParser {
                            batch->device, batch);
     d["rows"] = batch->rows;
     d["dim"] = dim;
+    d["batch"] = py::cast(batch);
     return d;
   }
   bool Next() {
@@ -474,6 +480,44 @@ class PyDeviceParser {
   std::shared_ptr<gpu::DeviceParser<I>> p_;
 };
 
+/*! \brief the `#cache` page file on the GPU route (gpu/device_page_cache.h) */
+template <typename I>
+class PyPageCache {
+ public:
+  explicit PyPageCache(std::unique_ptr<gpu::DevicePageCache<I>> c) : c_(std::move(c)) {}
+  static py::object Open(const std::string& path, int device) {
+    std::unique_ptr<gpu::DevicePageCache<I>> c;
+    {
+      py::gil_scoped_release nogil;
+      c = gpu::DevicePageCache<I>::Open(path, device);
+    }
+    if (c == nullptr) return py::none();
+    return py::cast(new PyPageCache<I>(std::move(c)), py::return_value_policy::take_ownership);
+  }
+  static size_t Write(PyDeviceCSR<I>& csr, const std::string& path, double page_mb) {  // NOLINT
+    py::gil_scoped_release nogil;
+    return gpu::DevicePageCache<I>::Write(*csr.csr_, path, static_cast<size_t>(page_mb * (1 << 20)));
+  }
+  void Load(PyDeviceCSR<I>& out) {  // NOLINT
+    py::gil_scoped_release nogil;
+    c_->Load(out.csr_.get());
+  }
+  py::list Pages() const {
+    py::list l;
+    for (const auto& p : c_->pages()) {
+      py::dict d;
+      d["rows"] = p.rows;
+      d["nnz"] = p.nnz;
+      d["begin"] = p.begin;
+      d["end"] = p.end;
+      d["max_index"] = p.max_index;
+      l.append(d);
+    }
+    return l;
+  }
+  std::unique_ptr<gpu::DevicePageCache<I>> c_;
+};
+
 template <typename I>
 void BindIndexType(py::module_& m, const std::string& suffix) {
   py::class_<PyParser<I>>(m, ("Parser" + suffix).c_str())
@@ -501,12 +545,23 @@ void BindIndexType(py::module_& m, const std::string& suffix) {
       .def("capsules", &PyDeviceCSR<I>::Capsules)
       .def("to_host", &PyDeviceCSR<I>::ToHost)
       .def("clear", &PyDeviceCSR<I>::Clear);
+  py::class_<PyPageCache<I>>(m, ("PageCache" + suffix).c_str())
+      .def_static("open", &PyPageCache<I>::Open, py::arg("path"), py::arg("device") = -1)
+      .def_static("write", &PyPageCache<I>::Write, py::arg("csr"), py::arg("path"),
+                  py::arg("page_mb") = 64.0)
+      .def("load", &PyPageCache<I>::Load)
+      .def("pages", &PyPageCache<I>::Pages)
+      .def_property_readonly("rows", [](const PyPageCache<I>& c) { return c.c_->rows(); })
+      .def_property_readonly("nnz", [](const PyPageCache<I>& c) { return c.c_->nnz(); })
+      .def_property_readonly("bytes", [](const PyPageCache<I>& c) { return c.c_->bytes(); })
+      .def_property_readonly("zero_copy", [](const PyPageCache<I>& c) { return c.c_->zero_copy(); });
   py::class_<PyDeviceParser<I>>(m, ("DeviceParser" + suffix).c_str())
       .def(py::init<const std::string&, unsigned, unsigned, py::dict>(), py::arg("uri"),
            py::arg("part") = 0, py::arg("nparts") = 1, py::arg("config") = py::dict())
       .def("parse_all", &PyDeviceParser<I>::ParseAll)
       .def("parse_all_hashed", &PyDeviceParser<I>::ParseAllHashed, py::arg("dim"),
-           py::arg("scale") = 1.0f, py::arg("seed") = 0u, py::arg("fp8") = true)
+           py::arg("scale") = 1.0f, py::arg("seed") = 0u, py::arg("fp8") = true,
+           py::arg("out") = py::none())
       .def("next", &PyDeviceParser<I>::Next)
       .def("value_to_host", &PyDeviceParser<I>::ValueToHost)
       .def("value_shape", &PyDeviceParser<I>::ValueShape)
@@ -611,6 +666,10 @@ void BindRecordIO(py::module_& m) {
 PYBIND11_MODULE(_dmlc, m) {
   m.doc() = "dmlc-core for MI355X: native runtime bindings";
   py::register_exception<dmlc::Error>(m, "DMLCError");
+  py::class_<gpu::DeviceHashedBatch, std::shared_ptr<gpu::DeviceHashedBatch>>(m, "HashedBatch")
+      .def_readonly("rows", &gpu::DeviceHashedBatch::rows)
+      .def_readonly("row_capacity", &gpu::DeviceHashedBatch::row_cap)
+      .def_readonly("dim", &gpu::DeviceHashedBatch::dim);
   BindIndexType<uint32_t>(m, "");
   BindIndexType<uint64_t>(m, "64");
   BindRecordIO(m);

@@ -1,0 +1,121 @@
+"""`uri#cache` on the GPU route: DiskRowIter's binary page file, written from
+an HBM CSR and DMA'd back into one (gpu/device_page_cache.h).
+
+Reference: src/data.cc:87-107 (the #cache branch of RowBlockIter::Create),
+src/data/disk_row_iter.h:94-141 (build / load), src/data/row_block.h:191-215
+(the page format).  The CPU DiskRowIter of this repo is the parity oracle:
+  * same shard -> the GPU-built cache file is byte-identical to the CPU one
+    (both flush a page when MemCostBytes() reaches 64 MiB, tested per row);
+  * a CSR loaded from either file equals the CSR parsed from the text;
+  * an existing cache is loaded, never re-parsed (the text may be gone).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from dmlc_core_amd import data
+
+pytestmark = pytest.mark.gpu
+
+
+def _host(csr):
+    return csr.to_host()
+
+
+def _equal(a, b):
+    for k in ("offset", "label", "index", "value", "field", "weight", "qid"):
+        x, y = a.get(k), b.get(k)
+        if x is None or y is None:
+            assert (x is None or len(x) == 0) and (y is None or len(y) == 0), k
+            continue
+        np.testing.assert_array_equal(np.asarray(x), np.asarray(y), err_msg=k)
+
+
+@pytest.fixture(scope="module")
+def big_libsvm(tmp_path_factory):
+    """~170 MB of text: the CSR spans three 64 MiB pages"""
+    p = str(tmp_path_factory.mktemp("c") / "big.libsvm")
+    data.write_synthetic(p, 0, 260_000, format="libsvm", seed=5, nthread=8)
+    return p
+
+
+def test_gpu_cache_bytes_equal_cpu_cache(big_libsvm, tmp_path):
+    gcache, ccache = str(tmp_path / "g.cache"), str(tmp_path / "c.cache")
+    it = data.RowBlockIter(big_libsvm + "?device=gpu#" + gcache, type="libsvm")
+    assert os.path.exists(gcache)
+    cpu = data.RowBlockIter(big_libsvm + "?nthread=4#" + ccache, type="libsvm")
+    assert it.num_col() == cpu.num_col()
+    with open(gcache, "rb") as f1, open(ccache, "rb") as f2:
+        g, c = f1.read(), f2.read()
+    assert len(g) == len(c) and g == c
+    pc = data.PageCache(gcache)
+    assert len(pc.pages()) >= 3 and pc.zero_copy
+
+
+def test_cpu_cache_pages_do_not_depend_on_threads(big_libsvm, tmp_path):
+    a, b = str(tmp_path / "a.cache"), str(tmp_path / "b.cache")
+    data.RowBlockIter(big_libsvm + "?nthread=1#" + a, type="libsvm")
+    data.RowBlockIter(big_libsvm + "?nthread=7#" + b, type="libsvm")
+    with open(a, "rb") as f1, open(b, "rb") as f2:
+        assert f1.read() == f2.read()
+
+
+def test_gpu_cache_load_equals_text_parse(big_libsvm, tmp_path):
+    ref = data.GPUParser(big_libsvm).parse_all()
+    cache = str(tmp_path / "x.cache")
+    n = data.write_page_cache(ref, cache)
+    assert n >= 3
+    pc = data.PageCache(cache)
+    assert pc.rows == ref.rows and pc.nnz == ref.nnz
+    got = data.DeviceCSR()
+    for _ in range(2):  # reload into the same CSR
+        pc.load(got)
+        assert got.rows == ref.rows and got.nnz == ref.nnz
+        assert got.max_index == ref.max_index
+        _equal(_host(got), _host(ref))
+    # the CPU-written file of the same shard loads to the same CSR
+    ccache = str(tmp_path / "cpu.cache")
+    data.RowBlockIter(big_libsvm + "#" + ccache, type="libsvm")
+    data.PageCache(ccache).load(got)
+    _equal(_host(got), _host(ref))
+
+
+@pytest.mark.parametrize("fmt", ["libsvm", "libfm"])
+def test_gpu_rowblockiter_cache_roundtrip(tmp_path, fmt):
+    """build on first use, load afterwards -- also with the text deleted; small
+    pages (page_mb) exercise the per-page rebase and column fills"""
+    p = str(tmp_path / f"d.{fmt}")
+    data.write_synthetic(p, 0, 3000, format=fmt, seed=2)
+    with open(p, "a") as f:  # weights, qid, valueless features in some rows
+        f.write("1:0.5 qid:3 1:2 4\n0 qid:3 7:1.5\n" if fmt == "libsvm" else "1:2 0:5:1 2:8\n")
+    want = _host(data.GPUParser(p, format=fmt).parse_all())
+    cache = str(tmp_path / "r.cache")
+    it = data.RowBlockIter(p + "?device=gpu#" + cache, type=fmt)
+    blocks = [b for b in iter(lambda: it.value() if it.next() else None, None)]
+    assert len(blocks) == 1
+    _equal(blocks[0], want)
+    os.remove(p)
+    it2 = data.RowBlockIter(p + "?device=gpu#" + cache, type=fmt)
+    assert it2.next()
+    _equal(it2.value(), want)
+    # many tiny pages (the text is gone: rebuilt from the cache): the same CSR
+    full = data.DeviceCSR()
+    data.PageCache(cache).load(full)
+    small = str(tmp_path / "s.cache")
+    assert data.write_page_cache(full, small, page_mb=0.01) > 5
+    again = data.DeviceCSR()
+    data.PageCache(small).load(again)
+    _equal(_host(again), want)
+
+
+def test_page_cache_rejects_truncated_file(tmp_path):
+    p = str(tmp_path / "t.libsvm")
+    data.write_synthetic(p, 0, 500, format="libsvm", seed=1)
+    cache = str(tmp_path / "t.cache")
+    data.write_page_cache(data.GPUParser(p).parse_all(), cache)
+    with open(cache, "r+b") as f:
+        f.truncate(os.path.getsize(cache) - 5)
+    with pytest.raises(Exception):
+        data.PageCache(cache)
+    assert data.PageCache(str(tmp_path / "absent.cache")) is None

@@ -112,9 +112,10 @@ def test_hashed_fm_on_fused_fp8_batch(dataset):
     print("HashedFM gemm path:", model.gemm)
 
 
-def test_fused_tile_kernel_long_lines_fall_back(tmp_path):
-    """Lines longer than the tile kernel's 4 KiB extension are rebuilt by the
-    exact per-line kernel; short and long lines mixed, output equals K9."""
+def test_fused_tile_kernel_long_lines(tmp_path):
+    """A wave follows its tile's last line past the tile end for any length:
+    lines of ~20 KB (several tiles, tiles that own no line) mixed with short
+    ones stay on the tile kernel (no exact fallback) and equal K9."""
     rng = np.random.default_rng(2)
     lines = []
     for r in range(300):
@@ -127,10 +128,67 @@ def test_fused_tile_kernel_long_lines_fall_back(tmp_path):
         f.write("\n".join(lines) + "\n")
     g = data.GPUParser(p, format="libfm", chunk_bytes=256 * 1024)
     fused = g.parse_all_hashed(256, seed=3, fp8=False)
-    assert g.stats()["exact_chunks"] > 0
+    assert g.stats()["exact_chunks"] == 0
     csr = data.csr_to_torch(data.GPUParser(p, format="libfm").parse_all())
     k9 = ops.hashed_dense(csr, 256, seed=3, fp8=False)
     np.testing.assert_allclose(fused["x"].cpu().numpy(), k9.cpu().numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(fused["label"].cpu().numpy(), csr["label"].cpu().numpy())
+
+
+@pytest.mark.parametrize("fmt", ["libsvm", "libfm"])
+@pytest.mark.parametrize("eol", ["\n", "\r\n"])
+def test_fused_tile_kernel_line_shapes(tmp_path, fmt, eol):
+    """label-only rows, runs of tiny lines (many rows per decode round), blank
+    lines, exponent / long-mantissa values (generic token path), CRLF, and a
+    last line without EOL: fused == exact per-line kernel == K9."""
+    rng = np.random.default_rng(7)
+    lines = []
+    for r in range(4000):
+        k = r % 7
+        lab = f"{r % 3 - 1}"
+        if k == 0:
+            lines.append(lab)  # label only
+        elif k == 1:
+            lines.append("")  # blank line (no row)
+            continue
+        n = 1 if k == 2 else int(rng.integers(1, 30))
+        toks = []
+        for _ in range(n):
+            i = int(rng.integers(0, 1 << 22))
+            v = [f"{rng.random():.6f}", f"{rng.random():.3e}", f"{rng.random():.12f}", "7"][r % 4]
+            toks.append(f"{i}:{v}" if fmt == "libsvm" else f"{int(rng.integers(0, 9))}:{i}:{v}")
+        lines.append(lab + " " + " ".join(toks))
+    p = str(tmp_path / f"s.{fmt}")
+    with open(p, "w", newline="") as f:
+        f.write(eol.join(lines))  # no EOL after the last line
+    fused = data.GPUParser(p, format=fmt, chunk_bytes=64 * 1024).parse_all_hashed(
+        192, seed=5, fp8=False, strategy="fused")
+    exact = data.GPUParser(p, format=fmt, chunk_bytes=64 * 1024, fast_path=0).parse_all_hashed(
+        192, seed=5, fp8=False, strategy="fused")
+    csr = data.csr_to_torch(data.GPUParser(p, format=fmt, chunk_bytes=64 * 1024).parse_all())
+    k9 = ops.hashed_dense(csr, 192, seed=5, fp8=False).cpu().numpy()
+    np.testing.assert_array_equal(fused["label"].cpu().numpy(), exact["label"].cpu().numpy())
+    np.testing.assert_array_equal(fused["label"].cpu().numpy(), csr["label"].cpu().numpy())
+    np.testing.assert_allclose(fused["x"].cpu().numpy(), exact["x"].cpu().numpy(), rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(fused["x"].cpu().numpy(), k9, rtol=1e-6, atol=1e-6)
+
+
+def test_fused_batch_reuse(dataset):
+    """out=<earlier result> refills the same HBM buffers (no new allocation)
+    and yields the same batch; a different dim reallocates."""
+    fmt, p, _ = dataset
+    g = data.GPUParser(p, format=fmt, chunk_bytes=128 * 1024, hbm_cache=1)
+    a = g.parse_all_hashed(1024, seed=4)
+    want = a["x"].view(torch.uint8).clone()
+    ptr = a["x"].data_ptr()
+    for _ in range(2):
+        g.before_first()
+        b = g.parse_all_hashed(1024, seed=4, out=a)
+        assert b["x"].data_ptr() == ptr
+        assert torch.equal(b["x"].view(torch.uint8), want)
+    g.before_first()
+    c = g.parse_all_hashed(256, seed=4, out=b)
+    assert tuple(c["x"].shape) == (want.shape[0], 256)
 
 
 @pytest.mark.parametrize("fmt,junk", [("libsvm", "0 junk 3:1\n1 qid:4 5:1\n"),
