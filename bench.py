@@ -83,6 +83,14 @@ def parse_args():
                          "HBM and timed epochs parse it from there (kernel-bound); "
                          "cache: the `#cache` binary page file (DiskRowIter format, built once "
                          "from a GPU parse) is DMA'd zero-copy into the device CSR every step")
+    ap.add_argument("--shape", default="uniform", choices=["uniform", "skewed", "mixed"],
+                    help="synthetic row shape (dmlc/synthetic.h): uniform 20-60 tokens of "
+                         "0.dddddd; skewed power-law tokens per line (some lines > 8 KiB), "
+                         "Zipf-like ids; mixed = skewed + exponent / long / integer / "
+                         "valueless values, weights and qid")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="every rank uses GPU 0 (gloo control plane): rehearses the multi-rank "
+                         "GPU branch on a one-GPU box (RCCL refuses two ranks on one device)")
     args = ap.parse_args()
     if args.rows <= 0:
         args.rows = FORMATS[args.format]["rows"]
@@ -92,7 +100,9 @@ def parse_args():
 def dataset_dir(args, world: int) -> str:
     # one copy per world size: the page cache of a part lives on the NUMA node
     # of the rank that wrote it, which must be the rank that reads it
-    return os.path.join(args.data_dir, f"{args.format}_{args.rows}r_{NUM_PARTS}p_seed0_w{world}")
+    shape = "" if args.shape == "uniform" else f"_{args.shape}"
+    return os.path.join(args.data_dir,
+                        f"{args.format}_{args.rows}r_{NUM_PARTS}p_seed0{shape}_w{world}")
 
 
 def ensure_dataset(args, rank: int, world: int, barrier) -> str:
@@ -123,7 +133,8 @@ def ensure_dataset(args, rank: int, world: int, barrier) -> str:
             continue
         b, e = p * per, min(args.rows, (p + 1) * per)
         tmp = path + f".tmp{rank}"
-        write_synthetic(tmp, b, e, format=args.format, seed=0, nthread=nthread)
+        write_synthetic(tmp, b, e, format=args.format, seed=0, nthread=nthread,
+                        shape=args.shape if args.format != "recordio" else "uniform")
         os.replace(tmp, path)
         open(done, "w").close()
     barrier()
@@ -153,8 +164,9 @@ def launch_ranks(args) -> int:
 
     n = args.gpus
     child = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
+    per_node = 1 if args.share_gpu else n  # share-gpu: every rank's local index is 0
     cmd = [sys.executable, "-m", "dmlc_core_amd.parallel.launch.submit", "--cluster", "local",
-           "--num-workers", str(n), "--gpus-per-node", str(n), "--host-ip", "127.0.0.1",
+           "--num-workers", str(n), "--gpus-per-node", str(per_node), "--host-ip", "127.0.0.1",
            "--auto-file-cache", "0"] + [shlex.quote(c) for c in child]
     env = dict(os.environ)
     env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
@@ -162,6 +174,37 @@ def launch_ranks(args) -> int:
     if os.environ.get("DMLC_BENCH_CHECK_MAPS") == "1":
         print(f"bench launcher: libamdhip64 mapped = {_parent_maps_hip()}", file=sys.stderr)
     return rc
+
+
+def allreduce_probe(dist, cdev, world: int, sizes=(4 << 20, 256 << 20), iters: int = 5):
+    """All-reduce bus bandwidth of the bench's process group, measured after
+    the timed region: f32 buffers of 4 MB and 256 MB, 2 untimed + `iters` timed
+    calls each; busbw = 2 (n - 1) / n * bytes / t (the ring's per-link load,
+    what xGMI's point-to-point links bound).  Under gloo (--share-gpu) the
+    buffers live on the host and the number describes the control plane."""
+    import torch
+
+    out = {"backend": dist.get_backend(), "device": cdev.type}
+    for nbytes in sizes:
+        x = torch.ones(nbytes // 4, dtype=torch.float32, device=cdev)
+        for _ in range(2):
+            dist.all_reduce(x)
+        if cdev.type == "cuda":
+            torch.cuda.synchronize(cdev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            dist.all_reduce(x)
+        if cdev.type == "cuda":
+            torch.cuda.synchronize(cdev)
+        t = (time.perf_counter() - t0) / iters
+        # the slowest rank's time is the collective's time
+        tt = torch.tensor([t], dtype=torch.float64, device=cdev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+        out[f"{nbytes >> 20}MB"] = round(2 * (world - 1) / world * nbytes / t / 1e9, 2)
+        del x
+    return out
 
 
 def main():
@@ -178,7 +221,7 @@ def main():
     use_gpu = args.device == "gpu" or (args.device == "auto" and torch.cuda.is_available())
     # torchrun (RANK/WORLD_SIZE/MASTER_*) or dmlc-submit (DMLC_TRACKER_URI/PORT:
     # the tracker assigns the rank and brokers the process-group address)
-    info = ddist.init("nccl" if use_gpu else "gloo")
+    info = ddist.init("nccl" if use_gpu and not args.share_gpu else "gloo")
     rank, world, local_rank = info["rank"], info["world_size"], info["local_rank"]
     if args.gpus != world:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started a world of "
@@ -190,6 +233,9 @@ def main():
         torch.cuda.set_device(local_rank)
 
     dev = torch.device("cuda", local_rank) if use_gpu else torch.device("cpu")
+    # collectives run on the process group's device: the GPU under RCCL, the
+    # host under gloo (--share-gpu, or no GPU)
+    cdev = dev if use_gpu and not args.share_gpu else torch.device("cpu")
     numa = {"numa_node": -1}
     if use_gpu:
         from dmlc_core_amd.parallel.affinity import bind_to_gpu
@@ -198,7 +244,7 @@ def main():
 
     def barrier():
         if dist is not None:
-            if use_gpu:
+            if cdev.type == "cuda":
                 dist.barrier(device_ids=[local_rank])
             else:
                 dist.barrier()
@@ -288,8 +334,8 @@ def main():
     def global_counts(rows, nnz, max_index, nbytes):
         if dist is None:  # one rank: the totals are its own (no device round trip)
             return [float(rows), float(nnz), float(nbytes)], int(max_index)
-        t = torch.tensor([rows, nnz, nbytes], dtype=torch.float64, device=dev)
-        m = torch.tensor([max_index], dtype=torch.float64, device=dev)
+        t = torch.tensor([rows, nnz, nbytes], dtype=torch.float64, device=cdev)
+        m = torch.tensor([max_index], dtype=torch.float64, device=cdev)
         dist.all_reduce(t)
         dist.all_reduce(m, op=dist.ReduceOp.MAX)
         return t.tolist(), int(m.item())
@@ -313,7 +359,7 @@ def main():
     st = parser.stats() if use_gpu and args.mode != "cache" else {}
     mine = torch.tensor([rank, local["rows"], local["bytes"], elapsed,
                          st.get("wait_reader_sec", 0.0), st.get("wait_gpu_sec", 0.0)],
-                        dtype=torch.float64, device=dev)
+                        dtype=torch.float64, device=cdev)
     gathered = [torch.zeros_like(mine) for _ in range(world)]
     if dist is not None:
         dist.all_gather(gathered, mine)
@@ -333,7 +379,9 @@ def main():
 
     rec = {"rows": local["rows"], "bytes": local["bytes"], "elapsed_sec": float(mine[3])}
     rec.update(parser_record(st))
-    reduced = reduce_across_ranks(rec, device=dev)
+    reduced = reduce_across_ranks(rec, device=cdev)
+    probe = (allreduce_probe(dist, cdev, world, iters=5 if cdev.type == "cuda" else 2)
+             if world > 1 else None)
     with MetricsLogger() as ml:
         ml.log("ingest", steps=args.steps, **rec)
         if rank == 0:
@@ -363,13 +411,15 @@ def main():
             "scaling": "strong",
             "vs_baseline": round(value / fmt["baseline"], 3),
             "dtype": fmt["dtype"],
-            "data": f"synthetic (deterministic {args.format}, 16 part files)",
+            "data": f"synthetic (deterministic {args.format}, 16 part files"
+                    + (f", {args.shape} rows" if args.shape != "uniform" else "") + ")",
             "config": {
                 "model": fmt["model"],
                 "global_batch": int(rows),
                 "seq_len": None,
                 "parallelism": (f"dp{world} (InputSplit byte-range shards, "
-                                + ("RCCL" if use_gpu else "gloo") + " NumCol all-reduce)"
+                                + ("RCCL" if cdev.type == "cuda" else "gloo") + " NumCol all-reduce"
+                                + (", all ranks on GPU 0" if args.share_gpu else "") + ")"
                                 if world > 1 else "dp1 (one InputSplit shard, no collective)"),
                 "format": args.format,
                 "rows": int(rows),
@@ -385,9 +435,11 @@ def main():
             "per_gpu_rows_per_sec": round(value / max(1, world), 1),
             "input_GBps": round(nbytes * args.steps / elapsed / 1e9, 3),
             "mode": args.mode,
+            "shape": args.shape,
             "baseline_value": fmt["baseline"],
         }
         out["per_rank"] = per_rank
+        out["allreduce_busbw_GBps"] = probe
         if use_gpu and args.mode == "cache":
             out["metric"] = fmt["metric"].replace("->CSR", " #cache pages->CSR")
             out["cache"] = {"bytes": parser.bytes, "pages": len(parser.pages()),

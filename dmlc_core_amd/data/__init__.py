@@ -189,17 +189,17 @@ class GPUParser:
         return self._p.partition_bytes()
 
 
-class ShuffledGPUParser:
+class ShuffledGPUParser(GPUParser):
     """GPU counterpart of ``InputSplitShuffle`` (reference
-    ``include/dmlc/input_split_shuffle.h``): the rank's shard is cut into
-    ``num_shuffle_parts`` sub-shards, visited each epoch in the order the CPU
-    split uses (``std::mt19937(666 + part + nparts + num_shuffle_parts +
-    seed)``, reshuffled by ``before_first``).  Sub-shard ``i`` is partition
-    ``part * num_shuffle_parts + i`` of ``nparts * num_shuffle_parts`` and is
-    parsed by a :class:`GPUParser` created when it is reached (one at a time,
-    so the pinned ring and device slots exist once).  Same ``parse_all`` /
-    ``next`` / ``value_*`` surface as GPUParser; rows come out in the CPU
-    split's record order.
+    ``include/dmlc/input_split_shuffle.h``), native: the rank's shard is cut
+    into ``num_shuffle_parts`` sub-shards (partition ``part * K + i`` of
+    ``nparts * K``) visited each epoch in the order the CPU split uses
+    (``std::mt19937(666 + part + nparts + K + seed)``, reshuffled by
+    ``before_first``).  ONE C++ DeviceParser pipeline serves every sub-shard
+    (``?shuffle_parts=K&shuffle_seed=S``): its reader / zero-copy source is
+    re-targeted per epoch, and with ``hbm_cache=1`` every sub-shard's chunks
+    replay from HBM in each epoch's order.  Rows come out in the CPU split's
+    record order; ``state_dict`` carries the epoch and the cursor.
     """
 
     def __init__(self, uri: str, part: int = 0, nparts: int = 1, num_shuffle_parts: int = 2,
@@ -207,75 +207,29 @@ class ShuffledGPUParser:
                  **config):
         if num_shuffle_parts < 1:
             raise ValueError("num_shuffle_parts must be >= 1")
-        self.uri, self.part, self.nparts = uri, int(part), int(nparts)
         self.k, self.seed = int(num_shuffle_parts), int(shuffle_seed)
-        self.format, self.index64, self._config = format, index64, dict(config)
-        self._epoch = 0
-        self._order = self._order_of(0)
-        self._pos = 0
-        self._cur = None
-        self._done_stats: Dict[str, float] = {}
-
-    def _order_of(self, epoch: int):
-        return list(_dmlc.shuffle_parts_order(self.part, self.nparts, self.k, self.seed, epoch))
+        super().__init__(uri, part, nparts, format=format, index64=index64,
+                         shuffle_parts=self.k, shuffle_seed=self.seed, **config)
+        self._where.update(num_shuffle_parts=self.k, shuffle_seed=self.seed)
 
     @property
     def order(self):
         """sub-shard visiting order of the current epoch"""
-        return list(self._order)
+        return list(self._p.visit_order())
 
-    def _open(self, sub: int) -> "GPUParser":
-        return GPUParser(self.uri, self.part * self.k + sub, self.nparts * self.k, format=self.format,
-                         index64=self.index64, **self._config)
+    @property
+    def epoch(self) -> int:
+        return self._p.epoch()
 
-    def _close(self):
-        if self._cur is not None:
-            for key, v in self._cur.stats().items():
-                if isinstance(v, (int, float)) and not isinstance(v, bool):
-                    self._done_stats[key] = self._done_stats.get(key, 0) + v
-            self._cur = None
+    def state_dict(self) -> Dict:
+        return dict(self._where, epoch=self.epoch, cursor=self.tell())
 
-    def parse_all(self, out=None):
-        """Parse the rest of this epoch into ``out`` (a DeviceCSR, appended)."""
-        if out is None:
-            out = DeviceCSR(self.index64)
-        if self._cur is not None:  # finish a sub-shard that next() started
-            self._cur.parse_all(out)
-            self._close()
-            self._pos += 1
-        while self._pos < self.k:
-            self._cur = self._open(self._order[self._pos])
-            self._cur.parse_all(out)
-            self._close()
-            self._pos += 1
-        return out
-
-    def next(self) -> bool:
-        while self._pos < self.k:
-            if self._cur is None:
-                self._cur = self._open(self._order[self._pos])
-            if self._cur.next():
-                return True
-            self._close()
-            self._pos += 1
-        return False
-
-    def value_to_host(self) -> Dict:
-        return self._cur.value_to_host()
-
-    def value_torch(self) -> Dict:
-        return self._cur.value_torch()
-
-    def before_first(self) -> None:
-        """Start the next epoch with a new visiting order."""
-        self._close()
-        self._epoch += 1
-        self._order = self._order_of(self._epoch)
-        self._pos = 0
-
-    def stats(self) -> Dict:
-        """Counters summed over the sub-shard parsers closed so far."""
-        return dict(self._done_stats)
+    def load_state_dict(self, state: Dict) -> None:
+        for k in ("uri", "part", "nparts", "format", "num_shuffle_parts", "shuffle_seed"):
+            if state[k] != self._where[k]:
+                raise ValueError(f"state is for {k}={state[k]!r}, parser has {self._where[k]!r}")
+        self._p.set_epoch(int(state["epoch"]))
+        self.seek(state["cursor"])
 
 
 def csr_to_torch(csr) -> Dict[str, Optional["object"]]:

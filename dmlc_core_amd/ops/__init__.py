@@ -87,31 +87,42 @@ def hashed_dense(csr: Dict, dim: int, seed: int = 0, fp8: bool = True,
 def transpose(csr: Dict, num_features: int) -> Dict:
     """The CSR's transpose (CSC / inverted index) on the device, as a
     CSR-shaped dict whose rows are the features: ``offset`` int64
-    [num_features + 1], ``index`` int32 row ids, ``value`` (or None).
+    [num_features + 1], ``index`` int32 row ids (ascending within every
+    column), ``value`` (or None).
 
-    Built once with a stable device sort of the feature ids, it turns the
-    gradient X^T d into a gather SpMV (K11 over the transpose): every output
-    is summed on chip and written once, instead of one memory-side f32
-    atomic per nonzero, which runs ~17x below the contiguous atomic rate when
-    64 lanes hit 64 different rows (MI355X_MICROARCH.md, Global float
-    atomics).  Feature ids must be < 2^31."""
+    Built by the hand-written stable two-level counting sort of
+    src/gpu/transpose_kernels.hip (bucket histogram -> scan -> stable bucket
+    scatter -> per-bucket column histogram -> scan -> stable column scatter;
+    ballot ranks, no atomics on the ordering), it turns the gradient X^T d into
+    a gather SpMV (K11 over the transpose): every output is summed on chip and
+    written once, instead of one memory-side f32 atomic per nonzero, which
+    runs ~17x below the contiguous atomic rate when 64 lanes hit 64 different
+    rows (MI355X_MICROARCH.md, Global float atomics).  Feature ids must be
+    < num_features <= ``_dmlc.csr_transpose_max_features()`` (2^22); an id
+    outside raises."""
     _check(csr)
     offset, index, value = csr["offset"], csr["index"], csr.get("value")
     nrows, dev = offset.numel() - 1, index.device
+    if num_features <= 0 or num_features > _dmlc.csr_transpose_max_features():
+        raise ValueError(f"transpose: num_features must be in (0, "
+                         f"{_dmlc.csr_transpose_max_features()}], got {num_features}")
     off = offset.view(torch.int64) if offset.dtype != torch.int64 else offset
     # the rows may be a slice of a larger CSR: entries [off[0], off[-1]) of index / value
     lo, hi = (int(off[0]), int(off[-1])) if nrows > 0 else (0, 0)
-    index = index[lo:hi]
-    value = value[lo:hi] if value is not None else None
-    counts = off[1:] - off[:-1]
-    rows = torch.repeat_interleave(torch.arange(nrows, dtype=torch.int32, device=dev), counts,
-                                   output_size=hi - lo)
-    key = index.view(torch.int32) if index.element_size() == 4 else index.view(torch.int64)
-    skey, perm = torch.sort(key, stable=True)
-    bounds = torch.arange(num_features + 1, dtype=skey.dtype, device=dev)
-    col_ptr = torch.searchsorted(skey, bounds).to(torch.int64)
-    return {"offset": col_ptr.contiguous(), "index": rows[perm].contiguous(),
-            "value": value[perm].contiguous() if value is not None else None}
+    nnz = hi - lo
+    col_ptr = torch.empty(num_features + 1, dtype=torch.int64, device=dev)
+    rows = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
+    vals = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev) if value is not None else None
+    scratch = torch.empty(_dmlc.csr_transpose_scratch_bytes(nnz, num_features), dtype=torch.uint8,
+                          device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    _dmlc.csr_transpose(_ptr(offset), nrows, lo, nnz, _ptr(index), _ptr(value), int(num_features),
+                        _ptr(col_ptr), _ptr(rows), _ptr(vals), _ptr(scratch), _ptr(err), _stream(),
+                        _index64(csr))
+    if int(err.item()) != 0:
+        raise ValueError(f"transpose: a feature id is >= num_features ({num_features})")
+    return {"offset": col_ptr, "index": rows[:nnz],
+            "value": vals[:nnz] if vals is not None else None}
 
 
 def _source_key(csr: Dict, num_features: int):
@@ -122,13 +133,23 @@ def _source_key(csr: Dict, num_features: int):
     return (num_features, one(csr["offset"]), one(csr["index"]), one(csr.get("value")))
 
 
+def _whole(csr: Dict) -> bool:
+    """the dict is a whole CSR (its row pointer is a complete tensor of its
+    own, as csr_to_torch returns), not a row slice of a larger one -- decided
+    from the tensor's storage, without reading device memory"""
+    off = csr["offset"]
+    return off.storage_offset() == 0 and \
+        off.numel() * off.element_size() == off.untyped_storage().nbytes()
+
+
 class SpMVFunction(torch.autograd.Function):
     """Autograd wrapper: forward = spmv, backward d/dw = X^T g -- a gather
     SpMV over the transpose cached in ``csr['transpose']``, or the f32-atomic
     spmv_t.  ``grad``: "transpose" builds the transpose on the first backward;
-    "auto" builds it on the second backward through the same dict (a batch
-    made per step -- e.g. a row slice -- keeps the atomic form, which costs
-    less than one sort); "atomic" never builds it."""
+    "auto" builds it on the first backward of a whole CSR (it is reused every
+    epoch) and on the second backward through the same dict otherwise (a
+    batch made per step -- e.g. a row slice -- keeps the atomic form, which
+    costs less than one transpose); "atomic" never builds it."""
 
     @staticmethod
     def forward(ctx, w, bias, csr_tuple, holder, grad):
@@ -151,7 +172,7 @@ class SpMVFunction(torch.autograd.Function):
                 uses = 1
             ctx.holder["_backward_calls"] = uses
             ctx.holder["_calls_key"] = key
-            if ctx.grad == "transpose" or uses >= 2:
+            if ctx.grad == "transpose" or uses >= 2 or _whole(ctx.csr):
                 t = transpose(ctx.csr, ctx.num_features)
                 ctx.holder["transpose"] = t
                 ctx.holder["_transpose_key"] = key
@@ -166,9 +187,11 @@ class SpMVFunction(torch.autograd.Function):
 def csr_spmv(csr: Dict, w: torch.Tensor, bias: torch.Tensor, grad: str = "auto") -> torch.Tensor:
     """Differentiable y = X w + b for a device CSR batch.  X^T g runs as a
     gather SpMV over the CSR's transpose cached in ``csr['transpose']`` (one
-    device sort; ~16x faster than atomics on a 10 M x 1 M batch) or as an
-    f32-atomic scatter: grad="auto" (the default) builds the transpose once
-    the same dict is seen a second time, "transpose" at once, "atomic" never."""
+    hand-written counting-sort transpose; ~16x faster than atomics on a
+    10 M x 1 M batch) or as an
+    f32-atomic scatter: grad="auto" (the default) builds the transpose on the
+    first backward of a whole CSR and once a row-slice dict is seen a second
+    time, "transpose" at once, "atomic" never."""
     if grad not in ("auto", "transpose", "atomic"):
         raise ValueError(f"grad must be 'auto', 'transpose' or 'atomic', got {grad!r}")
     return SpMVFunction.apply(w, bias, (csr["offset"], csr["index"], csr.get("value")), csr, grad)

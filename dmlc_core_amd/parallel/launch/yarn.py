@@ -13,6 +13,9 @@ Two ways to reach a cluster:
   ApplicationMaster's policy to the containers the service reports
   (`yarn_am.py`): a memory-limit kill aborts the job, other failures are
   retried by YARN up to DMLC_MAX_ATTEMPT, and more than that aborts.
+  The node of every failed container is blacklisted (the service AM is asked
+  to with ``yarn.service.node-blacklist.threshold`` = 1, and a task re-placed
+  on such a node counts as a failed attempt).
   ``--files`` / ``--archives`` (and auto-cached command files) are uploaded
   through the WebHDFS backend to ``$DMLC_YARN_STAGING/<job>/`` and localised
   in the spec (`stage_files`), as the reference Client does with -file /
@@ -151,7 +154,12 @@ def service_spec(args, envs: Dict[str, object], name: str,
             "resource": res, "restart_policy": "ON_FAILURE",
             "configuration": {
                 "env": dict(env, DMLC_ROLE=role),
-                "properties": {"yarn.service.container-failure.retry.max": str(max_attempt - 1)},
+                "properties": {
+                    "yarn.service.container-failure.retry.max": str(max_attempt - 1),
+                    # the dmlc AM blacklists the node of every failed container
+                    # (reference ApplicationMaster.java:511-617, updateBlacklist
+                    # on each failure): the service AM does it after 1 failure
+                    "yarn.service.node-blacklist.threshold": "1"},
                 "files": [dict(f) for f in (files or [])]},
         })
     return {"name": name, "version": "1.0", "queue": args.queue, "components": comps}
@@ -186,27 +194,52 @@ class YarnServiceJob:
     def kill(self) -> None:
         self._call("DELETE", f"/{self.name}")
 
+    @staticmethod
+    def _host(c: dict) -> str:
+        return str(c.get("bare_host") or c.get("hostname") or c.get("ip") or "")
+
     def wait(self, poll: float = 2.0, max_attempt: Optional[int] = None,
              timeout: Optional[float] = None) -> "tuple[bool, str]":
-        """Poll until the service finishes.  (ok, diagnostics)."""
+        """Poll until the service finishes.  (ok, diagnostics).
+
+        The dmlc AM's policy over the containers the service reports: a
+        memory-limit kill aborts; every failure counts an attempt of its task
+        and blacklists its node (``self.blacklist``; the spec asks the service
+        AM to exclude it, ``yarn.service.node-blacklist.threshold`` = 1); a
+        task re-placed on a blacklisted node counts as one more failed attempt
+        (the placement broke the policy); max_attempt attempts abort."""
         max_attempt = max_attempt or int(os.environ.get("DMLC_MAX_ATTEMPT", "3"))
         failures: Dict[str, int] = {}
-        seen = set()  # failed container ids already counted
+        seen = set()  # failed / misplaced container ids already counted
+        self.blacklist = set()
         deadline = None if timeout is None else time.monotonic() + timeout
         while True:
             st = self.status()
             state = st.get("state", "")
             for comp in st.get("components", []):
                 for c in comp.get("containers", []):
+                    key = f"{comp['name']}/{c.get('component_instance_name', c.get('id'))}"
+                    host = self._host(c)
+                    if (c.get("state") in ("RUNNING_BUT_UNREADY", "READY", "RUNNING")
+                            and host in self.blacklist and key in failures
+                            and c.get("id") not in seen):
+                        seen.add(c.get("id"))
+                        failures[key] += 1
+                        if failures[key] >= max_attempt:
+                            self.kill()
+                            return False, (f"[DMLC] Task {key} placed on blacklisted node {host} "
+                                           f"after {failures[key]} attempts")
+                        continue
                     if c.get("state") != "FAILED" or c.get("id") in seen:
                         continue
                     seen.add(c.get("id"))
+                    if host:
+                        self.blacklist.add(host)
                     diag = str(c.get("diagnostics", ""))
                     if any(m in diag for m in _MEMORY_KILL):
                         self.kill()
                         return False, (f"[DMLC] {comp['name']} container {c.get('id')} killed because of "
                                        f"exceeding allocated memory: {diag}")
-                    key = f"{comp['name']}/{c.get('component_instance_name', c.get('id'))}"
                     failures[key] = failures.get(key, 0) + 1
                     if failures[key] >= max_attempt:
                         self.kill()

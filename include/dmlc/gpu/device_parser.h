@@ -24,6 +24,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "./device_row_block.h"
 
@@ -81,9 +82,22 @@ struct DeviceParserConfig {
    *  thread falls back to 20 us sleeps (src/gpu/host_wait.h)
    */
   double wait_spin_us{50};
+  /*!
+   * \brief coarse shuffling, the GPU twin of InputSplitShuffle (reference
+   *  include/dmlc/input_split_shuffle.h): the shard is cut into shuffle_parts
+   *  sub-shards (partition part * K + i of nparts * K) visited each epoch in
+   *  the order of std::mt19937(666 + part + nparts + K + seed), reshuffled by
+   *  every BeforeFirst.  One pipeline serves all sub-shards (its reader is
+   *  re-targeted, never rebuilt); with hbm_cache every sub-shard's chunks are
+   *  replayed from HBM in each epoch's order.  1 = off.
+   *  (`?shuffle_parts=`, `?shuffle_seed=`)
+   */
+  unsigned shuffle_parts{1};
+  int shuffle_seed{0};
   /*! \brief apply `?k=v` overrides (chunk_mb, pinned_slots, device_slots,
    *  read_threads, device, format, label_column, weight_column, delimiter,
-   *  fast_path, zero_copy, zc_pin_budget_mb, zc_window_mb, hbm_cache, replay_chunk_mb) */
+   *  fast_path, zero_copy, zc_pin_budget_mb, zc_window_mb, hbm_cache, replay_chunk_mb,
+   *  shuffle_parts, shuffle_seed) */
   void Update(const std::map<std::string, std::string>& args);
 };
 
@@ -149,6 +163,16 @@ class DeviceParser {
   virtual size_t Tell() const = 0;
   /*! \brief continue from a Tell() cursor (drains in-flight work first) */
   virtual void Seek(size_t cursor) = 0;
+  /*!
+   * \brief shuffled mode: epochs started so far (0 after construction, +1 per
+   *  BeforeFirst) -- the visiting order is a function of it, so a resume
+   *  restores it with SetEpoch before Seek
+   */
+  virtual unsigned Epoch() const { return 0; }
+  /*! \brief shuffled mode: switch to epoch e's visiting order, rewound */
+  virtual void SetEpoch(unsigned /*e*/) {}
+  /*! \brief shuffled mode: the current epoch's sub-shard visiting order */
+  virtual std::vector<unsigned> VisitOrder() const { return {0}; }
   /*! \brief parse the next chunk; the block is ready on return */
   virtual bool Next() = 0;
   /*! \brief block of the last Next() (valid until the next call) */

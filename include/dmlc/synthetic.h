@@ -35,6 +35,19 @@ struct Spec {
   uint32_t weight_every{0};
   /*! \brief emit `qid:` tokens */
   bool qid{false};
+  /*!
+   * \brief row shape (text formats):
+   *  uniform  min_nnz..max_nnz tokens per line, `0.dddddd` values (the
+   *           benchmark shape above);
+   *  skewed   power-law tokens per line (Pareto, alpha 1.1, 2 .. 4000 tokens:
+   *           most lines short, ~0.5 % longer than 8 KiB) and Zipf-like
+   *           feature ids (short index digits dominate);
+   *  mixed    skewed lines whose values mix `0.dddddd` with `1.5e-3`-style
+   *           exponents, 9-12-digit mantissas, integers and valueless binary
+   *           features, plus a weight on every 13th label and (LibSVM)
+   *           `qid:` on every 17th line.
+   */
+  std::string shape{"uniform"};
 };
 
 /*!

@@ -8,7 +8,7 @@ out=gpurun_out/$1; shift
 mkdir -p "$out"
 export TMPDIR=/tmp
 if [ -n "$1" ]; then
-  timeout -k 10 900 python -u -m pytest $1 -x -q --timeout 120 --timeout-method thread \
+  timeout -k 10 900 python -u -m pytest $1 -q --timeout 120 --timeout-method thread \
     -p no:cacheprovider > "$out/pytest.log" 2>&1
   rc=$?
   tail -3 "$out/pytest.log"

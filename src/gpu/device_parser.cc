@@ -20,6 +20,7 @@
  */
 #include <dmlc/gpu/device_parser.h>
 #include <dmlc/fault.h>
+#include <dmlc/input_split_shuffle.h>
 #include <dmlc/logging.h>
 #include <dmlc/threadediter.h>
 #include <dmlc/timer.h>
@@ -83,6 +84,10 @@ void DeviceParserConfig::Update(const std::map<std::string, std::string>& args) 
       hbm_cache = v != "0" && v != "false";
     } else if (k == "wait_spin_us") {
       wait_spin_us = std::atof(v.c_str());
+    } else if (k == "shuffle_parts") {
+      shuffle_parts = static_cast<unsigned>(std::atoi(v.c_str()));
+    } else if (k == "shuffle_seed") {
+      shuffle_seed = std::atoi(v.c_str());
     } else if (k == "zero_copy") {
       zero_copy = (v == "auto" || v == "-1") ? -1 : ((v == "0" || v == "false") ? 0 : 1);
     }
@@ -95,6 +100,7 @@ void DeviceParserConfig::Update(const std::map<std::string, std::string>& args) 
   CHECK_LT(replay_chunk_bytes, size_t(1) << 31) << "replay_chunk_bytes must be < 2 GiB";
   CHECK_GE(pinned_slots, 1);
   CHECK_GE(device_slots, 1);
+  CHECK_GE(shuffle_parts, 1U) << "shuffle_parts must be >= 1";
 }
 
 namespace {
@@ -141,7 +147,31 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     tcfg_.delimiter = cfg_.delimiter;
     io::URI path(uri.c_str());
     split_.reset(new io::LineSplitter(io::FileSystem::GetInstance(path), uri.c_str(), part, nparts));
-    reader_.reset(new io::ShardReader(split_.get(), cfg_.read_threads));
+    part_ = part;
+    nparts_ = nparts;
+    if (cfg_.shuffle_parts > 1) {
+      // sub-shard i = partition part * K + i of nparts * K (record-aligned
+      // byte ranges, as InputSplitShuffle's source splits); the pipeline reads
+      // the epoch's concatenation of them
+      const unsigned k = cfg_.shuffle_parts;
+      for (unsigned i = 0; i < k; ++i) {
+        split_->ResetPartition(part * k + i, nparts * k);
+        sub_first_.push_back(all_segs_.size());
+        size_t bytes = 0;
+        for (const auto& sg : split_->ShardSegments()) {
+          if (sg.end <= sg.begin) continue;
+          all_segs_.push_back(sg);
+          bytes += sg.end - sg.begin;
+        }
+        sub_bytes_.push_back(bytes);
+      }
+      sub_first_.push_back(all_segs_.size());
+      ApplyOrder();  // epoch 0
+      reader_.reset(new io::ShardReader(split_.get(), cfg_.read_threads, EpochSegments(),
+                                        EpochStops()));
+    } else {
+      reader_.reset(new io::ShardReader(split_.get(), cfg_.read_threads));
+    }
     compute_.reset(new Stream());
     copy_.reset(new Stream());
     for (int d = 0; d < cfg_.device_slots; ++d) {
@@ -178,12 +208,14 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       zc_.reset(new ZeroCopySource());
       const double t0 = GetTime();
       zc_->SetDrain([this]() { copy_->Synchronize(); });
-      if (!zc_->Init(split_.get(), cfg_.chunk_bytes, cfg_.zc_pin_budget, cfg_.zc_window_bytes)) {
+      if (!zc_->Init(split_.get(), cfg_.chunk_bytes, cfg_.zc_pin_budget, cfg_.zc_window_bytes,
+                     cfg_.shuffle_parts > 1 ? &all_segs_ : nullptr)) {
         CHECK(cfg_.zero_copy != 1) << "zero_copy=1 but the input cannot be mmap'ed + registered";
         zc_.reset();
       } else {
         stats_.register_sec = GetTime() - t0;
         stats_.zero_copy = true;
+        if (cfg_.shuffle_parts > 1) zc_->Reorder(EpochSegmentIndices());
       }
     }
     if (zc_ == nullptr) StartReader();
@@ -204,7 +236,33 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     zc_.reset();
   }
 
-  void BeforeFirst() override { Seek(0); }
+  void BeforeFirst() override {
+    if (cfg_.shuffle_parts > 1) {
+      SetEpoch(epoch_ + 1);  // reshuffle (reference InputSplitShuffle::BeforeFirst)
+      return;
+    }
+    Seek(0);
+  }
+
+  unsigned Epoch() const override { return epoch_; }
+
+  void SetEpoch(unsigned e) override {
+    if (cfg_.shuffle_parts <= 1) {
+      Seek(0);
+      return;
+    }
+    DrainInflight();
+    epoch_ = e;
+    ApplyOrder();
+    if (zc_ != nullptr) {
+      zc_->Reorder(EpochSegmentIndices());
+    } else {
+      reorder_reader_ = true;  // applied by the reader thread's rewind (Seek)
+    }
+    Seek(0);
+  }
+
+  std::vector<unsigned> VisitOrder() const override { return order_; }
 
   size_t Tell() const override { return cursor_; }
 
@@ -215,9 +273,11 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     caching_ = false;
     if (cfg_.hbm_cache) {
       if (cache_complete_) {
-        // replay from the cache when the cursor is a chunk boundary of it
-        for (size_t i = 0; i <= cached_.size(); ++i) {
-          const size_t b = i < cached_.size() ? cached_[i].begin_pos : PartitionBytes();
+        // replay from the cache when the cursor is a chunk boundary of this
+        // epoch's order (sub-shards in visiting order, chunks in text order)
+        BuildReplayList();
+        for (size_t i = 0; i <= replay_list_.size(); ++i) {
+          const size_t b = i < replay_list_.size() ? replay_begin_[i] : PartitionBytes();
           if (b == cursor) {
             replay_ = true;
             replay_idx_ = i;
@@ -239,6 +299,79 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       iter_.BeforeFirst();
     }
     cursor_ = cursor;
+  }
+
+  // ---------------------------------------------------------- shuffled mode
+  /*! \brief this epoch's visiting order and each sub-shard's epoch offset */
+  void ApplyOrder() {
+    order_ = InputSplitShuffle::VisitOrder(part_, nparts_, cfg_.shuffle_parts, cfg_.shuffle_seed,
+                                           epoch_);
+    sub_pos_.assign(cfg_.shuffle_parts, 0);
+    size_t pos = 0;
+    for (unsigned j : order_) {
+      sub_pos_[j] = pos;
+      pos += sub_bytes_[j];
+    }
+  }
+  std::vector<size_t> EpochSegmentIndices() const {
+    std::vector<size_t> idx;
+    for (unsigned j : order_) {
+      for (size_t g = sub_first_[j]; g < sub_first_[j + 1]; ++g) idx.push_back(g);
+    }
+    return idx;
+  }
+  std::vector<io::InputSplitBase::Segment> EpochSegments() const {
+    std::vector<io::InputSplitBase::Segment> segs;
+    for (size_t g : EpochSegmentIndices()) segs.push_back(all_segs_[g]);
+    return segs;
+  }
+  /*! \brief a pinned fill ends with each sub-shard (chunks never mix two) */
+  std::vector<bool> EpochStops() const {
+    std::vector<bool> stop;
+    for (unsigned j : order_) {
+      for (size_t g = sub_first_[j]; g < sub_first_[j + 1]; ++g) {
+        stop.push_back(g + 1 == sub_first_[j + 1]);
+      }
+    }
+    return stop;
+  }
+  /*! \brief sub-shard holding epoch cursor `pos` (the first one starting at or
+   *  before it with bytes left), and the offset inside it */
+  unsigned SubOf(size_t pos, size_t* local) const {
+    if (cfg_.shuffle_parts <= 1) {
+      *local = pos;
+      return 0;
+    }
+    for (unsigned j : order_) {
+      if (pos >= sub_pos_[j] && pos < sub_pos_[j] + sub_bytes_[j]) {
+        *local = pos - sub_pos_[j];
+        return j;
+      }
+    }
+    *local = 0;
+    return order_.back();
+  }
+  /*! \brief cached chunks in this epoch's order, with their epoch cursors */
+  void BuildReplayList() {
+    replay_list_.clear();
+    replay_begin_.clear();
+    replay_end_.clear();
+    if (cfg_.shuffle_parts <= 1) {
+      for (size_t i = 0; i < cached_.size(); ++i) {
+        replay_list_.push_back(i);
+        replay_begin_.push_back(cached_[i].begin_pos);
+        replay_end_.push_back(cached_[i].end_pos);
+      }
+      return;
+    }
+    for (unsigned j : order_) {
+      for (size_t i = 0; i < cached_.size(); ++i) {
+        if (cached_[i].sub != j) continue;
+        replay_list_.push_back(i);
+        replay_begin_.push_back(sub_pos_[j] + cached_[i].sub_begin);
+        replay_end_.push_back(sub_pos_[j] + cached_[i].sub_end);
+      }
+    }
   }
 
   bool Next() override {
@@ -286,6 +419,9 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   /*! \brief a chunk held in the HBM epoch cache */
   struct CachedChunk {
     size_t off, size, begin_pos, end_pos;
+    unsigned sub;                // shuffled mode: its sub-shard
+    size_t sub_begin, sub_end;   // and its cursor range inside it
+    bool eol_end;                // its text ends with an EOL byte (mergeable with the next)
   };
 
   void StartReader() {
@@ -314,7 +450,13 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
         },
         // BeforeFirst / Seek: the consumer sets seek_pos_ before the
         // ThreadedIter handshake, which orders it before this call
-        [this, reader]() { reader->Seek(seek_pos_); });
+        [this, reader]() {
+          if (reorder_reader_) {  // shuffled mode: this epoch's sub-shard order
+            reader->SetSegments(EpochSegments(), EpochStops());
+            reorder_reader_ = false;
+          }
+          reader->Seek(seek_pos_);
+        });
   }
 
   /*!
@@ -326,21 +468,26 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     if (replay_) {
       // HBM epoch cache: chunks are already resident, no copy and no slot
       while (static_cast<int>(inflight_.size()) < cfg_.device_slots &&
-             replay_idx_ < cached_.size()) {
-        const CachedChunk& c = cached_[replay_idx_++];
-        size_t size = c.size, end_pos = c.end_pos;
-        // ParseAll over resident text: adjacent cached chunks are parsed as
-        // one larger chunk (fewer launches and host round trips per byte)
-        while (merge_replay_ && replay_idx_ < cached_.size() &&
-               cached_[replay_idx_].off == c.off + size &&
-               size + cached_[replay_idx_].size <= cfg_.replay_chunk_bytes) {
-          size += cached_[replay_idx_].size;
-          end_pos = cached_[replay_idx_].end_pos;
+             replay_idx_ < replay_list_.size()) {
+        const CachedChunk& c = cached_[replay_list_[replay_idx_]];
+        size_t size = c.size, end_pos = replay_end_[replay_idx_];
+        ++replay_idx_;
+        // ParseAll over resident text: chunks adjacent in the arena and in
+        // this epoch's order are parsed as one larger chunk (fewer launches
+        // and host round trips per byte)
+        // (a chunk whose text ends without EOL -- a file's unterminated last
+        // line on the zero-copy path -- must stay its own chunk)
+        while (merge_replay_ && replay_idx_ < replay_list_.size() &&
+               cached_[replay_list_[replay_idx_ - 1]].eol_end &&
+               cached_[replay_list_[replay_idx_]].off == c.off + size &&
+               size + cached_[replay_list_[replay_idx_]].size <= cfg_.replay_chunk_bytes) {
+          size += cached_[replay_list_[replay_idx_]].size;
+          end_pos = replay_end_[replay_idx_];
           ++replay_idx_;
         }
         inflight_.push_back(Inflight{nullptr, -1, size, end_pos, arena_->get<char>() + c.off});
       }
-      reader_done_ = replay_idx_ == cached_.size();
+      reader_done_ = replay_idx_ == replay_list_.size();
       return;
     }
     while (static_cast<int>(inflight_.size()) + busy_ < cfg_.device_slots && !reader_done_) {
@@ -387,7 +534,19 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
         const size_t begin_pos = cached_.empty() ? 0 : cached_.back().end_pos;
         CHECK_LE(arena_fill_ + size, arena_bytes_) << "HBM cache arena overflow";
         dst = arena_->get<char>() + arena_fill_;
-        cached_.push_back(CachedChunk{arena_fill_, size, begin_pos, end_pos});
+        const char last = size != 0 ? static_cast<const char*>(src)[size - 1] : '\n';
+        CachedChunk c{arena_fill_, size, begin_pos, end_pos, 0, begin_pos, end_pos,
+                      last == '\n' || last == '\r'};
+        if (cfg_.shuffle_parts > 1) {
+          // the sub-shard the chunk belongs to (chunks never span two: the
+          // zero-copy pieces stop at segment ends, the pinned fills at group ends)
+          size_t local = 0;
+          c.sub = SubOf(begin_pos, &local);
+          c.sub_begin = local;
+          c.sub_end = local + (end_pos - begin_pos);
+          CHECK_LE(c.sub_end, sub_bytes_[c.sub]) << "internal error: a chunk spans two sub-shards";
+        }
+        cached_.push_back(c);
         arena_fill_ += size;
       }
       DMLC_HIP_CHECK(hipStreamWaitEvent(copy_->get(), parsed_[d]->get(), 0));
@@ -402,7 +561,9 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     arena_fill_ = 0;
     cache_complete_ = false;
     if (arena_ == nullptr) {
-      arena_bytes_ = PartitionBytes();
+      // + the '\n' the pinned reader inserts after a segment whose last line
+      // has no EOL (one per segment at most)
+      arena_bytes_ = PartitionBytes() + std::max(split_->files().size(), all_segs_.size()) + 16;
       arena_.reset(new DeviceBuffer(arena_bytes_ + kTextPadBytes));
       DMLC_HIP_CHECK(hipMemsetAsync(arena_->get(), 0, arena_bytes_ + kTextPadBytes, copy_->get()));
     }
@@ -906,6 +1067,13 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   HostSlot* cur_slot_{nullptr};
   /*! \brief resume cursor (partition offset after the last delivered chunk) */
   size_t cursor_{0};
+  // shuffled mode (cfg_.shuffle_parts > 1)
+  unsigned part_{0}, nparts_{1}, epoch_{0};
+  std::vector<unsigned> order_{0};
+  std::vector<io::InputSplitBase::Segment> all_segs_;  // sub-shard 0's, 1's, ...
+  std::vector<size_t> sub_first_, sub_bytes_, sub_pos_;
+  std::vector<size_t> replay_list_, replay_begin_, replay_end_;
+  bool reorder_reader_{false};
   /*! \brief where the reader restarts on the next BeforeFirst handshake */
   size_t seek_pos_{0};
   int next_dslot_{0};

@@ -332,6 +332,22 @@ void LaunchOffsetRebase(const uint64_t* src_offset, size_t nrows, uint64_t src_b
  */
 void LaunchPageRebase(uint64_t* offset, size_t nrows, const uint64_t* page_row_end,
                       const uint64_t* page_nnz_base, int npages, hipStream_t stream);
+/*!
+ * \brief CSR -> CSC (transpose_kernels.hip): rows [0, nrows) of a CSR whose
+ *  entries are [base, base + nnz) of index / value; writes col_ptr
+ *  [num_features + 1] (u64, from 0), row_out [nnz] (u32 row ids, ascending
+ *  within each column) and val_out [nnz] (when value != null).  Feature ids
+ *  >= num_features are clamped and set *error (device u32) to 1.
+ *  num_features <= CSRTransposeMaxFeatures(); scratch of
+ *  CSRTransposeScratchBytes(nnz, num_features) bytes (256-byte aligned).
+ */
+template <typename IndexType>
+void LaunchCSRTranspose(const uint64_t* offset, size_t nrows, uint64_t base, uint64_t nnz,
+                        const IndexType* index, const float* value, uint64_t num_features,
+                        uint64_t* col_ptr, uint32_t* row_out, float* val_out, void* scratch,
+                        uint32_t* error, hipStream_t stream);
+size_t CSRTransposeScratchBytes(uint64_t nnz, uint64_t num_features);
+uint64_t CSRTransposeMaxFeatures();
 /*! \brief fill n floats with v */
 void LaunchFill(float* p, size_t n, float v, hipStream_t stream);
 

@@ -1,0 +1,403 @@
+/*!
+ * \file src/gpu/transpose_kernels.hip
+ * \brief CSR -> CSC (the transpose / inverted index of a device CSR) on gfx950:
+ *  a stable two-level counting sort of the entries by feature id, so every
+ *  column lists its rows in ascending order (deterministic gradient sums).
+ *
+ *  Reference demonstrator of the operation: the row loop of
+ *  include/dmlc/data.h:143-157 (Row::SDot) -- the transpose turns X^T d into
+ *  the same gather over columns.
+ *
+ *  Column c = (bucket c >> kLowBits, low key c & (L - 1)), L = 4096 columns per
+ *  bucket, at most kMaxBuckets buckets (so feature ids < 2^22):
+ *   T1 k_bucket_hist  one workgroup per block of kBlockElems entries (in CSR
+ *      order): LDS histogram of buckets -> G[bucket][block].
+ *   T2 exclusive scan of G (bucket-major): where each (bucket, block) run
+ *      lands in the bucket-ordered intermediate arrays.
+ *   T3 k_bucket_scatter  same blocks; each wave owns a contiguous quarter of
+ *      the block, counts it per bucket, and scatters it in order: ranks among
+ *      equal buckets of a 64-entry group come from ballots over the bucket
+ *      bits (no atomics, so the scatter is stable); the row id of every entry
+ *      is walked forward from its group's first row.  Writes (low key u16,
+ *      row u32, value f32) -- runs of ~block/buckets entries, coalesced.
+ *   T4a k_lowkey_hist  one wave per (bucket, segment) of the bucket: LDS
+ *      histogram of the L low keys -> H[bucket][segment][L].
+ *   T4b k_lowkey_scan  one workgroup per bucket: column totals over segments,
+ *      exclusive scan over the bucket's columns -> col_ptr, and per-segment
+ *      starting cursors (in place in H).
+ *   T4c k_lowkey_scatter  one wave per (bucket, segment): cursors in LDS,
+ *      the segment's entries in order, ranks by ballots over the low-key
+ *      bits -> row / value at their final CSC position.
+ *  Traffic for 400 M entries: keys read 3x + (row, value) written and read
+ *  once through the intermediate arrays, ~17 GB, no global atomics.
+ */
+#include <dmlc/gpu/hip_utils.h>
+#include <dmlc/logging.h>
+#include <hip/hip_runtime.h>
+
+#include "./device_common.h"
+#include "./kernels.h"
+
+namespace dmlc {
+namespace gpu {
+
+namespace {
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / dev::kWave;
+constexpr int kLowBits = 12;
+constexpr uint32_t kLow = 1u << kLowBits;  // columns per bucket
+constexpr uint32_t kMaxBuckets = 1024;
+constexpr size_t kBlockElems = 32768;      // T1 / T3 block (per workgroup)
+constexpr size_t kWaveElems = kBlockElems / kWaves;
+constexpr int kSegments = 16;              // T4 segments per bucket
+
+/*! \brief a feature id as a column below num_features (out-of-range ids are
+ *  clamped for memory safety and reported through the error word by T1) */
+template <typename IndexType>
+__device__ __forceinline__ uint32_t column(IndexType c, uint64_t num_features) {
+  return static_cast<uint32_t>(static_cast<uint64_t>(c) < num_features ? static_cast<uint64_t>(c)
+                                                                       : num_features - 1);
+}
+
+/*! \brief lanes of this wave whose `key` (low `bits` bits) equals mine, among `valid` */
+__device__ __forceinline__ uint64_t match_lanes(uint32_t key, int bits, bool valid) {
+  uint64_t m = __ballot(valid);
+  for (int i = 0; i < bits; ++i) {
+    const bool b = (key >> i) & 1u;
+    const uint64_t v = __ballot(b);
+    m &= b ? v : ~v;
+  }
+  return m;
+}
+
+__device__ __forceinline__ uint64_t lanes_below() {
+  const int lane = dev::lane_id();
+  return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+/*! \brief first row whose entries end after entry e (offsets relative to base) */
+__device__ __forceinline__ uint32_t row_of(const uint64_t* __restrict__ offset, size_t nrows,
+                                           uint64_t base, uint64_t e) {
+  size_t lo = 0, hi = nrows;  // offset[lo] - base <= e < offset[hi] - base
+  while (hi - lo > 1) {
+    const size_t mid = (lo + hi) >> 1;
+    if (offset[mid] - base <= e) {
+      lo = mid;
+    } else {
+      hi = mid;
+    }
+  }
+  return static_cast<uint32_t>(lo);
+}
+
+template <typename IndexType>
+__global__ __launch_bounds__(kThreads) void k_bucket_hist(const IndexType* __restrict__ index,
+                                                          uint64_t nnz, uint64_t num_features,
+                                                          uint32_t nbuckets,
+                                                          uint64_t* __restrict__ G,
+                                                          size_t nblocks,
+                                                          uint32_t* __restrict__ error) {
+  __shared__ uint32_t hist[kMaxBuckets];
+  for (uint32_t b = threadIdx.x; b < nbuckets; b += kThreads) hist[b] = 0;
+  __syncthreads();
+  const uint64_t e0 = static_cast<uint64_t>(blockIdx.x) * kBlockElems;
+  const uint64_t e1 = e0 + kBlockElems < nnz ? e0 + kBlockElems : nnz;
+  bool bad = false;
+  for (uint64_t e = e0 + threadIdx.x; e < e1; e += kThreads) {
+    const IndexType c = index[e];
+    bad |= static_cast<uint64_t>(c) >= num_features;
+    atomicAdd(&hist[column(c, num_features) >> kLowBits], 1u);
+  }
+  if (__any(bad) && dev::lane_id() == 0) atomicOr(error, 1u);
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nbuckets; b += kThreads) {
+    G[static_cast<size_t>(b) * nblocks + blockIdx.x] = hist[b];
+  }
+}
+
+template <typename IndexType>
+__global__ __launch_bounds__(kThreads) void k_bucket_scatter(
+    const uint64_t* __restrict__ offset, size_t nrows, uint64_t base,
+    const IndexType* __restrict__ index, const float* __restrict__ value, uint64_t nnz,
+    uint64_t num_features, uint32_t nbuckets, int bucket_bits, const uint64_t* __restrict__ G,
+    size_t nblocks,
+    uint16_t* __restrict__ t_key, uint32_t* __restrict__ t_row, float* __restrict__ t_val) {
+  __shared__ uint32_t cnt[kWaves][kMaxBuckets];  // per-wave counts, then per-wave cursors (low 32 bits)
+  __shared__ uint64_t bpos[kMaxBuckets];
+  const int w = threadIdx.x / dev::kWave;
+  const int lane = dev::lane_id();
+  for (uint32_t b = threadIdx.x; b < nbuckets; b += kThreads) {
+    for (int q = 0; q < kWaves; ++q) cnt[q][b] = 0;
+    bpos[b] = G[static_cast<size_t>(b) * nblocks + blockIdx.x];
+  }
+  __syncthreads();
+  const uint64_t blk0 = static_cast<uint64_t>(blockIdx.x) * kBlockElems;
+  const uint64_t w0 = blk0 + static_cast<uint64_t>(w) * kWaveElems;
+  const uint64_t w1 = w0 + kWaveElems < nnz ? w0 + kWaveElems : nnz;
+  // ---- count this wave's quarter per bucket
+  for (uint64_t e = w0 + lane; e < w1; e += dev::kWave) {
+    atomicAdd(&cnt[w][column(index[e], num_features) >> kLowBits], 1u);
+  }
+  __syncthreads();
+  // ---- per-wave starting cursor of each bucket (offset from the block's
+  // position of the bucket): the counts of the earlier waves
+  for (uint32_t b = threadIdx.x; b < nbuckets; b += kThreads) {
+    uint64_t acc = bpos[b];
+    for (int q = 0; q < kWaves; ++q) {
+      const uint32_t c = cnt[q][b];
+      cnt[q][b] = static_cast<uint32_t>(acc - bpos[b]);  // offset from the block position
+      acc += c;
+    }
+  }
+  __syncthreads();
+  if (w0 >= w1) return;  // an empty quarter (the last block): nothing below synchronises
+  // ---- scatter in order, 64 entries per group
+  uint32_t r = row_of(offset, nrows, base, w0);  // row of the quarter's first entry
+  for (uint64_t g = w0; g < w1; g += dev::kWave) {
+    const uint64_t e = g + lane;
+    const bool valid = e < w1;
+    const uint32_t col = valid ? column(index[e], num_features) : 0u;
+    const float v = (valid && value != nullptr) ? value[e] : 0.0f;
+    // row: forward from the group's first row (a few row ends per group)
+    uint32_t row = r;
+    if (valid) {
+      while (offset[row + 1] - base <= e) ++row;
+    }
+    const uint32_t bk = col >> kLowBits;
+    const uint64_t m = match_lanes(bk, bucket_bits, valid);
+    const uint32_t rank = static_cast<uint32_t>(__popcll(m & lanes_below()));
+    const uint32_t n = static_cast<uint32_t>(__popcll(m));
+    const uint32_t before = valid ? cnt[w][bk] : 0u;
+    dev::wave_sync();  // every lane has read its cursor
+    if (valid) {
+      const uint64_t pos = bpos[bk] + before + rank;
+      t_key[pos] = static_cast<uint16_t>(col & (kLow - 1u));
+      t_row[pos] = row;
+      if (value != nullptr) t_val[pos] = v;
+      if (rank + 1 == n) cnt[w][bk] = before + n;  // the group's last lane of this bucket
+    }
+    dev::wave_sync();
+    r = __shfl(row, dev::kWave - 1, dev::kWave);  // last lane's row (invalid lanes keep r)
+  }
+}
+
+/*! \brief [begin, end) of segment s of bucket b (T4), from the bucket starts */
+__device__ __forceinline__ void segment(const uint64_t* __restrict__ bstart, uint32_t b, int s,
+                                        uint64_t* begin, uint64_t* end) {
+  const uint64_t b0 = bstart[b], b1 = bstart[b + 1];
+  const uint64_t n = b1 - b0;
+  *begin = b0 + n * static_cast<uint64_t>(s) / kSegments;
+  *end = b0 + n * static_cast<uint64_t>(s + 1) / kSegments;
+}
+
+__global__ __launch_bounds__(dev::kWave) void k_lowkey_hist(const uint16_t* __restrict__ t_key,
+                                                            const uint64_t* __restrict__ bstart,
+                                                            uint32_t* __restrict__ H) {
+  __shared__ uint32_t hist[kLow];
+  const uint32_t b = blockIdx.x / kSegments;
+  const int s = static_cast<int>(blockIdx.x % kSegments);
+  const int lane = dev::lane_id();
+  for (uint32_t c = lane; c < kLow; c += dev::kWave) hist[c] = 0;
+  dev::wave_sync();
+  uint64_t e0, e1;
+  segment(bstart, b, s, &e0, &e1);
+  for (uint64_t e = e0 + lane; e < e1; e += dev::kWave) atomicAdd(&hist[t_key[e]], 1u);
+  dev::wave_sync();
+  uint32_t* out = H + static_cast<size_t>(blockIdx.x) * kLow;
+  for (uint32_t c = lane; c < kLow; c += dev::kWave) out[c] = hist[c];
+}
+
+/*! \brief per bucket: column totals over segments -> col_ptr; per-segment cursors in H */
+__global__ __launch_bounds__(kThreads) void k_lowkey_scan(uint32_t* __restrict__ H,
+                                                          const uint64_t* __restrict__ bstart,
+                                                          uint64_t num_features,
+                                                          uint64_t* __restrict__ col_ptr) {
+  __shared__ uint64_t swave[kWaves];
+  constexpr uint32_t kPer = kLow / kThreads;  // columns per thread, contiguous
+  const uint32_t b = blockIdx.x;
+  uint32_t* Hb = H + static_cast<size_t>(b) * kSegments * kLow;
+  const uint32_t c0 = threadIdx.x * kPer;
+  uint32_t tot[kPer];
+  uint64_t sum = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) {
+    uint32_t acc = 0;
+    for (int s = 0; s < kSegments; ++s) {
+      const uint32_t h = Hb[static_cast<size_t>(s) * kLow + c0 + i];
+      Hb[static_cast<size_t>(s) * kLow + c0 + i] = acc;  // offset inside the column
+      acc += h;
+    }
+    tot[i] = acc;
+    sum += acc;
+  }
+  uint64_t wtot;
+  const uint64_t wx = dev::wave_excl_scan(sum, &wtot);
+  const int w = threadIdx.x / dev::kWave;
+  if (dev::lane_id() == 0) swave[w] = wtot;
+  __syncthreads();
+  uint64_t before = wx;
+  for (int q = 0; q < w; ++q) before += swave[q];
+  const uint64_t base = bstart[b];
+  uint64_t x = base + before;
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) {
+    const uint64_t c = static_cast<uint64_t>(b) * kLow + c0 + i;
+    if (c < num_features) col_ptr[c] = x;
+    // cursors become absolute CSC positions (u32 offsets from the bucket base)
+    for (int s = 0; s < kSegments; ++s) {
+      Hb[static_cast<size_t>(s) * kLow + c0 + i] += static_cast<uint32_t>(x - base);
+    }
+    x += tot[i];
+  }
+}
+
+__global__ __launch_bounds__(dev::kWave) void k_lowkey_scatter(
+    const uint16_t* __restrict__ t_key, const uint32_t* __restrict__ t_row,
+    const float* __restrict__ t_val, const uint64_t* __restrict__ bstart,
+    const uint32_t* __restrict__ H, uint32_t* __restrict__ row_out, float* __restrict__ val_out) {
+  __shared__ uint32_t cur[kLow];
+  const uint32_t b = blockIdx.x / kSegments;
+  const int s = static_cast<int>(blockIdx.x % kSegments);
+  const int lane = dev::lane_id();
+  const uint32_t* Hs = H + static_cast<size_t>(blockIdx.x) * kLow;
+  for (uint32_t c = lane; c < kLow; c += dev::kWave) cur[c] = Hs[c];
+  dev::wave_sync();
+  uint64_t e0, e1;
+  segment(bstart, b, s, &e0, &e1);
+  const uint64_t base = bstart[b];
+  for (uint64_t g = e0; g < e1; g += dev::kWave) {
+    const uint64_t e = g + lane;
+    const bool valid = e < e1;
+    const uint32_t k = valid ? t_key[e] : 0u;
+    const uint32_t row = valid ? t_row[e] : 0u;
+    const float v = (valid && val_out != nullptr) ? t_val[e] : 0.0f;
+    const uint64_t m = match_lanes(k, kLowBits, valid);
+    const uint32_t rank = static_cast<uint32_t>(__popcll(m & lanes_below()));
+    const uint32_t n = static_cast<uint32_t>(__popcll(m));
+    const uint32_t before = valid ? cur[k] : 0u;
+    dev::wave_sync();
+    if (valid) {
+      const uint64_t pos = base + before + rank;
+      row_out[pos] = row;
+      if (val_out != nullptr) val_out[pos] = v;
+      if (rank + 1 == n) cur[k] = before + n;
+    }
+    dev::wave_sync();
+  }
+}
+
+__global__ void k_transpose_close(const uint64_t* __restrict__ bstart, uint32_t nbuckets,
+                                  uint64_t num_features, uint64_t* __restrict__ col_ptr) {
+  col_ptr[num_features] = bstart[nbuckets];
+}
+
+size_t AlignUp(size_t n) { return (n + 255) & ~size_t(255); }
+
+struct TransposePlan {
+  uint32_t nbuckets;
+  int bucket_bits;
+  size_t nblocks;
+  size_t g_words, partials_words, h_words;
+  size_t key_off, row_off, val_off, g_off, partials_off, h_off, total;
+};
+
+TransposePlan Plan(uint64_t nnz, uint64_t num_features) {
+  TransposePlan p;
+  p.nbuckets = static_cast<uint32_t>((num_features + kLow - 1) / kLow);
+  if (p.nbuckets == 0) p.nbuckets = 1;
+  p.bucket_bits = 0;
+  while ((1u << p.bucket_bits) < p.nbuckets) ++p.bucket_bits;
+  p.nblocks = (nnz + kBlockElems - 1) / kBlockElems;
+  if (p.nblocks == 0) p.nblocks = 1;
+  p.g_words = static_cast<size_t>(p.nbuckets) * p.nblocks + 1;  // + the bucket-end sentinel
+  p.partials_words = ScanPartials(p.g_words) + 2;
+  p.h_words = static_cast<size_t>(p.nbuckets) * kSegments * kLow;
+  size_t off = 0;
+  p.key_off = off;
+  off += AlignUp(nnz * sizeof(uint16_t));
+  p.row_off = off;
+  off += AlignUp(nnz * sizeof(uint32_t));
+  p.val_off = off;
+  off += AlignUp(nnz * sizeof(float));
+  p.g_off = off;
+  off += AlignUp(p.g_words * sizeof(uint64_t));
+  p.partials_off = off;
+  off += AlignUp(p.partials_words * sizeof(uint64_t));
+  p.h_off = off;
+  off += AlignUp(p.h_words * sizeof(uint32_t));
+  p.total = off;
+  return p;
+}
+
+/*! \brief bucket starts: bstart[b] = G[b * nblocks] after the scan; bstart[nb] = nnz */
+__global__ void k_bucket_starts(const uint64_t* __restrict__ G, size_t nblocks, uint32_t nbuckets,
+                                uint64_t nnz, uint64_t* __restrict__ bstart) {
+  for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b <= nbuckets;
+       b += gridDim.x * blockDim.x) {
+    bstart[b] = b < nbuckets ? G[static_cast<size_t>(b) * nblocks] : nnz;
+  }
+}
+}  // namespace
+
+size_t CSRTransposeScratchBytes(uint64_t nnz, uint64_t num_features) {
+  // + the bucket-start table
+  return Plan(nnz, num_features).total + AlignUp((kMaxBuckets + 1) * sizeof(uint64_t));
+}
+
+uint64_t CSRTransposeMaxFeatures() { return static_cast<uint64_t>(kMaxBuckets) * kLow; }
+
+template <typename IndexType>
+void LaunchCSRTranspose(const uint64_t* offset, size_t nrows, uint64_t base, uint64_t nnz,
+                        const IndexType* index, const float* value, uint64_t num_features,
+                        uint64_t* col_ptr, uint32_t* row_out, float* val_out, void* scratch,
+                        uint32_t* error, hipStream_t stream) {
+  CHECK_GT(num_features, 0U);
+  CHECK_LE(num_features, CSRTransposeMaxFeatures()) << "transpose: num_features above the limit";
+  CHECK_LT(nnz, uint64_t(1) << 32) << "transpose: at most 2^32 - 1 entries";
+  CHECK_LT(nrows, size_t(1) << 32) << "transpose: at most 2^32 - 1 rows";
+  const TransposePlan p = Plan(nnz, num_features);
+  char* sc = static_cast<char*>(scratch);
+  uint16_t* t_key = reinterpret_cast<uint16_t*>(sc + p.key_off);
+  uint32_t* t_row = reinterpret_cast<uint32_t*>(sc + p.row_off);
+  float* t_val = value != nullptr ? reinterpret_cast<float*>(sc + p.val_off) : nullptr;
+  uint64_t* G = reinterpret_cast<uint64_t*>(sc + p.g_off);
+  uint64_t* partials = reinterpret_cast<uint64_t*>(sc + p.partials_off);
+  uint32_t* H = reinterpret_cast<uint32_t*>(sc + p.h_off);
+  uint64_t* bstart = reinterpret_cast<uint64_t*>(sc + p.total);
+  const IndexType* idx = index + base;  // entries [base, base + nnz) of the arrays
+  const float* val = value != nullptr ? value + base : nullptr;
+  // T1 + T2
+  DMLC_HIP_CHECK(hipMemsetAsync(G, 0, p.g_words * sizeof(uint64_t), stream));
+  if (nnz != 0) {
+    hipLaunchKernelGGL(k_bucket_hist<IndexType>, dim3(p.nblocks), dim3(kThreads), 0, stream, idx,
+                       nnz, num_features, p.nbuckets, G, p.nblocks, error);
+  }
+  LaunchScanU64(G, p.g_words, partials, partials + p.partials_words - 1, stream);
+  hipLaunchKernelGGL(k_bucket_starts, dim3((p.nbuckets + kThreads) / kThreads), dim3(kThreads), 0,
+                     stream, G, p.nblocks, p.nbuckets, nnz, bstart);
+  // T3
+  if (nnz != 0) {
+    hipLaunchKernelGGL(k_bucket_scatter<IndexType>, dim3(p.nblocks), dim3(kThreads), 0, stream,
+                       offset, nrows, base, idx, val, nnz, num_features, p.nbuckets,
+                       p.bucket_bits, G, p.nblocks, t_key, t_row, t_val);
+  }
+  // T4
+  const unsigned nseg = p.nbuckets * kSegments;
+  hipLaunchKernelGGL(k_lowkey_hist, dim3(nseg), dim3(dev::kWave), 0, stream, t_key, bstart, H);
+  hipLaunchKernelGGL(k_lowkey_scan, dim3(p.nbuckets), dim3(kThreads), 0, stream, H, bstart,
+                     num_features, col_ptr);
+  hipLaunchKernelGGL(k_lowkey_scatter, dim3(nseg), dim3(dev::kWave), 0, stream, t_key, t_row,
+                     t_val, bstart, H, row_out, val_out);
+  hipLaunchKernelGGL(k_transpose_close, dim3(1), dim3(1), 0, stream, bstart, p.nbuckets,
+                     num_features, col_ptr);
+}
+
+template void LaunchCSRTranspose<uint32_t>(const uint64_t*, size_t, uint64_t, uint64_t,
+                                           const uint32_t*, const float*, uint64_t, uint64_t*,
+                                           uint32_t*, float*, void*, uint32_t*, hipStream_t);
+template void LaunchCSRTranspose<uint64_t>(const uint64_t*, size_t, uint64_t, uint64_t,
+                                           const uint64_t*, const float*, uint64_t, uint64_t*,
+                                           uint32_t*, float*, void*, uint32_t*, hipStream_t);
+
+}  // namespace gpu
+}  // namespace dmlc

@@ -75,16 +75,21 @@ class ZeroCopySource {
    * \param window_bytes window size of the windowed mode
    */
   bool Init(io::InputSplitBase* split, size_t chunk_bytes, size_t pin_budget = 64UL << 30,
-            size_t window_bytes = 1UL << 30) {
+            size_t window_bytes = 1UL << 30,
+            const std::vector<io::InputSplitBase::Segment>* segments = nullptr) {
     chunk_bytes_ = chunk_bytes;
     page_ = static_cast<size_t>(sysconf(_SC_PAGESIZE));
     window_bytes_ = std::max(window_bytes, 2 * chunk_bytes);
-    for (const auto& seg : split->ShardSegments()) {
+    // explicit segments: the shuffled mode's sub-shards (Reorder permutes them)
+    const std::vector<io::InputSplitBase::Segment> own =
+        segments != nullptr ? *segments : split->ShardSegments();
+    for (size_t i = 0; i < own.size(); ++i) {
+      const auto& seg = own[i];
       if (seg.end <= seg.begin) continue;
       const int fd = split->filesystem()->OpenRawFd(split->files()[seg.file_index].path);
       if (fd < 0) return Fail();
       fds_.push_back(fd);
-      segs_.push_back(Seg{fds_.size() - 1, seg.begin, seg.end - seg.begin, nullptr});
+      segs_.push_back(Seg{fds_.size() - 1, seg.begin, seg.end - seg.begin, nullptr, i});
     }
     windowed_ = PartitionBytes() > pin_budget;
     if (windowed_) {
@@ -102,7 +107,31 @@ class ZeroCopySource {
       s.eager = m.data;
       eager_.push_back(m);
     }
+    all_ = segs_;
     return true;
+  }
+  /*!
+   * \brief visit the Init segments in a new order: `order[i]` = index (in the
+   *  Init list) of the i-th segment to visit.  Eager mappings are kept;
+   *  windows are released (after the drain callback).  Rewinds to the start.
+   */
+  void Reorder(const std::vector<size_t>& order) {
+    if (all_.empty() && !segs_.empty()) all_ = segs_;
+    if (windowed_) {
+      JoinPending();
+      if (!windows_.empty() && drain_) drain_();
+      for (auto& w : windows_) Unmap(&w);
+      windows_.clear();
+    }
+    std::vector<Seg> next;
+    for (size_t want : order) {
+      for (const Seg& s : all_) {
+        if (s.init_index == want) next.push_back(s);
+      }
+    }
+    segs_ = next;
+    seg_ = 0;
+    off_ = 0;
   }
   /*!
    * \brief called before a window is released: must wait until no transfer
@@ -191,6 +220,7 @@ class ZeroCopySource {
     size_t file_begin;  // first byte of the segment in its file
     size_t size;
     const char* eager;  // eager mode: mapped segment start
+    size_t init_index;  // position in the Init segment list
   };
   struct Mapping {
     void* map{nullptr};
@@ -327,6 +357,7 @@ class ZeroCopySource {
   bool windowed_{false};
   std::vector<int> fds_;
   std::vector<Seg> segs_;
+  std::vector<Seg> all_;  // the Init list (Reorder's source)
   std::vector<Mapping> eager_;
   std::deque<Mapping> windows_;
   std::future<Mapping> pending_;

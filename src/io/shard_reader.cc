@@ -108,20 +108,37 @@ void PreadFull(int fd, char* dst, size_t len, size_t off) {
 
 ShardReader::ShardReader(InputSplitBase* split, int nthread)
     : split_(split), pool_(new ReadPool(nthread)) {
-  const auto segs = split->ShardSegments();
   fds_.assign(split->files().size(), -2);  // -2: not opened yet
+  const auto segs = split->ShardSegments();
+  SetSegments(segs, std::vector<bool>(segs.size(), false));
+}
+
+ShardReader::ShardReader(InputSplitBase* split, int nthread,
+                         const std::vector<InputSplitBase::Segment>& segs,
+                         const std::vector<bool>& stop_after)
+    : split_(split), pool_(new ReadPool(nthread)) {
+  fds_.assign(split->files().size(), -2);
+  SetSegments(segs, stop_after);
+}
+
+void ShardReader::SetSegments(const std::vector<InputSplitBase::Segment>& segs,
+                              const std::vector<bool>& stop_after) {
+  CHECK_EQ(segs.size(), stop_after.size());
+  segs_.clear();
+  part_bytes_ = 0;
   for (size_t i = 0; i < segs.size(); ++i) {
-    Seg s{segs[i].file_index, segs[i].begin, segs[i].end, false};
+    Seg s{segs[i].file_index, segs[i].begin, segs[i].end, false, stop_after[i]};
     part_bytes_ += s.end - s.begin;
-    if (split->IsTextParser() && i + 1 < segs.size()) {
-      // '\n' between files whose last line has no EOL (as InputSplitBase::Read)
+    if (split_->IsTextParser() && i + 1 < segs.size()) {
+      // '\n' after a segment whose last line has no EOL (a file end; as
+      // InputSplitBase::Read between files)
       char last = '\n';
       const int fd = Fd(s.file);
       if (fd >= 0) {
         PreadFull(fd, &last, 1, s.end - 1);
       } else {
-        std::unique_ptr<SeekStream> st(split->filesystem()->OpenForReadSized(
-            split->files()[s.file].path, split->files()[s.file].size));
+        std::unique_ptr<SeekStream> st(split_->filesystem()->OpenForReadSized(
+            split_->files()[s.file].path, split_->files()[s.file].size));
         st->Seek(s.end - 1);
         CHECK_EQ(st->Read(&last, 1), 1U);
       }
@@ -129,6 +146,7 @@ ShardReader::ShardReader(InputSplitBase* split, int nthread)
     }
     segs_.push_back(s);
   }
+  Reset();
 }
 
 ShardReader::~ShardReader() {
@@ -165,6 +183,7 @@ void ShardReader::Reset() {
   seg_idx_ = 0;
   seg_off_ = 0;
   pending_newline_ = false;
+  stop_pending_ = false;
   carry_.clear();
   bytes_read_ = 0;
 }
@@ -181,10 +200,16 @@ size_t ShardReader::Fill(char* buf, size_t cap) {
   carry_.clear();
   std::vector<std::function<void()>> jobs;
   const size_t min_piece = 4UL << 20;
+  bool group_end = false;
   while (pos < cap) {
     if (pending_newline_) {
       buf[pos++] = '\n';
       pending_newline_ = false;
+      if (stop_pending_) {  // that newline closed a group (buffer was full)
+        stop_pending_ = false;
+        group_end = true;
+        break;
+      }
       continue;
     }
     if (seg_idx_ >= segs_.size()) break;
@@ -232,12 +257,22 @@ size_t ShardReader::Fill(char* buf, size_t cap) {
       if (s.newline_after) pending_newline_ = true;
       ++seg_idx_;
       seg_off_ = 0;
+      if (s.stop_after) {
+        // end of a group: the buffer ends on a record boundary here
+        if (pending_newline_ && pos < cap) {
+          buf[pos++] = '\n';
+          pending_newline_ = false;
+        }
+        group_end = !pending_newline_;
+        stop_pending_ = pending_newline_;
+        break;
+      }
     }
   }
   pool_->Run(jobs);
   if (pos == 0) return 0;
   const bool at_end = seg_idx_ >= segs_.size() && !pending_newline_;
-  if (at_end) return pos;
+  if (at_end || group_end) return pos;
   const char* last = split_->FindLastRecordBegin(buf, buf + pos);
   if (last == buf) {
     // one record is longer than the buffer: keep what was read, grow, retry

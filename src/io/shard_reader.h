@@ -59,7 +59,19 @@ class ShardReader {
    * \param nthread parallel reads per Fill
    */
   ShardReader(InputSplitBase* split, int nthread);
+  /*!
+   * \brief read an explicit list of segments of the split's files instead of
+   *  its partition (the GPU parser's shuffled mode: sub-shards in an epoch's
+   *  visiting order).  A Fill never crosses a segment whose `stop_after` is
+   *  set: it returns at the end of such a segment (a record boundary), so no
+   *  buffer mixes two groups.
+   */
+  ShardReader(InputSplitBase* split, int nthread, const std::vector<InputSplitBase::Segment>& segs,
+              const std::vector<bool>& stop_after);
   ~ShardReader();
+  /*! \brief replace the segment list (as the constructor above) and rewind */
+  void SetSegments(const std::vector<InputSplitBase::Segment>& segs,
+                   const std::vector<bool>& stop_after);
   /*!
    * \brief fill buf (capacity `cap`, multiple of the split's alignment) with
    *  whole records.
@@ -92,6 +104,7 @@ class ShardReader {
     size_t file;
     size_t begin, end;
     bool newline_after;  // text: insert '\n' after this segment
+    bool stop_after;     // Fill returns at the end of this segment
   };
   InputSplitBase* split_;
   std::unique_ptr<ReadPool> pool_;
@@ -100,6 +113,7 @@ class ShardReader {
   size_t part_bytes_{0};
   size_t seg_idx_{0}, seg_off_{0};
   bool pending_newline_{false};
+  bool stop_pending_{false};  // the pending newline ends a group
   std::string carry_;
   size_t need_cap_{0};
   size_t bytes_read_{0};

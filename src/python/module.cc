@@ -439,6 +439,12 @@ class PyDeviceParser {
     py::gil_scoped_release nogil;
     p_->Seek(cursor);
   }
+  unsigned Epoch() const { return p_->Epoch(); }
+  void SetEpoch(unsigned e) {
+    py::gil_scoped_release nogil;
+    p_->SetEpoch(e);
+  }
+  std::vector<unsigned> VisitOrder() const { return p_->VisitOrder(); }
   size_t PartitionBytes() const { return p_->PartitionBytes(); }
   py::dict Stats() const {
     const auto& s = p_->Stats();
@@ -569,6 +575,9 @@ void BindIndexType(py::module_& m, const std::string& suffix) {
       .def("before_first", &PyDeviceParser<I>::BeforeFirst)
       .def("tell", &PyDeviceParser<I>::Tell)
       .def("seek", &PyDeviceParser<I>::Seek)
+      .def("epoch", &PyDeviceParser<I>::Epoch)
+      .def("set_epoch", &PyDeviceParser<I>::SetEpoch)
+      .def("visit_order", &PyDeviceParser<I>::VisitOrder)
       .def("partition_bytes", &PyDeviceParser<I>::PartitionBytes)
       .def("stats", &PyDeviceParser<I>::Stats)
       .def("stream", &PyDeviceParser<I>::Stream);
@@ -714,7 +723,7 @@ PYBIND11_MODULE(_dmlc, m) {
       [](const std::string& path, uint64_t row_begin, uint64_t row_end, const std::string& format,
          uint64_t seed, uint32_t min_nnz, uint32_t max_nnz, uint64_t num_features,
          uint32_t num_fields, uint32_t csv_columns, uint32_t record_bytes, uint32_t weight_every,
-         bool qid, int nthread) {
+         bool qid, int nthread, const std::string& shape) {
         synthetic::Spec s;
         s.format = format;
         s.seed = seed;
@@ -726,6 +735,7 @@ PYBIND11_MODULE(_dmlc, m) {
         s.record_bytes = record_bytes;
         s.weight_every = weight_every;
         s.qid = qid;
+        s.shape = shape;
         py::gil_scoped_release nogil;
         return synthetic::WriteRows(s, path, row_begin, row_end, nthread);
       },
@@ -733,7 +743,7 @@ PYBIND11_MODULE(_dmlc, m) {
       py::arg("seed") = 0, py::arg("min_nnz") = 20, py::arg("max_nnz") = 60,
       py::arg("num_features") = 1000000, py::arg("num_fields") = 32, py::arg("csv_columns") = 29,
       py::arg("record_bytes") = 512, py::arg("weight_every") = 0, py::arg("qid") = false,
-      py::arg("nthread") = 8);
+      py::arg("nthread") = 8, py::arg("shape") = "uniform");
   // ---- HIP feature kernels on raw device pointers (torch tensors' data_ptr) ----
   auto stream_of = [](uintptr_t s) { return reinterpret_cast<hipStream_t>(s); };
   m.def(
@@ -800,6 +810,36 @@ PYBIND11_MODULE(_dmlc, m) {
       },
       py::arg("offset"), py::arg("index"), py::arg("value"), py::arg("nrows"), py::arg("d"),
       py::arg("g"), py::arg("stream"), py::arg("index64") = false);
+  m.def(
+      "csr_transpose",
+      [stream_of](uintptr_t offset, size_t nrows, uint64_t base, uint64_t nnz, uintptr_t index,
+                  uintptr_t value, uint64_t num_features, uintptr_t col_ptr, uintptr_t row_out,
+                  uintptr_t val_out, uintptr_t scratch, uintptr_t error, uintptr_t stream,
+                  bool index64) {
+        auto* off = reinterpret_cast<const uint64_t*>(offset);
+        auto* val = reinterpret_cast<const float*>(value);
+        auto* cp = reinterpret_cast<uint64_t*>(col_ptr);
+        auto* ro = reinterpret_cast<uint32_t*>(row_out);
+        auto* vo = reinterpret_cast<float*>(val_out);
+        auto* err = reinterpret_cast<uint32_t*>(error);
+        void* sc = reinterpret_cast<void*>(scratch);
+        if (index64) {
+          gpu::LaunchCSRTranspose<uint64_t>(off, nrows, base, nnz,
+                                            reinterpret_cast<const uint64_t*>(index), val,
+                                            num_features, cp, ro, vo, sc, err, stream_of(stream));
+        } else {
+          gpu::LaunchCSRTranspose<uint32_t>(off, nrows, base, nnz,
+                                            reinterpret_cast<const uint32_t*>(index), val,
+                                            num_features, cp, ro, vo, sc, err, stream_of(stream));
+        }
+      },
+      py::arg("offset"), py::arg("nrows"), py::arg("base"), py::arg("nnz"), py::arg("index"),
+      py::arg("value"), py::arg("num_features"), py::arg("col_ptr"), py::arg("row_out"),
+      py::arg("val_out"), py::arg("scratch"), py::arg("error"), py::arg("stream"),
+      py::arg("index64") = false);
+  m.def("csr_transpose_scratch_bytes", &gpu::CSRTransposeScratchBytes, py::arg("nnz"),
+        py::arg("num_features"));
+  m.def("csr_transpose_max_features", &gpu::CSRTransposeMaxFeatures);
   m.def(
       "hashed_dense",
       [stream_of](uintptr_t offset, uintptr_t index, uintptr_t value, uintptr_t field,

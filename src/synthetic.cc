@@ -8,6 +8,7 @@
 #include <dmlc/synthetic.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -51,12 +52,68 @@ inline char* PutFrac6(char* p, uint64_t r) {
   return p + 6;
 }
 
-/*! \brief one text row into p (buffer large enough); returns end */
+/*! \brief "0." + k digits (k <= 18) */
+inline char* PutFracK(char* p, uint64_t r, int k) {
+  *p++ = '0';
+  *p++ = '.';
+  for (int i = 0; i < k; ++i) {
+    *p++ = static_cast<char>('0' + r % 10);
+    r /= 10;
+  }
+  return p;
+}
+
+/*! \brief a value of the mixed shape: mostly 0.dddddd, else another spelling */
+inline char* PutMixedValue(char* p, uint64_t r) {
+  switch ((r >> 40) % 16) {
+    case 10:
+    case 11: {  // d.ddde-d  (exponent: the generic strtonum path)
+      *p++ = static_cast<char>('1' + r % 9);
+      *p++ = '.';
+      for (int i = 0; i < 3; ++i) *p++ = static_cast<char>('0' + (r >> (4 * i + 8)) % 10);
+      *p++ = 'e';
+      *p++ = '-';
+      *p++ = static_cast<char>('1' + (r >> 24) % 5);
+      return p;
+    }
+    case 12:  // 9 - 12 fraction digits
+      return PutFracK(p, r, 9 + static_cast<int>((r >> 20) % 4));
+    case 15:  // integer value
+      return PutU64(p, 1 + r % 9);
+    default:
+      return PutFrac6(p, r);
+  }
+}
+
+/*! \brief tokens of a skewed line: Pareto(alpha = 1.1, x_min = 2), capped */
+inline uint32_t ParetoNnz(uint64_t r) {
+  const double u = (static_cast<double>(r >> 11) + 1.0) * (1.0 / 9007199254740992.0);
+  const double x = 2.0 * std::pow(u, -1.0 / 1.1);
+  return static_cast<uint32_t>(std::min(x, 4000.0));
+}
+
+/*! \brief Zipf-like feature id: log-uniform over [1, num_features) */
+inline uint64_t SkewedIndex(uint64_t r, uint64_t num_features) {
+  const double u = static_cast<double>(r >> 11) * (1.0 / 9007199254740992.0);
+  const uint64_t v = static_cast<uint64_t>(std::exp(u * std::log(static_cast<double>(num_features))));
+  return std::min<uint64_t>(v, num_features - 1);
+}
+
+/*! \brief longest line TextRow can write for this spec */
+size_t MaxRowBytes(const Spec& s) {
+  if (s.format == "csv") return 16 + 12 * s.csv_columns;
+  const size_t tokens = s.shape == "uniform" ? s.max_nnz : 4000;
+  return 96 + tokens * 56;
+}
+
+/*! \brief one text row into p (MaxRowBytes(s) of room); returns end */
 char* TextRow(const Spec& s, uint64_t row, char* p, std::vector<uint64_t>* idx) {
   uint64_t st = s.seed * 0x100000001b3ull + row * 0x9e3779b97f4a7c15ull + 1;
   const uint64_t r0 = SplitMix(&st);
+  const bool skewed = s.shape == "skewed" || s.shape == "mixed";
+  const bool mixed = s.shape == "mixed";
   *p++ = (r0 & 1) ? '1' : '0';
-  if (s.weight_every != 0 && row % s.weight_every == 0) {
+  if ((s.weight_every != 0 && row % s.weight_every == 0) || (mixed && row % 13 == 0)) {
     *p++ = ':';
     p = PutFrac6(p, SplitMix(&st));
   }
@@ -68,14 +125,22 @@ char* TextRow(const Spec& s, uint64_t row, char* p, std::vector<uint64_t>* idx) 
     *p++ = '\n';
     return p;
   }
-  if (s.qid && s.format == "libsvm") {
+  if (s.format == "libsvm" && (s.qid || (mixed && row % 17 == 0))) {
     std::memcpy(p, " qid:", 5);
     p = PutU64(p + 5, row / 16);
   }
-  const uint32_t span = s.max_nnz - s.min_nnz + 1;
-  const uint32_t nnz = s.min_nnz + static_cast<uint32_t>(SplitMix(&st) % span);
+  uint32_t nnz;
+  if (skewed) {
+    nnz = ParetoNnz(SplitMix(&st));
+  } else {
+    const uint32_t span = s.max_nnz - s.min_nnz + 1;
+    nnz = s.min_nnz + static_cast<uint32_t>(SplitMix(&st) % span);
+  }
   idx->resize(nnz);
-  for (uint32_t i = 0; i < nnz; ++i) (*idx)[i] = SplitMix(&st) % s.num_features;
+  for (uint32_t i = 0; i < nnz; ++i) {
+    const uint64_t r = SplitMix(&st);
+    (*idx)[i] = skewed ? SkewedIndex(r, s.num_features) : r % s.num_features;
+  }
   std::sort(idx->begin(), idx->end());
   for (uint32_t i = 0; i < nnz; ++i) {
     *p++ = ' ';
@@ -84,8 +149,15 @@ char* TextRow(const Spec& s, uint64_t row, char* p, std::vector<uint64_t>* idx) 
       *p++ = ':';
     }
     p = PutU64(p, (*idx)[i]);
-    *p++ = ':';
-    p = PutFrac6(p, SplitMix(&st));
+    const uint64_t r = SplitMix(&st);
+    if (mixed) {
+      if ((r >> 40) % 16 == 13 || (r >> 40) % 16 == 14) continue;  // valueless binary feature
+      *p++ = ':';
+      p = PutMixedValue(p, r);
+    } else {
+      *p++ = ':';
+      p = PutFrac6(p, r);
+    }
   }
   *p++ = '\n';
   return p;
@@ -95,6 +167,8 @@ char* TextRow(const Spec& s, uint64_t row, char* p, std::vector<uint64_t>* idx) 
 uint64_t WriteRows(const Spec& spec, const std::string& path, uint64_t row_begin,
                    uint64_t row_end, int nthread) {
   CHECK(spec.min_nnz <= spec.max_nnz) << "min_nnz > max_nnz";
+  CHECK(spec.shape == "uniform" || spec.shape == "skewed" || spec.shape == "mixed")
+      << "shape must be uniform, skewed or mixed, not " << spec.shape;
   std::unique_ptr<Stream> fo(Stream::Create(path.c_str(), "w"));
   nthread = std::max(1, nthread);
   const uint64_t kBlockRows = 16384;
@@ -129,13 +203,13 @@ uint64_t WriteRows(const Spec& spec, const std::string& path, uint64_t row_begin
             w.WriteRecord(payload.data(), payload.size());
           }
         } else {
-          const size_t per_row = spec.format == "csv"
-                                     ? 16 + 12 * spec.csv_columns
-                                     : 64 + static_cast<size_t>(spec.max_nnz) * 48;
-          buf.resize((e - b) * per_row);
-          char* p = &buf[0];
-          for (uint64_t r = b; r < e; ++r) p = TextRow(spec, r, p, &idx);
-          buf.resize(p - &buf[0]);
+          const size_t room = MaxRowBytes(spec);
+          size_t used = 0;
+          for (uint64_t r = b; r < e; ++r) {
+            if (buf.size() < used + room) buf.resize(std::max(2 * buf.size(), used + room));
+            used = TextRow(spec, r, &buf[0] + used, &idx) - &buf[0];
+          }
+          buf.resize(used);
         }
       });
     }

@@ -34,7 +34,7 @@ def _equal(a, b):
 
 @pytest.fixture(scope="module")
 def big_libsvm(tmp_path_factory):
-    """~170 MB of text: the CSR spans three 64 MiB pages"""
+    """~170 MB of text: the CSR spans two 64 MiB pages"""
     p = str(tmp_path_factory.mktemp("c") / "big.libsvm")
     data.write_synthetic(p, 0, 260_000, format="libsvm", seed=5, nthread=8)
     return p
@@ -50,7 +50,7 @@ def test_gpu_cache_bytes_equal_cpu_cache(big_libsvm, tmp_path):
         g, c = f1.read(), f2.read()
     assert len(g) == len(c) and g == c
     pc = data.PageCache(gcache)
-    assert len(pc.pages()) >= 3 and pc.zero_copy
+    assert len(pc.pages()) >= 2 and pc.zero_copy
 
 
 def test_cpu_cache_pages_do_not_depend_on_threads(big_libsvm, tmp_path):
@@ -65,7 +65,7 @@ def test_gpu_cache_load_equals_text_parse(big_libsvm, tmp_path):
     ref = data.GPUParser(big_libsvm).parse_all()
     cache = str(tmp_path / "x.cache")
     n = data.write_page_cache(ref, cache)
-    assert n >= 3
+    assert n >= 2
     pc = data.PageCache(cache)
     assert pc.rows == ref.rows and pc.nnz == ref.nnz
     got = data.DeviceCSR()

@@ -170,3 +170,57 @@ def test_cached_transpose_follows_the_dict_tensors(csr_t):
     m.loss(holder).backward()
     ref.loss({k: holder[k] for k in ("offset", "index", "value", "label")}).backward()
     torch.testing.assert_close(m.weight.grad, ref.weight.grad, rtol=1e-4, atol=1e-6)
+
+
+def _ref_transpose(t, nfeat):
+    off = t["offset"].cpu().numpy().astype(np.int64)
+    lo, hi = off[0], off[-1]
+    idx = t["index"].cpu().numpy().astype(np.int64)[lo:hi]
+    val = t["value"].cpu().numpy()[lo:hi]
+    rows = np.repeat(np.arange(len(off) - 1), np.diff(off))
+    order = np.argsort(idx, kind="stable")  # stable: rows ascending within a column
+    ptr = np.searchsorted(idx[order], np.arange(nfeat + 1))
+    return ptr, rows[order].astype(np.int32), val[order]
+
+
+@pytest.mark.parametrize("nfeat,rows,index64", [(5000, 3000, False), (1 << 22, 20000, False),
+                                                  (70000, 5000, True), (1, 50, False)])
+def test_transpose_kernel_is_a_stable_csc(tmp_path, nfeat, rows, index64):
+    """the HIP counting-sort transpose equals numpy's stable argsort CSC
+    exactly (row ids ascending within every column, values moved with them),
+    across bucket counts (1 .. 1024 buckets of 4096 columns), 64-bit indices,
+    and a single column"""
+    p = str(tmp_path / "t.libsvm")
+    data.write_synthetic(p, 0, rows, seed=5, num_features=nfeat, min_nnz=1, max_nnz=40)
+    t = data.csr_to_torch(data.GPUParser(p, index64=index64).parse_all(data.DeviceCSR(index64)))
+    tt = ops.transpose(t, nfeat)
+    ptr, r, v = _ref_transpose(t, nfeat)
+    np.testing.assert_array_equal(tt["offset"].cpu().numpy(), ptr)
+    np.testing.assert_array_equal(tt["index"].cpu().numpy(), r)
+    np.testing.assert_array_equal(tt["value"].cpu().numpy(), v)
+
+
+def test_transpose_rejects_out_of_range_ids(csr_t):
+    t, csr = csr_t
+    with pytest.raises(ValueError, match="num_features"):
+        ops.transpose(t, int(csr.max_index))  # the largest id is out of range
+    with pytest.raises(ValueError):
+        ops.transpose(t, (1 << 22) + 1)
+
+
+def test_auto_grad_builds_the_transpose_on_a_whole_csr(csr_t):
+    """grad='auto': a whole CSR (csr_to_torch) gets its transpose on the
+    first backward; the gradient equals the atomic form"""
+    import torch
+    from dmlc_core_amd.models import SparseLogReg
+    t, csr = csr_t
+    nfeat = int(csr.max_index) + 1
+    m = SparseLogReg(nfeat).cuda()
+    m.loss(t).backward()
+    assert "transpose" in t
+    a = SparseLogReg(nfeat, grad="atomic").cuda()
+    with torch.no_grad():
+        a.weight.copy_(m.weight)
+        a.bias.copy_(m.bias)
+    a.loss({k: v for k, v in t.items() if k in ("offset", "index", "value", "label")}).backward()
+    torch.testing.assert_close(m.weight.grad, a.weight.grad, rtol=1e-4, atol=1e-6)

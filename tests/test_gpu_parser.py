@@ -471,29 +471,33 @@ def test_replay_chunk_limit_is_enforced(tmp_path):
         io.GPURecordIO(r, hbm_cache=1, replay_chunk_mb=8192)
 
 
-@pytest.mark.parametrize("nparts", [1, 2])
-def test_shuffled_gpu_parser_follows_input_split_shuffle(tmp_path, nparts):
+@pytest.mark.parametrize("nparts,zero_copy,hbm", [(1, "auto", 0), (2, "auto", 0), (2, "0", 0),
+                                                   (2, "auto", 1), (1, "0", 1)])
+def test_shuffled_gpu_parser_follows_input_split_shuffle(tmp_path, nparts, zero_copy, hbm):
     """ShuffledGPUParser visits the sub-shards in InputSplitShuffle's per-epoch
     order: each epoch's CSR (parse_all and streaming next) equals the CPU
-    parser's rows of the sub-shards in that order."""
+    parser's rows of the sub-shards in that order -- on the zero-copy and the
+    pinned-ring readers, and replayed from the HBM cache in each new order."""
     from dmlc_core_amd import _dmlc
     d = tmp_path / "s"
     d.mkdir()
     for i in range(3):
         data.write_synthetic(str(d / f"p{i}.libsvm"), i * 1500, (i + 1) * 1500, seed=23)
+    with open(str(d / "p1.libsvm"), "ab") as f:  # a file whose last line has no EOL
+        f.write(b"1 3:0.5 9:1")
     uri, k, seed = str(d), 4, 9
     for part in range(nparts):
         sp = data.ShuffledGPUParser(uri, part, nparts, num_shuffle_parts=k, shuffle_seed=seed,
-                                    chunk_bytes=64 * 1024)
+                                    chunk_bytes=64 * 1024, zero_copy=zero_copy, hbm_cache=hbm)
         orders = []
-        for epoch in range(3):
+        for epoch in range(4 if hbm else 3):
             if epoch:
                 sp.before_first()
             order = list(_dmlc.shuffle_parts_order(part, nparts, k, seed, epoch))
             assert sp.order == order
             orders.append(order)
             want = cpu_rows_parts(uri, [part * k + s for s in order], nparts * k)
-            if epoch < 2:
+            if epoch < 2 or (hbm and epoch == 3):
                 got = pyref.concat_blocks([sp.parse_all().to_host()])
             else:
                 blocks = []
@@ -502,6 +506,8 @@ def test_shuffled_gpu_parser_follows_input_split_shuffle(tmp_path, nparts):
                 got = pyref.concat_blocks(blocks)
             assert_same(got, want)
         assert len({tuple(o) for o in orders}) > 1  # the order changes between epochs
+        if hbm:
+            assert sp.stats()["chunks"] > 0
 
 
 def cpu_rows_parts(uri, parts, nparts):
@@ -509,3 +515,33 @@ def cpu_rows_parts(uri, parts, nparts):
     for p in parts:
         blocks.extend(data.iter_blocks(uri, p, nparts, type="libsvm"))
     return pyref.concat_blocks(blocks)
+
+
+def test_shuffled_gpu_parser_resume_mid_epoch(tmp_path):
+    """state_dict = (epoch, cursor): a new parser restores the epoch's visiting
+    order and continues at the cursor; the rest of the epoch equals the CPU
+    rows after the delivered ones.  Also reachable as ?shuffle_parts=&shuffle_seed=."""
+    p = str(tmp_path / "r.libsvm")
+    data.write_synthetic(p, 0, 6000, seed=31)
+    k, seed = 5, 3
+    sp = data.ShuffledGPUParser(p, 0, 1, num_shuffle_parts=k, shuffle_seed=seed,
+                                chunk_bytes=32 * 1024)
+    sp.before_first()
+    sp.before_first()  # epoch 2
+    want = cpu_rows_parts(p, sp.order, k)
+    head = []
+    for _ in range(3):
+        assert sp.next()
+        head.append(sp.value_to_host())
+    state = sp.state_dict()
+    assert state["epoch"] == 2
+    sp2 = data.ShuffledGPUParser(p, 0, 1, num_shuffle_parts=k, shuffle_seed=seed,
+                                 chunk_bytes=32 * 1024)
+    sp2.load_state_dict(state)
+    assert sp2.order == sp.order
+    tail = []
+    while sp2.next():
+        tail.append(sp2.value_to_host())
+    assert_same(pyref.concat_blocks(head + tail), want)
+    g = data.GPUParser(p + f"?shuffle_parts={k}&shuffle_seed={seed}", chunk_bytes=32 * 1024)
+    assert_same(g.parse_all().to_host(), cpu_rows_parts(p, g._p.visit_order(), k))

@@ -39,3 +39,26 @@ def test_two_ranks_share_one_gpu(tmp_path):
     assert sum(r[1] for r in ranks) == rows  # complete and disjoint
     assert sum(r[2] for r in ranks) == nnz
     assert sum(r[3] for r in ranks) == csum
+
+
+@pytest.mark.parametrize("mode", ["stream", "cache"])
+def test_bench_share_gpu_two_ranks(tmp_path, mode):
+    """bench.py's own multi-rank GPU branch (launcher -> tracker ranks ->
+    per-world dataset -> NUMA binding -> barriers -> NumCol all-reduce ->
+    per-rank gather -> all-reduce probe), two ranks on GPU 0 over gloo: the
+    JSON line a SCALE run prints, with rows summing to the dataset."""
+    env = dict(os.environ, PYTHONPATH=ROOT, DMLC_HEARTBEAT_PERIOD="1")
+    cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-gpu",
+           "--steps", "2", "--warmup", "1", "--rows", "120000", "--mode", mode,
+           "--data-dir", str(tmp_path / "bench")]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-5000:]
+    line = [x for x in p.stdout.splitlines() if x.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["n_gpus"] == 2 and out["steps"] == 2 and out["warmup"] == 1
+    assert out["config"]["rows"] == 120000 and out["config"]["global_batch"] == 120000
+    assert "all ranks on GPU 0" in out["config"]["parallelism"]
+    assert sorted(r["rank"] for r in out["per_rank"]) == [0, 1]
+    assert sum(r["rows"] for r in out["per_rank"]) == 120000
+    probe = out["allreduce_busbw_GBps"]
+    assert probe["backend"] == "gloo" and probe["4MB"] > 0 and probe["256MB"] > 0

@@ -242,3 +242,30 @@ def test_service_staging_requires_a_target(monkeypatch, tmp_path):
     monkeypatch.setenv("DMLC_WEBHDFS_ENDPOINT", "http://nn:9870")
     assert yarn.staging_root(args) == "webhdfs://nn:9870/tmp"
     assert yarn.stage_files(args, "j", upload=False)[0]["src_file"] == "/tmp/j/a.txt"
+
+
+def test_service_job_blacklists_failed_nodes(rm):
+    """a failed container's node is blacklisted: the spec asks the service AM
+    to exclude it (node-blacklist threshold 1, as the reference AM's
+    updateBlacklist on each failure), and a retry placed on it anyway counts
+    as a failed attempt of that task"""
+    spec = yarn.service_spec(_args(), {}, "j3")
+    for comp in spec["components"]:
+        assert comp["configuration"]["properties"]["yarn.service.node-blacklist.threshold"] == "1"
+    job = yarn.YarnServiceJob(rm, "j3")
+    job.submit(spec)
+
+    def st(*cs):
+        return {"state": "STARTED", "components": [{"name": "worker", "containers": list(cs)}]}
+    fail_a = {"id": "c1", "component_instance_name": "worker-0", "state": "FAILED",
+              "bare_host": "nodeA", "diagnostics": "exit 1"}
+    on_b = {"id": "c2", "component_instance_name": "worker-0", "state": "READY", "bare_host": "nodeB"}
+    _RM.script = [st(fail_a), st(fail_a, on_b), {"state": "SUCCEEDED"}]
+    assert job.wait(poll=0.01, max_attempt=3) == (True, "SUCCEEDED")
+    assert job.blacklist == {"nodeA"}
+    # re-placed on the blacklisted node, twice: the attempts run out
+    on_a = [{"id": f"c{i}", "component_instance_name": "worker-0", "state": "READY",
+             "bare_host": "nodeA"} for i in (3, 4)]
+    _RM.script = [st(fail_a), st(fail_a, on_a[0]), st(fail_a, on_a[1])]
+    ok, diag = job.wait(poll=0.01, max_attempt=3)
+    assert not ok and "blacklisted node nodeA" in diag

@@ -1,7 +1,9 @@
 // dmlc_gen: deterministic synthetic datasets of the benchmark shapes
 // (LibSVM 20-60 nnz/row, LibFM, CSV 29 columns, RecordIO 512 B).
 //
-//   dmlc_gen <format> <rows> <out_prefix> [parts=1] [seed=0] [threads=8]
+//   dmlc_gen <format> <rows> <out_prefix> [parts=1] [seed=0] [threads=8] [shape=uniform]
+//
+// shape: uniform | skewed | mixed (dmlc/synthetic.h)
 //
 // Writes <out_prefix>-<k>.<format> for k < parts; rows are split evenly and
 // the same (format, rows, seed) always produces the same bytes.
@@ -15,7 +17,9 @@
 
 int main(int argc, char** argv) {
   if (argc < 4) {
-    std::fprintf(stderr, "usage: %s libsvm|libfm|csv|recordio rows out_prefix [parts] [seed] [threads]\n",
+    std::fprintf(stderr,
+                 "usage: %s libsvm|libfm|csv|recordio rows out_prefix [parts] [seed] [threads] "
+                 "[uniform|skewed|mixed]\n",
                  argv[0]);
     return 2;
   }
@@ -26,6 +30,7 @@ int main(int argc, char** argv) {
   unsigned parts = argc > 4 ? std::atoi(argv[4]) : 1;
   spec.seed = argc > 5 ? std::strtoull(argv[5], nullptr, 10) : 0;
   int threads = argc > 6 ? std::atoi(argv[6]) : 8;
+  if (argc > 7) spec.shape = argv[7];
   CHECK_GT(parts, 0U);
   double t0 = dmlc::GetTime();
   uint64_t bytes = 0, per = (rows + parts - 1) / parts;
