@@ -88,6 +88,9 @@ def parse_args():
                          "0.dddddd; skewed power-law tokens per line (some lines > 8 KiB), "
                          "Zipf-like ids; mixed = skewed + exponent / long / integer / "
                          "valueless values, weights and qid")
+    ap.add_argument("--shuffle-parts", type=int, default=1,
+                    help="K > 1: shuffled epochs (InputSplitShuffle's GPU twin: K sub-shards per "
+                         "rank visited in a new order every epoch, one pipeline)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="every rank uses GPU 0 (gloo control plane): rehearses the multi-rank "
                          "GPU branch on a one-GPU box (RCCL refuses two ranks on one device)")
@@ -276,7 +279,10 @@ def main():
             return b["size"], b["bytes"], 0, parser.partition_bytes
     elif use_gpu and args.mode == "cache":
         extra = {"label_column": 0} if args.format == "csv" else {}
-        cache_path = os.path.join(ddir, f"rowblock_r{rank}of{world}.cache")
+        # beside the dataset directory, never inside it (the parser reads every
+        # file of the directory)
+        cache_path = os.path.join(args.data_dir,
+                                  f"rowcache_{os.path.basename(ddir)}_r{rank}of{world}.bin")
         if not os.path.exists(cache_path):
             build = data.GPUParser(ddir, rank, world, format=args.format, chunk_mb=args.chunk_mb,
                                    read_threads=read_threads, device=local_rank,
@@ -299,7 +305,8 @@ def main():
                                 read_threads=read_threads, pinned_slots=args.pinned_slots,
                                 device_slots=args.device_slots, device=local_rank,
                                 zero_copy=args.zero_copy,
-                                hbm_cache=int(args.mode == "hbm"), **extra)
+                                hbm_cache=int(args.mode == "hbm"),
+                                shuffle_parts=args.shuffle_parts, **extra)
         csr = data.DeviceCSR()
 
         def step():
@@ -436,6 +443,7 @@ def main():
             "input_GBps": round(nbytes * args.steps / elapsed / 1e9, 3),
             "mode": args.mode,
             "shape": args.shape,
+            "shuffle_parts": args.shuffle_parts,
             "baseline_value": fmt["baseline"],
         }
         out["per_rank"] = per_rank

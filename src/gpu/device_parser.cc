@@ -721,9 +721,16 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     plan->nlines = sizes.nlines;
     plan->nrows = sizes.nrows;
     plan->nnz = sizes.nnz;
+    // LibSVM `qid:` tokens: the column is needed (LibFM has none: a 'q'
+    // token there is irregular and the chunk goes to the exact kernels)
+    if (tcfg_.format == TextFormat::kLibSVM) plan->flags |= sizes.flags & kFlagQid;
     bool need_weight = false;
     for (;;) {
       FillTarget<IndexType> tgt = PrepareOutput(out, row_base, nnz_base, *plan, need_weight, nbytes);
+      if (tgt.qid != nullptr && plan->nrows != 0) {
+        // rows without a `qid:` token have qid 0; the fill writes the others
+        DMLC_HIP_CHECK(hipMemsetAsync(tgt.qid + row_base, 0, plan->nrows * sizeof(uint64_t), s));
+      }
       LaunchTileFill<IndexType>(text, nbytes, tcfg_.format, tcounts_.get<uint64_t>(), tgt,
                                 slots_.get<MetaPartial>(), dmeta, hm, s);
       PrelaunchCount();

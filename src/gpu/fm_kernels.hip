@@ -62,6 +62,27 @@ __device__ __forceinline__ void fp8x8(uint32_t lo, uint32_t hi, float f[8]) {
   f[7] = d[1];
 }
 
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+/*! \brief two dwords of fp8 e4m3 codes -> 8 bf16 (exact: e4m3 fits bf16),
+ *  gfx950's packed scaled conversion, 4 instructions */
+__device__ __forceinline__ bf16x8 fp8x8_bf16(uint32_t lo, uint32_t hi) {
+  const bf16x2 a = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(static_cast<int>(lo), 1.0f, false);
+  const bf16x2 b = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(static_cast<int>(lo), 1.0f, true);
+  const bf16x2 c = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(static_cast<int>(hi), 1.0f, false);
+  const bf16x2 d = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(static_cast<int>(hi), 1.0f, true);
+  bf16x8 v;
+  v[0] = a[0];
+  v[1] = a[1];
+  v[2] = b[0];
+  v[3] = b[1];
+  v[4] = c[0];
+  v[5] = c[1];
+  v[6] = d[0];
+  v[7] = d[1];
+  return v;
+}
+
 __device__ __forceinline__ bf16x8 to_bf16x8(const float f[8]) {
   bf16x8 v;
 #pragma unroll
@@ -118,7 +139,7 @@ __global__ __launch_bounds__(kFwdThreads) void k_fm_fwd(const uint8_t* __restric
     const bool valid = row < rows;
     const uint8_t* xr = x + (valid ? row : 0) * dim + 64 * h;
     f32x16 acc = {};
-    float x2q = 0.0f;
+    f32x2 x2q2 = {0.0f, 0.0f};
     uint4 cur[4], nxt[4];
     load64(xr, valid, cur);
     for (int kb = 0; kb < nblk; ++kb) {
@@ -126,21 +147,27 @@ __global__ __launch_bounds__(kFwdThreads) void k_fm_fwd(const uint8_t* __restric
       const int kbase = 128 * kb + 64 * h;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
+        const uint32_t lo = word(cur, 2 * i), hi = word(cur, 2 * i + 1);
         float f[8];
-        fp8x8(word(cur, 2 * i), word(cur, 2 * i + 1), f);
+        fp8x8(lo, hi, f);
         const float4 q0 = *reinterpret_cast<const float4*>(s_q + kbase + 8 * i);
         const float4 q1 = *reinterpret_cast<const float4*>(s_q + kbase + 8 * i + 4);
-        x2q += f[0] * f[0] * q0.x + f[1] * f[1] * q0.y + f[2] * f[2] * q0.z + f[3] * f[3] * q0.w +
-               f[4] * f[4] * q1.x + f[5] * f[5] * q1.y + f[6] * f[6] * q1.z + f[7] * f[7] * q1.w;
+        // x^2.q in packed f32 (v_pk_mul / v_pk_fma), two partial sums
+        f32x2 sq[4] = {{f[0], f[1]}, {f[2], f[3]}, {f[4], f[5]}, {f[6], f[7]}};
+        const f32x2 qq[4] = {{q0.x, q0.y}, {q0.z, q0.w}, {q1.x, q1.y}, {q1.z, q1.w}};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x2q2 = __builtin_elementwise_fma(sq[k] * sq[k], qq[k], x2q2);
         const bf16x8 b = col < kFmCols
                              ? *reinterpret_cast<const bf16x8*>(s_wt + col * ldw + kbase + 8 * i)
                              : zero8;
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(to_bf16x8(f), b, acc, 0, 0, 0);
+        // A straight from the fp8 codes (exact), not through f32
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fp8x8_bf16(lo, hi), b, acc, 0, 0, 0);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) cur[i] = nxt[i];
     }
     // lanes r and r + 32 hold the two halves of row r's x^2.q
+    float x2q = x2q2[0] + x2q2[1];
     x2q += __shfl_xor(x2q, 32, kWave);
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {

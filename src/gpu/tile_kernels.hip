@@ -86,6 +86,16 @@ __device__ __forceinline__ void classify16(uint4 v, uint32_t* sep, uint32_t* eol
   *ctl = c;
 }
 
+/*! \brief bytes of v with bit 6 set (letters and the like: no number starts
+ *  so), as a 16-bit mask -- the C1 test of letter-started tokens */
+__device__ __forceinline__ uint32_t letter_mask(uint4 v) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) m |= gather_hi((w[i] << 1) & 0x80808080u) << (4 * i);
+  return m;
+}
+
 __device__ __forceinline__ bool num_start(uint32_t c) {
   return (c >= '0' && c <= '9') || c == '+' || c == '-' || c == '.';
 }
@@ -151,7 +161,7 @@ __device__ __forceinline__ uint32_t prev_byte(const uint8_t* __restrict__ text, 
  */
 template <bool kFull>
 __device__ __forceinline__ bool count16(uint4 v, uint32_t pc, size_t pos, size_t n,
-                                        uint32_t* lines, uint32_t* toks) {
+                                        uint32_t* lines, uint32_t* toks, uint32_t* qtoks) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
   // bytes at or past n are "separators" (no starts there); kFull: the whole
   // tile lies before n (every tile but a chunk's last), no per-word masks
@@ -175,7 +185,12 @@ __device__ __forceinline__ bool count16(uint4 v, uint32_t pc, size_t pos, size_t
     const uint32_t eol_before = (eol << 8) | prev_eol;
     const uint32_t tm = ~sep & sep_before & 0x80808080u;
     const uint32_t lm = ~eol & eol_before & valid & 0x80808080u;
+    // tokens starting with a letter (byte bit 6 set; digits, signs and '.'
+    // have it clear) are no entries of the CSR: LibSVM `qid:` tokens, which
+    // the fill decodes beside its list, or junk that sends the chunk to the
+    // exact kernels.  Bit 6 of each byte, moved to bit 7: x << 1.
     *toks += __popc(tm);
+    *qtoks += __popc(tm & (x << 1));
     *lines += __popc(lm);
     bad |= (lm & ~tm) != 0;  // a line that starts with a blank
     // (token starts outside [0-9+-.] are flagged by the fill / hash kernels:
@@ -213,7 +228,7 @@ __global__ __launch_bounds__(kThreads) void k_tile_count(const uint8_t* __restri
 #pragma unroll
   for (int j = 0; j < kCountLoads; ++j) v[j] = load16(text, base + j * 1024 + lane * 16, n);
   const uint32_t first = base == 0 ? static_cast<uint32_t>('\n') : text[base - 1];
-  uint32_t lines = 0, toks = 0;
+  uint32_t lines = 0, toks = 0, qtoks = 0;
   bool bad = false;
   auto count_tile = [&](auto full) {
 #pragma unroll
@@ -222,7 +237,7 @@ __global__ __launch_bounds__(kThreads) void k_tile_count(const uint8_t* __restri
       const uint32_t wrap = j == 0 ? first : __shfl(v[j - 1].w >> 24, dev::kWave - 1, dev::kWave);
       const uint32_t pc = lane == 0 ? wrap : left;
       bad |= count16<decltype(full)::value>(v[j], pc, base + j * 1024 + lane * 16, n, &lines,
-                                            &toks);
+                                            &toks, &qtoks);
     }
   };
   if (base + kTileBytes <= n) {  // wave-uniform: every tile but a chunk's last
@@ -232,10 +247,12 @@ __global__ __launch_bounds__(kThreads) void k_tile_count(const uint8_t* __restri
   }
   lines = dev::wave_sum(lines);
   toks = dev::wave_sum(toks);
+  qtoks = dev::wave_sum(qtoks);
   const bool any_bad = __any(bad);
   if (lane == 0) {
-    counts[tile] = (static_cast<uint64_t>(lines) << 32) | toks;
-    flags[tile] = any_bad ? kFlagIrregular : 0u;
+    // letter-started tokens (LibSVM `qid:`) are no CSR entries: out of the count
+    counts[tile] = (static_cast<uint64_t>(lines) << 32) | (toks - qtoks);
+    flags[tile] = (any_bad ? kFlagIrregular : 0u) | (qtoks != 0 ? kFlagQid : 0u);
   }
 }
 
@@ -657,6 +674,50 @@ __device__ __noinline__ GenericResult generic_token(const uint8_t* __restrict__ 
 }
 
 /*!
+ * \brief a letter-started token at chunk offset gp: true when it is the
+ *  row's `qid:` token -- the second token of its line (only blanks and one
+ *  token, the label, between the line start and it) spelled `qid:` + integer
+ *  (the CPU parser's grammar, src/data/libsvm_parser.h) -- and *qid its
+ *  value.  Anything else is for the exact kernels.  Rare path: byte loads from
+ *  global memory (L2-resident text).
+ */
+struct QidResult {
+  uint64_t value;
+  bool ok;
+};
+
+__device__ __noinline__ QidResult qid_token(const uint8_t* __restrict__ text, size_t n, size_t gp) {
+  QidResult r{0, false};
+  auto blank = [](uint32_t c) { return c == ' ' || c == '\t'; };
+  auto eol = [](uint32_t c) { return c == '\n' || c == '\r'; };
+  if (gp + 4 > n || text[gp] != 'q' || text[gp + 1] != 'i' || text[gp + 2] != 'd' ||
+      text[gp + 3] != ':') {
+    return r;
+  }
+  // backward: blanks, then the label token, then the line start
+  size_t p = gp;
+  while (p > 0 && blank(text[p - 1])) --p;
+  if (p == 0 || p == gp || eol(text[p - 1])) return r;  // no label before it
+  while (p > 0 && !blank(text[p - 1]) && !eol(text[p - 1])) --p;
+  if (p != 0 && !eol(text[p - 1])) return r;  // another token before the label
+  // the value: StrToInt<int64_t> over the token's bytes after "qid:"
+  size_t q = gp + 4;
+  bool neg = false;
+  if (q < n && (text[q] == '-' || text[q] == '+')) {
+    neg = text[q] == '-';
+    ++q;
+  }
+  uint64_t v = 0;
+  for (int k = 0; k < 20 && q < n && text[q] >= '0' && text[q] <= '9'; ++k, ++q) {
+    v = v * 10 + (text[q] - '0');
+  }
+  if (q < n && !blank(text[q]) && !eol(text[q])) return r;  // junk after the digits
+  r.value = neg ? 0 - v : v;
+  r.ok = true;
+  return r;
+}
+
+/*!
  * \brief C3: wave-autonomous tile fill.  Each wave of the workgroup owns one
  *  8 KiB tile and never synchronises with the others (no __syncthreads):
  *   1. all 8 KiB (+ the 64 bytes after it) are loaded into registers at once;
@@ -807,6 +868,9 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
   uint64_t* const off_at = out.offset + R - 1;
   float* const wgt_at = out.weight != nullptr ? out.weight + R - 1 : nullptr;
   uint64_t* const qid_at = out.qid != nullptr ? out.qid + R - 1 : nullptr;
+  // the count pass saw 'q' token starts in this chunk (the host then enables
+  // the qid column): only such chunks look for `qid:` tokens
+  const bool qid_chunk = F == TextFormat::kLibSVM && out.qid != nullptr;
 
   uint32_t tok0 = 0;   // tile token ordinal of list position 0
   uint32_t lcnt = 0;   // line starts of this tile so far
@@ -854,6 +918,16 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
       (void)lane_masks<false>(a, pc_a, pos_a, n, &lm_a, &tm_a);
       (void)lane_masks<false>(b, pc_b, pos_a + 1024, n, &lm_b, &tm_b);
     }
+    // `qid:` tokens (C1 left them out of the entry counts): taken out of the
+    // list here, decoded by their lane after the scan (wave-uniform test:
+    // only chunks that have them pay)
+    uint32_t qa = 0, qb = 0;
+    if (qid_chunk) {
+      qa = tm_a & letter_mask(a);
+      qb = tm_b & letter_mask(b);
+      tm_a &= ~qa;
+      tm_b &= ~qb;
+    }
     // one 64-bit scan of four 16-bit counts: tokens / lines of both slices
     const uint64_t cnt = static_cast<uint64_t>(__popc(tm_a)) |
                          (static_cast<uint64_t>(__popc(tm_b)) << 16) |
@@ -869,6 +943,26 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
                lcnt + static_cast<uint32_t>((before >> 32) & 0xFFFFu), lane);
     list_slice(sl, tm_b, lm_b, carry + ntok_a + static_cast<uint32_t>((before >> 16) & 0xFFFFu),
                sbase + 1024 + lane * 16, lcnt + nline_a + static_cast<uint32_t>(before >> 48), lane);
+    if (qid_chunk && __any((qa | qb) != 0)) {
+      const uint32_t lbase[2] = {lcnt + static_cast<uint32_t>((before >> 32) & 0xFFFFu),
+                                 lcnt + nline_a + static_cast<uint32_t>(before >> 48)};
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t lmh = h == 0 ? lm_a : lm_b;
+        for (uint32_t m = h == 0 ? qa : qb; m != 0; m &= m - 1) {
+          const uint32_t j = static_cast<uint32_t>(__builtin_ctz(m));
+          // its row: the tile's line starts up to this byte (a line that
+          // starts with 'q' has no label: exact kernels)
+          const uint32_t lc = lbase[h] + static_cast<uint32_t>(__popc(lmh & ((2u << j) - 1u)));
+          const QidResult q = qid_token(text, n, pos_a + static_cast<size_t>(h) * 1024 + j);
+          // (lc 0: the tile's first, unfinished line -- the row before R)
+          const bool ok = q.ok && ((lmh >> j) & 1u) == 0 &&
+                          static_cast<int32_t>(lc) - 1 < row_room && qid_at != nullptr;
+          if (ok) qid_at[lc] = q.value;
+          irregular |= !ok;
+        }
+      }
+    }
     dev::wave_sync();  // the staged text and the list are visible to every lane
 
     // ---- 3. decode 64 listed tokens per round.  Only whole rounds run: the
@@ -890,7 +984,17 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
       t.u0_hi = t.u1_hi = 0;
       t.u1 = 0;
       bool bad = false;
-      const bool ok = tok::decode<F>(st, off, is_label, &t);
+      bool ok = tok::decode<F>(st, off, is_label, &t);
+      // exponents / long fractions: the extended decoder on the lane (only
+      // rounds that have such a token pay for it)
+      if (__any(active & !ok)) {
+        if (active & !ok) {
+          const tok::ExtToken x = tok::decode_ext<F>(
+              st, off, is_label, off >= kSlotBytes ? 2 * kSlotBytes : kSlotBytes);
+          if (x.ok) t = x.t;
+          ok = x.ok;
+        }
+      }
       if (active & !ok) {
         // the step a slot holds: s, or s - 1 for a carried token
         const uint32_t in_slot = off >= kSlotBytes ? 1u : 0u;
@@ -915,7 +1019,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
         lab_at[lc] = t.f0;
         off_at[lc] = C + 1 + (static_cast<int64_t>(i) - static_cast<int64_t>(lc));
         if (wgt_at != nullptr) wgt_at[lc] = t.r == 2 ? t.f1 : 1.0f;
-        if (qid_at != nullptr) qid_at[lc] = 0;  // qid lines take the exact path
+        // (qid: zero-filled by the host, the qid token's lane writes it)
       }
       need_w |= active & is_label & (wgt_at == nullptr) & (t.r == 2);
       any_weight |= active & is_label & (t.r == 2);
@@ -1140,6 +1244,24 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
         (void)lane_masks<false>(a, pc_a, pos_a, n, &lm_a, &tm_a);
         (void)lane_masks<false>(b, pc_b, pos_a + 1024, n, &lm_b, &tm_b);
       }
+      if (F == TextFormat::kLibSVM) {
+        // `qid:` tokens are no features of the batch: dropped (checked; any
+        // other 'q' token sends the chunk to the exact kernels)
+        const uint32_t qa = tm_a & letter_mask(a), qb = tm_b & letter_mask(b);
+        if (__any((qa | qb) != 0)) {
+          tm_a &= ~qa;
+          tm_b &= ~qb;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const uint32_t lmh = h == 0 ? lm_a : lm_b;
+            for (uint32_t m = h == 0 ? qa : qb; m != 0; m &= m - 1) {
+              const uint32_t j = static_cast<uint32_t>(__builtin_ctz(m));
+              irregular |= ((lmh >> j) & 1u) != 0 ||
+                           !qid_token(text, n, pos_a + static_cast<size_t>(h) * 1024 + j).ok;
+            }
+          }
+        }
+      }
       uint64_t cnt = static_cast<uint64_t>(__popc(tm_a)) |
                      (static_cast<uint64_t>(__popc(tm_b)) << 16) |
                      (static_cast<uint64_t>(__popc(lm_a)) << 32) |
@@ -1182,7 +1304,15 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
         t.u0_hi = t.u1_hi = 0;
         t.u1 = 0;
         bool bad = false;
-        const bool ok = tok::decode<F>(st, off, is_label, &t);
+        bool ok = tok::decode<F>(st, off, is_label, &t);
+        if (__any(active & !ok)) {
+          if (active & !ok) {
+            const tok::ExtToken x = tok::decode_ext<F>(
+                st, off, is_label, off >= kSlotBytes ? 2 * kSlotBytes : kSlotBytes);
+            if (x.ok) t = x.t;
+            ok = x.ok;
+          }
+        }
         if (active & !ok) {
           const uint32_t in_slot = off >= kSlotBytes ? 1u : 0u;
           const int step = in_slot == (static_cast<uint32_t>(s) & 1u) ? s : s - 1;

@@ -250,6 +250,181 @@ __device__ __forceinline__ bool decode(const uint4* lds, uint32_t a, bool is_lab
   return is_label ? pair_ok : triple_ok;
 }
 
+/*! \brief the dword starting at byte 4q (q <= 7) of a 32-byte window g0|g1 */
+__device__ __forceinline__ uint32_t win_dw(uint4 g0, uint4 g1, uint32_t q) {
+  return q < 4 ? (q < 2 ? (q == 0 ? g0.x : g0.y) : (q == 2 ? g0.z : g0.w))
+               : (q < 6 ? (q == 4 ? g1.x : g1.y) : (q == 6 ? g1.z : g1.w));
+}
+
+/*! \brief byte i (0..31) of the window (i lane-varying) */
+__device__ __forceinline__ uint32_t win_byte(uint4 g0, uint4 g1, uint32_t i) {
+  return (win_dw(g0, g1, i >> 2) >> (8u * (i & 3u))) & 0xFFu;
+}
+
+/*! \brief the 4 bytes starting at byte i (i <= 28) of the window */
+__device__ __forceinline__ uint32_t win_word(uint4 g0, uint4 g1, uint32_t i) {
+  const uint32_t q = i >> 2;
+  return __builtin_amdgcn_alignbyte(win_dw(g0, g1, q < 7 ? q + 1 : 7u), win_dw(g0, g1, q), i & 3u);
+}
+
+/*!
+ * \brief a float in the full reference grammar (strtonum.h StrToFloatT):
+ *  `[+-] digits [. digits] [(e|E) [+-] digits]`, read from a 32-byte window at
+ *  LDS byte a -- the numbers the 16-byte fast decoder leaves out: exponents
+ *  (`1.5e-3`) and fractions of 8 to 16 digits.  Same arithmetic as the
+ *  reference, so bit-identical: the integer part (<= 7 digits) is exact in
+ *  float; the fraction is float(double(F) / double(10^n)) with F, 10^n exact
+ *  (n <= 16); the exponent scale is built by the reference's loop of rounded
+ *  double products, then one IEEE float multiply or divide.  ok is false for
+ *  anything longer (the generic parser takes it); `limit` bounds the staged
+ *  bytes the number may use.
+ */
+struct ExtNum {
+  float fval;
+  uint32_t end, term;
+  bool ok;
+};
+
+__device__ __forceinline__ ExtNum parse_num_ext(const uint4* lds, uint32_t a, uint32_t limit) {
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+  ExtNum o;
+  const uint4 g0 = ext16(lds, a), g1 = ext16(lds, a + 16);
+  const uint32_t c0 = g0.x & 0xFFu;
+  const bool neg = c0 == '-';
+  const uint32_t s = (neg || c0 == '+') ? 1u : 0u;
+  // integer digits (<= 7 for an exact float; 8 or more: generic)
+  uint32_t v0, v1;
+  const uint32_t k0 = lead_digits(win_word(g0, g1, s), &v0);
+  const uint32_t k1 = lead_digits(win_word(g0, g1, s + 4), &v1);
+  const uint32_t k = k0 == 4 ? 4u + k1 : k0;
+  const uint32_t iv = k0 == 4 ? v0 * pow10_u(k1) + v1 : v0;
+  uint32_t pos = s + k;
+  const bool dot = win_byte(g0, g1, pos) == '.';
+  // fraction digits, four 4-byte groups (<= 16 digits)
+  uint64_t fv = 0, pw = 1;
+  uint32_t nf = 0;
+  if (dot) {
+    const uint32_t fs = pos + 1;
+    bool more = true;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      uint32_t v;
+      const uint32_t kk = lead_digits(win_word(g0, g1, fs + 4 * j), &v);
+      if (more) {
+        const uint64_t m = pow10_u(kk);
+        fv = fv * m + v;
+        pw *= m;
+        nf += kk;
+        more = kk == 4;
+      }
+    }
+    pos = fs + nf;
+  }
+  // exponent: (e|E) [+-] digits (<= 4)
+  const uint32_t ce = win_byte(g0, g1, pos);
+  const bool has_e = ce == 'e' || ce == 'E';
+  bool eneg = false;
+  uint32_t ex = 0, ne = 0;
+  if (has_e) {
+    const uint32_t cs = win_byte(g0, g1, pos + 1);
+    eneg = cs == '-';
+    const uint32_t es = pos + 1 + ((cs == '-' || cs == '+') ? 1u : 0u);
+    uint32_t v;
+    ne = lead_digits(win_word(g0, g1, es < 28 ? es : 28u), &v);
+    ex = v;
+    pos = es + ne;
+  }
+  o.term = win_byte(g0, g1, pos < 31 ? pos : 31u);
+  o.end = a + pos;
+  o.ok = k <= 7 && (k | nf) != 0 && nf < 16 && ne < 4 && pos < 28 && a + pos < limit;
+  // the reference arithmetic (strtonum.h StrToFloatT)
+  float value = static_cast<float>(iv);
+  if (dot) value += static_cast<float>(static_cast<double>(fv) / static_cast<double>(pw));
+  if (has_e) {
+    float scale = 1.0f;
+    uint32_t e = ex > 38 ? 38u : ex;
+    while (e >= 8) {
+      scale = static_cast<float>(static_cast<double>(scale) * 1e8);
+      e -= 8;
+    }
+    while (e > 0) {
+      scale = static_cast<float>(static_cast<double>(scale) * 10.0);
+      e -= 1;
+    }
+    value = eneg ? (value / scale) : (value * scale);
+  }
+  o.fval = neg ? -value : value;
+  return o;
+}
+
+/*!
+ * \brief decode() for the tokens it declined, with parse_num_ext for every
+ *  float field (labels, weights, values): exponents and long fractions stay
+ *  on the lane instead of the generic global-memory parser.  Integer fields
+ *  are parse_int's as in decode().  limit: end of the token's staging slot.
+ */
+struct ExtToken {
+  Token t;
+  bool ok;
+};
+
+template <TextFormat F>
+__device__ __forceinline__ bool decode_ext_into(const uint4* lds, uint32_t a, bool is_label,
+                                                uint32_t limit, Token* t) {
+  if (is_label) {
+    const ExtNum n1 = parse_num_ext(lds, a, limit);
+    const bool c1 = n1.term == ':';
+    ExtNum n2 = n1;
+    if (c1) n2 = parse_num_ext(lds, n1.end + 1, limit);
+    t->f0 = n1.fval;
+    t->f1 = n2.fval;
+    t->r = c1 ? 2 : 1;
+    return n1.ok && (c1 ? (n2.ok && is_end(n2.term)) : is_end(n1.term));
+  }
+  const Num n1 = parse_int(lds, a);
+  const bool c1 = n1.term == ':';
+  t->u0 = n1.ival;
+  if (F == TextFormat::kLibSVM) {
+    if (!c1) {
+      t->r = 1;
+      t->f0 = 1.0f;
+      return n1.ok_uint && is_end(n1.term);
+    }
+    const ExtNum v = parse_num_ext(lds, n1.end + 1, limit);
+    t->f0 = v.fval;
+    t->r = 2;
+    return n1.ok_uint && v.ok && is_end(v.term);
+  }
+  // LibFM field:index[:value]
+  const Num n2 = parse_int(lds, n1.end + 1);
+  const bool c2 = n2.term == ':';
+  t->u1 = n2.ival;
+  if (!c2) {
+    t->r = 2;
+    t->f0 = 1.0f;
+    return c1 && n1.ok_uint && n2.ok_uint && is_end(n2.term);
+  }
+  const ExtNum v = parse_num_ext(lds, n2.end + 1, limit);
+  t->f0 = v.fval;
+  t->r = 3;
+  return c1 && n1.ok_uint && n2.ok_uint && v.ok && is_end(v.term);
+}
+
+/*! \brief out of line and by value (a result pointer into the caller's
+ *  frame would put the token on the stack) */
+template <TextFormat F>
+__device__ __noinline__ ExtToken decode_ext(const uint4* lds, uint32_t a, bool is_label,
+                                            uint32_t limit) {
+  ExtToken r;
+  r.t.u0 = r.t.u1 = r.t.u0_hi = r.t.u1_hi = 0;
+  r.t.f0 = r.t.f1 = 0.0f;
+  r.t.r = 0;
+  r.ok = decode_ext_into<F>(lds, a, is_label, limit, &r.t);
+  return r;
+}
+
 }  // namespace tok
 }  // namespace gpu
 }  // namespace dmlc

@@ -135,6 +135,7 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
   const uint64_t w0 = blk0 + static_cast<uint64_t>(w) * kWaveElems;
   const uint64_t w1 = w0 + kWaveElems < nnz ? w0 + kWaveElems : nnz;
   // ---- count this wave's quarter per bucket
+#pragma unroll 8
   for (uint64_t e = w0 + lane; e < w1; e += dev::kWave) {
     atomicAdd(&cnt[w][column(index[e], num_features) >> kLowBits], 1u);
   }
@@ -153,15 +154,45 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
   if (w0 >= w1) return;  // an empty quarter (the last block): nothing below synchronises
   // ---- scatter in order, 64 entries per group
   uint32_t r = row_of(offset, nrows, base, w0);  // row of the quarter's first entry
+  auto load = [&](uint64_t e, uint32_t* col, float* v) {
+    const bool ok = e < w1;
+    *col = ok ? column(index[e], num_features) : 0u;
+    *v = (ok && value != nullptr) ? value[e] : 0.0f;
+  };
+  uint32_t ncol;
+  float nv;
+  load(w0 + lane, &ncol, &nv);
   for (uint64_t g = w0; g < w1; g += dev::kWave) {
     const uint64_t e = g + lane;
     const bool valid = e < w1;
-    const uint32_t col = valid ? column(index[e], num_features) : 0u;
-    const float v = (valid && value != nullptr) ? value[e] : 0.0f;
-    // row: forward from the group's first row (a few row ends per group)
-    uint32_t row = r;
-    if (valid) {
-      while (offset[row + 1] - base <= e) ++row;
+    const uint32_t col = ncol;
+    const float v = nv;
+    load(e + dev::kWave, &ncol, &nv);  // next group's loads in flight
+    // row: the ends of rows r .. r + 63 come in with one coalesced load (lane
+    // i holds row r + i's end, relative to the group start); an entry's row
+    // is r + the number of those ends at or before it -- a binary search over
+    // the lanes.  More than 64 row ends inside one group (empty rows) take
+    // another window.
+    const uint32_t pos = lane;  // this entry's position in the group
+    uint32_t row = 0;
+    bool found = !valid;
+    for (uint32_t rr = r;; rr += dev::kWave) {
+      const size_t ri = static_cast<size_t>(rr) + 1 + lane;
+      const uint64_t end = ri <= nrows ? offset[ri] - base : ~0ull;
+      const uint32_t rel = end - g >= 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(end - g);
+      uint32_t cnt = 0;  // lanes [0, cnt) have rel <= pos
+#pragma unroll
+      for (uint32_t step = 32; step >= 1; step >>= 1) {
+        const uint32_t probe = __shfl(rel, static_cast<int>(cnt + step - 1), dev::kWave);
+        if (probe <= pos) cnt += step;
+      }
+      const uint32_t last = __shfl(rel, dev::kWave - 1, dev::kWave);
+      if (cnt == dev::kWave - 1 && last <= pos) cnt = dev::kWave;
+      if (!found && cnt < static_cast<uint32_t>(dev::kWave)) {
+        row = rr + cnt;
+        found = true;
+      }
+      if (__all(found)) break;
     }
     const uint32_t bk = col >> kLowBits;
     const uint64_t m = match_lanes(bk, bucket_bits, valid);
@@ -201,6 +232,7 @@ __global__ __launch_bounds__(dev::kWave) void k_lowkey_hist(const uint16_t* __re
   dev::wave_sync();
   uint64_t e0, e1;
   segment(bstart, b, s, &e0, &e1);
+#pragma unroll 8
   for (uint64_t e = e0 + lane; e < e1; e += dev::kWave) atomicAdd(&hist[t_key[e]], 1u);
   dev::wave_sync();
   uint32_t* out = H + static_cast<size_t>(blockIdx.x) * kLow;
@@ -265,12 +297,22 @@ __global__ __launch_bounds__(dev::kWave) void k_lowkey_scatter(
   uint64_t e0, e1;
   segment(bstart, b, s, &e0, &e1);
   const uint64_t base = bstart[b];
+  // the next group's loads are in flight while this group is ranked / stored
+  auto load = [&](uint64_t e, uint32_t* k, uint32_t* row, float* v) {
+    const bool ok = e < e1;
+    *k = ok ? t_key[e] : 0u;
+    *row = ok ? t_row[e] : 0u;
+    *v = (ok && val_out != nullptr) ? t_val[e] : 0.0f;
+  };
+  uint32_t nk, nrow;
+  float nv;
+  load(e0 + lane, &nk, &nrow, &nv);
   for (uint64_t g = e0; g < e1; g += dev::kWave) {
     const uint64_t e = g + lane;
     const bool valid = e < e1;
-    const uint32_t k = valid ? t_key[e] : 0u;
-    const uint32_t row = valid ? t_row[e] : 0u;
-    const float v = (valid && val_out != nullptr) ? t_val[e] : 0.0f;
+    const uint32_t k = nk, row = nrow;
+    const float v = nv;
+    load(e + dev::kWave, &nk, &nrow, &nv);
     const uint64_t m = match_lanes(k, kLowBits, valid);
     const uint32_t rank = static_cast<uint32_t>(__popcll(m & lanes_below()));
     const uint32_t n = static_cast<uint32_t>(__popcll(m));

@@ -319,7 +319,7 @@ def test_hbm_replay_prelaunched_counts(tmp_path, replay_mb):
         data.write_synthetic(str(d / f"p{i}.libsvm"), i * 1500, (i + 1) * 1500, seed=37,
                              weight_every=5 if i == 2 else 0)
     with open(d / "p1.libsvm", "a") as f:
-        f.write("1 qid:3 4:1\n")
+        f.write("1 junk 4:1\n")  # a token the tile path leaves to the exact kernels
     c = cpu_rows(str(d), "libsvm")
     gp = data.GPUParser(str(d), chunk_bytes=32 * 1024, hbm_cache=1, replay_chunk_mb=replay_mb)
     csr = data.DeviceCSR()
@@ -544,4 +544,59 @@ def test_shuffled_gpu_parser_resume_mid_epoch(tmp_path):
         tail.append(sp2.value_to_host())
     assert_same(pyref.concat_blocks(head + tail), want)
     g = data.GPUParser(p + f"?shuffle_parts={k}&shuffle_seed={seed}", chunk_bytes=32 * 1024)
-    assert_same(g.parse_all().to_host(), cpu_rows_parts(p, g._p.visit_order(), k))
+    assert_same(pyref.concat_blocks([g.parse_all().to_host()]),
+                cpu_rows_parts(p, g._p.visit_order(), k))
+
+
+@pytest.mark.parametrize("fmt", ["libsvm", "libfm"])
+@pytest.mark.parametrize("shape", ["skewed", "mixed"])
+def test_realistic_shapes_stay_on_the_tile_path(tmp_path, fmt, shape):
+    """power-law lines (some > 8 KiB), exponent / 9-12-digit / integer /
+    valueless values, weights and LibSVM `qid:` tokens: the tile fast path
+    takes every chunk (qid tokens are decoded beside the token list; odd
+    numbers by the generic strtonum path on their lane) and equals the CPU
+    parser bit for bit"""
+    p = str(tmp_path / f"m.{fmt}")
+    data.write_synthetic(p, 0, 30000, format=fmt, seed=13, shape=shape)
+    g = data.GPUParser(p, format=fmt, chunk_bytes=256 * 1024)
+    got = pyref.concat_blocks([g.parse_all().to_host()])
+    assert g.stats()["exact_chunks"] == 0
+    assert_same(got, cpu_rows(p, fmt), field=fmt == "libfm")
+
+
+def test_qid_tokens_on_the_tile_path(tmp_path):
+    """qid on every line (LETOR style), on some lines, negative and huge
+    values, and tokens that only look like qid (not the second token, junk
+    after the digits, a line starting with q): valid ones stay on the tile
+    path, the rest send their chunk to the exact kernels; all equal the CPU"""
+    p = str(tmp_path / "q.libsvm")
+    data.write_synthetic(p, 0, 3000, format="libsvm", seed=2, qid=True, weight_every=3)
+    g = data.GPUParser(p, chunk_bytes=64 * 1024)
+    assert_same(pyref.concat_blocks([g.parse_all().to_host()]), cpu_rows(p, "libsvm"))
+    assert g.stats()["exact_chunks"] == 0
+    odd = str(tmp_path / "o.libsvm")
+    with open(odd, "w") as f:
+        f.write("1 qid:-5 3:1\n0 qid:18446744073709551615 4:2\n1 qid:7 qid:8 5:1\n")
+        f.write("0 2:1 qid:9\n1 qid:3x 6:1\nqid:4 1 2:2\n1 qid: 7:1\n")
+    gg = data.GPUParser(odd)
+    assert_same(pyref.concat_blocks([gg.parse_all().to_host()]), cpu_rows(odd, "libsvm"))
+
+
+def test_extended_number_decoder_edge_values(tmp_path):
+    """the lane decoder for exponents and long fractions (token_decode.h
+    parse_num_ext) against the CPU strtonum grammar: exponent clamp at 38,
+    upper-case E, explicit signs, denormal results, empty exponents, 8-16
+    fraction digits, and shapes it declines (8+ integer digits, 16+ fraction
+    digits) that the generic path takes"""
+    vals = ["1e38", "1e39", "1.5E+2", "-2.5e-40", "3e0", ".5e1", "5.e2", "1e", "2e+", "7e-",
+            "0.1234567890123", "0.123456789012345", "0.1234567890123456", "12345678.5",
+            "1234567.25e-3", "9.999999e-1", "+4.25e1", "-0.0e5", "6e07", "1.1e-45", "3.4e38"]
+    p = str(tmp_path / "e.libsvm")
+    with open(p, "w") as f:
+        for r in range(400):
+            v = vals[r % len(vals)]
+            lab = vals[(r * 7) % len(vals)] if r % 3 == 0 else str(r % 2)
+            f.write(f"{lab} {r % 50}:{v} {100 + r}:{vals[(r + 5) % len(vals)]} 7\n")
+    g = data.GPUParser(p, chunk_bytes=4096)
+    assert_same(pyref.concat_blocks([g.parse_all().to_host()]), cpu_rows(p, "libsvm"))
+    assert g.stats()["exact_chunks"] == 0
