@@ -281,6 +281,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
           if (b == cursor) {
             replay_ = true;
             replay_idx_ = i;
+            merge_cap_ = 0;
             cursor_ = cursor;
             return;
           }
@@ -476,11 +477,16 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
         // this epoch's order are parsed as one larger chunk (fewer launches
         // and host round trips per byte)
         // (a chunk whose text ends without EOL -- a file's unterminated last
-        // line on the zero-copy path -- must stay its own chunk)
+        // line on the zero-copy path -- must stay its own chunk).  The merged
+        // size grows 4x per chunk from kFirstMerge: the first chunk's count +
+        // scan is the only one not hidden behind a previous chunk's fill
+        // (the next count runs on count_stream_ meanwhile, ~1/4 of a fill)
+        merge_cap_ = merge_cap_ == 0 ? kFirstMerge : merge_cap_ * 4;
+        const size_t cap = std::min(merge_cap_, cfg_.replay_chunk_bytes);
         while (merge_replay_ && replay_idx_ < replay_list_.size() &&
                cached_[replay_list_[replay_idx_ - 1]].eol_end &&
                cached_[replay_list_[replay_idx_]].off == c.off + size &&
-               size + cached_[replay_list_[replay_idx_]].size <= cfg_.replay_chunk_bytes) {
+               size + cached_[replay_list_[replay_idx_]].size <= cap) {
           size += cached_[replay_list_[replay_idx_]].size;
           end_pos = replay_end_[replay_idx_];
           ++replay_idx_;
@@ -1069,6 +1075,9 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   /*! \brief HBM epoch cache (cfg_.hbm_cache): the partition's chunks, resident */
   std::unique_ptr<DeviceBuffer> arena_;
   size_t arena_bytes_{0}, arena_fill_{0}, replay_idx_{0};
+  /*! \brief merged replay chunk cap of the pass (0: the next is the first) */
+  size_t merge_cap_{0};
+  static constexpr size_t kFirstMerge = size_t(64) << 20;
   std::vector<CachedChunk> cached_;
   bool caching_{false}, cache_complete_{false}, replay_{false}, merge_replay_{false};
   HostSlot* cur_slot_{nullptr};

@@ -14,13 +14,16 @@
  *      order): LDS histogram of buckets -> G[bucket][block].
  *   T2 exclusive scan of G (bucket-major): where each (bucket, block) run
  *      lands in the bucket-ordered intermediate arrays.
- *   T3 k_bucket_scatter  same blocks; each wave owns a contiguous quarter of
- *      the block, counts it per bucket, and scatters it in order: ranks among
- *      equal buckets of a 64-entry group come from ballots over the bucket
- *      bits (no atomics, so the scatter is stable); the row id of every entry
- *      is walked forward from its group's first row.  Writes (low key u16,
- *      row u32, value f32) -- runs of ~block/buckets entries, coalesced.
- *   T4a k_lowkey_hist  one wave per (bucket, segment) of the bucket: LDS
+ *   T3 k_bucket_scatter  same blocks, in sub-tiles of kSubElems entries: the
+ *      sub-tile is counted per bucket, scanned in (bucket, position) order and
+ *      ranked into LDS -- ranks among equal buckets of a 64-entry group come
+ *      from ballots over the bucket bits (no atomics, so the sort is stable);
+ *      row ids come from a per-chunk row table (k_chunk_rows) and a lane
+ *      binary search over 64 row ends -- then leaves in bucket runs, so one
+ *      store instruction touches a few lines / pages instead of 64 (the
+ *      direct scatter was bound by partial lines and TLB misses: 16 ms at
+ *      400 M entries).  Writes (low key u16, row u32, value f32).
+ *   T4a k_lowkey_hist  one workgroup per (bucket, segment) of the bucket: LDS
  *      histogram of the L low keys -> H[bucket][segment][L].
  *   T4b k_lowkey_scan  one workgroup per bucket: column totals over segments,
  *      exclusive scan over the bucket's columns -> col_ptr, and per-segment
@@ -48,7 +51,9 @@ constexpr int kLowBits = 12;
 constexpr uint32_t kLow = 1u << kLowBits;  // columns per bucket
 constexpr uint32_t kMaxBuckets = 1024;
 constexpr size_t kBlockElems = 32768;      // T1 / T3 block (per workgroup)
-constexpr size_t kWaveElems = kBlockElems / kWaves;
+constexpr uint32_t kSubElems = 4096;        // T3 sub-tile, sorted in LDS
+constexpr uint32_t kChunk = kSubElems / kWaves;  // entries per wave per sub-tile
+constexpr int kPerLane = kChunk / dev::kWave;
 constexpr int kSegments = 16;              // T4 segments per bucket
 
 /*! \brief a feature id as a column below num_features (out-of-range ids are
@@ -115,100 +120,156 @@ __global__ __launch_bounds__(kThreads) void k_bucket_hist(const IndexType* __res
   }
 }
 
+/*! \brief row of the first entry of every kChunk-entry chunk (T3 waves start
+ *  at any chunk without a dependent binary search of their own) */
+__global__ void k_chunk_rows(const uint64_t* __restrict__ offset, size_t nrows, uint64_t base,
+                             uint64_t nnz, uint32_t* __restrict__ chunk_row) {
+  const uint64_t c = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (c * kChunk < nnz) chunk_row[c] = row_of(offset, nrows, base, c * kChunk);
+}
+
 template <typename IndexType>
 __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
     const uint64_t* __restrict__ offset, size_t nrows, uint64_t base,
     const IndexType* __restrict__ index, const float* __restrict__ value, uint64_t nnz,
     uint64_t num_features, uint32_t nbuckets, int bucket_bits, const uint64_t* __restrict__ G,
-    size_t nblocks,
+    size_t nblocks, const uint32_t* __restrict__ chunk_row,
     uint16_t* __restrict__ t_key, uint32_t* __restrict__ t_row, float* __restrict__ t_val) {
-  __shared__ uint32_t cnt[kWaves][kMaxBuckets];  // per-wave counts, then per-wave cursors (low 32 bits)
-  __shared__ uint64_t bpos[kMaxBuckets];
+  // the sub-tile, sorted by (bucket, position) in LDS before it leaves
+  __shared__ uint32_t s_col[kSubElems];
+  __shared__ uint32_t s_row[kSubElems];
+  __shared__ float s_val[kSubElems];
+  __shared__ uint32_t cnt[kWaves][kMaxBuckets];  // per-wave counts, then LDS cursors
+  __shared__ uint32_t lstart[kMaxBuckets + 1];   // bucket starts inside the sub-tile
+  __shared__ uint64_t gcur[kMaxBuckets];         // the block's next position per bucket
+  __shared__ uint32_t swave[kWaves];
   const int w = threadIdx.x / dev::kWave;
   const int lane = dev::lane_id();
   for (uint32_t b = threadIdx.x; b < nbuckets; b += kThreads) {
     for (int q = 0; q < kWaves; ++q) cnt[q][b] = 0;
-    bpos[b] = G[static_cast<size_t>(b) * nblocks + blockIdx.x];
+    gcur[b] = G[static_cast<size_t>(b) * nblocks + blockIdx.x];
   }
   __syncthreads();
   const uint64_t blk0 = static_cast<uint64_t>(blockIdx.x) * kBlockElems;
-  const uint64_t w0 = blk0 + static_cast<uint64_t>(w) * kWaveElems;
-  const uint64_t w1 = w0 + kWaveElems < nnz ? w0 + kWaveElems : nnz;
-  // ---- count this wave's quarter per bucket
-#pragma unroll 8
-  for (uint64_t e = w0 + lane; e < w1; e += dev::kWave) {
-    atomicAdd(&cnt[w][column(index[e], num_features) >> kLowBits], 1u);
-  }
-  __syncthreads();
-  // ---- per-wave starting cursor of each bucket (offset from the block's
-  // position of the bucket): the counts of the earlier waves
-  for (uint32_t b = threadIdx.x; b < nbuckets; b += kThreads) {
-    uint64_t acc = bpos[b];
-    for (int q = 0; q < kWaves; ++q) {
-      const uint32_t c = cnt[q][b];
-      cnt[q][b] = static_cast<uint32_t>(acc - bpos[b]);  // offset from the block position
-      acc += c;
-    }
-  }
-  __syncthreads();
-  if (w0 >= w1) return;  // an empty quarter (the last block): nothing below synchronises
-  // ---- scatter in order, 64 entries per group
-  uint32_t r = row_of(offset, nrows, base, w0);  // row of the quarter's first entry
-  auto load = [&](uint64_t e, uint32_t* col, float* v) {
-    const bool ok = e < w1;
-    *col = ok ? column(index[e], num_features) : 0u;
-    *v = (ok && value != nullptr) ? value[e] : 0.0f;
-  };
-  uint32_t ncol;
-  float nv;
-  load(w0 + lane, &ncol, &nv);
-  for (uint64_t g = w0; g < w1; g += dev::kWave) {
-    const uint64_t e = g + lane;
-    const bool valid = e < w1;
-    const uint32_t col = ncol;
-    const float v = nv;
-    load(e + dev::kWave, &ncol, &nv);  // next group's loads in flight
-    // row: the ends of rows r .. r + 63 come in with one coalesced load (lane
-    // i holds row r + i's end, relative to the group start); an entry's row
-    // is r + the number of those ends at or before it -- a binary search over
-    // the lanes.  More than 64 row ends inside one group (empty rows) take
-    // another window.
-    const uint32_t pos = lane;  // this entry's position in the group
-    uint32_t row = 0;
-    bool found = !valid;
-    for (uint32_t rr = r;; rr += dev::kWave) {
-      const size_t ri = static_cast<size_t>(rr) + 1 + lane;
-      const uint64_t end = ri <= nrows ? offset[ri] - base : ~0ull;
-      const uint32_t rel = end - g >= 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(end - g);
-      uint32_t cnt = 0;  // lanes [0, cnt) have rel <= pos
+  const uint64_t blk1 = blk0 + kBlockElems < nnz ? blk0 + kBlockElems : nnz;
+  for (uint64_t s0 = blk0; s0 < blk1; s0 += kSubElems) {
+    const uint32_t nsub = static_cast<uint32_t>(blk1 - s0 < kSubElems ? blk1 - s0 : kSubElems);
+    // ---- this wave's chunk: kPerLane coalesced groups, all loads in flight
+    const uint64_t c0 = s0 + static_cast<uint64_t>(w) * kChunk;
+    const uint64_t c1 = c0 + kChunk < blk1 ? c0 + kChunk : blk1;
+    uint32_t col[kPerLane];
+    float v[kPerLane];
 #pragma unroll
-      for (uint32_t step = 32; step >= 1; step >>= 1) {
-        const uint32_t probe = __shfl(rel, static_cast<int>(cnt + step - 1), dev::kWave);
-        if (probe <= pos) cnt += step;
-      }
-      const uint32_t last = __shfl(rel, dev::kWave - 1, dev::kWave);
-      if (cnt == dev::kWave - 1 && last <= pos) cnt = dev::kWave;
-      if (!found && cnt < static_cast<uint32_t>(dev::kWave)) {
-        row = rr + cnt;
-        found = true;
-      }
-      if (__all(found)) break;
+    for (int i = 0; i < kPerLane; ++i) {
+      const uint64_t e = c0 + static_cast<uint64_t>(i) * dev::kWave + lane;
+      col[i] = e < c1 ? column(index[e], num_features) : 0u;
+      v[i] = (e < c1 && value != nullptr) ? value[e] : 0.0f;
     }
-    const uint32_t bk = col >> kLowBits;
-    const uint64_t m = match_lanes(bk, bucket_bits, valid);
-    const uint32_t rank = static_cast<uint32_t>(__popcll(m & lanes_below()));
-    const uint32_t n = static_cast<uint32_t>(__popcll(m));
-    const uint32_t before = valid ? cnt[w][bk] : 0u;
-    dev::wave_sync();  // every lane has read its cursor
-    if (valid) {
-      const uint64_t pos = bpos[bk] + before + rank;
-      t_key[pos] = static_cast<uint16_t>(col & (kLow - 1u));
-      t_row[pos] = row;
-      if (value != nullptr) t_val[pos] = v;
-      if (rank + 1 == n) cnt[w][bk] = before + n;  // the group's last lane of this bucket
+#pragma unroll
+    for (int i = 0; i < kPerLane; ++i) {
+      if (c0 + static_cast<uint64_t>(i) * dev::kWave + lane < c1) {
+        atomicAdd(&cnt[w][col[i] >> kLowBits], 1u);
+      }
     }
-    dev::wave_sync();
-    r = __shfl(row, dev::kWave - 1, dev::kWave);  // last lane's row (invalid lanes keep r)
+    __syncthreads();
+    // ---- exclusive scan in (bucket, wave) order: thread t owns 4 buckets
+    {
+      constexpr uint32_t kOwn = kMaxBuckets / kThreads;
+      const uint32_t b0 = threadIdx.x * kOwn;
+      uint32_t sum = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < kOwn; ++i) {
+        if (b0 + i < nbuckets) {
+          for (int q = 0; q < kWaves; ++q) sum += cnt[q][b0 + i];
+        }
+      }
+      uint32_t wtot;
+      const uint32_t wx = dev::wave_excl_scan(sum, &wtot);
+      if (lane == 0) swave[w] = wtot;
+      __syncthreads();
+      uint32_t x = wx;
+      for (int q = 0; q < w; ++q) x += swave[q];
+#pragma unroll
+      for (uint32_t i = 0; i < kOwn; ++i) {
+        const uint32_t b = b0 + i;
+        if (b < nbuckets) {
+          lstart[b] = x;
+          for (int q = 0; q < kWaves; ++q) {
+            const uint32_t c = cnt[q][b];
+            cnt[q][b] = x;
+            x += c;
+          }
+        }
+      }
+      if (threadIdx.x == 0) lstart[nbuckets] = nsub;
+    }
+    __syncthreads();
+    // ---- rank every group into the LDS sub-tile; rows from the chunk's first
+    // row: the ends of rows r .. r + 63 come in with one coalesced load, and an
+    // entry's row is r + the number of those ends at or before it (a binary
+    // search over the lanes); more than 64 row ends inside one group (empty
+    // rows) take another window
+    uint32_t r = c0 < c1 ? chunk_row[c0 / kChunk] : 0u;
+#pragma unroll
+    for (int i = 0; i < kPerLane; ++i) {
+      const uint64_t g = c0 + static_cast<uint64_t>(i) * dev::kWave;
+      const bool valid = g + lane < c1;
+      if (!__any(valid)) continue;  // the tail of the last chunk
+      const uint32_t pos = lane;
+      uint32_t row = r;
+      bool found = !valid;
+      for (uint32_t rr = r;; rr += dev::kWave) {
+        const size_t ri = static_cast<size_t>(rr) + 1 + lane;
+        const uint64_t end = ri <= nrows ? offset[ri] - base : ~0ull;
+        const uint32_t rel =
+            end - g >= 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(end - g);
+        uint32_t n = 0;  // lanes [0, n) have rel <= pos
+#pragma unroll
+        for (uint32_t step = 32; step >= 1; step >>= 1) {
+          const uint32_t probe = __shfl(rel, static_cast<int>(n + step - 1), dev::kWave);
+          if (probe <= pos) n += step;
+        }
+        const uint32_t last = __shfl(rel, dev::kWave - 1, dev::kWave);
+        if (n == dev::kWave - 1 && last <= pos) n = dev::kWave;
+        if (!found && n < static_cast<uint32_t>(dev::kWave)) {
+          row = rr + n;
+          found = true;
+        }
+        if (__all(found)) break;
+      }
+      const uint32_t bk = col[i] >> kLowBits;
+      const uint64_t m = match_lanes(bk, bucket_bits, valid);
+      const uint32_t rank = static_cast<uint32_t>(__popcll(m & lanes_below()));
+      const uint32_t n = static_cast<uint32_t>(__popcll(m));
+      const uint32_t before = valid ? cnt[w][bk] : 0u;
+      dev::wave_sync();  // every lane has read its cursor
+      if (valid) {
+        const uint32_t slot = before + rank;
+        s_col[slot] = col[i];
+        s_row[slot] = row;
+        s_val[slot] = v[i];
+        if (rank + 1 == n) cnt[w][bk] = before + n;  // the group's last lane of this bucket
+      }
+      dev::wave_sync();
+      r = __shfl(row, dev::kWave - 1, dev::kWave);  // last lane's row (invalid lanes keep r)
+    }
+    __syncthreads();
+    // ---- the sorted sub-tile leaves in runs: consecutive threads, consecutive
+    // positions of one bucket's run
+    for (uint32_t j = threadIdx.x; j < nsub; j += kThreads) {
+      const uint32_t c = s_col[j];
+      const uint32_t b = c >> kLowBits;
+      const uint64_t p = gcur[b] + (j - lstart[b]);
+      t_key[p] = static_cast<uint16_t>(c & (kLow - 1u));
+      t_row[p] = s_row[j];
+      if (value != nullptr) t_val[p] = s_val[j];
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nbuckets; b += kThreads) {
+      gcur[b] += lstart[b + 1] - lstart[b];
+      for (int q = 0; q < kWaves; ++q) cnt[q][b] = 0;
+    }
+    __syncthreads();
   }
 }
 
@@ -221,22 +282,22 @@ __device__ __forceinline__ void segment(const uint64_t* __restrict__ bstart, uin
   *end = b0 + n * static_cast<uint64_t>(s + 1) / kSegments;
 }
 
-__global__ __launch_bounds__(dev::kWave) void k_lowkey_hist(const uint16_t* __restrict__ t_key,
-                                                            const uint64_t* __restrict__ bstart,
-                                                            uint32_t* __restrict__ H) {
+__global__ __launch_bounds__(kThreads) void k_lowkey_hist(const uint16_t* __restrict__ t_key,
+                                                          const uint64_t* __restrict__ bstart,
+                                                          uint32_t* __restrict__ H) {
+  // counts need no order: the whole workgroup shares one histogram
   __shared__ uint32_t hist[kLow];
   const uint32_t b = blockIdx.x / kSegments;
   const int s = static_cast<int>(blockIdx.x % kSegments);
-  const int lane = dev::lane_id();
-  for (uint32_t c = lane; c < kLow; c += dev::kWave) hist[c] = 0;
-  dev::wave_sync();
+  for (uint32_t c = threadIdx.x; c < kLow; c += kThreads) hist[c] = 0;
+  __syncthreads();
   uint64_t e0, e1;
   segment(bstart, b, s, &e0, &e1);
 #pragma unroll 8
-  for (uint64_t e = e0 + lane; e < e1; e += dev::kWave) atomicAdd(&hist[t_key[e]], 1u);
-  dev::wave_sync();
+  for (uint64_t e = e0 + threadIdx.x; e < e1; e += kThreads) atomicAdd(&hist[t_key[e]], 1u);
+  __syncthreads();
   uint32_t* out = H + static_cast<size_t>(blockIdx.x) * kLow;
-  for (uint32_t c = lane; c < kLow; c += dev::kWave) out[c] = hist[c];
+  for (uint32_t c = threadIdx.x; c < kLow; c += kThreads) out[c] = hist[c];
 }
 
 /*! \brief per bucket: column totals over segments -> col_ptr; per-segment cursors in H */
@@ -339,8 +400,8 @@ struct TransposePlan {
   uint32_t nbuckets;
   int bucket_bits;
   size_t nblocks;
-  size_t g_words, partials_words, h_words;
-  size_t key_off, row_off, val_off, g_off, partials_off, h_off, total;
+  size_t g_words, partials_words, h_words, nchunks;
+  size_t key_off, row_off, val_off, g_off, partials_off, h_off, chunk_off, total;
 };
 
 TransposePlan Plan(uint64_t nnz, uint64_t num_features) {
@@ -354,6 +415,7 @@ TransposePlan Plan(uint64_t nnz, uint64_t num_features) {
   p.g_words = static_cast<size_t>(p.nbuckets) * p.nblocks + 1;  // + the bucket-end sentinel
   p.partials_words = ScanPartials(p.g_words) + 2;
   p.h_words = static_cast<size_t>(p.nbuckets) * kSegments * kLow;
+  p.nchunks = (nnz + kChunk - 1) / kChunk;
   size_t off = 0;
   p.key_off = off;
   off += AlignUp(nnz * sizeof(uint16_t));
@@ -367,6 +429,8 @@ TransposePlan Plan(uint64_t nnz, uint64_t num_features) {
   off += AlignUp(p.partials_words * sizeof(uint64_t));
   p.h_off = off;
   off += AlignUp(p.h_words * sizeof(uint32_t));
+  p.chunk_off = off;
+  off += AlignUp((p.nchunks + 1) * sizeof(uint32_t));
   p.total = off;
   return p;
 }
@@ -405,6 +469,7 @@ void LaunchCSRTranspose(const uint64_t* offset, size_t nrows, uint64_t base, uin
   uint64_t* G = reinterpret_cast<uint64_t*>(sc + p.g_off);
   uint64_t* partials = reinterpret_cast<uint64_t*>(sc + p.partials_off);
   uint32_t* H = reinterpret_cast<uint32_t*>(sc + p.h_off);
+  uint32_t* chunk_row = reinterpret_cast<uint32_t*>(sc + p.chunk_off);
   uint64_t* bstart = reinterpret_cast<uint64_t*>(sc + p.total);
   const IndexType* idx = index + base;  // entries [base, base + nnz) of the arrays
   const float* val = value != nullptr ? value + base : nullptr;
@@ -419,13 +484,15 @@ void LaunchCSRTranspose(const uint64_t* offset, size_t nrows, uint64_t base, uin
                      stream, G, p.nblocks, p.nbuckets, nnz, bstart);
   // T3
   if (nnz != 0) {
+    hipLaunchKernelGGL(k_chunk_rows, dim3((p.nchunks + kThreads - 1) / kThreads), dim3(kThreads),
+                       0, stream, offset, nrows, base, nnz, chunk_row);
     hipLaunchKernelGGL(k_bucket_scatter<IndexType>, dim3(p.nblocks), dim3(kThreads), 0, stream,
                        offset, nrows, base, idx, val, nnz, num_features, p.nbuckets,
-                       p.bucket_bits, G, p.nblocks, t_key, t_row, t_val);
+                       p.bucket_bits, G, p.nblocks, chunk_row, t_key, t_row, t_val);
   }
   // T4
   const unsigned nseg = p.nbuckets * kSegments;
-  hipLaunchKernelGGL(k_lowkey_hist, dim3(nseg), dim3(dev::kWave), 0, stream, t_key, bstart, H);
+  hipLaunchKernelGGL(k_lowkey_hist, dim3(nseg), dim3(kThreads), 0, stream, t_key, bstart, H);
   hipLaunchKernelGGL(k_lowkey_scan, dim3(p.nbuckets), dim3(kThreads), 0, stream, H, bstart,
                      num_features, col_ptr);
   hipLaunchKernelGGL(k_lowkey_scatter, dim3(nseg), dim3(dev::kWave), 0, stream, t_key, t_row,
