@@ -11,7 +11,7 @@ import torch
 
 from ..ops import csr_spmv, hashed_dense
 
-__all__ = ["SparseLogReg", "HashedFM", "fp8_gemm_available"]
+__all__ = ["SparseLogReg", "HashedFM"]
 
 
 class SparseLogReg(torch.nn.Module):
@@ -35,25 +35,12 @@ class SparseLogReg(torch.nn.Module):
             logits, label, weight=w, reduction="mean")
 
 
-def fp8_gemm_available(device=None) -> bool:
-    """True when torch._scaled_mm runs OCP fp8 e4m3 GEMMs on this device."""
-    if not torch.cuda.is_available():
-        return False
-    try:
-        a = torch.zeros(16, 16, device=device or "cuda").to(torch.float8_e4m3fn)
-        one = torch.ones((), device=a.device)
-        torch._scaled_mm(a, a.t().contiguous().t(), scale_a=one, scale_b=one,
-                         out_dtype=torch.float32)
-        return True
-    except (RuntimeError, NotImplementedError, TypeError):
-        return False
-
-
 class _HashedFMFunction(torch.autograd.Function):
     """HashedFM forward / backward as two HIP kernels over the fp8 batch
     (src/gpu/fm_kernels.hip): F1 reads the batch once and writes y and xV,
     F2 reads it once more and writes per-block partials of G^T X and
-    (X^2)^T g, summed here; no fp32 / bf16 copy of the batch exists."""
+    (X^2)^T g, F3/F4 sum them and form dw, dV; no fp32 / bf16 copy of the
+    batch exists."""
 
     @staticmethod
     def forward(ctx, x8, sx: float, w, v, bias):
@@ -79,11 +66,14 @@ class _HashedFMFunction(torch.autograd.Function):
         part = torch.empty((nblk, v.shape[1] + 2, dim), dtype=torch.float32, device=x8.device)
         _dmlc().fm_backward(x8.data_ptr(), rows, dim, g.data_ptr(), xv.data_ptr(), nblk,
                             part.data_ptr(), _stream())
-        z = part.sum(0)
-        sx = ctx.sx
-        gw = (sx * z[0]).unsqueeze(1)
-        gv = sx * z[1:1 + v.shape[1]].t() - v * (sx * sx * z[-1]).unsqueeze(1)
-        return None, None, gw, gv, g.sum().reshape(1)
+        # F3 + F4: partials summed and turned into dw, dV on the device
+        vf = v.float().contiguous()
+        z = torch.empty((v.shape[1] + 2, dim), dtype=torch.float32, device=x8.device)
+        gw = torch.empty((dim, 1), dtype=torch.float32, device=x8.device)
+        gv = torch.empty((dim, v.shape[1]), dtype=torch.float32, device=x8.device)
+        _dmlc().fm_reduce_grads(part.data_ptr(), nblk, dim, vf.data_ptr(), ctx.sx, z.data_ptr(),
+                                gw.data_ptr(), gv.data_ptr(), _stream())
+        return None, None, gw.to(v.dtype), gv.to(v.dtype), g.sum().reshape(1)
 
 
 def _dmlc():

@@ -8,9 +8,10 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY"
 P2="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS"
-P3="FETCH_SIZE WRITE_SIZE GRBM_GUI_ACTIVE GRBM_COUNT"
+P3="FETCH_SIZE GRBM_GUI_ACTIVE GRBM_COUNT"
+P4="WRITE_SIZE"
 i=0
-for P in "$P1" "$P2" "$P3"; do
+for P in "$P1" "$P2" "$P3" "$P4"; do
   i=$((i+1))
   timeout -s KILL 150 rocprofv3 --pmc $P -d "$OUT/p$i" -o run --output-format csv -- "$@" \
     > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }

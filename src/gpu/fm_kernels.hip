@@ -21,9 +21,12 @@
  *   index, so X must arrive with rows along K: an identity MFMA turns each
  *   32 x 32 X tile into an accumulator with features on lanes and rows in
  *   registers, which is exactly the B operand of the next MFMA (G^T from LDS
- *   in the matching permuted row order).  Eight waves share one G tile; each
+ *   in the matching permuted row order).  Eight waves share one G tile
+ *   (double-buffered in LDS: one barrier per 32-row tile); each
  *   keeps 128 features of Z in 64 accumulator registers and writes one
- *   partial per workgroup (summed by the caller).
+ *   partial per workgroup.
+ * F3 k_fm_reduce + F4 k_fm_grads: the partials summed in a fixed order and
+ *   turned into dw, dV on the device (no torch reduction over the partials).
  */
 #include <hip/hip_runtime.h>
 
@@ -83,13 +86,6 @@ __device__ __forceinline__ bf16x8 fp8x8_bf16(uint32_t lo, uint32_t hi) {
   return v;
 }
 
-__device__ __forceinline__ bf16x8 to_bf16x8(const float f[8]) {
-  bf16x8 v;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = static_cast<__bf16>(f[j]);
-  return v;
-}
-
 __device__ __forceinline__ uint32_t word(const uint4 (&v)[4], int i) {
   const uint4 q = v[i >> 2];
   const int k = i & 3;
@@ -133,17 +129,30 @@ __global__ __launch_bounds__(kFwdThreads) void k_fm_fwd(const uint8_t* __restric
   const float b0 = *bias;
   const int nblk = dim / 128;
   const bf16x8 zero8 = {};
-  for (int64_t t = static_cast<int64_t>(blockIdx.x) * waves + threadIdx.x / kWave; t < ntiles;
-       t += static_cast<int64_t>(gridDim.x) * waves) {
-    const int64_t row = t * 32 + col;  // the row of this lane's A fragment
-    const bool valid = row < rows;
-    const uint8_t* xr = x + (valid ? row : 0) * dim + 64 * h;
+  // loads run two 128-feature blocks ahead of the MFMAs, across row tiles too
+  // (2 x 4 KB per wave in flight): the wave's (tile, block) sequence is one
+  // stream, so the next tile's first blocks arrive during this tile's last
+  const int64_t tfirst = static_cast<int64_t>(blockIdx.x) * waves + threadIdx.x / kWave;
+  const int64_t tstride = static_cast<int64_t>(gridDim.x) * waves;
+  int64_t lt = tfirst;  // the load cursor: tile, block
+  int lkb = 0;
+  auto issue = [&](uint4 (&v)[4]) {
+    const int64_t r = lt * 32 + col;
+    const bool ok = lt < ntiles && r < rows;
+    load64(x + (ok ? r : 0) * dim + 64 * h + 128 * lkb, ok, v);
+    if (++lkb == nblk) {
+      lkb = 0;
+      lt += tstride;
+    }
+  };
+  uint4 cur[4], nx1[4], nx2[4];
+  issue(cur);
+  issue(nx1);
+  for (int64_t t = tfirst; t < ntiles; t += tstride) {
     f32x16 acc = {};
     f32x2 x2q2 = {0.0f, 0.0f};
-    uint4 cur[4], nxt[4];
-    load64(xr, valid, cur);
     for (int kb = 0; kb < nblk; ++kb) {
-      if (kb + 1 < nblk) load64(xr + 128 * (kb + 1), valid, nxt);
+      issue(nx2);
       const int kbase = 128 * kb + 64 * h;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -164,7 +173,10 @@ __global__ __launch_bounds__(kFwdThreads) void k_fm_fwd(const uint8_t* __restric
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fp8x8_bf16(lo, hi), b, acc, 0, 0, 0);
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) cur[i] = nxt[i];
+      for (int i = 0; i < 4; ++i) {
+        cur[i] = nx1[i];
+        nx1[i] = nx2[i];
+      }
     }
     // lanes r and r + 32 hold the two halves of row r's x^2.q
     float x2q = x2q2[0] + x2q2[1];
@@ -201,14 +213,16 @@ __global__ __launch_bounds__(kBwdThreads) void k_fm_bwd(const uint8_t* __restric
                                                         const float* __restrict__ xv,
                                                         int64_t rows_per_block,
                                                         float* __restrict__ part) {
-  __shared__ __bf16 s_gt[32][32 + 8];  // G^T [column][row], columns 17..31 zero
-  __shared__ float s_g[32];
+  // G^T [column][row] (columns 17..31 zero) and g, double-buffered: the next
+  // tile's G is written while this one is consumed, one barrier per tile
+  __shared__ __bf16 s_gt[2][32][32 + 8];
+  __shared__ float s_g[2][32];
   const int lane = lane_id();
   const int h = lane >> 5, n = lane & 31;
   const int wave = threadIdx.x / kWave;
   const int fbase = 1024 * blockIdx.y + kBwdWaveFeatures * wave;
   const bool active = fbase < dim;
-  for (int i = threadIdx.x; i < 32 * 40; i += kBwdThreads) (&s_gt[0][0])[i] = static_cast<__bf16>(0.0f);
+  for (int i = threadIdx.x; i < 2 * 32 * 40; i += kBwdThreads) (&s_gt[0][0][0])[i] = static_cast<__bf16>(0.0f);
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
   const int64_t r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
   // identity B fragments: element j of step s is 1 for column n's (h, s, j)
@@ -236,6 +250,16 @@ __global__ __launch_bounds__(kBwdThreads) void k_fm_bwd(const uint8_t* __restric
     const bool ok = active && r < r1;
     load64(x + (ok ? r : 0) * dim + fbase + 64 * h, ok, w);
   };
+  auto put_g = [&](int bf, float gv, float2 v) {
+    if (threadIdx.x < 256) {
+      s_gt[bf][1 + 2 * gpart][grow] = static_cast<__bf16>(gv * v.x);
+      s_gt[bf][2 + 2 * gpart][grow] = static_cast<__bf16>(gv * v.y);
+      if (gpart == 0) {
+        s_gt[bf][0][grow] = static_cast<__bf16>(gv);
+        s_g[bf][grow] = gv;
+      }
+    }
+  };
   float gv_n = 0.0f;
   float2 v_n = make_float2(0.0f, 0.0f);
   uint4 xw[4], xw_n[4];
@@ -243,56 +267,55 @@ __global__ __launch_bounds__(kBwdThreads) void k_fm_bwd(const uint8_t* __restric
     load_g(r0, &gv_n, &v_n);
     load_x(r0, xw_n);
   }
+  __syncthreads();  // the zeroed buffers
+  put_g(0, gv_n, v_n);
+  if (r0 + 32 < r1) load_g(r0 + 32, &gv_n, &v_n);
+  __syncthreads();
+  int cb = 0;
   for (int64_t t0 = r0; t0 < r1; t0 += 32) {
-    __syncthreads();  // the previous tile's G is consumed
-    if (threadIdx.x < 256) {
-      s_gt[1 + 2 * gpart][grow] = static_cast<__bf16>(gv_n * v_n.x);
-      s_gt[2 + 2 * gpart][grow] = static_cast<__bf16>(gv_n * v_n.y);
-      if (gpart == 0) {
-        s_gt[0][grow] = static_cast<__bf16>(gv_n);
-        s_g[grow] = gv_n;
-      }
-    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) xw[i] = xw_n[i];
     if (t0 + 32 < r1) {
-      load_g(t0 + 32, &gv_n, &v_n);
       load_x(t0 + 32, xw_n);
+      put_g(cb ^ 1, gv_n, v_n);  // the next tile's G (its buffer was consumed last tile)
+      if (t0 + 64 < r1) load_g(t0 + 64, &gv_n, &v_n);
     }
-    __syncthreads();
-    if (!active) continue;
-    // G^T fragments: element j of step s = row 16 s + 8 (j >> 2) + 4 h + (j & 3)
-    bf16x8 ga[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ga[s][j] = s_gt[n][16 * s + 8 * (j >> 2) + 4 * h + (j & 3)];
-    }
-    float gr[16];
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) gr[reg] = s_g[(reg & 3) + 8 * (reg >> 2) + 4 * h];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      // T: this block's 32 x 32 X tile, features on lanes, rows in registers
-      f32x16 tt = {};
+    if (active) {
+      // G^T fragments: element j of step s = row 16 s + 8 (j >> 2) + 4 h + (j & 3)
+      bf16x8 ga[2];
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        float f[8];
-        fp8x8(word(xw, 2 * (2 * b + s)), word(xw, 2 * (2 * b + s) + 1), f);
-        tt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(to_bf16x8(f), eye[s], tt, 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ga[s][j] = s_gt[cb][n][16 * s + 8 * (j >> 2) + 4 * h + (j & 3)];
       }
-      float ta = 0.0f;
+      float gr[16];
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) ta += tt[reg] * tt[reg] * gr[reg];
-      tacc[b] += ta;
+      for (int reg = 0; reg < 16; ++reg) gr[reg] = s_g[cb][(reg & 3) + 8 * (reg >> 2) + 4 * h];
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8 tb;
+      for (int b = 0; b < 4; ++b) {
+        // T: this block's 32 x 32 X tile, features on lanes, rows in registers
+        f32x16 tt = {};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) tb[j] = static_cast<__bf16>(tt[8 * s + j]);
-        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[s], tb, acc[b], 0, 0, 0);
+        for (int s = 0; s < 2; ++s) {
+          tt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              fp8x8_bf16(word(xw, 2 * (2 * b + s)), word(xw, 2 * (2 * b + s) + 1)), eye[s], tt,
+              0, 0, 0);
+        }
+        float ta = 0.0f;
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) ta += tt[reg] * tt[reg] * gr[reg];
+        tacc[b] += ta;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 tb;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) tb[j] = static_cast<__bf16>(tt[8 * s + j]);
+          acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[s], tb, acc[b], 0, 0, 0);
+        }
       }
     }
+    __syncthreads();  // buffer cb consumed; buffer cb ^ 1 written
+    cb ^= 1;
   }
   if (!active) return;
   float* out = part + static_cast<size_t>(blockIdx.x) * (kFmCols + 1) * dim;
@@ -310,7 +333,74 @@ __global__ __launch_bounds__(kBwdThreads) void k_fm_bwd(const uint8_t* __restric
   }
 }
 
+/*!
+ * F3.  Z[c][n] = sum over the F2 workgroups of part[b][c][n]: workgroup
+ * (64 features, column c), wave w sums blocks w, w + 4, ... (8 loads in flight
+ * per lane), LDS combine in a fixed order (deterministic).
+ */
+constexpr int kRedThreads = 256;
+__global__ __launch_bounds__(kRedThreads) void k_fm_reduce(const float* __restrict__ part,
+                                                           int nblk, int dim,
+                                                           float* __restrict__ z) {
+  __shared__ float s[kRedThreads / kWave][kWave];
+  const int lane = lane_id(), w = threadIdx.x / kWave;
+  const int n = blockIdx.x * kWave + lane, c = blockIdx.y;
+  const size_t stride = static_cast<size_t>(kFmCols + 1) * dim;
+  const float* p = part + static_cast<size_t>(c) * dim + n;
+  constexpr int kWaves = kRedThreads / kWave;
+  float acc = 0.0f;
+  if (n < dim) {
+    int b = w;
+    for (; b + 7 * kWaves < nblk; b += 8 * kWaves) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p[static_cast<size_t>(b + u * kWaves) * stride];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; b < nblk; b += kWaves) acc += p[static_cast<size_t>(b) * stride];
+  }
+  s[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && n < dim) {
+    float t = s[0][lane];
+#pragma unroll
+    for (int q = 1; q < kWaves; ++q) t += s[q][lane];
+    z[static_cast<size_t>(c) * dim + n] = t;
+  }
+}
+
+/*! \brief F4.  dw = s Z_0, dV_nf = s Z_{1+f,n} - V_nf s^2 t_n (t = Z_17) */
+__global__ __launch_bounds__(kWave) void k_fm_grads(const float* __restrict__ z, int dim,
+                                                    const float* __restrict__ v, float sx,
+                                                    float* __restrict__ gw,
+                                                    float* __restrict__ gv) {
+  const int n = blockIdx.x * kWave + lane_id();
+  if (n >= dim) return;
+  gw[n] = sx * z[n];
+  const float t = sx * sx * z[static_cast<size_t>(kFmCols) * dim + n];
+  const float4* vr = reinterpret_cast<const float4*>(v + static_cast<size_t>(n) * kFmRank);
+  float4* gr = reinterpret_cast<float4*>(gv + static_cast<size_t>(n) * kFmRank);
+#pragma unroll
+  for (int q = 0; q < kFmRank / 4; ++q) {
+    const float4 a = vr[q];
+    const float* zc = z + static_cast<size_t>(1 + 4 * q) * dim + n;
+    gr[q] = make_float4(sx * zc[0] - a.x * t, sx * zc[dim] - a.y * t,
+                        sx * zc[2 * static_cast<size_t>(dim)] - a.z * t,
+                        sx * zc[3 * static_cast<size_t>(dim)] - a.w * t);
+  }
+}
+
 }  // namespace
+
+void LaunchFmReduceGrads(const float* part, int nblocks, int dim, const float* v, float sx,
+                         float* z, float* gw, float* gv, hipStream_t stream) {
+  if (dim == 0) return;
+  const int fb = (dim + kWave - 1) / kWave;
+  hipLaunchKernelGGL(k_fm_reduce, dim3(fb, kFmCols + 1), dim3(kRedThreads), 0, stream, part,
+                     nblocks, dim, z);
+  hipLaunchKernelGGL(k_fm_grads, dim3(fb), dim3(kWave), 0, stream, z, dim, v, sx, gw, gv);
+}
 
 size_t FmForwardSharedBytes(int dim) {
   return static_cast<size_t>(kFmCols) * (dim + 8) * sizeof(__bf16) + static_cast<size_t>(dim) * 4;

@@ -321,6 +321,10 @@ void LaunchFmForward(const uint8_t* x, int64_t rows, int dim, const void* wt_bf1
  */
 void LaunchFmBackward(const uint8_t* x, int64_t rows, int dim, const float* g, const float* xv,
                       int nblocks, float* part, hipStream_t stream);
+/*! \brief sum the LaunchFmBackward partials (z: [kFmCols + 1][dim] scratch)
+ *  and write dw [dim] and dV [dim][kFmRank] (v: [dim][kFmRank] f32) */
+void LaunchFmReduceGrads(const float* part, int nblocks, int dim, const float* v, float sx,
+                         float* z, float* gw, float* gv, hipStream_t stream);
 
 /*! \brief K10: dst_offset[i] = src_offset[i] - src_base + dst_base for i<=nrows */
 void LaunchOffsetRebase(const uint64_t* src_offset, size_t nrows, uint64_t src_base,

@@ -718,6 +718,88 @@ __device__ __noinline__ QidResult qid_token(const uint8_t* __restrict__ text, si
 }
 
 /*!
+ * \brief the `qid:` token at staged LDS byte a (the 32 bytes from a are
+ *  staged: a step slot holds 64 bytes past the step), same grammar as
+ *  qid_token; a zero byte (past the text end) ends the digits like the end of
+ *  the text does.
+ */
+__device__ __forceinline__ QidResult qid_lds(const uint4* lds, uint32_t a) {
+  QidResult r{0, false};
+  const uint4 g0 = tok::ext16(lds, a), g1 = tok::ext16(lds, a + 16);
+  if (g0.x != 0x3A646971u) return r;  // "qid:"
+  uint32_t i = 4;
+  const uint32_t c0 = tok::win_byte(g0, g1, 4);
+  const bool neg = c0 == '-';
+  if (neg || c0 == '+') i = 5;
+  uint64_t v = 0;
+  for (int k = 0; k < 20; ++k, ++i) {
+    const uint32_t c = tok::win_byte(g0, g1, i);
+    if (c - '0' > 9u) break;
+    v = v * 10 + (c - '0');
+  }
+  const uint32_t c = tok::win_byte(g0, g1, i);
+  if (c != ' ' && c != '\t' && c != '\n' && c != '\r' && c != 0) return r;  // junk after the digits
+  r.value = neg ? 0 - v : v;
+  r.ok = true;
+  return r;
+}
+
+/*! \brief status of the last token start of a 16-byte slice: 0 none, 2 a token
+ *  that does not start a line, 3 one that does (a label) */
+__device__ __forceinline__ uint32_t slice_last(uint32_t tm, uint32_t lm) {
+  return tm != 0 ? 2u | ((lm >> (31 - __builtin_clz(tm))) & 1u) : 0u;
+}
+
+/*!
+ * \brief for a `qid:` token start: the status of the token start before it --
+ *  a `qid:` is the line's second token iff that one starts the line (3).
+ *  Slices of a step in text order are all lanes' a slices, then the b slices;
+ *  `carried` is the status at the step start (0: no token yet in this tile,
+ *  then the global-memory check decides).  Wave-uniform call.
+ */
+struct PrevTok {
+  uint32_t a, b;
+};
+__device__ __forceinline__ PrevTok prev_token_status(uint32_t tm_a, uint32_t lm_a, uint32_t tm_b,
+                                                     uint32_t lm_b, uint32_t carried, int lane) {
+  auto scan = [lane](uint32_t v) {  // inclusive max over lanes <= lane
+#pragma unroll
+    for (int d = 1; d < dev::kWave; d <<= 1) {
+      const uint32_t u = __shfl_up(v, d, dev::kWave);
+      if (lane >= d) v = u > v ? u : v;
+    }
+    return v;
+  };
+  const uint32_t ia = scan(tm_a != 0 ? ((lane + 1u) << 2) | slice_last(tm_a, lm_a) : 0u);
+  const uint32_t ib = scan(tm_b != 0 ? ((lane + 1u) << 2) | slice_last(tm_b, lm_b) : 0u);
+  uint32_t xa = __shfl_up(ia, 1, dev::kWave), xb = __shfl_up(ib, 1, dev::kWave);
+  if (lane == 0) xa = xb = 0;
+  const uint32_t ta = __shfl(ia, dev::kWave - 1, dev::kWave);
+  PrevTok r;
+  r.a = xa != 0 ? (xa & 3u) : carried;
+  r.b = xb != 0 ? (xb & 3u) : (ta != 0 ? (ta & 3u) : carried);
+  return r;
+}
+
+/*! \brief the status after a step (its last token start's), or `carried` */
+__device__ __forceinline__ uint32_t step_last_status(uint32_t tm_a, uint32_t lm_a, uint32_t tm_b,
+                                                     uint32_t lm_b, uint32_t carried) {
+  const uint64_t bb = __ballot(tm_b != 0), ba = __ballot(tm_a != 0);
+  const uint32_t sb = __shfl(slice_last(tm_b, lm_b), bb ? 63 - __builtin_clzll(bb) : 0, dev::kWave);
+  const uint32_t sa = __shfl(slice_last(tm_a, lm_a), ba ? 63 - __builtin_clzll(ba) : 0, dev::kWave);
+  // wave-uniform: kept in a scalar register
+  return __builtin_amdgcn_readfirstlane(bb ? sb : (ba ? sa : carried));
+}
+
+/*! \brief status of the token start before bit j of a slice, given the status
+ *  before the slice */
+__device__ __forceinline__ uint32_t status_before(uint32_t tm, uint32_t lm, uint32_t j,
+                                                  uint32_t before_slice) {
+  const uint32_t inside = tm & ((1u << j) - 1u);
+  return inside != 0 ? slice_last(inside, lm) : before_slice;
+}
+
+/*!
  * \brief C3: wave-autonomous tile fill.  Each wave of the workgroup owns one
  *  8 KiB tile and never synchronises with the others (no __syncthreads):
  *   1. all 8 KiB (+ the 64 bytes after it) are loaded into registers at once;
@@ -743,12 +825,30 @@ constexpr int kSteps = static_cast<int>(kTileBytes / kStepBytes);
 constexpr uint32_t kSlotBytes = kStepBytes + 64;           // a step + 64 B of the next
 constexpr uint32_t kStageVecs = 2 * kSlotBytes / 16;       // two slots: step s and s - 1
 constexpr uint32_t kListCap = kDecodeCarry + kStepBytes / 2;  // carried + a step's tokens
+// k_tile_hash: no carried entries, and a step of more tokens is irregular --
+// sized so that 4 workgroups fit a CU with a 1024-wide f32 row per wave
+constexpr uint32_t kHashListCap = 896;
 
 /*!
  * \brief the 16 B at chunk offset pos, bytes at or past n zeroed (the
  *  decoder's end marker), without branches: lanes past n load from a clamped
  *  in-bounds address and mask everything
  */
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+/*! \brief a buffer resource over [base, base + avail) (raw, gfx9 dword3): the
+ *  address lives in scalar registers, loads take a 32-bit lane offset */
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t text_rsrc(const uint8_t* base, size_t avail) {
+  const uint32_t nr = avail > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(avail);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0, nr, 0x00020000);
+}
+
+/*! \brief 16 bytes at voff + soff of a text_rsrc (in range: the caller checks) */
+__device__ __forceinline__ uint4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 __device__ __forceinline__ uint4 load16_clip(const uint8_t* __restrict__ text, size_t pos, size_t n) {
   const size_t at = pos < n ? pos : 0;
   const uint4 v = *reinterpret_cast<const uint4*>(text + at);
@@ -779,6 +879,7 @@ __device__ __forceinline__ uint32_t list_entry(uint32_t tm_bit_j, uint32_t lm, u
   return (base + j) | (((lm >> j) & 1u) << 13) | ((line0 + __popc(upto)) << 14);
 }
 
+template <uint32_t kCap = kListCap>
 __device__ __forceinline__ void list_slice(uint32_t* sl, uint32_t tm, uint32_t lm, uint32_t at,
                                            uint32_t base, uint32_t line0, int lane) {
   uint32_t m = tm;
@@ -786,7 +887,7 @@ __device__ __forceinline__ void list_slice(uint32_t* sl, uint32_t tm, uint32_t l
   for (int t = 0; t < 2; ++t) {
     const uint32_t j = static_cast<uint32_t>(__builtin_ctz(m | 0x10000u));
     const bool has = m != 0;
-    sl[has ? at : kListCap + lane] = list_entry(j & 15u, lm, base, line0);
+    sl[has ? at : kCap + lane] = list_entry(j & 15u, lm, base, line0);  // (the list holds kCap + 64)
     at += has ? 1u : 0u;
     m &= m - 1;
   }
@@ -832,12 +933,16 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
                                                         MetaPartial* __restrict__ partials) {
   __shared__ uint4 s_text[kFillWaves][kStageVecs];
   __shared__ uint32_t s_list[kFillWaves][kListCap + 64];  // + a dummy slot per lane
+  __shared__ uint32_t s_dq[kFillWaves][2][2 * dev::kWave];   // deferred tokens: entry, ordinal
   const int wave = threadIdx.x / dev::kWave;
   const int lane = dev::lane_id();
   const size_t tile = static_cast<size_t>(blockIdx.x) * kFillWaves + wave;
   if (tile >= ntiles) return;  // whole waves leave; nothing below synchronises waves
   uint4* const st = s_text[wave];
   uint32_t* const sl = s_list[wave];
+  uint32_t* const dq_e = s_dq[wave][0];
+  uint32_t* const dq_i = s_dq[wave][1];
+  uint32_t qn = 0;  // queued tokens
   const uint32_t slot = round_slot(lane);
   const size_t tile0 = tile * kTileBytes;
 
@@ -845,6 +950,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
   // last one prefetches the 64 bytes past the tile)
   uint4 a = load16_clip(text, tile0 + lane * 16, n);
   uint4 b = load16_clip(text, tile0 + 1024 + lane * 16, n);
+  const __amdgpu_buffer_rsrc_t trs = text_rsrc(text + tile0, n - tile0);
   uint32_t carry_pc = tile0 == 0 ? static_cast<uint32_t>('\n') : text[tile0 - 1];
   const uint64_t pre = prefix[tile];
   const uint64_t line_base = pre >> 32;
@@ -875,6 +981,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
   uint32_t tok0 = 0;   // tile token ordinal of list position 0
   uint32_t lcnt = 0;   // line starts of this tile so far
   uint32_t carry = 0;  // list entries left for the next step's rounds (listed, not decoded)
+  uint32_t qid_prev = 0;  // status of the last token start so far (prev_token_status)
   // maxima in the index width (32-bit compares for u32 indices)
   using MaxT = typename std::conditional<sizeof(IndexType) == 4, uint32_t, uint64_t>::type;
   MaxT mx_index = 0, mx_field = 0;
@@ -887,8 +994,11 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
     const bool last = s + 1 == kSteps;
     uint4 na, nb = make_uint4(0, 0, 0, 0);
     if (nxt + kStepBytes <= n) {  // wave-uniform: no byte of the next step is past n
-      na = *reinterpret_cast<const uint4*>(text + nxt + lane * 16);
-      if (!last) nb = *reinterpret_cast<const uint4*>(text + nxt + 1024 + lane * 16);
+      // buffer loads: scalar base, 32-bit lane offset (no 64-bit address pair
+      // kept live across the step)
+      const uint32_t so = static_cast<uint32_t>(s + 1) * kStepBytes;
+      na = bload16(trs, static_cast<uint32_t>(lane) * 16, so);
+      if (!last) nb = bload16(trs, static_cast<uint32_t>(lane) * 16, so + 1024);
     } else {
       na = load16_clip(text, nxt + lane * 16, n);
       if (!last) nb = load16_clip(text, nxt + 1024 + lane * 16, n);
@@ -943,27 +1053,41 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
                lcnt + static_cast<uint32_t>((before >> 32) & 0xFFFFu), lane);
     list_slice(sl, tm_b, lm_b, carry + ntok_a + static_cast<uint32_t>((before >> 16) & 0xFFFFu),
                sbase + 1024 + lane * 16, lcnt + nline_a + static_cast<uint32_t>(before >> 48), lane);
-    if (qid_chunk && __any((qa | qb) != 0)) {
-      const uint32_t lbase[2] = {lcnt + static_cast<uint32_t>((before >> 32) & 0xFFFFu),
-                                 lcnt + nline_a + static_cast<uint32_t>(before >> 48)};
+    dev::wave_sync();  // the staged text and the list are visible to every lane
+    if (qid_chunk) {
+      if (__any((qa | qb) != 0)) {
+        const PrevTok pv = prev_token_status(tm_a | qa, lm_a, tm_b | qb, lm_b, qid_prev, lane);
+        const uint32_t lbase[2] = {lcnt + static_cast<uint32_t>((before >> 32) & 0xFFFFu),
+                                   lcnt + nline_a + static_cast<uint32_t>(before >> 48)};
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint32_t lmh = h == 0 ? lm_a : lm_b;
-        for (uint32_t m = h == 0 ? qa : qb; m != 0; m &= m - 1) {
-          const uint32_t j = static_cast<uint32_t>(__builtin_ctz(m));
-          // its row: the tile's line starts up to this byte (a line that
-          // starts with 'q' has no label: exact kernels)
-          const uint32_t lc = lbase[h] + static_cast<uint32_t>(__popc(lmh & ((2u << j) - 1u)));
-          const QidResult q = qid_token(text, n, pos_a + static_cast<size_t>(h) * 1024 + j);
-          // (lc 0: the tile's first, unfinished line -- the row before R)
-          const bool ok = q.ok && ((lmh >> j) & 1u) == 0 &&
-                          static_cast<int32_t>(lc) - 1 < row_room && qid_at != nullptr;
-          if (ok) qid_at[lc] = q.value;
-          irregular |= !ok;
+        for (int h = 0; h < 2; ++h) {
+          // token starts with the letter ones: a `qid:` after another letter
+          // token is not the second token
+          const uint32_t lmh = h == 0 ? lm_a : lm_b, tmh = h == 0 ? tm_a | qa : tm_b | qb;
+          for (uint32_t m = h == 0 ? qa : qb; m != 0; m &= m - 1) {
+            const uint32_t j = static_cast<uint32_t>(__builtin_ctz(m));
+            // its row: the tile's line starts up to this byte (a line that
+            // starts with 'q' has no label: exact kernels)
+            const uint32_t lc = lbase[h] + static_cast<uint32_t>(__popc(lmh & ((2u << j) - 1u)));
+            // the second token of its line: the token start before it is the
+            // line's label (from the masks; the tile's first token: global check)
+            const uint32_t prev = status_before(tmh, lmh, j, h == 0 ? pv.a : pv.b);
+            QidResult q{0, false};
+            if (prev == 3u) {
+              q = qid_lds(st, sbase + static_cast<uint32_t>(h) * 1024 + lane * 16 + j);
+            } else if (prev == 0u) {
+              q = qid_token(text, n, pos_a + static_cast<size_t>(h) * 1024 + j);
+            }
+            // (lc 0: the tile's first, unfinished line -- the row before R)
+            const bool ok = q.ok && ((lmh >> j) & 1u) == 0 &&
+                            static_cast<int32_t>(lc) - 1 < row_room && qid_at != nullptr;
+            if (ok) qid_at[lc] = q.value;
+            irregular |= !ok;
+          }
         }
       }
+      qid_prev = step_last_status(tm_a | qa, lm_a, tm_b | qb, lm_b, qid_prev);
     }
-    dev::wave_sync();  // the staged text and the list are visible to every lane
 
     // ---- 3. decode 64 listed tokens per round.  Only whole rounds run: the
     // rest of this step's tokens (< 64) wait for the next step's rounds, so a
@@ -972,43 +1096,11 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
     const uint32_t total = carry + ntok;
     const uint32_t rest = total % dev::kWave < ntok ? total % dev::kWave : ntok;
     const uint32_t ndec = last ? total : total - rest;
-    for (uint32_t r0 = 0; r0 < ndec; r0 += dev::kWave) {
-      const uint32_t li = r0 + slot;
-      const bool active = li < ndec;
-      const uint32_t e = active ? sl[li] : 0u;
+    // a decoded token's outputs (every write is at a position derived from
+    // the token / line ordinals, so deferred tokens may write later)
+    auto emit = [&](bool active, uint32_t e, uint32_t i, const tok::Token& t, bool bad) {
       const bool is_label = active && ((e >> 13) & 1u) != 0;
-      const uint32_t off = e & 0x1FFFu;  // 0 in idle lanes: they decode harmless bytes
       const uint32_t lc = e >> 14;
-      const uint32_t i = tok0 + li;
-      tok::Token t;
-      t.u0_hi = t.u1_hi = 0;
-      t.u1 = 0;
-      bool bad = false;
-      bool ok = tok::decode<F>(st, off, is_label, &t);
-      // exponents / long fractions: the extended decoder on the lane (only
-      // rounds that have such a token pay for it)
-      if (__any(active & !ok)) {
-        if (active & !ok) {
-          const tok::ExtToken x = tok::decode_ext<F>(
-              st, off, is_label, off >= kSlotBytes ? 2 * kSlotBytes : kSlotBytes);
-          if (x.ok) t = x.t;
-          ok = x.ok;
-        }
-      }
-      if (active & !ok) {
-        // the step a slot holds: s, or s - 1 for a carried token
-        const uint32_t in_slot = off >= kSlotBytes ? 1u : 0u;
-        const int step = in_slot == (static_cast<uint32_t>(s) & 1u) ? s : s - 1;
-        // by value: result pointers into this frame would put t / bad on the
-        // stack, with a scratch store + load (and a vmcnt(0) wait) every round
-        const size_t gpos =
-            tile0 + static_cast<size_t>(step) * kStepBytes + off - in_slot * kSlotBytes;
-        const GenericResult g = generic_token<F, IndexType>(text, n, gpos, is_label);
-        t = g.t;
-        bad = g.bad;
-        // qid:, comments, junk: the exact kernels own the reference semantics
-        irregular |= !num_start(text[gpos]);
-      }
       const int32_t rel = static_cast<int32_t>(i) - static_cast<int32_t>(lc);
       const bool row_ok = static_cast<int32_t>(lc) - 1 < row_room;
       const bool nnz_ok = rel < nnz_room;
@@ -1047,6 +1139,84 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
         mx_field = feat && fu > mx_field ? fu : mx_field;
       }
       neg |= active && bad;
+    };
+    // tokens the register-window decoder declines (exponents, long fractions,
+    // anything for the generic parser) are queued and decoded 64 at a time in
+    // rounds of their own, so a round with one such token does not pay the
+    // long decoder for all 64 lanes; the queue is drained before the slots it
+    // points into are restaged (by the end of every step).  One loop, one
+    // emit site: list rounds and queue rounds share the code after decode.
+    for (uint32_t r0 = 0;;) {
+      const bool qround = qn >= static_cast<uint32_t>(dev::kWave) || (r0 >= ndec && qn != 0);
+      if (!qround && r0 >= ndec) break;
+      bool active;
+      uint32_t e, i;
+      tok::Token t;
+      t.u0_hi = t.u1_hi = 0;
+      t.u1 = 0;
+      bool bad = false;
+      if (!qround) {
+        const uint32_t li = r0 + slot;
+        active = li < ndec;
+        e = active ? sl[li] : 0u;
+        i = tok0 + li;
+        const bool is_label = active && ((e >> 13) & 1u) != 0;
+        // 0 in idle lanes: they decode harmless bytes
+        const bool ok = tok::decode<F>(st, e & 0x1FFFu, is_label, &t);
+        const bool defer = active & !ok;
+        const uint64_t dm = __ballot(defer);
+        if (dm != 0) {
+          const uint32_t rank = static_cast<uint32_t>(__popcll(dm & ((1ull << lane) - 1ull)));
+          if (defer) {
+            dq_e[qn + rank] = e;
+            dq_i[qn + rank] = i;
+          }
+          qn += static_cast<uint32_t>(__popcll(dm));
+        }
+        active = active & ok;
+        r0 += dev::kWave;
+      } else {
+        dev::wave_sync();  // queue entries visible
+        const uint32_t cnt = qn < static_cast<uint32_t>(dev::kWave) ? qn : dev::kWave;
+        active = slot < cnt;
+        e = active ? dq_e[slot] : 0u;
+        i = active ? dq_i[slot] : 0u;
+        // the rest (< 64) moves to the front (read, sync, write)
+        const uint32_t keep = qn - cnt;
+        const bool mv = lane < static_cast<int>(keep);
+        const uint32_t me = mv ? dq_e[dev::kWave + lane] : 0u;
+        const uint32_t mi = mv ? dq_i[dev::kWave + lane] : 0u;
+        dev::wave_sync();
+        if (mv) {
+          dq_e[lane] = me;
+          dq_i[lane] = mi;
+        }
+        qn = keep;
+        const bool is_label = active && ((e >> 13) & 1u) != 0;
+        const uint32_t off = e & 0x1FFFu;
+        bool ok = false;
+        if (active) {
+          const tok::ExtToken x = tok::decode_ext<F>(
+              st, off, is_label, off >= kSlotBytes ? 2 * kSlotBytes : kSlotBytes);
+          t = x.t;
+          ok = x.ok;
+        }
+        if (active & !ok) {
+          // the step a slot holds: s, or s - 1 for a carried token
+          const uint32_t in_slot = off >= kSlotBytes ? 1u : 0u;
+          const int step = in_slot == (static_cast<uint32_t>(s) & 1u) ? s : s - 1;
+          // by value: result pointers into this frame would put t / bad on the
+          // stack, with a scratch store + load (and a vmcnt(0) wait) every round
+          const size_t gpos =
+              tile0 + static_cast<size_t>(step) * kStepBytes + off - in_slot * kSlotBytes;
+          const GenericResult g = generic_token<F, IndexType>(text, n, gpos, is_label);
+          t = g.t;
+          bad = g.bad;
+          // qid:, comments, junk: the exact kernels own the reference semantics
+          irregular |= !num_start(text[gpos]);
+        }
+      }
+      emit(active, e, i, t, bad);
     }
     // the undecoded rest moves to the front of the list (all lanes read before any writes)
     const uint32_t left = total - ndec;
@@ -1096,9 +1266,10 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
  *      prefetch only the 64 B tail (lines > 2 KiB past the tile are rare);
  *   3. every decoded feature adds +-value at bucket hash % dim of ONE f32 row
  *      in the wave's LDS (ds_add_f32); when a round moves past a line, that row
- *      is flushed: each lane reads its 16 columns, zeroes them, converts to
- *      OCP fp8 e4m3 (v_cvt_pk_fp8_f32) and writes one 16 B store -- a whole
- *      row per wave store, zero spans included, no separate memset pass.
+ *      is flushed: each lane reads a float4 per 256 columns (lane-interleaved,
+ *      conflict-free), zeroes it, converts to OCP fp8 e4m3 (v_cvt_pk_fp8_f32)
+ *      and stores 4 B -- 256 contiguous bytes per wave store, zero spans
+ *      included, no separate memset pass.
  *  The label token's lane writes the label.  No CSR, no per-row LDS buffers
  *  per workgroup, no barrier.  Hash and bucket are K9's (dev::hash_u64), so
  *  the fp8 bytes equal tile CSR + K9.  Reference token loop:
@@ -1134,8 +1305,11 @@ template <TextFormat F, typename IndexType, bool kFP8>
 __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
     const uint8_t* __restrict__ text, size_t n, size_t ntiles,
     const uint64_t* __restrict__ prefix, HashTarget out, MetaPartial* __restrict__ partials) {
-  __shared__ uint4 s_text[kFillWaves][kStageVecs];
-  __shared__ uint32_t s_list[kFillWaves][kListCap + 64];
+  // one staging slot and a list without carried entries: every step decodes
+  // all its tokens, so the LDS per wave (+ the dim-wide f32 row) leaves room
+  // for 4 workgroups per CU up to dim 1024
+  __shared__ uint4 s_text[kFillWaves][kSlotBytes / 16];
+  __shared__ uint32_t s_list[kFillWaves][kHashListCap + 64];
   extern __shared__ __attribute__((aligned(16))) float s_hrow[];  // kFillWaves x dim
   const int wave = threadIdx.x / dev::kWave;
   const int lane = dev::lane_id();
@@ -1158,29 +1332,22 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
     for (int c = lane * 4; c < dim; c += dev::kWave * 4) {
       *reinterpret_cast<float4*>(row + c) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
-    // one row out: read + zero this lane's columns, convert, one 16 B store
+    // one row out: read + zero this lane's columns, convert, store
     auto flush = [&](uint32_t lc) {
       dev::wave_sync();  // the row's adds are done
       const uint64_t g = R + lc - 1;
       const bool ok = lc <= own;
       if constexpr (kFP8) {
+        // lane-interleaved float4s (consecutive lanes, consecutive 16 B: no
+        // bank conflicts on the b128 read / zero), 4 fp8 bytes per lane store
         uint8_t* o = static_cast<uint8_t*>(out.x) + g * static_cast<uint64_t>(dim);
-        for (int c = lane * 16; c < dim; c += dev::kWave * 16) {
+        for (int c = lane * 4; c < dim; c += dev::kWave * 4) {
           float4* r4 = reinterpret_cast<float4*>(row + c);
-          float4 x[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            x[q] = r4[q];
-            r4[q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-          }
-          uint32_t w[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            int pk = __builtin_amdgcn_cvt_pk_fp8_f32(x[q].x * out.scale, x[q].y * out.scale, 0, false);
-            pk = __builtin_amdgcn_cvt_pk_fp8_f32(x[q].z * out.scale, x[q].w * out.scale, pk, true);
-            w[q] = static_cast<uint32_t>(pk);
-          }
-          if (ok) *reinterpret_cast<uint4*>(o + c) = make_uint4(w[0], w[1], w[2], w[3]);
+          const float4 x = *r4;
+          *r4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+          int pk = __builtin_amdgcn_cvt_pk_fp8_f32(x.x * out.scale, x.y * out.scale, 0, false);
+          pk = __builtin_amdgcn_cvt_pk_fp8_f32(x.z * out.scale, x.w * out.scale, pk, true);
+          if (ok) *reinterpret_cast<uint32_t*>(o + c) = static_cast<uint32_t>(pk);
         }
       } else {
         float* o = static_cast<float*>(out.x) + g * static_cast<uint64_t>(dim);
@@ -1198,8 +1365,8 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
     uint4 b = load16_clip(text, tile0 + 1024 + lane * 16, n);
     uint32_t carry_pc = tile0 == 0 ? static_cast<uint32_t>('\n') : text[tile0 - 1];
     uint32_t lcnt = 0;   // line starts seen so far (this tile's ordinals)
-    uint32_t carry = 0;  // list entries left for the next step's rounds
     uint32_t open = 0;   // ordinal of the row being accumulated (0: none yet)
+    uint32_t qid_prev = 0;  // LibSVM: status of the last token start (prev_token_status)
     bool have_full = true;  // a / b hold the whole current step
 #pragma unroll 1
     for (int s = 0;; ++s) {
@@ -1224,11 +1391,10 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
       } else if (lane < 4) {
         na = load16_clip(text, nxt + lane * 16, n);
       }
-      const uint32_t sbase = (static_cast<uint32_t>(s) & 1u) * kSlotBytes;
-      uint4* const ss = st + sbase / 16;
-      ss[lane] = a;
-      ss[64 + lane] = b;
-      if (lane < 4) ss[128 + lane] = na;
+      constexpr uint32_t sbase = 0;  // the one slot
+      st[lane] = a;
+      st[64 + lane] = b;
+      if (lane < 4) st[128 + lane] = na;
       const size_t pos_a = cur + lane * 16;
       const uint32_t left_a = __shfl_up(a.w >> 24, 1, dev::kWave);
       const uint32_t pc_a = lane == 0 ? carry_pc : left_a;
@@ -1245,22 +1411,32 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
         (void)lane_masks<false>(b, pc_b, pos_a + 1024, n, &lm_b, &tm_b);
       }
       if (F == TextFormat::kLibSVM) {
-        // `qid:` tokens are no features of the batch: dropped (checked; any
-        // other 'q' token sends the chunk to the exact kernels)
+        // `qid:` tokens are no features of the batch: dropped (checked as in
+        // the fill, from the staged text; any other letter token sends the
+        // chunk to the exact kernels)
         const uint32_t qa = tm_a & letter_mask(a), qb = tm_b & letter_mask(b);
         if (__any((qa | qb) != 0)) {
-          tm_a &= ~qa;
-          tm_b &= ~qb;
+          const PrevTok pv = prev_token_status(tm_a, lm_a, tm_b, lm_b, qid_prev, lane);
+          dev::wave_sync();  // the staged step is visible to every lane
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            const uint32_t lmh = h == 0 ? lm_a : lm_b;
+            const uint32_t lmh = h == 0 ? lm_a : lm_b, tmh = h == 0 ? tm_a : tm_b;
             for (uint32_t m = h == 0 ? qa : qb; m != 0; m &= m - 1) {
               const uint32_t j = static_cast<uint32_t>(__builtin_ctz(m));
-              irregular |= ((lmh >> j) & 1u) != 0 ||
-                           !qid_token(text, n, pos_a + static_cast<size_t>(h) * 1024 + j).ok;
+              const uint32_t prev = status_before(tmh, lmh, j, h == 0 ? pv.a : pv.b);
+              bool ok = false;
+              if (prev == 3u) {
+                ok = qid_lds(st, sbase + static_cast<uint32_t>(h) * 1024 + lane * 16 + j).ok;
+              } else if (prev == 0u) {
+                ok = qid_token(text, n, pos_a + static_cast<size_t>(h) * 1024 + j).ok;
+              }
+              irregular |= ((lmh >> j) & 1u) != 0 || !ok;
             }
           }
         }
+        qid_prev = step_last_status(tm_a, lm_a, tm_b, lm_b, qid_prev);
+        tm_a &= ~qa;
+        tm_b &= ~qb;
       }
       uint64_t cnt = static_cast<uint64_t>(__popc(tm_a)) |
                      (static_cast<uint64_t>(__popc(tm_b)) << 16) |
@@ -1281,18 +1457,21 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
       }
       const uint32_t ntok_a = static_cast<uint32_t>(tot & 0xFFFFu);
       const uint32_t ntok = ntok_a + static_cast<uint32_t>((tot >> 16) & 0xFFFFu);
-      list_slice(sl, tm_a, lm_a, carry + static_cast<uint32_t>(before & 0xFFFFu), sbase + lane * 16,
-                 la0, lane);
-      list_slice(sl, tm_b, lm_b, carry + ntok_a + static_cast<uint32_t>((before >> 16) & 0xFFFFu),
-                 sbase + 1024 + lane * 16, lb0, lane);
+      if (ntok > kHashListCap) {  // wave-uniform: > 0.44 tokens per byte -- exact kernels
+        irregular = true;
+        break;
+      }
+      list_slice<kHashListCap>(sl, tm_a, lm_a, static_cast<uint32_t>(before & 0xFFFFu),
+                               sbase + lane * 16, la0, lane);
+      list_slice<kHashListCap>(sl, tm_b, lm_b,
+                               ntok_a + static_cast<uint32_t>((before >> 16) & 0xFFFFu),
+                               sbase + 1024 + lane * 16, lb0, lane);
       dev::wave_sync();
       lcnt += nline;
       const bool eol_end = carry_pc == '\n' || carry_pc == '\r';
       const bool last = nxt >= n || lcnt > own || (s + 1 >= kSteps && lcnt == own && eol_end);
 
-      const uint32_t total = carry + ntok;
-      const uint32_t rest = total % dev::kWave < ntok ? total % dev::kWave : ntok;
-      const uint32_t ndec = last ? total : total - rest;
+      const uint32_t ndec = ntok;
       for (uint32_t r0 = 0; r0 < ndec; r0 += dev::kWave) {
         const uint32_t li = r0 + slot;
         const bool active = li < ndec;
@@ -1307,17 +1486,13 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
         bool ok = tok::decode<F>(st, off, is_label, &t);
         if (__any(active & !ok)) {
           if (active & !ok) {
-            const tok::ExtToken x = tok::decode_ext<F>(
-                st, off, is_label, off >= kSlotBytes ? 2 * kSlotBytes : kSlotBytes);
+            const tok::ExtToken x = tok::decode_ext<F>(st, off, is_label, kSlotBytes);
             if (x.ok) t = x.t;
             ok = x.ok;
           }
         }
         if (active & !ok) {
-          const uint32_t in_slot = off >= kSlotBytes ? 1u : 0u;
-          const int step = in_slot == (static_cast<uint32_t>(s) & 1u) ? s : s - 1;
-          const size_t gpos =
-              tile0 + static_cast<size_t>(step) * kStepBytes + off - in_slot * kSlotBytes;
+          const size_t gpos = cur + off;
           const GenericResult gr = generic_token<F, IndexType>(text, n, gpos, is_label);
           t = gr.t;
           bad = gr.bad;
@@ -1359,12 +1534,6 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
         }
       }
       if (last) break;
-      // the undecoded rest moves to the front of the list (all lanes read before any writes)
-      const uint32_t left = total - ndec;
-      const uint32_t moved = lane < static_cast<int>(left) ? sl[ndec + lane] : 0u;
-      dev::wave_sync();
-      if (lane < static_cast<int>(left)) sl[lane] = moved;
-      carry = left;
       a = na;
       b = nb;
       have_full = full_next;

@@ -165,6 +165,13 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
       col[i] = e < c1 ? column(index[e], num_features) : 0u;
       v[i] = (e < c1 && value != nullptr) ? value[e] : 0.0f;
     }
+    // the row window of the rank phase below, in flight during count + scan
+    uint32_t wbase = c0 < c1 ? chunk_row[c0 / kChunk] : 0u;
+    auto window = [&](uint32_t wb) {
+      const size_t ri = static_cast<size_t>(wb) + 1 + lane;
+      return ri <= nrows ? offset[ri] - base : ~0ull;
+    };
+    uint64_t wend = window(wbase);
 #pragma unroll
     for (int i = 0; i < kPerLane; ++i) {
       if (c0 + static_cast<uint64_t>(i) * dev::kWave + lane < c1) {
@@ -204,25 +211,24 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
       if (threadIdx.x == 0) lstart[nbuckets] = nsub;
     }
     __syncthreads();
-    // ---- rank every group into the LDS sub-tile; rows from the chunk's first
-    // row: the ends of rows r .. r + 63 come in with one coalesced load, and an
-    // entry's row is r + the number of those ends at or before it (a binary
-    // search over the lanes); more than 64 row ends inside one group (empty
-    // rows) take another window
-    uint32_t r = c0 < c1 ? chunk_row[c0 / kChunk] : 0u;
+    // ---- rank every group into the LDS sub-tile.  Rows: lane i holds the end
+    // of row wbase + i (one coalesced load of 64 row ends, from the chunk's
+    // first row); an entry's row is wbase + the number of those ends at or
+    // before it (a binary search over the lanes).  The window only moves
+    // forward (rows are monotone in entry order), reloaded when a group runs
+    // past its 64 rows -- not a dependent global load per group
+
 #pragma unroll
     for (int i = 0; i < kPerLane; ++i) {
       const uint64_t g = c0 + static_cast<uint64_t>(i) * dev::kWave;
       const bool valid = g + lane < c1;
       if (!__any(valid)) continue;  // the tail of the last chunk
       const uint32_t pos = lane;
-      uint32_t row = r;
+      uint32_t row = wbase;
       bool found = !valid;
-      for (uint32_t rr = r;; rr += dev::kWave) {
-        const size_t ri = static_cast<size_t>(rr) + 1 + lane;
-        const uint64_t end = ri <= nrows ? offset[ri] - base : ~0ull;
+      for (;;) {
         const uint32_t rel =
-            end - g >= 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(end - g);
+            wend - g >= 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(wend - g);
         uint32_t n = 0;  // lanes [0, n) have rel <= pos
 #pragma unroll
         for (uint32_t step = 32; step >= 1; step >>= 1) {
@@ -232,10 +238,12 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
         const uint32_t last = __shfl(rel, dev::kWave - 1, dev::kWave);
         if (n == dev::kWave - 1 && last <= pos) n = dev::kWave;
         if (!found && n < static_cast<uint32_t>(dev::kWave)) {
-          row = rr + n;
+          row = wbase + n;
           found = true;
         }
         if (__all(found)) break;
+        wbase += dev::kWave;  // more than 64 row ends before some entry (empty rows)
+        wend = window(wbase);
       }
       const uint32_t bk = col[i] >> kLowBits;
       const uint64_t m = match_lanes(bk, bucket_bits, valid);
@@ -251,7 +259,6 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
         if (rank + 1 == n) cnt[w][bk] = before + n;  // the group's last lane of this bucket
       }
       dev::wave_sync();
-      r = __shfl(row, dev::kWave - 1, dev::kWave);  // last lane's row (invalid lanes keep r)
     }
     __syncthreads();
     // ---- the sorted sub-tile leaves in runs: consecutive threads, consecutive

@@ -770,6 +770,17 @@ PYBIND11_MODULE(_dmlc, m) {
       },
       py::arg("x"), py::arg("rows"), py::arg("dim"), py::arg("g"), py::arg("xv"),
       py::arg("nblocks"), py::arg("part"), py::arg("stream"));
+  m.def(
+      "fm_reduce_grads",
+      [stream_of](uintptr_t part, int nblocks, int dim, uintptr_t v, float sx, uintptr_t z,
+                  uintptr_t gw, uintptr_t gv, uintptr_t stream) {
+        gpu::LaunchFmReduceGrads(reinterpret_cast<const float*>(part), nblocks, dim,
+                                 reinterpret_cast<const float*>(v), sx, reinterpret_cast<float*>(z),
+                                 reinterpret_cast<float*>(gw), reinterpret_cast<float*>(gv),
+                                 stream_of(stream));
+      },
+      py::arg("part"), py::arg("nblocks"), py::arg("dim"), py::arg("v"), py::arg("sx"),
+      py::arg("z"), py::arg("gw"), py::arg("gv"), py::arg("stream"));
   m.attr("fm_rank") = gpu::kFmRank;
   m.def("shuffle_parts_order", &InputSplitShuffle::VisitOrder, py::arg("part"), py::arg("nparts"),
         py::arg("num_shuffle_parts"), py::arg("seed"), py::arg("epoch"),
