@@ -364,11 +364,18 @@ __global__ __launch_bounds__(kThreads) void k_csv_tile_fill(const uint8_t* __res
         const uint32_t col = en.y & 0xFFFFu;
         const uint32_t ent = en.y >> 16;
         const uint8_t* rb = reinterpret_cast<const uint8_t*>(ring);
-        const uint32_t c0 = rb[off];
+        // one LDS read per field: the 16 bytes from the field start serve the
+        // number, its first byte and (usually) the byte after its delimiter
+        const uint4 g16 = tok::ext16(ring, off);
+        const uint32_t c0 = g16.x & 0xFFu;
         // a field ended by a delimiter is still the row's last one when the
         // line ends right after that delimiter (no empty trailing field)
-        auto eol_at = [&](uint32_t o) {
-          const uint32_t c = rb[o];
+        const uint64_t glo = (static_cast<uint64_t>(g16.y) << 32) | g16.x;
+        const uint64_t ghi = (static_cast<uint64_t>(g16.w) << 32) | g16.z;
+        auto eol_at = [=](uint32_t o) {
+          const uint32_t i = o - off;  // a 64-bit shift, not an indexed array (scratch)
+          const uint32_t c = i < 16u ? static_cast<uint32_t>(((i < 8u ? glo : ghi) >> (8u * (i & 7u))) & 0xFFu)
+                                     : rb[o];
           return c == '\n' || c == '\r' || c == 0;
         };
         float v;
@@ -377,11 +384,13 @@ __global__ __launch_bounds__(kThreads) void k_csv_tile_fill(const uint8_t* __res
           v = 0.0f;  // empty field
           last = c0 != delim || eol_at(off + 1);
         } else {
-          const tok::Num x = tok::parse_num(ring, off);
+          const tok::Num x = tok::parse_num_g(g16, off);
           const bool t_eol = x.term == '\n' || x.term == '\r' || x.term == 0;
+          // (the window is dead before the generic call below)
+          const bool last_fast = t_eol || eol_at(x.end + 1);
           if (x.ok_float && (x.term == delim || t_eol)) {
             v = x.fval;
-            last = t_eol || eol_at(x.end + 1);
+            last = last_fast;
           } else {
             const size_t gpos = tile0 + s * kStep + (off - slot * 16u);
             const GenericField g = generic_field(reinterpret_cast<const char*>(text) + gpos,

@@ -102,12 +102,18 @@ struct Num {
   bool ok_float, ok_uint;
 };
 
+__device__ __forceinline__ Num parse_num_g(uint4 g, uint32_t a);
+
 __device__ __forceinline__ Num parse_num(const uint4* lds, uint32_t a) {
+  return parse_num_g(ext16(lds, a), a);
+}
+
+/*! \brief parse_num on the 16 bytes g already read from LDS byte a */
+__device__ __forceinline__ Num parse_num_g(uint4 g, uint32_t a) {
 #if defined(__clang__)
 #pragma clang fp contract(off)
 #endif
   Num o;
-  const uint4 g = ext16(lds, a);
   const uint32_t c0 = g.x & 0xFFu;
   const bool neg = c0 == '-';
   const uint32_t s = (neg || c0 == '+') ? 1u : 0u;

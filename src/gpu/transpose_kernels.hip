@@ -227,8 +227,11 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
       uint32_t row = wbase;
       bool found = !valid;
       for (;;) {
-        const uint32_t rel =
-            wend - g >= 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(wend - g);
+        // (ends before the group start -- rows of earlier groups still in the
+        // window -- count as at or before every entry)
+        const uint32_t rel = wend <= g ? 0u
+                             : wend - g >= 0xFFFFFFFFull ? 0xFFFFFFFFu
+                                                         : static_cast<uint32_t>(wend - g);
         uint32_t n = 0;  // lanes [0, n) have rel <= pos
 #pragma unroll
         for (uint32_t step = 32; step >= 1; step >>= 1) {
