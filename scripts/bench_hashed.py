@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--dim", type=int, default=1024)
     ap.add_argument("--sweep", default="128,256,1024",
                     help="extra dims timed for fused vs CSR+K9 (comma list, '' to skip)")
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--data", default="/tmp/dmlc_hashed_bench.libfm")
     args = ap.parse_args()
     import torch

@@ -309,20 +309,30 @@ __global__ __launch_bounds__(kThreads) void k_csv_tile_fill(const uint8_t* __res
   const uint32_t delim = cfg.delim;
   uint64_t mx = 0;
   bool irregular = false, any_value = false;
-  // slot 0 <- step 0 (+ mirror of its head past slot 1)
+  // slot 0 <- step 0 (+ mirror of its head past slot 1).  Step s + 1 is staged
+  // during step s from `pv`, which was loaded during step s - 1 (the load
+  // for step s + 2 then goes straight into `pv`: no copy of a load in flight,
+  // so no wait right behind it); bytes past n are zeroed where staged
   {
     const uint4 v = load16_clip(text, tile0 + 16u * lane, n);
     ring[lane] = v;
     if (lane < 2) ring[2 * kStep / 16 + lane] = v;
   }
+  const size_t at1 = tile0 + kStep + 16u * lane;
+  uint4 pv = *reinterpret_cast<const uint4*>(text + (at1 + 16 <= n ? at1 : 0));
   for (uint32_t s = 0; s < kMaxSteps; ++s) {
     const uint32_t slot = (s & 1u) * (kStep / 16);
-    // prefetch step s + 1 into the other slot (its head mirrored when that is slot 0)
+    // stage step s + 1 in the other slot (its head mirrored when that is slot 0)
     if (s + 1 < kMaxSteps) {
-      const uint4 v = load16_clip(text, tile0 + (s + 1) * kStep + 16u * lane, n);
+      const size_t at = tile0 + (s + 1) * kStep + 16u * lane;
+      const uint4 v = at + 16 <= n ? pv : load16_clip(text, at, n);
       const uint32_t nslot = ((s + 1) & 1u) * (kStep / 16);
       ring[nslot + lane] = v;
       if (nslot == 0 && lane < 2) ring[2 * kStep / 16 + lane] = v;
+      if (s + 2 < kMaxSteps) {
+        const size_t at2 = at + kStep;
+        pv = *reinterpret_cast<const uint4*>(text + (at2 + 16 <= n ? at2 : 0));
+      }
     }
     wave_sync();
     // the fill lists every field with its column: always the column scan
@@ -374,8 +384,8 @@ __global__ __launch_bounds__(kThreads) void k_csv_tile_fill(const uint8_t* __res
         const uint64_t ghi = (static_cast<uint64_t>(g16.w) << 32) | g16.z;
         auto eol_at = [=](uint32_t o) {
           const uint32_t i = o - off;  // a 64-bit shift, not an indexed array (scratch)
-          const uint32_t c = i < 16u ? static_cast<uint32_t>(((i < 8u ? glo : ghi) >> (8u * (i & 7u))) & 0xFFu)
-                                     : rb[o];
+          const uint64_t h = i < 8u ? glo : ghi;
+          const uint32_t c = i < 16u ? static_cast<uint32_t>((h >> (8u * (i & 7u))) & 0xFFu) : rb[o];
           return c == '\n' || c == '\r' || c == 0;
         };
         float v;

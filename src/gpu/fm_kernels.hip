@@ -222,7 +222,9 @@ __global__ __launch_bounds__(kBwdThreads) void k_fm_bwd(const uint8_t* __restric
   const int wave = threadIdx.x / kWave;
   const int fbase = 1024 * blockIdx.y + kBwdWaveFeatures * wave;
   const bool active = fbase < dim;
-  for (int i = threadIdx.x; i < 2 * 32 * 40; i += kBwdThreads) (&s_gt[0][0][0])[i] = static_cast<__bf16>(0.0f);
+  for (int i = threadIdx.x; i < 2 * 32 * 40; i += kBwdThreads) {
+    (&s_gt[0][0][0])[i] = static_cast<__bf16>(0.0f);
+  }
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
   const int64_t r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
   // identity B fragments: element j of step s is 1 for column n's (h, s, j)

@@ -195,19 +195,6 @@ __device__ __forceinline__ void wave_copy(const uint32_t* __restrict__ src, uint
   }
 }
 
-/*! \brief the check every part makes of the part that follows it */
-__device__ __forceinline__ uint32_t check_successor(const uint32_t* __restrict__ w, size_t n,
-                                                    size_t i, uint32_t cf, uint32_t len) {
-  const size_t q = i + 2 + (static_cast<size_t>(len) + 3) / 4;
-  const bool ends_record = cf == 0 || cf == 3;
-  if (q > n) return kRecErrTruncated;
-  if (q == n) return ends_record ? 0u : kRecErrTruncated;
-  if (q + 1 >= n || w[q] != kMagic) return kRecErrBadPart;
-  const uint32_t next = cflag_of(w[q + 1]);
-  const bool next_continues = next == 2 || next == 3;
-  return (ends_record == next_continues || next > 3) ? kRecErrBadPart : 0u;
-}
-
 struct BigPart {
   uint32_t word;  // chunk word index of the header
   uint32_t len;
@@ -223,6 +210,9 @@ __global__ __launch_bounds__(kThreads) void k_rec_tile_fill(const uint32_t* __re
                                                             uint64_t byte_base,
                                                             MetaPartial* __restrict__ partials) {
   __shared__ BigPart s_big[kWaves][kBigCap];
+  // the tile's words (+ the one after it): a part's successor check reads its
+  // header from here instead of a dependent global load per part
+  __shared__ uint4 s_tw[kWaves][kTileWords / 4 + 1];
   const int lane = lane_id();
   const int wave = threadIdx.x / kWave;
   const size_t tile = static_cast<size_t>(blockIdx.x) * kWaves + wave;
@@ -231,6 +221,16 @@ __global__ __launch_bounds__(kThreads) void k_rec_tile_fill(const uint32_t* __re
   const size_t base = tile * kTileWords;
   TileQuads t;
   load_tile(w, n, base, lane, &t);
+  uint32_t* const tw = reinterpret_cast<uint32_t*>(s_tw[wave]);
+#pragma unroll
+  for (int j = 0; j < kLoads; ++j) s_tw[wave][j * 64 + lane] = t.q[j];
+  if (lane == kWave - 1) tw[kTileWords] = t.after[kLoads - 1];
+  wave_sync();
+  // word q of the chunk (q < n): staged when inside the tile (+1), else global
+  auto word_at = [&](size_t q) {
+    const size_t r = q - base;
+    return r <= kTileWords ? tw[r] : w[q];
+  };
   const uint64_t pre = prefix[tile];
   uint64_t rec = pre >> 32;            // records before this 1 KiB sub-tile (chunk-relative)
   uint64_t pos = pre & 0xffffffffull;  // output bytes before it
@@ -256,7 +256,23 @@ __global__ __launch_bounds__(kThreads) void k_rec_tile_fill(const uint32_t* __re
       const uint32_t lrec = lrec_at(t.q[j], k, t.after[j]);
       const uint32_t cf = cflag_of(lrec), len = len_of(lrec);
       const size_t i = i0 + k;
-      err |= check_successor(w, n, i, cf, len);
+      {
+        // the part that follows: a continuation must follow a first / middle
+        // part, a head a whole / last part (read from the staged words)
+        const size_t q = i + 2 + (static_cast<size_t>(len) + 3) / 4;
+        const bool ends_record = cf == 0 || cf == 3;
+        if (q > n) {
+          err |= kRecErrTruncated;
+        } else if (q == n) {
+          err |= ends_record ? 0u : kRecErrTruncated;
+        } else if (q + 1 >= n || word_at(q) != kMagic) {
+          err |= kRecErrBadPart;
+        } else {
+          const uint32_t next = cflag_of(word_at(q + 1));
+          const bool next_continues = next == 2 || next == 3;
+          err |= (ends_record == next_continues || next > 3) ? kRecErrBadPart : 0u;
+        }
+      }
       if (cf <= 1) {
         offset[rec_base + r] = byte_base + p;
         ++r;
@@ -287,9 +303,47 @@ __global__ __launch_bounds__(kThreads) void k_rec_tile_fill(const uint32_t* __re
     pos += tot & 0xffffffffull;
   }
   wave_sync();  // the list is visible to every lane
-  for (uint32_t e = 0; e < nbig; ++e) {
-    const BigPart b = big[e];
-    wave_copy(w + b.word + 2, b.len, out + b.dst, lane);
+  // parts up to 1 KiB into 16-byte-aligned destinations (the common shape):
+  // kBatch parts per round, every lane's loads of all of them issued before
+  // any store, so a round waits for one memory latency instead of one per
+  // part; anything else takes the generic wave copy
+  constexpr uint32_t kBatch = 4;
+  for (uint32_t e0 = 0; e0 < nbig; e0 += kBatch) {
+    uint32_t v[kBatch][4];
+    BigPart bp[kBatch];
+    bool fast[kBatch];
+#pragma unroll
+    for (uint32_t q = 0; q < kBatch; ++q) {
+      fast[q] = false;
+      if (e0 + q < nbig) {
+        bp[q] = big[e0 + q];
+        fast[q] = bp[q].len <= 1024 && ((reinterpret_cast<uintptr_t>(out + bp[q].dst) & 15U) == 0);
+        const uint32_t b0 = static_cast<uint32_t>(lane) * 16;
+        if (fast[q] && b0 < bp[q].len) {
+          const uint32_t* src = w + bp[q].word + 2 + lane * 4;
+          const uint32_t nw = (bp[q].len - b0 + 3) / 4;  // words of this lane (<= 4)
+#pragma unroll
+          for (uint32_t k = 0; k < 4; ++k) v[q][k] = k < nw ? src[k] : 0u;
+        }
+      }
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kBatch; ++q) {
+      if (e0 + q >= nbig) break;
+      if (!fast[q]) {
+        wave_copy(w + bp[q].word + 2, bp[q].len, out + bp[q].dst, lane);
+        continue;
+      }
+      const uint32_t b0 = static_cast<uint32_t>(lane) * 16;
+      if (b0 >= bp[q].len) continue;
+      uint8_t* d = out + bp[q].dst + b0;
+      const uint32_t m = bp[q].len - b0;
+      if (m >= 16) {
+        *reinterpret_cast<uint4*>(d) = make_uint4(v[q][0], v[q][1], v[q][2], v[q][3]);
+      } else {
+        for (uint32_t k = 0; k < m; ++k) d[k] = static_cast<uint8_t>(v[q][k >> 2] >> (8 * (k & 3U)));
+      }
+    }
   }
   err = wave_or(err);
   if (lane == 0) {

@@ -836,16 +836,22 @@ constexpr uint32_t kHashListCap = 896;
  */
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
-/*! \brief a buffer resource over [base, base + avail) (raw, gfx9 dword3): the
- *  address lives in scalar registers, loads take a 32-bit lane offset */
+/*! \brief a buffer resource over the text from base on (raw, gfx9 dword3):
+ *  the address lives in scalar registers, loads take a 32-bit lane offset.
+ *  The range check zeroes whole dwords past num_records, so the record count
+ *  is the text rounded up to 16 bytes (every 16-byte load that starts inside
+ *  the text returns all its bytes; text buffers carry kTextPadBytes of
+ *  padding) and the caller zeroes the bytes past the text (clip16). */
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t text_rsrc(const uint8_t* base, size_t avail) {
-  const uint32_t nr = avail > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<uint32_t>(avail);
+  const size_t up = (avail + 15) & ~static_cast<size_t>(15);
+  const uint32_t nr = up > 0xFFFFFFF0ull ? 0xFFFFFFF0u : static_cast<uint32_t>(up);
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0, nr, 0x00020000);
 }
 
-/*! \brief 16 bytes at voff + soff of a text_rsrc (in range: the caller checks) */
-__device__ __forceinline__ uint4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+/*! \brief the 16 bytes at byte voff of a text_rsrc (zeros past its records).
+ *  The whole offset goes in voffset: the range check does not cover soffset */
+__device__ __forceinline__ uint4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0);
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
@@ -854,6 +860,15 @@ __device__ __forceinline__ uint4 load16_clip(const uint8_t* __restrict__ text, s
   const uint4 v = *reinterpret_cast<const uint4*>(text + at);
   const uint32_t keep = pos < n ? static_cast<uint32_t>(n - pos < 16 ? n - pos : 16) : 0u;
   // byte mask of the first `keep` bytes, per word
+  const uint64_t m_lo = keep >= 8 ? ~0ull : ((1ull << (8 * keep)) - 1ull);
+  const uint64_t m_hi = keep >= 16 ? ~0ull : (keep <= 8 ? 0ull : ((1ull << (8 * (keep - 8))) - 1ull));
+  return make_uint4(v.x & static_cast<uint32_t>(m_lo), v.y & static_cast<uint32_t>(m_lo >> 32),
+                    v.z & static_cast<uint32_t>(m_hi), v.w & static_cast<uint32_t>(m_hi >> 32));
+}
+
+/*! \brief v (the 16 bytes at pos) with the bytes at or past n zeroed */
+__device__ __forceinline__ uint4 clip16(uint4 v, size_t pos, size_t n) {
+  const uint32_t keep = pos < n ? static_cast<uint32_t>(n - pos < 16 ? n - pos : 16) : 0u;
   const uint64_t m_lo = keep >= 8 ? ~0ull : ((1ull << (8 * keep)) - 1ull);
   const uint64_t m_hi = keep >= 16 ? ~0ull : (keep <= 8 ? 0ull : ((1ull << (8 * (keep - 8))) - 1ull));
   return make_uint4(v.x & static_cast<uint32_t>(m_lo), v.y & static_cast<uint32_t>(m_lo >> 32),
@@ -934,7 +949,8 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
   __shared__ uint4 s_text[kFillWaves][kStageVecs];
   __shared__ uint32_t s_list[kFillWaves][kListCap + 64];  // + a dummy slot per lane
   __shared__ uint32_t s_dq[kFillWaves][2][2 * dev::kWave];   // deferred tokens: entry, ordinal
-  const int wave = threadIdx.x / dev::kWave;
+  // wave-uniform in a scalar register: the tile's buffer resource stays scalar
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / dev::kWave);
   const int lane = dev::lane_id();
   const size_t tile = static_cast<size_t>(blockIdx.x) * kFillWaves + wave;
   if (tile >= ntiles) return;  // whole waves leave; nothing below synchronises waves
@@ -946,11 +962,18 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
   const uint32_t slot = round_slot(lane);
   const size_t tile0 = tile * kTileBytes;
 
-  // ---- 1. the first step in flight; each step prefetches the next (the
-  // last one prefetches the 64 bytes past the tile)
-  uint4 a = load16_clip(text, tile0 + lane * 16, n);
-  uint4 b = load16_clip(text, tile0 + 1024 + lane * 16, n);
+  // ---- 1. the first step in flight.  Each step's loads go into the previous
+  // step's registers once its masks are built (no register copies of loads
+  // in flight, so no wait right behind the load), and the tail a step stages
+  // -- the next step's first 64 B -- is loaded one step ahead in `t`.  Bytes
+  // at or past n are zeroed where a step is staged (buffer loads past the
+  // resource return zeros; clip16 handles the last partial dword).
   const __amdgpu_buffer_rsrc_t trs = text_rsrc(text + tile0, n - tile0);
+  const uint32_t loff = static_cast<uint32_t>(lane) * 16;
+  uint4 a = bload16(trs, loff);
+  uint4 b = bload16(trs, loff + 1024);
+  uint4 t = make_uint4(0, 0, 0, 0);
+  if (lane < 4) t = bload16(trs, loff + kStepBytes);
   uint32_t carry_pc = tile0 == 0 ? static_cast<uint32_t>('\n') : text[tile0 - 1];
   const uint64_t pre = prefix[tile];
   const uint64_t line_base = pre >> 32;
@@ -989,29 +1012,20 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
 
 #pragma unroll 1
   for (int s = 0; s < kSteps; ++s) {
-    // prefetch: the next step (lanes 0..3 of it are also this step's tail)
-    const size_t nxt = tile0 + (s + 1) * kStepBytes;
     const bool last = s + 1 == kSteps;
-    uint4 na, nb = make_uint4(0, 0, 0, 0);
-    if (nxt + kStepBytes <= n) {  // wave-uniform: no byte of the next step is past n
-      // buffer loads: scalar base, 32-bit lane offset (no 64-bit address pair
-      // kept live across the step)
-      const uint32_t so = static_cast<uint32_t>(s + 1) * kStepBytes;
-      na = bload16(trs, static_cast<uint32_t>(lane) * 16, so);
-      if (!last) nb = bload16(trs, static_cast<uint32_t>(lane) * 16, so + 1024);
-    } else {
-      na = load16_clip(text, nxt + lane * 16, n);
-      if (!last) nb = load16_clip(text, nxt + 1024 + lane * 16, n);
+    const size_t pos_a = tile0 + s * kStepBytes + lane * 16;
+    if (tile0 + static_cast<size_t>(s + 1) * kStepBytes + 64 > n) {  // wave-uniform: the text ends here
+      a = clip16(a, pos_a, n);
+      b = clip16(b, pos_a + 1024, n);
+      t = clip16(t, pos_a + kStepBytes, n);
     }
-    if (last && lane >= 4) na = make_uint4(0, 0, 0, 0);
     // ---- 2. stage the step (+ the next 64 B) in slot s & 1 -- the other slot
     // still holds step s - 1 for the tokens carried from it -- and list its tokens
     const uint32_t sbase = (static_cast<uint32_t>(s) & 1u) * kSlotBytes;
     uint4* const ss = st + sbase / 16;
     ss[lane] = a;
     ss[64 + lane] = b;
-    if (lane < 4) ss[128 + lane] = na;
-    const size_t pos_a = tile0 + s * kStepBytes + lane * 16;
+    if (lane < 4) ss[128 + lane] = t;
     const uint32_t left_a = __shfl_up(a.w >> 24, 1, dev::kWave);
     const uint32_t pc_a = lane == 0 ? carry_pc : left_a;
     const uint32_t left_b = __shfl_up(b.w >> 24, 1, dev::kWave);
@@ -1037,6 +1051,13 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
       qb = tm_b & letter_mask(b);
       tm_a &= ~qa;
       tm_b &= ~qb;
+    }
+    // a, b, t are consumed: the next step's loads go straight into them
+    if (!last) {
+      const uint32_t so = static_cast<uint32_t>(s + 1) * kStepBytes;
+      a = bload16(trs, loff + so);
+      b = bload16(trs, loff + so + 1024);
+      if (lane < 4) t = bload16(trs, loff + so + kStepBytes);
     }
     // one 64-bit scan of four 16-bit counts: tokens / lines of both slices
     const uint64_t cnt = static_cast<uint64_t>(__popc(tm_a)) |
@@ -1226,8 +1247,6 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
     tok0 += ndec;
     carry = left;
     lcnt += nline;
-    a = na;
-    b = nb;
     dev::wave_sync();  // every lane is done with this step's text and list
   }
   unsigned fl = 0;
@@ -1311,7 +1330,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
   __shared__ uint4 s_text[kFillWaves][kSlotBytes / 16];
   __shared__ uint32_t s_list[kFillWaves][kHashListCap + 64];
   extern __shared__ __attribute__((aligned(16))) float s_hrow[];  // kFillWaves x dim
-  const int wave = threadIdx.x / dev::kWave;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / dev::kWave);
   const int lane = dev::lane_id();
   const size_t tile = static_cast<size_t>(blockIdx.x) * kFillWaves + wave;
   if (tile >= ntiles) return;  // whole waves leave; nothing below synchronises waves
@@ -1361,41 +1380,32 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
       dev::wave_sync();  // zeros land before the next row's adds
     };
 
-    uint4 a = load16_clip(text, tile0 + lane * 16, n);
-    uint4 b = load16_clip(text, tile0 + 1024 + lane * 16, n);
+    // loads as in k_tile_fill: the next step's go into a / b / t once they are
+    // consumed (no copies of loads in flight), clipped where staged
+    const __amdgpu_buffer_rsrc_t trs = text_rsrc(text + tile0, n - tile0);
+    const uint32_t loff = static_cast<uint32_t>(lane) * 16;
+    uint4 a = bload16(trs, loff);
+    uint4 b = bload16(trs, loff + 1024);
+    uint4 t = make_uint4(0, 0, 0, 0);
+    if (lane < 4) t = bload16(trs, loff + kStepBytes);
     uint32_t carry_pc = tile0 == 0 ? static_cast<uint32_t>('\n') : text[tile0 - 1];
     uint32_t lcnt = 0;   // line starts seen so far (this tile's ordinals)
     uint32_t open = 0;   // ordinal of the row being accumulated (0: none yet)
     uint32_t qid_prev = 0;  // LibSVM: status of the last token start (prev_token_status)
-    bool have_full = true;  // a / b hold the whole current step
 #pragma unroll 1
     for (int s = 0;; ++s) {
       const size_t cur = tile0 + static_cast<size_t>(s) * kStepBytes;
-      if (!have_full) {  // a line running > 2 KiB past the tile: load what was not prefetched
-        a = load16_clip(text, cur + lane * 16, n);
-        b = load16_clip(text, cur + 1024 + lane * 16, n);
-      }
-      // prefetch: the next step whole while it lies in the tile or is the first
-      // extension step, else only its first 64 B (this step's tail)
       const size_t nxt = cur + kStepBytes;
-      const bool full_next = s + 1 <= kSteps;
-      uint4 na = make_uint4(0, 0, 0, 0), nb = make_uint4(0, 0, 0, 0);
-      if (full_next) {
-        if (nxt + kStepBytes <= n) {
-          na = *reinterpret_cast<const uint4*>(text + nxt + lane * 16);
-          nb = *reinterpret_cast<const uint4*>(text + nxt + 1024 + lane * 16);
-        } else {
-          na = load16_clip(text, nxt + lane * 16, n);
-          nb = load16_clip(text, nxt + 1024 + lane * 16, n);
-        }
-      } else if (lane < 4) {
-        na = load16_clip(text, nxt + lane * 16, n);
+      const size_t pos_a = cur + lane * 16;
+      if (nxt + 64 > n) {  // wave-uniform: the text ends here
+        a = clip16(a, pos_a, n);
+        b = clip16(b, pos_a + 1024, n);
+        t = clip16(t, pos_a + kStepBytes, n);
       }
       constexpr uint32_t sbase = 0;  // the one slot
       st[lane] = a;
       st[64 + lane] = b;
-      if (lane < 4) st[128 + lane] = na;
-      const size_t pos_a = cur + lane * 16;
+      if (lane < 4) st[128 + lane] = t;
       const uint32_t left_a = __shfl_up(a.w >> 24, 1, dev::kWave);
       const uint32_t pc_a = lane == 0 ? carry_pc : left_a;
       const uint32_t left_b = __shfl_up(b.w >> 24, 1, dev::kWave);
@@ -1470,6 +1480,14 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
       lcnt += nline;
       const bool eol_end = carry_pc == '\n' || carry_pc == '\r';
       const bool last = nxt >= n || lcnt > own || (s + 1 >= kSteps && lcnt == own && eol_end);
+      // a, b, t are consumed: the next step's loads go straight into them (in
+      // flight during this step's rounds)
+      if (!last) {
+        const uint32_t so = static_cast<uint32_t>(s + 1) * kStepBytes;
+        a = bload16(trs, loff + so);
+        b = bload16(trs, loff + so + 1024);
+        if (lane < 4) t = bload16(trs, loff + so + kStepBytes);
+      }
 
       const uint32_t ndec = ntok;
       for (uint32_t r0 = 0; r0 < ndec; r0 += dev::kWave) {
@@ -1534,9 +1552,6 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
         }
       }
       if (last) break;
-      a = na;
-      b = nb;
-      have_full = full_next;
       dev::wave_sync();  // every lane is done with this step's text and list
     }
     if (open != 0) flush(open);

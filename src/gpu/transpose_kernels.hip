@@ -50,8 +50,8 @@ constexpr int kWaves = kThreads / dev::kWave;
 constexpr int kLowBits = 12;
 constexpr uint32_t kLow = 1u << kLowBits;  // columns per bucket
 constexpr uint32_t kMaxBuckets = 1024;
-constexpr size_t kBlockElems = 32768;      // T1 / T3 block (per workgroup)
-constexpr uint32_t kSubElems = 4096;        // T3 sub-tile, sorted in LDS
+constexpr uint32_t kSubElems = 3072;        // T3 sub-tile, sorted in LDS (3 workgroups / CU)
+constexpr size_t kBlockElems = 10 * kSubElems;  // T1 / T3 block (per workgroup)
 constexpr uint32_t kChunk = kSubElems / kWaves;  // entries per wave per sub-tile
 constexpr int kPerLane = kChunk / dev::kWave;
 constexpr int kSegments = 16;              // T4 segments per bucket
@@ -139,15 +139,19 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
   __shared__ uint32_t s_col[kSubElems];
   __shared__ uint32_t s_row[kSubElems];
   __shared__ float s_val[kSubElems];
-  __shared__ uint32_t cnt[kWaves][kMaxBuckets];  // per-wave counts, then LDS cursors
-  __shared__ uint32_t lstart[kMaxBuckets + 1];   // bucket starts inside the sub-tile
-  __shared__ uint64_t gcur[kMaxBuckets];         // the block's next position per bucket
+  // per-wave counts, then LDS cursors (<= kSubElems: 16 bits); bucket starts
+  // inside the sub-tile; the block's next output position per bucket (nnz <
+  // 2^32: 32 bits)
+  __shared__ uint16_t cnt[kWaves][kMaxBuckets];
+  __shared__ uint16_t lstart[kMaxBuckets + 2];
+  __shared__ uint32_t gcur[kMaxBuckets];
   __shared__ uint32_t swave[kWaves];
   const int w = threadIdx.x / dev::kWave;
   const int lane = dev::lane_id();
+  const uint64_t below = lanes_below();
   for (uint32_t b = threadIdx.x; b < nbuckets; b += kThreads) {
     for (int q = 0; q < kWaves; ++q) cnt[q][b] = 0;
-    gcur[b] = G[static_cast<size_t>(b) * nblocks + blockIdx.x];
+    gcur[b] = static_cast<uint32_t>(G[static_cast<size_t>(b) * nblocks + blockIdx.x]);
   }
   __syncthreads();
   const uint64_t blk0 = static_cast<uint64_t>(blockIdx.x) * kBlockElems;
@@ -172,11 +176,21 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
       return ri <= nrows ? offset[ri] - base : ~0ull;
     };
     uint64_t wend = window(wbase);
+    // ---- count per bucket: lanes of a group with equal buckets from ballots
+    // over the bucket bits (no atomics); each group's rank among its equal
+    // buckets and their number stay in registers for the rank phase
+    uint32_t rk[kPerLane];  // rank | n << 8 (n <= 64)
 #pragma unroll
     for (int i = 0; i < kPerLane; ++i) {
-      if (c0 + static_cast<uint64_t>(i) * dev::kWave + lane < c1) {
-        atomicAdd(&cnt[w][col[i] >> kLowBits], 1u);
-      }
+      const bool valid = c0 + static_cast<uint64_t>(i) * dev::kWave + lane < c1;
+      const uint32_t bk = col[i] >> kLowBits;
+      const uint64_t m = match_lanes(bk, bucket_bits, valid);
+      const uint32_t rank = static_cast<uint32_t>(__popcll(m & below));
+      const uint32_t n = static_cast<uint32_t>(__popcll(m));
+      rk[i] = rank | (n << 8);
+      // the group's last lane of each bucket adds the group's count (one
+      // lane per bucket: no conflicts; groups in program order)
+      if (valid && rank + 1 == n) cnt[w][bk] = static_cast<uint16_t>(cnt[w][bk] + n);
     }
     __syncthreads();
     // ---- exclusive scan in (bucket, wave) order: thread t owns 4 buckets
@@ -200,15 +214,15 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
       for (uint32_t i = 0; i < kOwn; ++i) {
         const uint32_t b = b0 + i;
         if (b < nbuckets) {
-          lstart[b] = x;
+          lstart[b] = static_cast<uint16_t>(x);
           for (int q = 0; q < kWaves; ++q) {
             const uint32_t c = cnt[q][b];
-            cnt[q][b] = x;
+            cnt[q][b] = static_cast<uint16_t>(x);
             x += c;
           }
         }
       }
-      if (threadIdx.x == 0) lstart[nbuckets] = nsub;
+      if (threadIdx.x == 0) lstart[nbuckets] = static_cast<uint16_t>(nsub);
     }
     __syncthreads();
     // ---- rank every group into the LDS sub-tile.  Rows: lane i holds the end
@@ -217,7 +231,6 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
     // before it (a binary search over the lanes).  The window only moves
     // forward (rows are monotone in entry order), reloaded when a group runs
     // past its 64 rows -- not a dependent global load per group
-
 #pragma unroll
     for (int i = 0; i < kPerLane; ++i) {
       const uint64_t g = c0 + static_cast<uint64_t>(i) * dev::kWave;
@@ -249,9 +262,7 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
         wend = window(wbase);
       }
       const uint32_t bk = col[i] >> kLowBits;
-      const uint64_t m = match_lanes(bk, bucket_bits, valid);
-      const uint32_t rank = static_cast<uint32_t>(__popcll(m & lanes_below()));
-      const uint32_t n = static_cast<uint32_t>(__popcll(m));
+      const uint32_t rank = rk[i] & 0xFFu, n = rk[i] >> 8;
       const uint32_t before = valid ? cnt[w][bk] : 0u;
       dev::wave_sync();  // every lane has read its cursor
       if (valid) {
@@ -259,7 +270,7 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
         s_col[slot] = col[i];
         s_row[slot] = row;
         s_val[slot] = v[i];
-        if (rank + 1 == n) cnt[w][bk] = before + n;  // the group's last lane of this bucket
+        if (rank + 1 == n) cnt[w][bk] = static_cast<uint16_t>(before + n);  // the group's last lane
       }
       dev::wave_sync();
     }
@@ -269,14 +280,14 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
     for (uint32_t j = threadIdx.x; j < nsub; j += kThreads) {
       const uint32_t c = s_col[j];
       const uint32_t b = c >> kLowBits;
-      const uint64_t p = gcur[b] + (j - lstart[b]);
+      const uint64_t p = static_cast<uint64_t>(gcur[b]) + (j - lstart[b]);
       t_key[p] = static_cast<uint16_t>(c & (kLow - 1u));
       t_row[p] = s_row[j];
       if (value != nullptr) t_val[p] = s_val[j];
     }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < nbuckets; b += kThreads) {
-      gcur[b] += lstart[b + 1] - lstart[b];
+      gcur[b] += static_cast<uint32_t>(lstart[b + 1] - lstart[b]);
       for (int q = 0; q < kWaves; ++q) cnt[q][b] = 0;
     }
     __syncthreads();
