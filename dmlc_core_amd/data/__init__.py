@@ -136,8 +136,17 @@ class GPUParser:
         handle = out.get("batch") if isinstance(out, dict) else out
         if handle is not None and torch.cuda.is_available():
             # the refill must not overtake torch work still reading the old batch
-            torch.cuda.ExternalStream(self._p.stream()).wait_stream(torch.cuda.current_stream())
+            if getattr(self, "_ext_stream", None) is None:
+                self._ext_stream = torch.cuda.ExternalStream(self._p.stream())
+            self._ext_stream.wait_stream(torch.cuda.current_stream())
         d = self._p.parse_all_hashed(int(dim), float(scale), int(seed) & 0xFFFFFFFF, bool(fp8), handle)
+        if isinstance(out, dict) and out.get("batch") is d["batch"] and "x" in out:
+            # refilled in place with the same shape: the tensors already alias it
+            x0 = out["x"]
+            if (tuple(x0.shape) == (d["rows"], d["dim"]) and x0.data_ptr() == d["x_ptr"]
+                    and out["label"].data_ptr() == d["label_ptr"]
+                    and (x0.dtype == torch.float8_e4m3fn) == bool(fp8)):
+                return out
         x = tdl.from_dlpack(d["x"]).view(d["rows"], d["dim"])
         if fp8:
             x = x.view(torch.float8_e4m3fn)

@@ -215,8 +215,8 @@ __global__ __launch_bounds__(kBwdThreads) void k_fm_bwd(const uint8_t* __restric
                                                         float* __restrict__ part) {
   // G^T [column][row] (columns 17..31 zero) and g, double-buffered: the next
   // tile's G is written while this one is consumed, one barrier per tile
-  __shared__ __bf16 s_gt[2][32][32 + 8];
-  __shared__ float s_g[2][32];
+  __shared__ __attribute__((aligned(16))) __bf16 s_gt[2][32][32 + 8];
+  __shared__ __attribute__((aligned(16))) float s_g[2][32];
   const int lane = lane_id();
   const int h = lane >> 5, n = lane & 31;
   const int wave = threadIdx.x / kWave;
@@ -241,16 +241,29 @@ __global__ __launch_bounds__(kBwdThreads) void k_fm_bwd(const uint8_t* __restric
   float tacc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   // the next tile's X fragment and G inputs are loaded while this tile computes
   const int grow = threadIdx.x >> 3, gpart = threadIdx.x & 7;  // G producer (threads < 256)
+  // loads are issued unconditionally (a clamped row, the value zeroed past
+  // the block's rows): every tile issues the same memory ops, so the wait for
+  // a load counts only the ops issued after it
+  const int64_t rlast = r1 > r0 ? r1 - 1 : r0;
   auto load_g = [&](int64_t t, float* gv, float2* v) {
     const int64_t r = t + grow;
     const bool ok = threadIdx.x < 256 && r < r1;
-    *gv = ok ? g[r] : 0.0f;
-    *v = ok ? *reinterpret_cast<const float2*>(xv + r * kFmRank + 2 * gpart) : make_float2(0.0f, 0.0f);
+    const int64_t rc = r < rlast ? r : rlast;
+    const float g0 = g[rc];
+    const float2 v0 = *reinterpret_cast<const float2*>(xv + rc * kFmRank + 2 * gpart);
+    *gv = ok ? g0 : 0.0f;
+    *v = ok ? v0 : make_float2(0.0f, 0.0f);
   };
   auto load_x = [&](int64_t t, uint4 (&w)[4]) {
     const int64_t r = t + n;  // the row of this lane's X fragment
     const bool ok = active && r < r1;
-    load64(x + (ok ? r : 0) * dim + fbase + 64 * h, ok, w);
+    const int64_t rc = r < rlast ? r : rlast;
+    const uint4* q = reinterpret_cast<const uint4*>(x + rc * dim + (active ? fbase : 0) + 64 * h);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint4 u = q[i];
+      w[i] = ok ? u : make_uint4(0, 0, 0, 0);
+    }
   };
   auto put_g = [&](int bf, float gv, float2 v) {
     if (threadIdx.x < 256) {
@@ -264,35 +277,45 @@ __global__ __launch_bounds__(kBwdThreads) void k_fm_bwd(const uint8_t* __restric
   };
   float gv_n = 0.0f;
   float2 v_n = make_float2(0.0f, 0.0f);
-  uint4 xw[4], xw_n[4];
-  if (r0 < r1) {
-    load_g(r0, &gv_n, &v_n);
-    load_x(r0, xw_n);
-  }
+  // X tiles rotate through three register buffers: tile i's fragment is
+  // loaded while tiles i - 2 and i - 1 compute, into the buffer tile i - 3
+  // just released (no register copies of loads in flight)
+  uint4 x0[4], x1[4], x2[4];
+  load_g(r0, &gv_n, &v_n);
+  load_x(r0, x0);
+  load_x(r0 + 32, x1);
+  load_x(r0 + 64, x2);
   __syncthreads();  // the zeroed buffers
   put_g(0, gv_n, v_n);
-  if (r0 + 32 < r1) load_g(r0 + 32, &gv_n, &v_n);
+  load_g(r0 + 32, &gv_n, &v_n);
   __syncthreads();
   int cb = 0;
-  for (int64_t t0 = r0; t0 < r1; t0 += 32) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) xw[i] = xw_n[i];
-    if (t0 + 32 < r1) {
-      load_x(t0 + 32, xw_n);
-      put_g(cb ^ 1, gv_n, v_n);  // the next tile's G (its buffer was consumed last tile)
-      if (t0 + 64 < r1) load_g(t0 + 64, &gv_n, &v_n);
-    }
+  // one 32-row tile: the next tile's G into the other buffer, this tile's
+  // products, then its X buffer takes the tile three ahead.  Tiles past the
+  // block's rows (to a multiple of three) see zero X and G: they add nothing
+  auto tile = [&](int64_t t0, uint4 (&xw)[4]) {
+    put_g(cb ^ 1, gv_n, v_n);  // the next tile's G (its buffer was consumed last tile)
+    load_g(t0 + 64, &gv_n, &v_n);
     if (active) {
       // G^T fragments: element j of step s = row 16 s + 8 (j >> 2) + 4 h + (j & 3)
+      // (8-byte LDS reads: elements j = 0..3 and 4..7 are 4 consecutive rows)
       bf16x8 ga[2];
+      const uint2* gt_row = reinterpret_cast<const uint2*>(&s_gt[cb][n][0]);
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ga[s][j] = s_gt[cb][n][16 * s + 8 * (j >> 2) + 4 * h + (j & 3)];
+        const uint2 lo = gt_row[4 * s + h], hi = gt_row[4 * s + 2 + h];
+        const uint4 q = make_uint4(lo.x, lo.y, hi.x, hi.y);
+        ga[s] = __builtin_bit_cast(bf16x8, q);
       }
       float gr[16];
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) gr[reg] = s_g[cb][(reg & 3) + 8 * (reg >> 2) + 4 * h];
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const float4 g4 = *reinterpret_cast<const float4*>(&s_g[cb][8 * r4 + 4 * h]);
+        gr[4 * r4 + 0] = g4.x;
+        gr[4 * r4 + 1] = g4.y;
+        gr[4 * r4 + 2] = g4.z;
+        gr[4 * r4 + 3] = g4.w;
+      }
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         // T: this block's 32 x 32 X tile, features on lanes, rows in registers
@@ -316,8 +339,14 @@ __global__ __launch_bounds__(kBwdThreads) void k_fm_bwd(const uint8_t* __restric
         }
       }
     }
+    load_x(t0 + 96, xw);
     __syncthreads();  // buffer cb consumed; buffer cb ^ 1 written
     cb ^= 1;
+  };
+  for (int64_t t0 = r0; t0 < r1; t0 += 96) {
+    tile(t0, x0);
+    tile(t0 + 32, x1);
+    tile(t0 + 64, x2);
   }
   if (!active) return;
   float* out = part + static_cast<size_t>(blockIdx.x) * (kFmCols + 1) * dim;

@@ -415,6 +415,8 @@ class PyDeviceParser {
                            batch->device, batch);
     d["rows"] = batch->rows;
     d["dim"] = dim;
+    d["x_ptr"] = reinterpret_cast<uintptr_t>(batch->x.get());
+    d["label_ptr"] = reinterpret_cast<uintptr_t>(batch->label.get());
     d["batch"] = py::cast(batch);
     return d;
   }

@@ -184,6 +184,7 @@ def test_fused_batch_reuse(dataset):
     for _ in range(2):
         g.before_first()
         b = g.parse_all_hashed(1024, seed=4, out=a)
+        assert b is a  # same shape: the tensors already alias the refilled batch
         assert b["x"].data_ptr() == ptr
         assert torch.equal(b["x"].view(torch.uint8), want)
     g.before_first()
