@@ -46,8 +46,12 @@ class _HashedFMFunction(torch.autograd.Function):
     def forward(ctx, x8, sx: float, w, v, bias):
         rows, dim = x8.shape
         dev = x8.device
-        wt = torch.cat([w, v], dim=1).detach().t().contiguous().to(torch.bfloat16)
-        q = (v.detach().float() ** 2).sum(1).contiguous()
+        # F0: [w | V]^T in bf16 and q = rowsum(V^2), one kernel
+        wf = w.detach().float().contiguous()
+        vf = v.detach().float().contiguous()
+        wt = torch.empty((v.shape[1] + 1, dim), dtype=torch.bfloat16, device=dev)
+        q = torch.empty(dim, dtype=torch.float32, device=dev)
+        _dmlc().fm_prep(wf.data_ptr(), vf.data_ptr(), dim, wt.data_ptr(), q.data_ptr(), _stream())
         b = bias.detach().float().contiguous()
         y = torch.empty(rows, dtype=torch.float32, device=dev)
         xv = torch.empty((rows, v.shape[1]), dtype=torch.float32, device=dev)

@@ -108,7 +108,8 @@ def transpose(csr: Dict, num_features: int) -> Dict:
                          f"{_dmlc.csr_transpose_max_features()}], got {num_features}")
     off = offset.view(torch.int64) if offset.dtype != torch.int64 else offset
     # the rows may be a slice of a larger CSR: entries [off[0], off[-1]) of index / value
-    lo, hi = (int(off[0]), int(off[-1])) if nrows > 0 else (0, 0)
+    # (one device read for both ends)
+    lo, hi = (int(v) for v in off[[0, -1]].tolist()) if nrows > 0 else (0, 0)
     nnz = hi - lo
     col_ptr = torch.empty(num_features + 1, dtype=torch.int64, device=dev)
     rows = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)

@@ -84,6 +84,28 @@ def main():
     torch.cuda.synchronize()
     res["hashed_fm_step_ms"] = round((time.perf_counter() - t0) / args.steps * 1e3, 3)
     res["hashed_fm_gemm"] = model.gemm
+    # the same step captured once as a HIP graph and replayed (forward, loss,
+    # backward into the parameters' .grad): no per-kernel host launch cost
+    xs, ls = batch["x"], batch["label"].clamp(0, 1)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            model.zero_grad(set_to_none=True)
+            torch.nn.functional.binary_cross_entropy_with_logits(model(xs, scale=0.5), ls).backward()
+    torch.cuda.current_stream().wait_stream(side)
+    model.zero_grad(set_to_none=True)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        static_loss = torch.nn.functional.binary_cross_entropy_with_logits(model(xs, scale=0.5), ls)
+        static_loss.backward()
+    graph.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        graph.replay()
+    torch.cuda.synchronize()
+    res["hashed_fm_step_graph_ms"] = round((time.perf_counter() - t0) / args.steps * 1e3, 3)
     res.update({"rows": int(batch["x"].shape[0]), "dim": args.dim, "text_bytes": nbytes,
                 "speedup_fused_vs_csr_k9": round(res["csr_then_k9"]["ms"] / res["fused"]["ms"], 3)})
     sweep = {}

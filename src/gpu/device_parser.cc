@@ -172,7 +172,11 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     } else {
       reader_.reset(new io::ShardReader(split_.get(), cfg_.read_threads));
     }
-    compute_.reset(new Stream());
+    // the parse kernels' stream outranks the prelaunched counts' (a fill's or
+    // hash's closing kernels are not queued behind the next chunk's count)
+    int least_prio = 0, greatest_prio = 0;
+    DMLC_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least_prio, &greatest_prio));
+    compute_.reset(new Stream(greatest_prio));
     copy_.reset(new Stream());
     for (int d = 0; d < cfg_.device_slots; ++d) {
       dtext_.emplace_back(new DeviceBuffer(cfg_.chunk_bytes + kTextPadBytes));
@@ -478,10 +482,11 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
         // and host round trips per byte)
         // (a chunk whose text ends without EOL -- a file's unterminated last
         // line on the zero-copy path -- must stay its own chunk).  The merged
-        // size grows 4x per chunk from kFirstMerge: the first chunk's count +
-        // scan is the only one not hidden behind a previous chunk's fill
-        // (the next count runs on count_stream_ meanwhile, ~1/4 of a fill)
-        merge_cap_ = merge_cap_ == 0 ? kFirstMerge : merge_cap_ * 4;
+        // size doubles per chunk from kFirstMerge: the first chunk's count +
+        // scan is the only one not hidden behind a previous chunk's fill (the
+        // next count runs on count_stream_ meanwhile, and next to a fill it
+        // takes about half the fill's time per byte: 2x keeps it hidden)
+        merge_cap_ = merge_cap_ == 0 ? kFirstMerge : merge_cap_ * 2;
         const size_t cap = std::min(merge_cap_, cfg_.replay_chunk_bytes);
         while (merge_replay_ && replay_idx_ < replay_list_.size() &&
                cached_[replay_list_[replay_idx_ - 1]].eol_end &&

@@ -422,7 +422,35 @@ __global__ __launch_bounds__(kWave) void k_fm_grads(const float* __restrict__ z,
   }
 }
 
+/*! \brief F0: [w | V]^T as bf16 [kFmCols][dim] and q = rowsum(V^2) (f32) */
+__global__ __launch_bounds__(256) void k_fm_prep(const float* __restrict__ w,
+                                                 const float* __restrict__ v, int dim,
+                                                 __bf16* __restrict__ wt, float* __restrict__ q) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= dim) return;
+  wt[k] = static_cast<__bf16>(w[k]);
+  const float4* vr = reinterpret_cast<const float4*>(v + static_cast<size_t>(k) * kFmRank);
+  float acc = 0.0f;
+#pragma unroll
+  for (int j = 0; j < kFmRank / 4; ++j) {
+    const float4 a = vr[j];
+    wt[static_cast<size_t>(1 + 4 * j) * dim + k] = static_cast<__bf16>(a.x);
+    wt[static_cast<size_t>(2 + 4 * j) * dim + k] = static_cast<__bf16>(a.y);
+    wt[static_cast<size_t>(3 + 4 * j) * dim + k] = static_cast<__bf16>(a.z);
+    wt[static_cast<size_t>(4 + 4 * j) * dim + k] = static_cast<__bf16>(a.w);
+    acc += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;
+  }
+  q[k] = acc;
+}
+
 }  // namespace
+
+void LaunchFmPrep(const float* w, const float* v, int dim, void* wt_bf16, float* q,
+                  hipStream_t stream) {
+  if (dim == 0) return;
+  hipLaunchKernelGGL(k_fm_prep, dim3((dim + 255) / 256), dim3(256), 0, stream, w, v, dim,
+                     static_cast<__bf16*>(wt_bf16), q);
+}
 
 void LaunchFmReduceGrads(const float* part, int nblocks, int dim, const float* v, float sx,
                          float* z, float* gw, float* gv, hipStream_t stream) {

@@ -323,6 +323,10 @@ void LaunchFmBackward(const uint8_t* x, int64_t rows, int dim, const float* g, c
                       int nblocks, float* part, hipStream_t stream);
 /*! \brief sum the LaunchFmBackward partials (z: [kFmCols + 1][dim] scratch)
  *  and write dw [dim] and dV [dim][kFmRank] (v: [dim][kFmRank] f32) */
+/*! \brief [w | V]^T in bf16 ([kFmCols][dim]) and q = rowsum(V^2) for LaunchFmForward
+ *  (w: [dim] f32, v: [dim][kFmRank] f32) */
+void LaunchFmPrep(const float* w, const float* v, int dim, void* wt_bf16, float* q,
+                  hipStream_t stream);
 void LaunchFmReduceGrads(const float* part, int nblocks, int dim, const float* v, float sx,
                          float* z, float* gw, float* gv, hipStream_t stream);
 

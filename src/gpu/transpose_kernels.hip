@@ -314,8 +314,27 @@ __global__ __launch_bounds__(kThreads) void k_lowkey_hist(const uint16_t* __rest
   __syncthreads();
   uint64_t e0, e1;
   segment(bstart, b, s, &e0, &e1);
-#pragma unroll 8
-  for (uint64_t e = e0 + threadIdx.x; e < e1; e += kThreads) atomicAdd(&hist[t_key[e]], 1u);
+  // eight keys per 16-byte load over the aligned middle of the segment, the
+  // unaligned head and tail one key at a time
+  const uint64_t a0 = (e0 + 7) & ~7ull, a1 = e1 & ~7ull;
+  if (a0 >= a1) {
+    for (uint64_t e = e0 + threadIdx.x; e < e1; e += kThreads) atomicAdd(&hist[t_key[e]], 1u);
+  } else {
+    for (uint64_t e = e0 + threadIdx.x; e < a0; e += kThreads) atomicAdd(&hist[t_key[e]], 1u);
+    for (uint64_t e = a1 + threadIdx.x; e < e1; e += kThreads) atomicAdd(&hist[t_key[e]], 1u);
+    const uint4* k8 = reinterpret_cast<const uint4*>(t_key + a0);
+    const uint64_t n8 = (a1 - a0) / 8;
+#pragma unroll 2
+    for (uint64_t i = threadIdx.x; i < n8; i += kThreads) {
+      const uint4 q = k8[i];
+      const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        atomicAdd(&hist[w[j] & 0xFFFFu], 1u);
+        atomicAdd(&hist[w[j] >> 16], 1u);
+      }
+    }
+  }
   __syncthreads();
   uint32_t* out = H + static_cast<size_t>(blockIdx.x) * kLow;
   for (uint32_t c = threadIdx.x; c < kLow; c += kThreads) out[c] = hist[c];

@@ -773,6 +773,14 @@ PYBIND11_MODULE(_dmlc, m) {
       py::arg("x"), py::arg("rows"), py::arg("dim"), py::arg("g"), py::arg("xv"),
       py::arg("nblocks"), py::arg("part"), py::arg("stream"));
   m.def(
+      "fm_prep",
+      [stream_of](uintptr_t w, uintptr_t v, int dim, uintptr_t wt, uintptr_t q, uintptr_t stream) {
+        gpu::LaunchFmPrep(reinterpret_cast<const float*>(w), reinterpret_cast<const float*>(v),
+                          dim, reinterpret_cast<void*>(wt), reinterpret_cast<float*>(q),
+                          stream_of(stream));
+      },
+      py::arg("w"), py::arg("v"), py::arg("dim"), py::arg("wt"), py::arg("q"), py::arg("stream"));
+  m.def(
       "fm_reduce_grads",
       [stream_of](uintptr_t part, int nblocks, int dim, uintptr_t v, float sx, uintptr_t z,
                   uintptr_t gw, uintptr_t gv, uintptr_t stream) {
