@@ -84,28 +84,18 @@ def main():
     torch.cuda.synchronize()
     res["hashed_fm_step_ms"] = round((time.perf_counter() - t0) / args.steps * 1e3, 3)
     res["hashed_fm_gemm"] = model.gemm
-    # the same step captured once as a HIP graph and replayed (forward, loss,
-    # backward into the parameters' .grad): no per-kernel host launch cost
-    xs, ls = batch["x"], batch["label"].clamp(0, 1)
-    side = torch.cuda.Stream()
-    side.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(side):
-        for _ in range(2):
-            model.zero_grad(set_to_none=True)
-            torch.nn.functional.binary_cross_entropy_with_logits(model(xs, scale=0.5), ls).backward()
-    torch.cuda.current_stream().wait_stream(side)
-    model.zero_grad(set_to_none=True)
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
-        static_loss = torch.nn.functional.binary_cross_entropy_with_logits(model(xs, scale=0.5), ls)
-        static_loss.backward()
-    graph.replay()
+    # GPU time of the same step (events around it: no host gaps between steps)
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
     for _ in range(args.steps):
-        graph.replay()
+        model.zero_grad()
+        y = model(batch["x"], scale=0.5)
+        loss = torch.nn.functional.binary_cross_entropy_with_logits(y, batch["label"].clamp(0, 1))
+        loss.backward()
+    ev1.record()
     torch.cuda.synchronize()
-    res["hashed_fm_step_graph_ms"] = round((time.perf_counter() - t0) / args.steps * 1e3, 3)
+    res["hashed_fm_step_event_ms"] = round(ev0.elapsed_time(ev1) / args.steps, 3)
     res.update({"rows": int(batch["x"].shape[0]), "dim": args.dim, "text_bytes": nbytes,
                 "speedup_fused_vs_csr_k9": round(res["csr_then_k9"]["ms"] / res["fused"]["ms"], 3)})
     sweep = {}

@@ -129,76 +129,98 @@ __global__ __launch_bounds__(kFwdThreads) void k_fm_fwd(const uint8_t* __restric
   const float b0 = *bias;
   const int nblk = dim / 128;
   const bf16x8 zero8 = {};
-  // loads run two 128-feature blocks ahead of the MFMAs, across row tiles too
-  // (2 x 4 KB per wave in flight): the wave's (tile, block) sequence is one
-  // stream, so the next tile's first blocks arrive during this tile's last
+  // The wave's (tile, block) pairs form one stream; blocks rotate through three
+  // register buffers, each refilled (two blocks ahead, across row tiles too)
+  // right after its MFMAs consumed it -- no register copies of loads in
+  // flight, so a block's wait only covers what was issued before it.  Loads
+  // are unconditional (clamped row, zeroed past the rows).
   const int64_t tfirst = static_cast<int64_t>(blockIdx.x) * waves + threadIdx.x / kWave;
   const int64_t tstride = static_cast<int64_t>(gridDim.x) * waves;
+  const int64_t rlast = rows - 1;
   int64_t lt = tfirst;  // the load cursor: tile, block
   int lkb = 0;
   auto issue = [&](uint4 (&v)[4]) {
     const int64_t r = lt * 32 + col;
     const bool ok = lt < ntiles && r < rows;
-    load64(x + (ok ? r : 0) * dim + 64 * h + 128 * lkb, ok, v);
+    const int64_t rc = r < rlast ? r : rlast;
+    const uint4* q = reinterpret_cast<const uint4*>(x + rc * dim + 64 * h + 128 * lkb);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint4 u = q[i];
+      v[i] = ok ? u : make_uint4(0, 0, 0, 0);
+    }
     if (++lkb == nblk) {
       lkb = 0;
       lt += tstride;
     }
   };
-  uint4 cur[4], nx1[4], nx2[4];
-  issue(cur);
-  issue(nx1);
-  for (int64_t t = tfirst; t < ntiles; t += tstride) {
-    f32x16 acc = {};
-    f32x2 x2q2 = {0.0f, 0.0f};
-    for (int kb = 0; kb < nblk; ++kb) {
-      issue(nx2);
-      const int kbase = 128 * kb + 64 * h;
+  int64_t t = tfirst;  // the compute cursor
+  int kb = 0;
+  f32x16 acc = {};
+  f32x2 x2q2 = {0.0f, 0.0f};
+  // one block of the current tile from buffer cur; the tile's epilogue after
+  // its last block.  false once the wave's tiles are done
+  auto step = [&](const uint4 (&cur)[4]) {
+    if (t >= ntiles) return false;
+    const int kbase = 128 * kb + 64 * h;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const uint32_t lo = word(cur, 2 * i), hi = word(cur, 2 * i + 1);
-        float f[8];
-        fp8x8(lo, hi, f);
-        const float4 q0 = *reinterpret_cast<const float4*>(s_q + kbase + 8 * i);
-        const float4 q1 = *reinterpret_cast<const float4*>(s_q + kbase + 8 * i + 4);
-        // x^2.q in packed f32 (v_pk_mul / v_pk_fma), two partial sums
-        f32x2 sq[4] = {{f[0], f[1]}, {f[2], f[3]}, {f[4], f[5]}, {f[6], f[7]}};
-        const f32x2 qq[4] = {{q0.x, q0.y}, {q0.z, q0.w}, {q1.x, q1.y}, {q1.z, q1.w}};
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t lo = word(cur, 2 * i), hi = word(cur, 2 * i + 1);
+      float f[8];
+      fp8x8(lo, hi, f);
+      const float4 q0 = *reinterpret_cast<const float4*>(s_q + kbase + 8 * i);
+      const float4 q1 = *reinterpret_cast<const float4*>(s_q + kbase + 8 * i + 4);
+      // x^2.q in packed f32 (v_pk_mul / v_pk_fma), two partial sums
+      f32x2 sq[4] = {{f[0], f[1]}, {f[2], f[3]}, {f[4], f[5]}, {f[6], f[7]}};
+      const f32x2 qq[4] = {{q0.x, q0.y}, {q0.z, q0.w}, {q1.x, q1.y}, {q1.z, q1.w}};
 #pragma unroll
-        for (int k = 0; k < 4; ++k) x2q2 = __builtin_elementwise_fma(sq[k] * sq[k], qq[k], x2q2);
-        const bf16x8 b = col < kFmCols
-                             ? *reinterpret_cast<const bf16x8*>(s_wt + col * ldw + kbase + 8 * i)
-                             : zero8;
-        // A straight from the fp8 codes (exact), not through f32
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fp8x8_bf16(lo, hi), b, acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        cur[i] = nx1[i];
-        nx1[i] = nx2[i];
-      }
+      for (int k = 0; k < 4; ++k) x2q2 = __builtin_elementwise_fma(sq[k] * sq[k], qq[k], x2q2);
+      const bf16x8 b = col < kFmCols
+                           ? *reinterpret_cast<const bf16x8*>(s_wt + col * ldw + kbase + 8 * i)
+                           : zero8;
+      // A straight from the fp8 codes (exact), not through f32
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fp8x8_bf16(lo, hi), b, acc, 0, 0, 0);
     }
-    // lanes r and r + 32 hold the two halves of row r's x^2.q
-    float x2q = x2q2[0] + x2q2[1];
-    x2q += __shfl_xor(x2q, 32, kWave);
+    if (++kb == nblk) {
+      // lanes r and r + 32 hold the two halves of row r's x^2.q
+      float x2q = x2q2[0] + x2q2[1];
+      x2q += __shfl_xor(x2q, 32, kWave);
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int m = (reg & 3) + 8 * (reg >> 2) + 4 * h;  // accumulator row (C/D map)
-      const float v = acc[reg];
-      float sq = (col >= 1 && col <= kFmRank) ? v * v : 0.0f;
+      for (int reg = 0; reg < 16; ++reg) {
+        const int m = (reg & 3) + 8 * (reg >> 2) + 4 * h;  // accumulator row (C/D map)
+        const float v = acc[reg];
+        float sq = (col >= 1 && col <= kFmRank) ? v * v : 0.0f;
 #pragma unroll
-      for (int d = 1; d < 32; d <<= 1) sq += __shfl_xor(sq, d, kWave);
-      const float lin = __shfl(v, h * 32, kWave);
-      const float xq = __shfl(x2q, m, kWave);
-      const int64_t r = t * 32 + m;
-      if (r < rows) {
-        if (col == 0) {
-          y[r] = b0 + sx * lin + 0.5f * sx * sx * (sq - xq);
-        } else if (col <= kFmRank) {
-          xv[r * kFmRank + (col - 1)] = sx * v;
+        for (int d = 1; d < 32; d <<= 1) sq += __shfl_xor(sq, d, kWave);
+        const float lin = __shfl(v, h * 32, kWave);
+        const float xq = __shfl(x2q, m, kWave);
+        const int64_t r = t * 32 + m;
+        if (r < rows) {
+          if (col == 0) {
+            y[r] = b0 + sx * lin + 0.5f * sx * sx * (sq - xq);
+          } else if (col <= kFmRank) {
+            xv[r * kFmRank + (col - 1)] = sx * v;
+          }
         }
       }
+      acc = f32x16{};
+      x2q2 = f32x2{0.0f, 0.0f};
+      kb = 0;
+      t += tstride;
     }
+    return true;
+  };
+  uint4 bA[4], bB[4], bC[4];
+  issue(bA);
+  issue(bB);
+  issue(bC);
+  for (;;) {
+    if (!step(bA)) break;
+    issue(bA);
+    if (!step(bB)) break;
+    issue(bB);
+    if (!step(bC)) break;
+    issue(bC);
   }
 }
 
