@@ -77,6 +77,10 @@ struct DeviceParserConfig {
    *  up to this many bytes per kernel pass (`?replay_chunk_mb=`)
    */
   size_t replay_chunk_bytes{1UL << 30};
+  /*! \brief the first merged chunk of a replay pass (`?replay_first_mb=`); each
+   *  next one doubles up to replay_chunk_bytes.  0: every merged chunk takes
+   *  replay_chunk_bytes (no ramp) */
+  size_t replay_first_bytes{64UL << 20};
   /*!
    * \brief busy-poll budget (us) of a chunk-metadata wait before the host
    *  thread falls back to 20 us sleeps (src/gpu/host_wait.h)
@@ -97,6 +101,7 @@ struct DeviceParserConfig {
   /*! \brief apply `?k=v` overrides (chunk_mb, pinned_slots, device_slots,
    *  read_threads, device, format, label_column, weight_column, delimiter,
    *  fast_path, zero_copy, zc_pin_budget_mb, zc_window_mb, hbm_cache, replay_chunk_mb,
+   *  replay_first_mb,
    *  shuffle_parts, shuffle_seed) */
   void Update(const std::map<std::string, std::string>& args);
 };

@@ -26,6 +26,10 @@ def main():
                     help="extra dims timed for fused vs CSR+K9 (comma list, '' to skip)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--data", default="/tmp/dmlc_hashed_bench.libfm")
+    ap.add_argument("--replay-first-mb", type=float, default=None,
+                    help="first merged replay chunk (0: no ramp; default: the parser's)")
+    ap.add_argument("--replay-chunk-mb", type=float, default=None,
+                    help="merged replay chunk cap (default: the parser's)")
     args = ap.parse_args()
     import torch
 
@@ -36,8 +40,13 @@ def main():
         data.write_synthetic(args.data + ".tmp", 0, args.rows, format="libfm", seed=0, nthread=16)
         os.replace(args.data + ".tmp", args.data)
     nbytes = os.path.getsize(args.data)
-    two = data.GPUParser(args.data, format="libfm", hbm_cache=1)
-    fused = data.GPUParser(args.data, format="libfm", hbm_cache=1)
+    cfg = {}
+    if args.replay_first_mb is not None:
+        cfg["replay_first_mb"] = args.replay_first_mb
+    if args.replay_chunk_mb is not None:
+        cfg["replay_chunk_mb"] = args.replay_chunk_mb
+    two = data.GPUParser(args.data, format="libfm", hbm_cache=1, **cfg)
+    fused = data.GPUParser(args.data, format="libfm", hbm_cache=1, **cfg)
 
     def step_two():
         two.before_first()
@@ -96,6 +105,7 @@ def main():
     ev1.record()
     torch.cuda.synchronize()
     res["hashed_fm_step_event_ms"] = round(ev0.elapsed_time(ev1) / args.steps, 3)
+    res["replay"] = cfg
     res.update({"rows": int(batch["x"].shape[0]), "dim": args.dim, "text_bytes": nbytes,
                 "speedup_fused_vs_csr_k9": round(res["csr_then_k9"]["ms"] / res["fused"]["ms"], 3)})
     sweep = {}

@@ -76,6 +76,8 @@ void DeviceParserConfig::Update(const std::map<std::string, std::string>& args) 
       fast_path = v != "0" && v != "false";
     } else if (k == "replay_chunk_mb") {
       replay_chunk_bytes = static_cast<size_t>(std::atof(v.c_str()) * (1 << 20));
+    } else if (k == "replay_first_mb") {
+      replay_first_bytes = static_cast<size_t>(std::atof(v.c_str()) * (1 << 20));
     } else if (k == "zc_pin_budget_mb") {
       zc_pin_budget = static_cast<size_t>(std::atof(v.c_str()) * (1 << 20));
     } else if (k == "zc_window_mb") {
@@ -482,11 +484,14 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
         // and host round trips per byte)
         // (a chunk whose text ends without EOL -- a file's unterminated last
         // line on the zero-copy path -- must stay its own chunk).  The merged
-        // size doubles per chunk from kFirstMerge: the first chunk's count +
+        // size doubles per chunk from replay_first_bytes: the first chunk's count +
         // scan is the only one not hidden behind a previous chunk's fill (the
         // next count runs on count_stream_ meanwhile, and next to a fill it
         // takes about half the fill's time per byte: 2x keeps it hidden)
-        merge_cap_ = merge_cap_ == 0 ? kFirstMerge : merge_cap_ * 2;
+        merge_cap_ = merge_cap_ == 0
+                         ? (cfg_.replay_first_bytes != 0 ? cfg_.replay_first_bytes
+                                                         : cfg_.replay_chunk_bytes)
+                         : merge_cap_ * 2;
         const size_t cap = std::min(merge_cap_, cfg_.replay_chunk_bytes);
         while (merge_replay_ && replay_idx_ < replay_list_.size() &&
                cached_[replay_list_[replay_idx_ - 1]].eol_end &&
@@ -1082,7 +1087,6 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   size_t arena_bytes_{0}, arena_fill_{0}, replay_idx_{0};
   /*! \brief merged replay chunk cap of the pass (0: the next is the first) */
   size_t merge_cap_{0};
-  static constexpr size_t kFirstMerge = size_t(64) << 20;
   std::vector<CachedChunk> cached_;
   bool caching_{false}, cache_complete_{false}, replay_{false}, merge_replay_{false};
   HostSlot* cur_slot_{nullptr};
