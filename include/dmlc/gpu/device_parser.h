@@ -129,6 +129,8 @@ struct DeviceParserStats {
   size_t nnz{0};
   /*! \brief chunks the fast path handed to the exact per-line kernels */
   size_t exact_chunks{0};
+  /*! \brief hashed-batch chunks built in one pass (look-back, no count kernel) */
+  size_t one_pass_chunks{0};
   /*! \brief seconds the host waited for the reader (pinned ring empty) */
   double wait_reader_sec{0};
   /*! \brief seconds the host waited for GPU results */

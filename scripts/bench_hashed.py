@@ -39,6 +39,7 @@ def main():
     if not os.path.exists(args.data):
         data.write_synthetic(args.data + ".tmp", 0, args.rows, format="libfm", seed=0, nthread=16)
         os.replace(args.data + ".tmp", args.data)
+        os.sync()  # no dirty-page writeback under the timed loops
     nbytes = os.path.getsize(args.data)
     cfg = {}
     if args.replay_first_mb is not None:

@@ -492,7 +492,8 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
                          ? (cfg_.replay_first_bytes != 0 ? cfg_.replay_first_bytes
                                                          : cfg_.replay_chunk_bytes)
                          : merge_cap_ * 2;
-        const size_t cap = std::min(merge_cap_, cfg_.replay_chunk_bytes);
+        const size_t cap =
+            std::min(merge_cap_, merge_limit_ != 0 ? merge_limit_ : cfg_.replay_chunk_bytes);
         while (merge_replay_ && replay_idx_ < replay_list_.size() &&
                cached_[replay_list_[replay_idx_ - 1]].eol_end &&
                cached_[replay_list_[replay_idx_]].off == c.off + size &&
@@ -980,11 +981,62 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     merge_replay_ = true;  // resident text: parse adjacent cached chunks together
     struct Unmerge {
       bool* f;
-      ~Unmerge() { *f = false; }
-    } unmerge{&merge_replay_};
+      size_t* limit;
+      ~Unmerge() {
+        *f = false;
+        *limit = 0;
+      }
+    } unmerge{&merge_replay_, &merge_limit_};
+    // resident text and a batch that already has rows (a reused one): one pass
+    // per chunk (k_tile_hash look-back, no C1 / C2), so nothing is gained by a
+    // small first chunk -- merge up to 2 x replay_chunk_bytes from the start
+    const bool one_pass = cfg_.fast_path && dim % 16 == 0 && replay_ && out->row_cap != 0;
+    if (one_pass) {
+      merge_limit_ = 2 * cfg_.replay_chunk_bytes;
+      if (merge_cap_ == 0) merge_cap_ = merge_limit_;
+    }
     while (WithNextChunk([&](const char* text, size_t nbytes) {
       ChunkMeta* dmeta = meta_.get<ChunkMeta>();
-      if (cfg_.fast_path && dim % 16 == 0) {
+      if (one_pass && nbytes != 0 && out->row_cap != 0) {
+        DropPrelaunch();
+        ChunkMeta* hm = hmap_.get<ChunkMeta>();
+        const size_t tiles = TileCount(nbytes);
+        if (hstatus_.bytes() < tiles * sizeof(uint64_t)) {
+          hstatus_.Reserve(tiles * sizeof(uint64_t));
+          DMLC_HIP_CHECK(hipMemsetAsync(hstatus_.get(), 0, hstatus_.bytes(), s));
+        }
+        if (hticket_.bytes() == 0) {
+          hticket_.Reserve(sizeof(unsigned long long));
+          DMLC_HIP_CHECK(hipMemsetAsync(hticket_.get(), 0, hticket_.bytes(), s));
+          hticket0_ = 0;
+        }
+        for (;;) {
+          if (++htag_ >= (1u << 30)) {  // tags wrapped: old words could match again
+            htag_ = 1;
+            DMLC_HIP_CHECK(hipMemsetAsync(hstatus_.get(), 0, hstatus_.bytes(), s));
+          }
+          const HashOnePass op{hstatus_.get<uint64_t>(), hticket_.get<unsigned long long>(),
+                               hticket0_, htag_, out->row_cap};
+          hticket0_ += LaunchTileHashed<IndexType>(
+              text, nbytes, tcfg_.format, nullptr, out->rows, 0, dim, scale, seed, fp8,
+              out->x.get(), out->label.get<float>(), slots_.get<MetaPartial>(), dmeta, hm, s, &op);
+          const ChunkMeta m = WaitMapped(hm);
+          AfterFirstSync();
+          CHECK(!(m.flags & kFlagNegIndex)) << "negative feature index in " << cfg_.format
+                                            << " input";
+          if (m.flags & kFlagIrregular) break;  // the exact kernels, below
+          if (m.flags & kFlagOverflow) {
+            // more rows than the batch holds: grow it, write the chunk again
+            reserve(m.nrows, nbytes);
+            continue;
+          }
+          out->rows += m.nrows;
+          stats_.rows += m.nrows;
+          stats_.one_pass_chunks += 1;
+          return;
+        }
+        stats_.exact_chunks += 1;
+      } else if (cfg_.fast_path && dim % 16 == 0) {
         // tile parser: C1 + C2 sizes, then the fused tile kernel builds the
         // rows of the lines each workgroup owns
         CountScanCurrent(text, nbytes);  // may adopt a prelaunched count + scan
@@ -1087,6 +1139,11 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   size_t arena_bytes_{0}, arena_fill_{0}, replay_idx_{0};
   /*! \brief merged replay chunk cap of the pass (0: the next is the first) */
   size_t merge_cap_{0};
+  size_t merge_limit_{0};  // merged replay chunk limit (0: replay_chunk_bytes)
+  // one-pass hashed batches: look-back words, workgroup tickets, launch tag
+  DeviceBuffer hstatus_, hticket_;
+  unsigned long long hticket0_{0};
+  uint32_t htag_{0};
   std::vector<CachedChunk> cached_;
   bool caching_{false}, cache_complete_{false}, replay_{false}, merge_replay_{false};
   HostSlot* cur_slot_{nullptr};

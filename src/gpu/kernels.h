@@ -191,12 +191,30 @@ void LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
  *  the chunk with LaunchTextHashed), merges kFlagNegIndex.  dim: multiple of
  *  16, <= 4096.
  */
+/*!
+ *  One pass (one_pass != nullptr; tile_prefix / nlines unused): no C1 / C2 --
+ *  each wave counts its tile's lines itself and takes the lines before it by
+ *  decoupled look-back; the chunk's nlines / nrows land in meta (and
+ *  host_meta) with the flags.  Rows at or past row_cap are not written and set
+ *  kFlagOverflow (grow the batch to meta->nrows and run the chunk again).
+ *  nbytes > 0 (an empty chunk has no tile to write the sizes).
+ *  Also sets kFlagIrregular for what C1 would have (blank-started lines,
+ *  control bytes other than \t \n \r).  Returns the workgroups launched:
+ *  advance ticket0 by it for the next launch on the same counter.
+ */
+struct HashOnePass {
+  uint64_t* status;            // >= TileCount(nbytes) words, zeroed once at allocation
+  unsigned long long* ticket;  // counter, zeroed once
+  unsigned long long ticket0;  // the counter's value before this launch
+  uint32_t tag;                // distinct per launch on the same status array, 1..2^30-1
+  uint64_t row_cap;            // rows of out / labels
+};
 template <typename IndexType>
-void LaunchTileHashed(const char* text, size_t nbytes, TextFormat format,
-                      const uint64_t* tile_prefix, uint64_t row_base, uint64_t nlines, int dim,
-                      float scale, uint32_t seed, bool fp8, void* out, float* labels,
-                      MetaPartial* partials, ChunkMeta* meta, ChunkMeta* host_meta,
-                      hipStream_t stream);
+size_t LaunchTileHashed(const char* text, size_t nbytes, TextFormat format,
+                        const uint64_t* tile_prefix, uint64_t row_base, uint64_t nlines, int dim,
+                        float scale, uint32_t seed, bool fp8, void* out, float* labels,
+                        MetaPartial* partials, ChunkMeta* meta, ChunkMeta* host_meta,
+                        hipStream_t stream, const HashOnePass* one_pass = nullptr);
 
 /*!
  * \brief C2 alone over caller-filled per-tile u64 counts (hi 32 bits: items,

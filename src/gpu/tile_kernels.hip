@@ -107,7 +107,7 @@ __device__ __forceinline__ bool num_start(uint32_t c) {
  *  control byte other than \t \n \r, a line starting with a blank, a token
  *  starting outside [0-9+-.]).
  */
-template <bool kCheck, bool kFull = false>
+template <bool kCheck, bool kFull = false, bool kCheckTokens = true>
 __device__ __forceinline__ bool lane_masks(uint4 v, uint32_t pc, size_t pos, size_t n,
                                            uint32_t* lm, uint32_t* tm) {
   uint32_t sep, eol, ctl;
@@ -125,7 +125,7 @@ __device__ __forceinline__ bool lane_masks(uint4 v, uint32_t pc, size_t pos, siz
   *tm = ~sep & ((sep << 1) | prev_sep) & valid & 0xFFFFu;
   if (!kCheck) return false;
   bool bad = (*lm & ~*tm) != 0;  // a line that starts with a blank
-  uint32_t t = *tm;
+  uint32_t t = kCheckTokens ? *tm : 0u;  // (else: the decoder's fallback flags them)
   while (t != 0) {
     const int j = __ffs(t) - 1;
     t &= t - 1;
@@ -208,6 +208,73 @@ __device__ __forceinline__ bool count16(uint4 v, uint32_t pc, size_t pos, size_t
     prev_eol = (eol >> 24) & 0x80u;
   }
   return bad;
+}
+
+/*! \brief line starts of 16 bytes (the lm of count16 alone); room: bytes before n */
+template <bool kFull>
+__device__ __forceinline__ uint32_t lines16(uint4 v, uint32_t pc, int room) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t prev_eol = (pc == '\n' || pc == '\r') ? 0x80u : 0u;
+  uint32_t lines = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t x = w[i];
+    const uint32_t lo7 = x & 0x7F7F7F7Fu;
+    const uint32_t le20 = ~((lo7 + 0x5F5F5F5Fu) | x) & 0x80808080u;
+    const uint32_t b6 = ((x & 0x06060606u) + 0x7E7E7E7Eu) & 0x80808080u;
+    const uint32_t eol = le20 & b6;
+    const int valid_bytes = room - 4 * i;
+    const uint32_t valid = kFull || valid_bytes >= 4
+                               ? 0x80808080u
+                               : (valid_bytes <= 0 ? 0u : (0x80808080u >> (8 * (4 - valid_bytes))));
+    lines += __popc(~eol & ((eol << 8) | prev_eol) & valid);
+    prev_eol = (eol >> 24) & 0x80u;
+  }
+  return lines;
+}
+
+/*!
+ * \brief decoupled look-back over per-tile line counts (one wave per tile):
+ *  publish this tile's count, sum the predecessors' counts back to the first
+ *  inclusive prefix (64 tiles per probe), publish the inclusive prefix, return
+ *  the exclusive one.  Status word: tag (30 bits, one per launch, so the array
+ *  needs no reset) << 34 | state (1: count, 2: inclusive) << 32 | value.
+ *  Tiles run in ticket order (k_tile_hash), so every tile waited on is resident
+ *  or done and the wait ends.
+ */
+__device__ __forceinline__ uint64_t lookback_lines(uint64_t* st, size_t tile, uint32_t own,
+                                                   uint32_t tag, int lane) {
+  const uint64_t tg = static_cast<uint64_t>(tag) << 34;
+  if (lane == 0) {
+    __hip_atomic_store(&st[tile], tg | ((tile == 0 ? 2ull : 1ull) << 32) | own, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tile == 0) return 0;
+  uint64_t excl = 0;
+  int64_t j = static_cast<int64_t>(tile) - 1;  // the nearest predecessor not summed yet
+  for (;;) {
+    const int64_t k = j - lane;
+    const uint64_t v = k >= 0 ? __hip_atomic_load(&st[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : (tg | (2ull << 32));  // before the chunk: inclusive 0
+    const uint32_t state = static_cast<uint32_t>(v >> 32) & 3u;
+    const bool ready = (v >> 34) == tag && state != 0;
+    const uint64_t inc = __ballot(ready && state == 2u);
+    const uint64_t waiting = __ballot(!ready);
+    const int first = inc != 0 ? __builtin_ctzll(inc) : dev::kWave - 1;
+    const uint64_t need = first >= dev::kWave - 1 ? ~0ull : ((2ull << first) - 1ull);
+    if ((waiting & need) != 0) {
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    excl += dev::wave_sum(lane <= first ? static_cast<uint32_t>(v) : 0u);
+    if (inc != 0) break;
+    j -= dev::kWave;
+  }
+  if (lane == 0) {
+    __hip_atomic_store(&st[tile], tg | (2ull << 32) | (excl + own), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return excl;
 }
 
 /*!
@@ -1298,10 +1365,17 @@ struct HashTarget {
   void* x;            // [row_limit, dim] fp8 bytes or f32
   float* label;
   uint64_t row_base;  // global row of the chunk's first line
-  uint64_t nlines;    // lines of the chunk (the C2 total)
+  uint64_t nlines;    // lines of the chunk (the C2 total; one-pass: unused)
   int dim;
   float scale;
   uint32_t seed;
+  // one pass (no C1 / C2): line counts by look-back, rows checked against row_cap
+  uint32_t tag;                 // this launch's status tag (!= 0)
+  uint64_t* status;             // per-tile look-back words
+  unsigned long long* ticket;   // workgroup ticket counter
+  unsigned long long ticket0;   // its value at this launch
+  uint64_t row_cap;             // rows of x / label
+  ChunkMeta* meta;              // nlines / nrows of the chunk (the last tile writes them)
 };
 
 /*! \brief keep the token starts of a slice whose line ordinals are in [1, own];
@@ -1320,7 +1394,7 @@ __device__ __forceinline__ uint32_t owned_tokens(uint32_t tm, uint32_t lm, uint3
   return m;
 }
 
-template <TextFormat F, typename IndexType, bool kFP8>
+template <TextFormat F, typename IndexType, bool kFP8, bool kOnePass>
 __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
     const uint8_t* __restrict__ text, size_t n, size_t ntiles,
     const uint64_t* __restrict__ prefix, HashTarget out, MetaPartial* __restrict__ partials) {
@@ -1332,7 +1406,16 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
   extern __shared__ __attribute__((aligned(16))) float s_hrow[];  // kFillWaves x dim
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / dev::kWave);
   const int lane = dev::lane_id();
-  const size_t tile = static_cast<size_t>(blockIdx.x) * kFillWaves + wave;
+  size_t group = blockIdx.x;
+  if constexpr (kOnePass) {
+    // tiles in ticket order: a workgroup looks back only at tiles of
+    // workgroups that started before it (whatever the dispatch order)
+    __shared__ uint32_t s_ticket;
+    if (threadIdx.x == 0) s_ticket = static_cast<uint32_t>(atomicAdd(out.ticket, 1ull) - out.ticket0);
+    __syncthreads();
+    group = s_ticket;
+  }
+  const size_t tile = group * kFillWaves + wave;
   if (tile >= ntiles) return;  // whole waves leave; nothing below synchronises waves
   uint4* const st = s_text[wave];
   uint32_t* const sl = s_list[wave];
@@ -1340,10 +1423,54 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
   float* const row = s_hrow + static_cast<size_t>(wave) * dim;
   const uint32_t slot = round_slot(lane);
   const size_t tile0 = tile * kTileBytes;
-  const uint64_t line_base = prefix[tile] >> 32;
-  const uint64_t line_next = tile + 1 < ntiles ? prefix[tile + 1] >> 32 : out.nlines;
-  const uint32_t own = static_cast<uint32_t>(line_next - line_base);
-  bool irregular = false, neg = false;
+  const __amdgpu_buffer_rsrc_t trs = text_rsrc(text + tile0, n - tile0);
+  const uint32_t loff = static_cast<uint32_t>(lane) * 16;
+  uint4 a = bload16(trs, loff);
+  uint4 b = bload16(trs, loff + 1024);
+  uint32_t carry_pc = tile0 == 0 ? static_cast<uint32_t>('\n') : text[tile0 - 1];
+  uint64_t line_base;
+  uint32_t own;
+  if constexpr (kOnePass) {
+    // the C1 line count of this tile (its other 6 KiB come into L2 for the
+    // steps), then the look-back for the lines before it
+    uint4 v[kCountLoads];
+    v[0] = a;
+    v[1] = b;
+#pragma unroll
+    for (int j = 2; j < kCountLoads; ++j) v[j] = bload16(trs, loff + j * 1024);
+    const bool full = tile0 + kTileBytes <= n;
+    uint32_t lines = 0;
+#pragma unroll
+    for (int j = 0; j < kCountLoads; ++j) {
+      const uint32_t left = __shfl_up(v[j].w >> 24, 1, dev::kWave);
+      const uint32_t wrap = j == 0 ? carry_pc : __shfl(v[j - 1].w >> 24, dev::kWave - 1, dev::kWave);
+      const uint32_t pc = lane == 0 ? wrap : left;
+      if (full) {
+        lines += lines16<true>(v[j], pc, 16);
+      } else {
+        const size_t pos = tile0 + j * 1024 + lane * 16;
+        const int room = pos >= n ? 0 : (n - pos < 16 ? static_cast<int>(n - pos) : 16);
+        lines += lines16<false>(v[j], pc, room);
+      }
+    }
+    own = dev::wave_sum(lines);
+    line_base = lookback_lines(out.status, tile, own, out.tag, lane);
+    if (tile + 1 == ntiles && lane == 0) {
+      ChunkMeta m;
+      m.nlines = m.nrows = line_base + own;
+      m.nnz = 0;
+      m.max_index = m.max_field = 0;
+      m.flags = 0;
+      m.pad = 0;
+      *out.meta = m;  // k_tile_finish (stream-ordered) adds the flags
+    }
+  } else {
+    line_base = prefix[tile] >> 32;
+    const uint64_t line_next = tile + 1 < ntiles ? prefix[tile + 1] >> 32 : out.nlines;
+    own = static_cast<uint32_t>(line_next - line_base);
+  }
+  const uint64_t row_cap = kOnePass ? out.row_cap : ~0ull;
+  bool irregular = false, neg = false, over = false;
   if (own != 0) {
     const uint64_t R = out.row_base + line_base;  // global row of tile line ordinal 1
     const bool pow2 = (dim & (dim - 1)) == 0;
@@ -1355,7 +1482,8 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
     auto flush = [&](uint32_t lc) {
       dev::wave_sync();  // the row's adds are done
       const uint64_t g = R + lc - 1;
-      const bool ok = lc <= own;
+      const bool ok = lc <= own && g < row_cap;
+      over |= lc <= own && g >= row_cap;
       if constexpr (kFP8) {
         // lane-interleaved float4s (consecutive lanes, consecutive 16 B: no
         // bank conflicts on the b128 read / zero), 4 fp8 bytes per lane store
@@ -1382,13 +1510,8 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
 
     // loads as in k_tile_fill: the next step's go into a / b / t once they are
     // consumed (no copies of loads in flight), clipped where staged
-    const __amdgpu_buffer_rsrc_t trs = text_rsrc(text + tile0, n - tile0);
-    const uint32_t loff = static_cast<uint32_t>(lane) * 16;
-    uint4 a = bload16(trs, loff);
-    uint4 b = bload16(trs, loff + 1024);
     uint4 t = make_uint4(0, 0, 0, 0);
     if (lane < 4) t = bload16(trs, loff + kStepBytes);
-    uint32_t carry_pc = tile0 == 0 ? static_cast<uint32_t>('\n') : text[tile0 - 1];
     uint32_t lcnt = 0;   // line starts seen so far (this tile's ordinals)
     uint32_t open = 0;   // ordinal of the row being accumulated (0: none yet)
     uint32_t qid_prev = 0;  // LibSVM: status of the last token start (prev_token_status)
@@ -1413,12 +1536,14 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
       const uint32_t pc_b = lane == 0 ? last_a : left_b;
       carry_pc = __shfl(b.w >> 24, dev::kWave - 1, dev::kWave);
       uint32_t lm_a, tm_a, lm_b, tm_b;
+      // one pass: C1's checks of blank-started lines and control bytes here
+      // (token starts outside [0-9+-.] fail the decoder and are flagged there)
       if (nxt <= n) {  // wave-uniform: a full step
-        (void)lane_masks<false, true>(a, pc_a, pos_a, n, &lm_a, &tm_a);
-        (void)lane_masks<false, true>(b, pc_b, pos_a + 1024, n, &lm_b, &tm_b);
+        irregular |= lane_masks<kOnePass, true, false>(a, pc_a, pos_a, n, &lm_a, &tm_a);
+        irregular |= lane_masks<kOnePass, true, false>(b, pc_b, pos_a + 1024, n, &lm_b, &tm_b);
       } else {
-        (void)lane_masks<false>(a, pc_a, pos_a, n, &lm_a, &tm_a);
-        (void)lane_masks<false>(b, pc_b, pos_a + 1024, n, &lm_b, &tm_b);
+        irregular |= lane_masks<kOnePass, false, false>(a, pc_a, pos_a, n, &lm_a, &tm_a);
+        irregular |= lane_masks<kOnePass, false, false>(b, pc_b, pos_a + 1024, n, &lm_b, &tm_b);
       }
       if (F == TextFormat::kLibSVM) {
         // `qid:` tokens are no features of the batch: dropped (checked as in
@@ -1516,7 +1641,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
           bad = gr.bad;
           irregular |= !num_start(text[gpos]);  // qid:, comments, junk: the exact kernels
         }
-        if (active & is_label) out.label[R + lc - 1] = t.f0;
+        if (active & is_label && R + lc - 1 < row_cap) out.label[R + lc - 1] = t.f0;
         bool feat = active & !is_label;
         uint64_t key;
         float val;
@@ -1559,6 +1684,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
   unsigned fl = 0;
   if (irregular) fl |= kFlagIrregular;
   if (neg) fl |= kFlagNegIndex;
+  if (over) fl |= kFlagOverflow;
   fl = dev::wave_or(fl);
   if (lane == 0) {
     MetaPartial p;
@@ -1762,44 +1888,61 @@ void LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
 }
 
 template <typename IndexType>
-void LaunchTileHashed(const char* text, size_t nbytes, TextFormat format,
-                      const uint64_t* tile_prefix, uint64_t row_base, uint64_t nlines, int dim,
-                      float scale, uint32_t seed, bool fp8, void* out, float* labels,
-                      MetaPartial* partials, ChunkMeta* meta, ChunkMeta* host_meta,
-                      hipStream_t stream) {
+size_t LaunchTileHashed(const char* text, size_t nbytes, TextFormat format,
+                        const uint64_t* tile_prefix, uint64_t row_base, uint64_t nlines, int dim,
+                        float scale, uint32_t seed, bool fp8, void* out, float* labels,
+                        MetaPartial* partials, ChunkMeta* meta, ChunkMeta* host_meta,
+                        hipStream_t stream, const HashOnePass* one_pass) {
   const size_t ntiles = TileCount(nbytes);
   const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
   const size_t smem = static_cast<size_t>(kFillWaves) * dim * sizeof(float);
-  HashTarget tgt{out, labels, row_base, nlines, dim, scale, seed};
+  HashTarget tgt{out, labels, row_base, nlines, dim, scale, seed, 0u, nullptr, nullptr, 0ull, 0ull,
+                 meta};
+  const size_t groups = (ntiles + kFillWaves - 1) / kFillWaves;
+  if (one_pass != nullptr) {
+    tgt.tag = one_pass->tag;
+    tgt.status = one_pass->status;
+    tgt.ticket = one_pass->ticket;
+    tgt.ticket0 = one_pass->ticket0;
+    tgt.row_cap = one_pass->row_cap;
+  }
   if (ntiles != 0) {
-    const dim3 grid(static_cast<unsigned>((ntiles + kFillWaves - 1) / kFillWaves));
-#define DMLC_TILE_HASH(FMT, FP8)                                                              \
-  hipLaunchKernelGGL((k_tile_hash<FMT, IndexType, FP8>), grid, dim3(kThreads), smem, stream, t, \
-                     nbytes, ntiles, tile_prefix, tgt, partials)
+    const dim3 grid(static_cast<unsigned>(groups));
+#define DMLC_TILE_HASH(FMT, FP8, ONE)                                                          \
+  hipLaunchKernelGGL((k_tile_hash<FMT, IndexType, FP8, ONE>), grid, dim3(kThreads), smem, stream, \
+                     t, nbytes, ntiles, tile_prefix, tgt, partials)
+#define DMLC_TILE_HASH_FMT(FMT)             \
+  if (one_pass != nullptr) {                \
+    if (fp8) {                              \
+      DMLC_TILE_HASH(FMT, true, true);      \
+    } else {                                \
+      DMLC_TILE_HASH(FMT, false, true);     \
+    }                                       \
+  } else if (fp8) {                         \
+    DMLC_TILE_HASH(FMT, true, false);       \
+  } else {                                  \
+    DMLC_TILE_HASH(FMT, false, false);      \
+  }
     if (format == TextFormat::kLibFM) {
-      if (fp8) {
-        DMLC_TILE_HASH(TextFormat::kLibFM, true);
-      } else {
-        DMLC_TILE_HASH(TextFormat::kLibFM, false);
-      }
+      DMLC_TILE_HASH_FMT(TextFormat::kLibFM)
     } else {
-      if (fp8) {
-        DMLC_TILE_HASH(TextFormat::kLibSVM, true);
-      } else {
-        DMLC_TILE_HASH(TextFormat::kLibSVM, false);
-      }
+      DMLC_TILE_HASH_FMT(TextFormat::kLibSVM)
     }
+#undef DMLC_TILE_HASH_FMT
 #undef DMLC_TILE_HASH
   }
   LaunchFinish(partials, ntiles, meta, host_meta, nullptr, 0ull, 0ull, stream);
+  return ntiles != 0 ? groups : 0;
 }
 
-template void LaunchTileHashed<uint32_t>(const char*, size_t, TextFormat, const uint64_t*,
-                                         uint64_t, uint64_t, int, float, uint32_t, bool, void*,
-                                         float*, MetaPartial*, ChunkMeta*, ChunkMeta*, hipStream_t);
-template void LaunchTileHashed<uint64_t>(const char*, size_t, TextFormat, const uint64_t*,
-                                         uint64_t, uint64_t, int, float, uint32_t, bool, void*,
-                                         float*, MetaPartial*, ChunkMeta*, ChunkMeta*, hipStream_t);
+template size_t LaunchTileHashed<uint32_t>(const char*, size_t, TextFormat, const uint64_t*,
+                                           uint64_t, uint64_t, int, float, uint32_t, bool, void*,
+                                           float*, MetaPartial*, ChunkMeta*, ChunkMeta*,
+                                           hipStream_t, const HashOnePass*);
+template size_t LaunchTileHashed<uint64_t>(const char*, size_t, TextFormat, const uint64_t*,
+                                           uint64_t, uint64_t, int, float, uint32_t, bool, void*,
+                                           float*, MetaPartial*, ChunkMeta*, ChunkMeta*,
+                                           hipStream_t, const HashOnePass*);
 
 template void LaunchTileFill<uint32_t>(const char*, size_t, TextFormat, const uint64_t*,
                                        const FillTarget<uint32_t>&, MetaPartial*, ChunkMeta*,

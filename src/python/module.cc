@@ -456,6 +456,7 @@ class PyDeviceParser {
     d["rows"] = s.rows;
     d["nnz"] = s.nnz;
     d["exact_chunks"] = s.exact_chunks;
+    d["one_pass_chunks"] = s.one_pass_chunks;
     d["wait_reader_sec"] = s.wait_reader_sec;
     d["wait_gpu_sec"] = s.wait_gpu_sec;
     d["zero_copy"] = s.zero_copy;

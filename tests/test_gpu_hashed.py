@@ -266,3 +266,56 @@ def test_fm_kernels_match_fp32(dim, rows):
     for got, want in ((model.w.grad, w.grad), (model.v.grad, v.grad), (model.bias.grad, b.grad)):
         err = (got - want).abs().max().item() / (want.abs().max().item() + 1e-6)
         assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("fmt", ["libsvm", "libfm"])
+def test_one_pass_hashed_matches_counted(tmp_path, fmt):
+    """A replayed pass into a reused batch runs one kernel per chunk (line
+    counts by decoupled look-back, no count kernel): the same fp8 bytes and
+    labels as the counted first pass; a batch too small for the partition
+    overflows, grows and the chunk is written again."""
+    p = str(tmp_path / f"big.{fmt}")
+    data.write_synthetic(p, 0, 30000, format=fmt, seed=11)
+    g = data.GPUParser(p, format=fmt, chunk_bytes=1 << 20, hbm_cache=1)
+    a = g.parse_all_hashed(512, seed=6)  # first pass: caching, C1 + C2 + hash
+    want_x = a["x"].view(torch.uint8).clone()
+    want_l = a["label"].clone()
+    assert g.stats()["one_pass_chunks"] == 0
+    g.before_first()
+    b = g.parse_all_hashed(512, seed=6, out=a)  # resident: one pass, merged chunks
+    assert g.stats()["one_pass_chunks"] >= 1
+    assert torch.equal(b["x"].view(torch.uint8), want_x)
+    assert torch.equal(b["label"], want_l)
+    small_p = str(tmp_path / f"small.{fmt}")
+    data.write_synthetic(small_p, 0, 50, format=fmt, seed=2)
+    small = data.GPUParser(small_p, format=fmt).parse_all_hashed(512, seed=6)
+    assert small["x"].shape[0] == 50
+    g.before_first()
+    c = g.parse_all_hashed(512, seed=6, out=small)
+    assert tuple(c["x"].shape) == tuple(want_x.shape)
+    assert torch.equal(c["x"].view(torch.uint8), want_x)
+    assert torch.equal(c["label"], want_l)
+
+
+@pytest.mark.parametrize("bad", ["0 1:1\n 1 2:1\n", "1 3:1\x0b 4:1\n"])
+def test_one_pass_hashed_irregular_falls_back(tmp_path, bad):
+    """Blank-started lines and stray control bytes, which the count kernel
+    flags on the counted pass, are flagged by the one-pass kernel itself: the
+    chunk takes the exact kernels and the batch equals the counted pass."""
+    p = str(tmp_path / "irr.libsvm")
+    data.write_synthetic(p, 0, 8000, format="libsvm", seed=5)
+    with open(p, "a") as f:
+        f.write(bad)
+    data.write_synthetic(str(tmp_path / "t"), 8000, 16000, format="libsvm", seed=5)
+    with open(p, "a") as f:
+        f.write(open(str(tmp_path / "t")).read())
+    g = data.GPUParser(p, format="libsvm", chunk_bytes=1 << 20, hbm_cache=1)
+    a = g.parse_all_hashed(256, seed=3, fp8=False)
+    want_x, want_l = a["x"].clone(), a["label"].clone()
+    e0 = g.stats()["exact_chunks"]
+    assert e0 >= 1
+    g.before_first()
+    b = g.parse_all_hashed(256, seed=3, fp8=False, out=a)
+    assert g.stats()["exact_chunks"] > e0
+    np.testing.assert_array_equal(b["label"].cpu().numpy(), want_l.cpu().numpy())
+    np.testing.assert_allclose(b["x"].cpu().numpy(), want_x.cpu().numpy(), rtol=1e-6, atol=1e-6)
