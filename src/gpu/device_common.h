@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 namespace dmlc {
 namespace gpu {
@@ -28,11 +29,53 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+/*! \brief x of lane - 1 (lane 0: 0): DPP wave_shr:1, no LDS crossbar trip */
+__device__ __forceinline__ uint32_t lane_shr1(uint32_t x) {
+  return static_cast<uint32_t>(
+      __builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x138, 0xF, 0xF, false));
+}
+
+/*! \brief x of lane 63, as a scalar (uniform to the compiler) */
+__device__ __forceinline__ uint32_t lane63(uint32_t x) {
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), 63));
+}
+
+/*! \brief a wave-uniform value made scalar (the compiler then keeps the
+ *  control flow on it uniform: scalar branches, no exec-mask bookkeeping) */
+__device__ __forceinline__ uint32_t uniform(uint32_t x) {
+  return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(x)));
+}
+__device__ __forceinline__ uint64_t uniform(uint64_t x) {
+  return static_cast<uint64_t>(uniform(static_cast<uint32_t>(x))) |
+         (static_cast<uint64_t>(uniform(static_cast<uint32_t>(x >> 32))) << 32);
+}
+
+/*!
+ * \brief inclusive u32 prefix sum over the wave with DPP only: row_shr 1/2/4/8
+ *  within each 16-lane row, then row_bcast:15 / row_bcast:31 across rows (the
+ *  GFX9 / CDNA cross-row broadcasts) -- six VALU ops against six LDS-crossbar
+ *  round trips of a __shfl_up ladder.  Lanes without a source add 0.
+ */
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+  int x = static_cast<int>(v);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+  return static_cast<uint32_t>(x);
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
+  if constexpr (std::is_integral<T>::value && sizeof(T) == 4) {
+    return static_cast<T>(lane63(wave_incl_scan_u32(static_cast<uint32_t>(v))));
+  } else {
 #pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, kWave);
-  return v;
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, kWave);
+    return v;
+  }
 }
 
 template <typename T>
@@ -48,15 +91,31 @@ __device__ __forceinline__ T wave_max(T v) {
 /*! \brief exclusive prefix sum across the wave; *total = wave sum */
 template <typename T>
 __device__ __forceinline__ T wave_excl_scan(T v, T* total) {
-  const int lane = lane_id();
-  T x = v;
+  if constexpr (std::is_integral<T>::value && sizeof(T) == 4) {
+    const uint32_t x = wave_incl_scan_u32(static_cast<uint32_t>(v));
+    *total = static_cast<T>(lane63(x));
+    return static_cast<T>(x - static_cast<uint32_t>(v));
+  } else {
+    const int lane = lane_id();
+    T x = v;
 #pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    T y = __shfl_up(x, d, kWave);
-    if (lane >= d) x += y;
+    for (int d = 1; d < kWave; d <<= 1) {
+      T y = __shfl_up(x, d, kWave);
+      if (lane >= d) x += y;
+    }
+    *total = __shfl(x, kWave - 1, kWave);
+    return x - v;
   }
-  *total = __shfl(x, kWave - 1, kWave);
-  return x - v;
+}
+
+/*! \brief wave_excl_scan of a u64 made of two u32 counters that never carry
+ *  into each other (packed per-lane counts): two DPP scans */
+__device__ __forceinline__ uint64_t wave_excl_scan_2x32(uint64_t v, uint64_t* total) {
+  uint32_t tlo, thi;
+  const uint32_t lo = wave_excl_scan(static_cast<uint32_t>(v), &tlo);
+  const uint32_t hi = wave_excl_scan(static_cast<uint32_t>(v >> 32), &thi);
+  *total = (static_cast<uint64_t>(thi) << 32) | tlo;
+  return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
 /*!

@@ -149,7 +149,7 @@ __device__ __forceinline__ uint4 load16(const uint8_t* __restrict__ text, size_t
 /*! \brief byte before `pos` of this lane: lane t-1's last byte, or memory for lane 0 */
 __device__ __forceinline__ uint32_t prev_byte(const uint8_t* __restrict__ text, size_t pos,
                                               uint4 v) {
-  const uint32_t from_left = __shfl_up(v.w >> 24, 1, dev::kWave);
+  const uint32_t from_left = dev::lane_shr1(v.w >> 24);
   if (dev::lane_id() != 0) return from_left;
   return pos == 0 ? static_cast<uint32_t>('\n') : text[pos - 1];
 }
@@ -300,8 +300,8 @@ __global__ __launch_bounds__(kThreads) void k_tile_count(const uint8_t* __restri
   auto count_tile = [&](auto full) {
 #pragma unroll
     for (int j = 0; j < kCountLoads; ++j) {
-      const uint32_t left = __shfl_up(v[j].w >> 24, 1, dev::kWave);
-      const uint32_t wrap = j == 0 ? first : __shfl(v[j - 1].w >> 24, dev::kWave - 1, dev::kWave);
+      const uint32_t left = dev::lane_shr1(v[j].w >> 24);
+      const uint32_t wrap = j == 0 ? first : dev::lane63(v[j - 1].w >> 24);
       const uint32_t pc = lane == 0 ? wrap : left;
       bad |= count16<decltype(full)::value>(v[j], pc, base + j * 1024 + lane * 16, n, &lines,
                                             &toks, &qtoks);
@@ -852,8 +852,10 @@ __device__ __forceinline__ PrevTok prev_token_status(uint32_t tm_a, uint32_t lm_
 __device__ __forceinline__ uint32_t step_last_status(uint32_t tm_a, uint32_t lm_a, uint32_t tm_b,
                                                      uint32_t lm_b, uint32_t carried) {
   const uint64_t bb = __ballot(tm_b != 0), ba = __ballot(tm_a != 0);
-  const uint32_t sb = __shfl(slice_last(tm_b, lm_b), bb ? 63 - __builtin_clzll(bb) : 0, dev::kWave);
-  const uint32_t sa = __shfl(slice_last(tm_a, lm_a), ba ? 63 - __builtin_clzll(ba) : 0, dev::kWave);
+  const uint32_t sb = __builtin_amdgcn_readlane(slice_last(tm_b, lm_b),
+                                                bb ? 63 - __builtin_clzll(bb) : 0);
+  const uint32_t sa = __builtin_amdgcn_readlane(slice_last(tm_a, lm_a),
+                                                ba ? 63 - __builtin_clzll(ba) : 0);
   // wave-uniform: kept in a scalar register
   return __builtin_amdgcn_readfirstlane(bb ? sb : (ba ? sa : carried));
 }
@@ -1093,14 +1095,14 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
     ss[lane] = a;
     ss[64 + lane] = b;
     if (lane < 4) ss[128 + lane] = t;
-    const uint32_t left_a = __shfl_up(a.w >> 24, 1, dev::kWave);
+    const uint32_t left_a = dev::lane_shr1(a.w >> 24);
     const uint32_t pc_a = lane == 0 ? carry_pc : left_a;
-    const uint32_t left_b = __shfl_up(b.w >> 24, 1, dev::kWave);
+    const uint32_t left_b = dev::lane_shr1(b.w >> 24);
     // cross-lane reads run in every lane (a shuffle inside `lane == 0 ? :`
     // would execute with only lane 0 active and read an inactive lane)
-    const uint32_t last_a = __shfl(a.w >> 24, dev::kWave - 1, dev::kWave);
+    const uint32_t last_a = dev::lane63(a.w >> 24);
     const uint32_t pc_b = lane == 0 ? last_a : left_b;
-    carry_pc = __shfl(b.w >> 24, dev::kWave - 1, dev::kWave);
+    carry_pc = dev::lane63(b.w >> 24);
     uint32_t lm_a, tm_a, lm_b, tm_b;
     if (tile0 + static_cast<size_t>(s + 1) * kStepBytes <= n) {  // wave-uniform: a full step
       (void)lane_masks<false, true>(a, pc_a, pos_a, n, &lm_a, &tm_a);
@@ -1132,7 +1134,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
                          (static_cast<uint64_t>(__popc(lm_a)) << 32) |
                          (static_cast<uint64_t>(__popc(lm_b)) << 48);
     uint64_t tot;
-    const uint64_t before = dev::wave_excl_scan(cnt, &tot);
+    const uint64_t before = dev::wave_excl_scan_2x32(cnt, &tot);  // 16-bit fields: no carries
     const uint32_t ntok_a = static_cast<uint32_t>(tot & 0xFFFFu);
     const uint32_t ntok = ntok_a + static_cast<uint32_t>((tot >> 16) & 0xFFFFu);
     const uint32_t nline_a = static_cast<uint32_t>((tot >> 32) & 0xFFFFu);
@@ -1442,8 +1444,8 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
     uint32_t lines = 0;
 #pragma unroll
     for (int j = 0; j < kCountLoads; ++j) {
-      const uint32_t left = __shfl_up(v[j].w >> 24, 1, dev::kWave);
-      const uint32_t wrap = j == 0 ? carry_pc : __shfl(v[j - 1].w >> 24, dev::kWave - 1, dev::kWave);
+      const uint32_t left = dev::lane_shr1(v[j].w >> 24);
+      const uint32_t wrap = j == 0 ? carry_pc : dev::lane63(v[j - 1].w >> 24);
       const uint32_t pc = lane == 0 ? wrap : left;
       if (full) {
         lines += lines16<true>(v[j], pc, 16);
@@ -1488,21 +1490,28 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
         // lane-interleaved float4s (consecutive lanes, consecutive 16 B: no
         // bank conflicts on the b128 read / zero), 4 fp8 bytes per lane store
         uint8_t* o = static_cast<uint8_t*>(out.x) + g * static_cast<uint64_t>(dim);
-        for (int c = lane * 4; c < dim; c += dev::kWave * 4) {
-          float4* r4 = reinterpret_cast<float4*>(row + c);
-          const float4 x = *r4;
-          *r4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-          int pk = __builtin_amdgcn_cvt_pk_fp8_f32(x.x * out.scale, x.y * out.scale, 0, false);
-          pk = __builtin_amdgcn_cvt_pk_fp8_f32(x.z * out.scale, x.w * out.scale, pk, true);
-          if (ok) *reinterpret_cast<uint32_t*>(o + c) = static_cast<uint32_t>(pk);
+#pragma unroll 4
+        for (int c0 = 0; c0 < dim; c0 += dev::kWave * 4) {  // uniform trip count
+          const int c = c0 + lane * 4;
+          if (c < dim) {  // (no break: the loop exit stays uniform)
+            float4* r4 = reinterpret_cast<float4*>(row + c);
+            const float4 x = *r4;
+            *r4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            int pk = __builtin_amdgcn_cvt_pk_fp8_f32(x.x * out.scale, x.y * out.scale, 0, false);
+            pk = __builtin_amdgcn_cvt_pk_fp8_f32(x.z * out.scale, x.w * out.scale, pk, true);
+            if (ok) *reinterpret_cast<uint32_t*>(o + c) = static_cast<uint32_t>(pk);
+          }
         }
       } else {
         float* o = static_cast<float*>(out.x) + g * static_cast<uint64_t>(dim);
-        for (int c = lane * 4; c < dim; c += dev::kWave * 4) {
-          float4* r4 = reinterpret_cast<float4*>(row + c);
-          const float4 x = *r4;
-          *r4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-          if (ok) *reinterpret_cast<float4*>(o + c) = make_float4(x.x, x.y, x.z, x.w);
+        for (int c0 = 0; c0 < dim; c0 += dev::kWave * 4) {
+          const int c = c0 + lane * 4;
+          if (c < dim) {
+            float4* r4 = reinterpret_cast<float4*>(row + c);
+            const float4 x = *r4;
+            *r4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (ok) *reinterpret_cast<float4*>(o + c) = make_float4(x.x, x.y, x.z, x.w);
+          }
         }
       }
       dev::wave_sync();  // zeros land before the next row's adds
@@ -1529,12 +1538,12 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
       st[lane] = a;
       st[64 + lane] = b;
       if (lane < 4) st[128 + lane] = t;
-      const uint32_t left_a = __shfl_up(a.w >> 24, 1, dev::kWave);
+      const uint32_t left_a = dev::lane_shr1(a.w >> 24);
       const uint32_t pc_a = lane == 0 ? carry_pc : left_a;
-      const uint32_t left_b = __shfl_up(b.w >> 24, 1, dev::kWave);
-      const uint32_t last_a = __shfl(a.w >> 24, dev::kWave - 1, dev::kWave);
+      const uint32_t left_b = dev::lane_shr1(b.w >> 24);
+      const uint32_t last_a = dev::lane63(a.w >> 24);
       const uint32_t pc_b = lane == 0 ? last_a : left_b;
-      carry_pc = __shfl(b.w >> 24, dev::kWave - 1, dev::kWave);
+      carry_pc = dev::lane63(b.w >> 24);
       uint32_t lm_a, tm_a, lm_b, tm_b;
       // one pass: C1's checks of blank-started lines and control bytes here
       // (token starts outside [0-9+-.] fail the decoder and are flagged there)
@@ -1578,7 +1587,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
                      (static_cast<uint64_t>(__popc(lm_a)) << 32) |
                      (static_cast<uint64_t>(__popc(lm_b)) << 48);
       uint64_t tot;
-      uint64_t before = dev::wave_excl_scan(cnt, &tot);
+      uint64_t before = dev::wave_excl_scan_2x32(cnt, &tot);  // 16-bit fields: no carries
       const uint32_t nline_a = static_cast<uint32_t>((tot >> 32) & 0xFFFFu);
       const uint32_t nline = nline_a + static_cast<uint32_t>(tot >> 48);
       const uint32_t la0 = lcnt + static_cast<uint32_t>((before >> 32) & 0xFFFFu);
@@ -1588,7 +1597,10 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
         tm_a = owned_tokens(tm_a, lm_a, la0, own);
         tm_b = owned_tokens(tm_b, lm_b, lb0, own);
         cnt = static_cast<uint64_t>(__popc(tm_a)) | (static_cast<uint64_t>(__popc(tm_b)) << 16);
-        before = (before & ~0xFFFFFFFFull) | dev::wave_excl_scan(cnt, &tot);
+        uint32_t t32;
+        const uint32_t b32 = dev::wave_excl_scan<uint32_t>(static_cast<uint32_t>(cnt), &t32);
+        before = (before & ~0xFFFFFFFFull) | b32;
+        tot = (tot & ~0xFFFFFFFFull) | t32;
       }
       const uint32_t ntok_a = static_cast<uint32_t>(tot & 0xFFFFu);
       const uint32_t ntok = ntok_a + static_cast<uint32_t>((tot >> 16) & 0xFFFFu);
@@ -1666,8 +1678,9 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
         }
         const float sv = (h & 0x80000000u) ? -val : val;
         // the round's rows, in text order: list entries r0 .. r0 + 63
-        const uint32_t lo = sl[r0] >> 14;
-        const uint32_t hi = sl[r0 + dev::kWave - 1 < ndec ? r0 + dev::kWave - 1 : ndec - 1] >> 14;
+        const uint32_t lo = dev::uniform(sl[r0] >> 14);
+        const uint32_t hi =
+            dev::uniform(sl[r0 + dev::kWave - 1 < ndec ? r0 + dev::kWave - 1 : ndec - 1] >> 14);
         for (uint32_t rr = lo; rr <= hi; ++rr) {
           if (rr != open) {
             if (open != 0) flush(open);
