@@ -894,9 +894,10 @@ constexpr int kSteps = static_cast<int>(kTileBytes / kStepBytes);
 constexpr uint32_t kSlotBytes = kStepBytes + 64;           // a step + 64 B of the next
 constexpr uint32_t kStageVecs = 2 * kSlotBytes / 16;       // two slots: step s and s - 1
 constexpr uint32_t kListCap = kDecodeCarry + kStepBytes / 2;  // carried + a step's tokens
-// k_tile_hash: no carried entries, and a step of more tokens is irregular --
-// sized so that 4 workgroups fit a CU with a 1024-wide f32 row per wave
-constexpr uint32_t kHashListCap = 896;
+// k_tile_hash: no carried entries; a step of more tokens is listed in two
+// halves.  Sized so that 5 workgroups fit a CU with a 1024-wide f32 row per
+// wave: 4 x (2112 B text + (428 + 64) x 4 B list) + 16 KiB rows + the ticket
+constexpr uint32_t kHashListCap = 428;
 
 /*!
  * \brief the 16 B at chunk offset pos, bytes at or past n zeroed (the
@@ -1604,21 +1605,19 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
       }
       const uint32_t ntok_a = static_cast<uint32_t>(tot & 0xFFFFu);
       const uint32_t ntok = ntok_a + static_cast<uint32_t>((tot >> 16) & 0xFFFFu);
-      if (ntok > kHashListCap) {  // wave-uniform: > 0.44 tokens per byte -- exact kernels
+      // a step of more tokens than the list holds is listed and decoded in
+      // its two 1 KiB halves (a half of more: the exact kernels)
+      const uint32_t ntok_b = ntok - ntok_a;
+      const bool split = ntok > kHashListCap;
+      if (split && (ntok_a > kHashListCap || ntok_b > kHashListCap)) {
         irregular = true;
         break;
       }
-      list_slice<kHashListCap>(sl, tm_a, lm_a, static_cast<uint32_t>(before & 0xFFFFu),
-                               sbase + lane * 16, la0, lane);
-      list_slice<kHashListCap>(sl, tm_b, lm_b,
-                               ntok_a + static_cast<uint32_t>((before >> 16) & 0xFFFFu),
-                               sbase + 1024 + lane * 16, lb0, lane);
-      dev::wave_sync();
       lcnt += nline;
       const bool eol_end = carry_pc == '\n' || carry_pc == '\r';
       const bool last = nxt >= n || lcnt > own || (s + 1 >= kSteps && lcnt == own && eol_end);
-      // a, b, t are consumed: the next step's loads go straight into them (in
-      // flight during this step's rounds)
+      // a, b, t are consumed (staged, masks taken): the next step's loads go
+      // straight into them (in flight during this step's rounds)
       if (!last) {
         const uint32_t so = static_cast<uint32_t>(s + 1) * kStepBytes;
         a = bload16(trs, loff + so);
@@ -1626,7 +1625,21 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
         if (lane < 4) t = bload16(trs, loff + so + kStepBytes);
       }
 
-      const uint32_t ndec = ntok;
+      list_slice<kHashListCap>(sl, tm_a, lm_a, static_cast<uint32_t>(before & 0xFFFFu),
+                               sbase + lane * 16, la0, lane);
+      // split: the b half is listed after the a half's rounds, from two packed
+      // registers (few live across the rounds)
+      const uint32_t pk_m = tm_b | (lm_b << 16);
+      const uint32_t pk_o = static_cast<uint32_t>((before >> 16) & 0xFFFFu) | (lb0 << 16);
+      if (!split) {
+        list_slice<kHashListCap>(sl, tm_b, lm_b,
+                                 ntok_a + static_cast<uint32_t>((before >> 16) & 0xFFFFu),
+                                 sbase + 1024 + lane * 16, lb0, lane);
+      }
+      dev::wave_sync();
+#pragma unroll 1
+      for (int part = 0;; ++part) {
+      const uint32_t ndec = !split ? ntok : (part == 0 ? ntok_a : ntok_b);
       for (uint32_t r0 = 0; r0 < ndec; r0 += dev::kWave) {
         const uint32_t li = r0 + slot;
         const bool active = li < ndec;
@@ -1689,6 +1702,12 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
           if (feat && lc == rr) atomicAdd(&row[bucket], sv);
         }
       }
+      if (!split || part == 1) break;
+      dev::wave_sync();  // the a half's rounds are done with the list
+      list_slice<kHashListCap>(sl, pk_m & 0xFFFFu, pk_m >> 16, pk_o & 0xFFFFu,
+                               sbase + 1024 + lane * 16, pk_o >> 16, lane);
+      dev::wave_sync();
+      }  // part
       if (last) break;
       dev::wave_sync();  // every lane is done with this step's text and list
     }

@@ -319,3 +319,29 @@ def test_one_pass_hashed_irregular_falls_back(tmp_path, bad):
     assert g.stats()["exact_chunks"] > e0
     np.testing.assert_array_equal(b["label"].cpu().numpy(), want_l.cpu().numpy())
     np.testing.assert_allclose(b["x"].cpu().numpy(), want_x.cpu().numpy(), rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("width", [2, 1])
+def test_fused_hash_dense_token_steps(tmp_path, width):
+    """Steps with more tokens than the hash kernel's list (valueless 2-digit
+    LibSVM features: ~680 tokens per 2 KiB step) are listed and decoded in
+    two halves; 1-digit ones (~1000 per step) go to the exact kernels.  Both
+    equal the all-exact batch."""
+    rng = np.random.default_rng(width)
+    lo, hi = (10, 100) if width == 2 else (1, 10)
+    lines = []
+    for i in range(3000):
+        feats = " ".join(str(v) for v in rng.integers(lo, hi, size=int(rng.integers(1, 60))))
+        lines.append(f"{i % 2} {feats}\n")
+    p = str(tmp_path / "dense.libsvm")
+    with open(p, "w") as f:
+        f.writelines(lines)
+    g = data.GPUParser(p, format="libsvm", chunk_bytes=64 * 1024)
+    fused = g.parse_all_hashed(256, seed=8, fp8=False, strategy="fused")
+    if width == 2:
+        assert g.stats()["exact_chunks"] == 0
+    exact = data.GPUParser(p, format="libsvm", chunk_bytes=64 * 1024, fast_path=0).parse_all_hashed(
+        256, seed=8, fp8=False, strategy="fused")
+    np.testing.assert_array_equal(fused["label"].cpu().numpy(), exact["label"].cpu().numpy())
+    np.testing.assert_allclose(fused["x"].cpu().numpy(), exact["x"].cpu().numpy(), rtol=1e-6,
+                               atol=1e-6)
