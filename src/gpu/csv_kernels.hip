@@ -131,21 +131,21 @@ __device__ __forceinline__ Slice step_slice(uint4 g, uint32_t s, uint32_t nrem, 
   const uint32_t inside = p >= nrem ? 0u : (nrem - p >= 16 ? 0xFFFFu : (1u << (nrem - p)) - 1u);
   const bool bad = ((ctl16(g) | z) & inside) != 0;
   const uint32_t last_e = (e >> 15) & 1u, last_d = (d >> 15) & 1u;
-  const uint32_t up_e = __shfl_up(last_e, 1, kWave);
-  const uint32_t up_d = __shfl_up(last_d, 1, kWave);
+  const uint32_t up_e = lane_shr1(last_e);
+  const uint32_t up_d = lane_shr1(last_d);
   const uint32_t pe = lane == 0 ? w->carry_eol : up_e;
   const uint32_t pd = lane == 0 ? w->carry_delim : up_d;
   uint32_t lm = ~e & ((e << 1) | pe) & 0xFFFFu;
   // a delimiter opens a field unless the line (or the chunk) ends right after
   // it: no empty last field for a trailing delimiter (reference csv_parser.h:83-96)
   uint32_t fm = lm | (((d << 1) | pd) & ~e & 0xFFFFu);
-  w->carry_eol = __shfl(last_e, kWave - 1, kWave);
-  w->carry_delim = __shfl(last_d, kWave - 1, kWave);
+  w->carry_eol = lane63(last_e);
+  w->carry_delim = lane63(last_d);
   // ownership: from the first row start in the tile to the first one after it
   uint32_t own = 0xFFFFu;
   const uint64_t any_ls = __ballot(lm != 0);
   const int first_lane = any_ls != 0 ? __builtin_ctzll(any_ls) : 0;
-  const uint32_t first_lm = __shfl(lm, first_lane, kWave);
+  const uint32_t first_lm = __builtin_amdgcn_readlane(lm, first_lane);  // (first_lane: uniform)
   const uint32_t first_bit = first_lm & (0u - first_lm);
   if (s < kTileSteps) {
     if (!w->started) {
@@ -182,10 +182,18 @@ __device__ __forceinline__ Slice step_slice(uint4 g, uint32_t s, uint32_t nrem, 
   } else {
     col_scan(cfg, true, lane, w, &o, &nx);
   }
+  // fields / rows (<= 1024 each per step: 16-bit halves) and excluded
+  // columns: two DPP scans, repacked to the 21-bit layout of f21
   const uint64_t packed = static_cast<uint64_t>(__popc(fm)) |
-                          (static_cast<uint64_t>(__popc(lm)) << 21) |
-                          (static_cast<uint64_t>(nx) << 42);
-  o.before = wave_excl_scan(packed, &o.total);
+                          (static_cast<uint64_t>(__popc(lm)) << 16) |
+                          (static_cast<uint64_t>(nx) << 32);
+  uint64_t tot;
+  const uint64_t bef = wave_excl_scan_2x32(packed, &tot);
+  auto repack = [](uint64_t v) {
+    return (v & 0xFFFFull) | (((v >> 16) & 0xFFFFull) << 21) | ((v >> 32) << 42);
+  };
+  o.before = repack(bef);
+  o.total = repack(tot);
   return o;
 }
 

@@ -35,6 +35,12 @@ __device__ __forceinline__ uint32_t lane_shr1(uint32_t x) {
       __builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x138, 0xF, 0xF, false));
 }
 
+/*! \brief x of lane + 1 (lane 63: 0): DPP wave_shl:1 */
+__device__ __forceinline__ uint32_t lane_shl1(uint32_t x) {
+  return static_cast<uint32_t>(
+      __builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x130, 0xF, 0xF, false));
+}
+
 /*! \brief x of lane 63, as a scalar (uniform to the compiler) */
 __device__ __forceinline__ uint32_t lane63(uint32_t x) {
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), 63));
@@ -106,6 +112,12 @@ __device__ __forceinline__ T wave_excl_scan(T v, T* total) {
     *total = __shfl(x, kWave - 1, kWave);
     return x - v;
   }
+}
+
+/*! \brief wave_sum of a u64 made of two u32 counters that never carry */
+__device__ __forceinline__ uint64_t wave_sum_2x32(uint64_t v) {
+  return (static_cast<uint64_t>(wave_sum(static_cast<uint32_t>(v >> 32))) << 32) |
+         wave_sum(static_cast<uint32_t>(v));
 }
 
 /*! \brief wave_excl_scan of a u64 made of two u32 counters that never carry

@@ -49,7 +49,11 @@ constexpr uint32_t kMagic = 0xced7230aU;
 constexpr size_t kTileWords = 2048;  // 8 loads x 64 lanes x 4 words
 constexpr int kLoads = static_cast<int>(kTileWords / 256);
 constexpr uint32_t kSmallPart = 64;  // bytes copied lane-by-lane
-constexpr int kBigCap = static_cast<int>(kTileWords / 16);  // parts > 64 B in a tile, at most
+// parts > 64 B whose header lies in a tile: headers >= 19 words apart (2 + 17),
+// so at most 108 in 2048 words.  112 keeps the fill at 40 KiB of LDS per
+// workgroup: 4 workgroups per CU (kTileWords / 16 = 128 made it 3)
+constexpr int kBigCap = 112;
+static_assert(kBigCap * 19 >= static_cast<int>(kTileWords) + 19, "kBigCap too small");
 
 __device__ __forceinline__ uint32_t cflag_of(uint32_t lrec) { return lrec >> 29; }
 __device__ __forceinline__ uint32_t len_of(uint32_t lrec) { return lrec & ((1U << 29) - 1U); }
@@ -100,10 +104,10 @@ __device__ __forceinline__ void load_tile(const uint32_t* __restrict__ w, size_t
   const uint32_t tail = past < n ? w[past] : 0u;
 #pragma unroll
   for (int j = 0; j < kLoads; ++j) {
-    const uint32_t right = __shfl_down(t->q[j].x, 1, kWave);
-    // every lane runs the shuffle (a shuffle under a lane condition would
+    const uint32_t right = lane_shl1(t->q[j].x);
+    // every lane runs the cross-lane ops (under a lane condition they would
     // read an inactive lane)
-    const uint32_t next0 = __shfl(t->q[j + 1 < kLoads ? j + 1 : j].x, 0, kWave);
+    const uint32_t next0 = __builtin_amdgcn_readlane(t->q[j + 1 < kLoads ? j + 1 : j].x, 0);
     const uint32_t wrap = j + 1 < kLoads ? next0 : tail;
     t->after[j] = lane == kWave - 1 ? wrap : right;
   }
@@ -144,7 +148,7 @@ __global__ __launch_bounds__(kThreads) void k_rec_tile_count(const uint32_t* __r
   // a chunk starts at a record head
   if (tile == 0 && lane == 0 && n != 0 && !(t.q[0].x == kMagic && n > 1 && cflag_of(t.q[0].y) <= 1))
     err |= kRecErrBadPart;
-  c = wave_sum(c);
+  c = wave_sum_2x32(c);  // heads << 32 | bytes: no carries
   err = wave_or(err);
   if (lane == 0) {
     counts[tile] = c;
@@ -243,7 +247,7 @@ __global__ __launch_bounds__(kThreads) void k_rec_tile_fill(const uint32_t* __re
     uint32_t unused = 0;
     const uint64_t c = quad_counts(t.q[j], t.after[j], i0, n, &unused);
     uint64_t tot;
-    const uint64_t before = wave_excl_scan(c, &tot);
+    const uint64_t before = wave_excl_scan_2x32(c, &tot);  // heads << 32 | bytes
     uint64_t r = rec + (before >> 32);
     uint64_t p = pos + (before & 0xffffffffull);
     // parts of more than 64 B are > 16 words apart: at most one per quad
