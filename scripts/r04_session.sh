@@ -7,12 +7,11 @@
 # usage (through gpurun): bash scripts/r04_session.sh OUTDIR A|B|C
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}" || exit 1
-o=$1
+o=$1/$2  # each part in its own directory (gpu_check numbers its commands from 1)
 case "$2" in
   A)
     bash scripts/gpu_check.sh "$o" "tests -m gpu" \
       "python bench.py --steps 20 --warmup 5" \
-      "HSA_ENABLE_SDMA=0 python bench.py --steps 20 --warmup 5" \
       "python bench.py --mode hbm --steps 10 --warmup 2" \
       "python bench.py --mode hbm --format libfm --steps 10 --warmup 2" \
       "python bench.py --mode hbm --format csv --steps 10 --warmup 2" \
