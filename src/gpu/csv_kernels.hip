@@ -209,13 +209,12 @@ __device__ __forceinline__ void col_scan(const CsvCfg& cfg, bool count, int lane
   } else {
     x = static_cast<uint32_t>(__popc(fm));
   }
-#pragma unroll
-  for (int dd = 1; dd < kWave; dd <<= 1) {
-    const uint32_t y = __shfl_up(x, dd, kWave);
-    if (lane >= dd && !(x & 0x80000000u)) x = (x + (y & 0x7FFFFFFFu)) | (y & 0x80000000u);
-  }
-  const uint32_t prev = __shfl_up(x, 1, kWave);
-  const uint32_t last = __shfl(x, kWave - 1, kWave);
+  // segmented sum (bit 31: a row starts in this lane), DPP ladder
+  x = wave_incl_scan_op(x, [](uint32_t y, uint32_t v) {
+    return (v & 0x80000000u) ? v : ((v + (y & 0x7FFFFFFFu)) | (y & 0x80000000u));
+  });
+  const uint32_t prev = lane_shr1(x);
+  const uint32_t last = lane63(x);
   o->col0 = lane == 0 ? w->col_carry
                       : (prev & 0x7FFFFFFFu) + ((prev & 0x80000000u) ? 0u : w->col_carry);
   w->col_carry = (last & 0x7FFFFFFFu) + ((last & 0x80000000u) ? 0u : w->col_carry);

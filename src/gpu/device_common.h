@@ -73,6 +73,28 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
   return static_cast<uint32_t>(x);
 }
 
+/*!
+ * \brief inclusive scan under an associative op whose identity is 0
+ *  (op(0, x) == x; op(earlier, later)), by the same DPP ladder as
+ *  wave_incl_scan_u32 -- e.g. a segmented sum with a reset flag bit
+ */
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint32_t dpp_pull(uint32_t x) {
+  return static_cast<uint32_t>(
+      __builtin_amdgcn_update_dpp(0, static_cast<int>(x), kCtrl, kRowMask, 0xF, false));
+}
+template <typename Op>
+__device__ __forceinline__ uint32_t wave_incl_scan_op(uint32_t v, Op op) {
+  uint32_t x = v;
+  x = op(dpp_pull<0x111, 0xF>(x), x);  // row_shr:1
+  x = op(dpp_pull<0x112, 0xF>(x), x);  // row_shr:2
+  x = op(dpp_pull<0x114, 0xF>(x), x);  // row_shr:4
+  x = op(dpp_pull<0x118, 0xF>(x), x);  // row_shr:8
+  x = op(dpp_pull<0x142, 0xA>(x), x);  // row_bcast:15 -> rows 1, 3
+  x = op(dpp_pull<0x143, 0xC>(x), x);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
   if constexpr (std::is_integral<T>::value && sizeof(T) == 4) {
@@ -161,9 +183,14 @@ __device__ __forceinline__ T block_sum_256(T v, T* smem) {
 
 template <typename T>
 __device__ __forceinline__ T wave_or(T v) {
+  if constexpr (std::is_integral<T>::value && sizeof(T) == 4) {
+    return static_cast<T>(lane63(wave_incl_scan_op(static_cast<uint32_t>(v),
+                                                    [](uint32_t a, uint32_t b) { return a | b; })));
+  } else {
 #pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v |= __shfl_xor(v, d, kWave);
-  return v;
+    for (int d = 32; d >= 1; d >>= 1) v |= __shfl_xor(v, d, kWave);
+    return v;
+  }
 }
 
 /*!
