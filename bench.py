@@ -83,6 +83,8 @@ def parse_args():
                          "HBM and timed epochs parse it from there (kernel-bound); "
                          "cache: the `#cache` binary page file (DiskRowIter format, built once "
                          "from a GPU parse) is DMA'd zero-copy into the device CSR every step")
+    ap.add_argument("--replay-first-mb", type=float, default=None,
+                    help="HBM replay: first merged chunk (0: no ramp; default: the parser's)")
     ap.add_argument("--shape", default="uniform", choices=["uniform", "skewed", "mixed"],
                     help="synthetic row shape (dmlc/synthetic.h): uniform 20-60 tokens of "
                          "0.dddddd; skewed power-law tokens per line (some lines > 8 KiB), "
@@ -301,6 +303,8 @@ def main():
             return csr.rows, csr.nnz, csr.max_index, parser.bytes
     elif use_gpu:
         extra = {"label_column": 0} if args.format == "csv" else {}
+        if args.replay_first_mb is not None:
+            extra["replay_first_mb"] = args.replay_first_mb
         parser = data.GPUParser(ddir, rank, world, format=args.format, chunk_mb=args.chunk_mb,
                                 read_threads=read_threads, pinned_slots=args.pinned_slots,
                                 device_slots=args.device_slots, device=local_rank,
