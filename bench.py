@@ -85,6 +85,8 @@ def parse_args():
                          "from a GPU parse) is DMA'd zero-copy into the device CSR every step")
     ap.add_argument("--replay-first-mb", type=float, default=None,
                     help="HBM replay: first merged chunk (0: no ramp; default: the parser's)")
+    ap.add_argument("--replay-chunk-mb", type=float, default=None,
+                    help="HBM replay: merged chunk cap (default: the parser's)")
     ap.add_argument("--shape", default="uniform", choices=["uniform", "skewed", "mixed"],
                     help="synthetic row shape (dmlc/synthetic.h): uniform 20-60 tokens of "
                          "0.dddddd; skewed power-law tokens per line (some lines > 8 KiB), "
@@ -305,6 +307,8 @@ def main():
         extra = {"label_column": 0} if args.format == "csv" else {}
         if args.replay_first_mb is not None:
             extra["replay_first_mb"] = args.replay_first_mb
+        if args.replay_chunk_mb is not None:
+            extra["replay_chunk_mb"] = args.replay_chunk_mb
         parser = data.GPUParser(ddir, rank, world, format=args.format, chunk_mb=args.chunk_mb,
                                 read_threads=read_threads, pinned_slots=args.pinned_slots,
                                 device_slots=args.device_slots, device=local_rank,

@@ -990,9 +990,11 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     // resident text and a batch that already has rows (a reused one): one pass
     // per chunk (k_tile_hash look-back, no C1 / C2), so nothing is gained by a
     // small first chunk -- merge up to 2 x replay_chunk_bytes from the start
+    // (below 2 GiB: an irregular chunk falls back to the exact kernels' 32-bit
+    // offsets, as DeviceParserConfig::Update checks for replay_chunk_bytes)
     const bool one_pass = cfg_.fast_path && dim % 16 == 0 && replay_ && out->row_cap != 0;
     if (one_pass) {
-      merge_limit_ = 2 * cfg_.replay_chunk_bytes;
+      merge_limit_ = std::min(2 * cfg_.replay_chunk_bytes, (size_t(1) << 31) - (size_t(64) << 20));
       if (merge_cap_ == 0) merge_cap_ = merge_limit_;
     }
     while (WithNextChunk([&](const char* text, size_t nbytes) {
