@@ -1639,74 +1639,74 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
       dev::wave_sync();
 #pragma unroll 1
       for (int part = 0;; ++part) {
-      const uint32_t ndec = !split ? ntok : (part == 0 ? ntok_a : ntok_b);
-      for (uint32_t r0 = 0; r0 < ndec; r0 += dev::kWave) {
-        const uint32_t li = r0 + slot;
-        const bool active = li < ndec;
-        const uint32_t e = active ? sl[li] : 0u;
-        const bool is_label = active && ((e >> 13) & 1u) != 0;
-        const uint32_t off = e & 0x1FFFu;
-        const uint32_t lc = e >> 14;
-        tok::Token t;
-        t.u0_hi = t.u1_hi = 0;
-        t.u1 = 0;
-        bool bad = false;
-        bool ok = tok::decode<F>(st, off, is_label, &t);
-        if (__any(active & !ok)) {
+        const uint32_t ndec = !split ? ntok : (part == 0 ? ntok_a : ntok_b);
+        for (uint32_t r0 = 0; r0 < ndec; r0 += dev::kWave) {
+          const uint32_t li = r0 + slot;
+          const bool active = li < ndec;
+          const uint32_t e = active ? sl[li] : 0u;
+          const bool is_label = active && ((e >> 13) & 1u) != 0;
+          const uint32_t off = e & 0x1FFFu;
+          const uint32_t lc = e >> 14;
+          tok::Token t;
+          t.u0_hi = t.u1_hi = 0;
+          t.u1 = 0;
+          bool bad = false;
+          bool ok = tok::decode<F>(st, off, is_label, &t);
+          if (__any(active & !ok)) {
+            if (active & !ok) {
+              const tok::ExtToken x = tok::decode_ext<F>(st, off, is_label, kSlotBytes);
+              if (x.ok) t = x.t;
+              ok = x.ok;
+            }
+          }
           if (active & !ok) {
-            const tok::ExtToken x = tok::decode_ext<F>(st, off, is_label, kSlotBytes);
-            if (x.ok) t = x.t;
-            ok = x.ok;
+            const size_t gpos = cur + off;
+            const GenericResult gr = generic_token<F, IndexType>(text, n, gpos, is_label);
+            t = gr.t;
+            bad = gr.bad;
+            irregular |= !num_start(text[gpos]);  // qid:, comments, junk: the exact kernels
+          }
+          if (active & is_label && R + lc - 1 < row_cap) out.label[R + lc - 1] = t.f0;
+          bool feat = active & !is_label;
+          uint64_t key;
+          float val;
+          const uint64_t u0 = (static_cast<uint64_t>(t.u0_hi) << 32) | t.u0;
+          if constexpr (F == TextFormat::kLibSVM) {
+            key = static_cast<uint64_t>(static_cast<IndexType>(u0));
+            val = t.r == 2 ? t.f0 : 1.0f;
+          } else {
+            const uint64_t u1 = (static_cast<uint64_t>(t.u1_hi) << 32) | t.u1;
+            feat &= t.r >= 2;  // not field:index: the CPU parser skips it too
+            key = dev::hash_key(static_cast<uint64_t>(static_cast<IndexType>(u1)),
+                                static_cast<uint64_t>(static_cast<IndexType>(u0)), true);
+            val = t.r == 3 ? t.f0 : 1.0f;
+          }
+          neg |= active && bad;
+          const uint32_t h = dev::hash_u64(key, out.seed);
+          uint32_t bucket;
+          if (pow2) {
+            bucket = h & dmask;
+          } else {
+            bucket = h % static_cast<uint32_t>(dim);
+          }
+          const float sv = (h & 0x80000000u) ? -val : val;
+          // the round's rows, in text order: list entries r0 .. r0 + 63
+          const uint32_t lo = dev::uniform(sl[r0] >> 14);
+          const uint32_t hi =
+              dev::uniform(sl[r0 + dev::kWave - 1 < ndec ? r0 + dev::kWave - 1 : ndec - 1] >> 14);
+          for (uint32_t rr = lo; rr <= hi; ++rr) {
+            if (rr != open) {
+              if (open != 0) flush(open);
+              open = rr;
+            }
+            if (feat && lc == rr) atomicAdd(&row[bucket], sv);
           }
         }
-        if (active & !ok) {
-          const size_t gpos = cur + off;
-          const GenericResult gr = generic_token<F, IndexType>(text, n, gpos, is_label);
-          t = gr.t;
-          bad = gr.bad;
-          irregular |= !num_start(text[gpos]);  // qid:, comments, junk: the exact kernels
-        }
-        if (active & is_label && R + lc - 1 < row_cap) out.label[R + lc - 1] = t.f0;
-        bool feat = active & !is_label;
-        uint64_t key;
-        float val;
-        const uint64_t u0 = (static_cast<uint64_t>(t.u0_hi) << 32) | t.u0;
-        if constexpr (F == TextFormat::kLibSVM) {
-          key = static_cast<uint64_t>(static_cast<IndexType>(u0));
-          val = t.r == 2 ? t.f0 : 1.0f;
-        } else {
-          const uint64_t u1 = (static_cast<uint64_t>(t.u1_hi) << 32) | t.u1;
-          feat &= t.r >= 2;  // not field:index: the CPU parser skips it too
-          key = dev::hash_key(static_cast<uint64_t>(static_cast<IndexType>(u1)),
-                              static_cast<uint64_t>(static_cast<IndexType>(u0)), true);
-          val = t.r == 3 ? t.f0 : 1.0f;
-        }
-        neg |= active && bad;
-        const uint32_t h = dev::hash_u64(key, out.seed);
-        uint32_t bucket;
-        if (pow2) {
-          bucket = h & dmask;
-        } else {
-          bucket = h % static_cast<uint32_t>(dim);
-        }
-        const float sv = (h & 0x80000000u) ? -val : val;
-        // the round's rows, in text order: list entries r0 .. r0 + 63
-        const uint32_t lo = dev::uniform(sl[r0] >> 14);
-        const uint32_t hi =
-            dev::uniform(sl[r0 + dev::kWave - 1 < ndec ? r0 + dev::kWave - 1 : ndec - 1] >> 14);
-        for (uint32_t rr = lo; rr <= hi; ++rr) {
-          if (rr != open) {
-            if (open != 0) flush(open);
-            open = rr;
-          }
-          if (feat && lc == rr) atomicAdd(&row[bucket], sv);
-        }
-      }
-      if (!split || part == 1) break;
-      dev::wave_sync();  // the a half's rounds are done with the list
-      list_slice<kHashListCap>(sl, pk_m & 0xFFFFu, pk_m >> 16, pk_o & 0xFFFFu,
-                               sbase + 1024 + lane * 16, pk_o >> 16, lane);
-      dev::wave_sync();
+        if (!split || part == 1) break;
+        dev::wave_sync();  // the a half's rounds are done with the list
+        list_slice<kHashListCap>(sl, pk_m & 0xFFFFu, pk_m >> 16, pk_o & 0xFFFFu,
+                                 sbase + 1024 + lane * 16, pk_o >> 16, lane);
+        dev::wave_sync();
       }  // part
       if (last) break;
       dev::wave_sync();  // every lane is done with this step's text and list
