@@ -126,10 +126,35 @@ $(BUILD)/dmlc_objserver: tools/dmlc_objserver.cc
 	@mkdir -p $(BUILD)
 	$(CXX) -std=c++17 -O2 -Wall -pthread $< -o $@
 
+$(BUILD)/dmlc_bench_split_cpu: tools/dmlc_bench_split_cpu.cc $(LIB) $(HEADERS)
+	@mkdir -p $(BUILD)
+	$(CXX) $(CXXFLAGS_BASE) $< -o $@ -L$(LIBDIR) -ldmlc -Wl,-rpath,$(abspath $(LIBDIR)) \
+	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64
+
 tools: $(BUILD)/dmlc_parameter_example $(BUILD)/dmlc_gen $(BUILD)/dmlc_bench_cpu $(BUILD)/dmlc_recordio_dist $(BUILD)/dmlc_fs \
-  $(BUILD)/dmlc_recordio $(BUILD)/dmlc_gpu_api_check $(BUILD)/dmlc_objserver
+  $(BUILD)/dmlc_recordio $(BUILD)/dmlc_gpu_api_check $(BUILD)/dmlc_objserver $(BUILD)/dmlc_bench_split_cpu
+
+# same-host baseline ("re-measure on the MI355X host's CPU"): the
+# reference's own sources, read in place from REF (never copied into this
+# tree), built as the survey built them (-O3 -msse2 -fopenmp, no HDFS/S3), and
+# this repo's public-API harnesses linked against them.  Optional: skipped when
+# REF is absent.
+REF ?= /root/reference
+REF_SRCS := io/line_split io/indexed_recordio_split io/recordio_split io/input_split_base io \
+  io/filesys io/local_filesys data recordio config
+REF_OBJS := $(patsubst %,$(BUILD)/refbench/obj/%.o,$(REF_SRCS))
+REF_FLAGS := -O3 -std=c++11 -msse2 -fopenmp -Wno-unknown-pragmas -DDMLC_USE_HDFS=0 -DDMLC_USE_S3=0 \
+  -DDMLC_USE_AZURE=0 -I$(REF)/include
+$(BUILD)/refbench/obj/%.o: $(REF)/src/%.cc
+	@mkdir -p $(dir $@)
+	$(CXX) $(REF_FLAGS) -c $< -o $@
+$(BUILD)/refbench/ref_bench_cpu: tools/dmlc_bench_cpu.cc $(REF_OBJS)
+	$(CXX) $(REF_FLAGS) $^ -o $@ -pthread
+$(BUILD)/refbench/ref_bench_split_cpu: tools/dmlc_bench_split_cpu.cc $(REF_OBJS)
+	$(CXX) $(REF_FLAGS) $^ -o $@ -pthread
+refbench: $(BUILD)/refbench/ref_bench_cpu $(BUILD)/refbench/ref_bench_split_cpu
 
 clean:
 	rm -rf $(BUILD) $(LIB) $(PYMOD)
 
-.PHONY: all clean test-bin tools tsan asan
+.PHONY: all clean test-bin tools tsan asan refbench

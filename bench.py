@@ -41,6 +41,16 @@ NUM_PARTS = 16
 
 # per format: the reference number it is compared with (measured
 # CPU reference), the metric name and the default dataset size
+# same-host CPU baseline (profiles/r05_cpu): the reference's own parsers built
+# from source and run on the MI355X box's CPU (2 x EPYC 9575F; 16 CPUs = one
+# GPU's share), best-of runs; recorded, not re-measured per bench run
+SAME_HOST_CPU = {
+    "libsvm": {"ref_8t": 7.105e6, "ref_16t": 13.631e6},
+    "libfm": {"ref_8t": 5.394e6, "ref_16t": 9.932e6},
+    "csv": {"ref_8t": 13.057e6, "ref_16t": 24.528e6},
+    "recordio": {"ref_1t": 57.477e6},
+}
+
 FORMATS = {
     "libsvm": dict(baseline=2.201e6, rows=10_000_000,
                    metric="parsed rows/sec (LibSVM->CSR in device memory), aggregate over GPUs",
@@ -453,6 +463,9 @@ def main():
             "shape": args.shape,
             "shuffle_parts": args.shuffle_parts,
             "baseline_value": fmt["baseline"],
+            "same_host_cpu_baseline": dict(SAME_HOST_CPU[args.format],
+                                           host="AMD EPYC 9575F (MI355X box)",
+                                           source="profiles/r05_cpu"),
         }
         out["per_rank"] = per_rank
         out["allreduce_busbw_GBps"] = probe

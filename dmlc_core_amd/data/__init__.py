@@ -119,8 +119,12 @@ class GPUParser:
 
         ``out``: an earlier result of this call whose tensors are no longer
         used; its HBM buffers are refilled in place (no multi-GB allocation
-        per epoch).  The earlier ``x`` / ``label`` tensors then alias the new
-        batch."""
+        per epoch) and, when the shape is unchanged, ``out`` itself is
+        returned (its ``x`` / ``label`` alias the new batch).  When the refill
+        has to grow or reshape the batch, a new dict is returned; tensors of
+        the earlier result keep their own (old, still valid) buffers, which
+        are freed when the last of them goes -- each DLPack capsule owns the
+        buffer it exports."""
         import torch
         import torch.utils.dlpack as tdl
 

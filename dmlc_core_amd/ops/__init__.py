@@ -173,7 +173,11 @@ class SpMVFunction(torch.autograd.Function):
                 uses = 1
             ctx.holder["_backward_calls"] = uses
             ctx.holder["_calls_key"] = key
-            if ctx.grad == "transpose" or uses >= 2 or _whole(ctx.csr):
+            # auto: only feature spaces the counting-sort transpose takes
+            # (<= 2^22 columns); wider models keep the atomic scatter, which
+            # has no column limit.  "transpose" asked for it: transpose() raises
+            fits = ctx.num_features <= _dmlc.csr_transpose_max_features()
+            if ctx.grad == "transpose" or (fits and (uses >= 2 or _whole(ctx.csr))):
                 t = transpose(ctx.csr, ctx.num_features)
                 ctx.holder["transpose"] = t
                 ctx.holder["_transpose_key"] = key
@@ -192,7 +196,8 @@ def csr_spmv(csr: Dict, w: torch.Tensor, bias: torch.Tensor, grad: str = "auto")
     10 M x 1 M batch) or as an
     f32-atomic scatter: grad="auto" (the default) builds the transpose on the
     first backward of a whole CSR and once a row-slice dict is seen a second
-    time, "transpose" at once, "atomic" never."""
+    time (only up to ``_dmlc.csr_transpose_max_features()`` columns; wider
+    models stay on the atomic form), "transpose" at once, "atomic" never."""
     if grad not in ("auto", "transpose", "atomic"):
         raise ValueError(f"grad must be 'auto', 'transpose' or 'atomic', got {grad!r}")
     return SpMVFunction.apply(w, bias, (csr["offset"], csr["index"], csr.get("value")), csr, grad)

@@ -67,7 +67,6 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--env", default=[], action="append",
                    help="KEY=VALUE exported to every task (repeatable)")
     p.add_argument("--yarn-app-classpath", type=str, default=None)
-    p.add_argument("--yarn-app-dir", type=str, default=None)
     p.add_argument("--mesos-master", type=str, default=None)
     p.add_argument("--ship-libcxx", default=None, type=str)
     p.add_argument("--sync-dst-dir", type=str, default=None)

@@ -1,13 +1,11 @@
 """YARN backend, client side (reference `tracker/dmlc_tracker/yarn.py:16-129`
 and `tracker/yarn/src/main/java/org/apache/hadoop/yarn/dmlc/Client.java`).
 
-Two ways to reach a cluster:
-
-* ``--yarn-app-dir DIR`` holding a ``dmlc-yarn.jar``: the reference-style
-  ``hadoop jar ... org.apache.hadoop.yarn.dmlc.Client`` invocation with the
-  resource env (DMLC_WORKER_CORES/MEMORY_MB, ...) and shipped files/archives.
-* otherwise (no JVM needed on the submitting host): the ResourceManager's YARN
-  Services REST API (``$YARN_RM_ADDRESS``, Hadoop >= 3.1).  One component per
+The reference submits through its own Java ApplicationMaster
+(``hadoop jar dmlc-yarn.jar org.apache.hadoop.yarn.dmlc.Client``).  This
+backend needs no JVM and no jar: the ResourceManager's YARN Services REST API
+(``$YARN_RM_ADDRESS``, Hadoop >= 3.1) runs the containers and the AM's
+per-task policy runs here, in `YarnServiceJob.wait`.  One component per
   role, one container per task, ``yarn.amd.com/gpu``-style GPU resources when
   ``--gpus-per-node`` is set.  `YarnServiceJob.wait` applies the dmlc
   ApplicationMaster's policy to the containers the service reports
@@ -25,7 +23,6 @@ from __future__ import annotations
 
 import json
 import os
-import subprocess
 import time
 import urllib.error
 import urllib.request
@@ -33,34 +30,6 @@ from typing import Dict, List, Optional
 
 from .. import tracker
 from .opts import get_cache_file_set, user_envs
-
-
-def hadoop_version() -> List[int]:
-    out = subprocess.run(["hadoop", "version"], capture_output=True, text=True).stdout
-    first = out.splitlines()[0] if out else ""
-    return [int(x) for x in first.split()[-1].split(".")[:2]] if first else [0, 0]
-
-
-def build_command(args, envs: Dict[str, object], jar: str) -> List[str]:
-    fset, cmd = get_cache_file_set(args)
-    env = dict(envs)
-    env.update({"DMLC_JOB_CLUSTER": "yarn", "DMLC_WORKER_CORES": args.worker_cores,
-                "DMLC_WORKER_MEMORY_MB": args.worker_memory_mb,
-                "DMLC_SERVER_CORES": args.server_cores,
-                "DMLC_SERVER_MEMORY_MB": args.server_memory_mb,
-                "DMLC_NUM_WORKER": args.num_workers, "DMLC_NUM_SERVER": args.num_servers,
-                "DMLC_JOB_ARCHIVES": ":".join(args.archives)})
-    env.update(user_envs(args))
-    argv = ["hadoop", "jar", jar, "org.apache.hadoop.yarn.dmlc.Client"]
-    for f in sorted(fset):
-        argv += ["-file", f]
-    for a in args.archives:
-        argv += ["-archive", a]
-    argv += ["-jobname", args.jobname or "dmlc", "-tempdir", args.hdfs_tempdir,
-             "-queue", args.queue]
-    for k, v in sorted(env.items()):
-        argv += ["-env", f"{k}={v}"]
-    return argv + ["./launcher.sh", cmd]
 
 
 def _mb(s) -> int:
@@ -207,22 +176,34 @@ class YarnServiceJob:
         and blacklists its node (``self.blacklist``; the spec asks the service
         AM to exclude it, ``yarn.service.node-blacklist.threshold`` = 1); a
         task re-placed on a blacklisted node counts as one more failed attempt
-        (the placement broke the policy); max_attempt attempts abort."""
+        (the placement broke the policy); max_attempt attempts abort.
+
+        Misplacement is judged at placement time: a container's host is
+        checked against the blacklist as it stood before the poll in which
+        the container first appears, so a healthy container whose node is
+        blacklisted later (by another task's failure) is never penalised --
+        as in the reference AM, which only blacklists on failure
+        (ApplicationMaster.java:511-617)."""
         max_attempt = max_attempt or int(os.environ.get("DMLC_MAX_ATTEMPT", "3"))
         failures: Dict[str, int] = {}
         seen = set()  # failed / misplaced container ids already counted
+        placed_bad: Dict[str, bool] = {}  # container id -> host blacklisted when first seen
         self.blacklist = set()
         deadline = None if timeout is None else time.monotonic() + timeout
         while True:
             st = self.status()
             state = st.get("state", "")
+            before = set(self.blacklist)  # this poll's placements are judged against it
             for comp in st.get("components", []):
                 for c in comp.get("containers", []):
                     key = f"{comp['name']}/{c.get('component_instance_name', c.get('id'))}"
                     host = self._host(c)
+                    cid = c.get("id")
+                    if cid not in placed_bad:
+                        placed_bad[cid] = host in before
                     if (c.get("state") in ("RUNNING_BUT_UNREADY", "READY", "RUNNING")
-                            and host in self.blacklist and key in failures
-                            and c.get("id") not in seen):
+                            and placed_bad[cid] and key in failures
+                            and cid not in seen):
                         seen.add(c.get("id"))
                         failures[key] += 1
                         if failures[key] >= max_attempt:
@@ -255,31 +236,13 @@ class YarnServiceJob:
 
 
 def submit(args):
-    app_dir = args.yarn_app_dir or os.environ.get("DMLC_YARN_APP_DIR", "")
-    jar = os.path.join(app_dir, "dmlc-yarn.jar")
+    """--cluster yarn: the Services REST path (the only one; see the module
+    docstring for why there is no ``hadoop jar`` mode)."""
     rm = os.environ.get("YARN_RM_ADDRESS", "")
-    if rm and not os.path.exists(jar):
-        return submit_service(args, rm)
-
-    def launch(nworker, nserver, envs):
-        c = build_command(args, envs, jar)
-        if args.dry_run:
-            print(" ".join(c))
-            return
-        if not os.path.exists(jar):
-            raise SystemExit(f"{jar} not found: build the YARN ApplicationMaster jar and pass "
-                             "--yarn-app-dir")
-        if hadoop_version()[0] < 2:
-            raise SystemExit("YARN backend needs Hadoop >= 2")
-        subprocess.check_call(c)
-
-    if args.dry_run:
-        launch(args.num_workers, args.num_servers, {})
-        return 0
-    tracker.submit(args.num_workers, args.num_servers, launch, host_ip=args.host_ip or "auto",
-                   pscmd=" ".join(args.command), timeout=args.timeout,
-                   heartbeat_timeout=args.heartbeat_timeout)
-    return 0
+    if not rm:
+        raise SystemExit("--cluster yarn submits through the YARN Services REST API: set "
+                         "YARN_RM_ADDRESS (e.g. http://resourcemanager:8088; Hadoop >= 3.1)")
+    return submit_service(args, rm)
 
 
 def submit_service(args, rm: str):

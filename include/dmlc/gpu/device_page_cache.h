@@ -9,10 +9,12 @@
  *  count + raw elements each), then max_field and max_index (I).  Both the
  *  CPU DiskRowIter and this class flush a page as soon as its MemCostBytes()
  *  reaches 64 MiB, checked after every row, so for the same shard the two
- *  builders write the same bytes (with one exception: the GPU route decides
- *  the optional weight / qid / value columns per shard, the CPU per page --
- *  identical whenever a column is present in every page or in none).  Either
- *  builder's file loads in either reader.
+ *  builders write the same bytes when every optional column (weight / qid /
+ *  value) is carried by every row of the shard or by none.  Otherwise they
+ *  may differ: the GPU route decides the optional columns per shard and
+ *  prices a page with full-length columns, while the CPU RowBlockContainer
+ *  fills them lazily (its MemCostBytes is lower mid-page, so its pages can
+ *  hold more rows).  Either builder's file loads in either reader.
  *
  *  Loading is the MI355X fast path of a cached epoch: the file is mmap'ed and
  *  registered with hipHostRegister once (zero-copy, as the text route), every

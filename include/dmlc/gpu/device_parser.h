@@ -110,10 +110,14 @@ struct DeviceParserConfig {
 /*!
  * \brief a hashed dense batch in HBM (BASELINE config 5): row r of `x` is the
  *  signed feature hash of line r into `dim` buckets, OCP fp8 e4m3 (1 byte) or
- *  f32, `label` its label.  Grows by doubling, like DeviceCSR.
+ *  f32, `label` its label.  Grows by doubling, like DeviceCSR.  The buffers
+ *  are shared: a consumer that exported them (DLPack) keeps its own
+ *  reference, so a Reserve that moves the batch to bigger buffers never frees
+ *  memory a tensor still points at.
  */
 struct DeviceHashedBatch {
-  DeviceBuffer x, label;
+  std::shared_ptr<DeviceBuffer> x{std::make_shared<DeviceBuffer>()};
+  std::shared_ptr<DeviceBuffer> label{std::make_shared<DeviceBuffer>()};
   size_t rows{0}, row_cap{0};
   int dim{0};
   bool fp8{true};

@@ -291,6 +291,10 @@ void DevicePageCache<IndexType>::LoadStaged(DeviceCSR<IndexType>* out, hipStream
     r0 += pg.rows;
     z0 += pg.nnz;
   }
+  // the last pages' DMAs read from the staging buffers: done before they go
+  for (int k = 0; k < 2; ++k) {
+    if (used[k]) done[k].Synchronize();
+  }
 }
 
 template <typename IndexType>

@@ -1021,7 +1021,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
                                hticket0_, htag_, out->row_cap};
           hticket0_ += LaunchTileHashed<IndexType>(
               text, nbytes, tcfg_.format, nullptr, out->rows, 0, dim, scale, seed, fp8,
-              out->x.get(), out->label.get<float>(), slots_.get<MetaPartial>(), dmeta, hm, s, &op);
+              out->x->get(), out->label->get<float>(), slots_.get<MetaPartial>(), dmeta, hm, s, &op);
           const ChunkMeta m = WaitMapped(hm);
           AfterFirstSync();
           CHECK(!(m.flags & kFlagNegIndex)) << "negative feature index in " << cfg_.format
@@ -1049,8 +1049,8 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
         if (!(sizes.flags & kFlagIrregular)) {
           reserve(sizes.nrows, nbytes);
           LaunchTileHashed<IndexType>(text, nbytes, tcfg_.format, tcounts_.get<uint64_t>(),
-                                      out->rows, sizes.nlines, dim, scale, seed, fp8, out->x.get(),
-                                      out->label.get<float>(), slots_.get<MetaPartial>(), dmeta,
+                                      out->rows, sizes.nlines, dim, scale, seed, fp8, out->x->get(),
+                                      out->label->get<float>(), slots_.get<MetaPartial>(), dmeta,
                                       hm, s);
           PrelaunchCount();
           const ChunkMeta m = WaitMapped(hm);
@@ -1082,7 +1082,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       DMLC_HIP_CHECK(hipMemsetAsync(dmeta, 0, sizeof(ChunkMeta), s));
       LaunchTextHashed<IndexType>(text, nbytes, lines_.get<uint32_t>(), nlines, tcfg_.format,
                                   info_.get<uint64_t>(), out->rows, dim, scale, seed, fp8,
-                                  out->x.get(), out->label.get<float>(), slots_.get<MetaPartial>(),
+                                  out->x->get(), out->label->get<float>(), slots_.get<MetaPartial>(),
                                   dmeta, s);
       const ChunkMeta m = ReadBack<ChunkMeta>(dmeta);
       CHECK(!(m.flags & kFlagNegIndex)) << "negative feature index in " << cfg_.format << " input";

@@ -99,14 +99,16 @@ void DeviceHashedBatch::Reserve(size_t want, hipStream_t stream) {
   if (want <= row_cap) return;
   const size_t cap = std::max(want, row_cap * 2);
   const size_t esize = fp8 ? 1 : sizeof(float);
-  DeviceBuffer nx(cap * static_cast<size_t>(dim) * esize), nl(cap * sizeof(float));
+  auto nx = std::make_shared<DeviceBuffer>(cap * static_cast<size_t>(dim) * esize);
+  auto nl = std::make_shared<DeviceBuffer>(cap * sizeof(float));
   if (rows != 0) {
-    DMLC_HIP_CHECK(hipMemcpyAsync(nx.get(), x.get(), rows * static_cast<size_t>(dim) * esize,
+    DMLC_HIP_CHECK(hipMemcpyAsync(nx->get(), x->get(), rows * static_cast<size_t>(dim) * esize,
                                   hipMemcpyDeviceToDevice, stream));
-    DMLC_HIP_CHECK(hipMemcpyAsync(nl.get(), label.get(), rows * sizeof(float),
+    DMLC_HIP_CHECK(hipMemcpyAsync(nl->get(), label->get(), rows * sizeof(float),
                                   hipMemcpyDeviceToDevice, stream));
   }
-  // the old buffers are freed only after the copies (hipFree synchronises)
+  // the old buffers are freed once their last owner (this batch, or a DLPack
+  // tensor exported from it) lets go -- after the copies (hipFree synchronises)
   x = std::move(nx);
   label = std::move(nl);
   row_cap = cap;

@@ -406,17 +406,19 @@ class PyDeviceParser {
     }
     py::dict d;
     const int64_t n = static_cast<int64_t>(batch->rows) * dim;
+    // each capsule owns the buffer it exports (not the batch): a later refill
+    // that reallocates leaves these tensors their own, still valid, memory
     if (fp8) {
-      d["x"] = ToCapsule(batch->x.get<uint8_t>(), n, batch->device, batch);
+      d["x"] = ToCapsule(batch->x->get<uint8_t>(), n, batch->device, batch->x);
     } else {
-      d["x"] = ToCapsule(batch->x.get<float>(), n, batch->device, batch);
+      d["x"] = ToCapsule(batch->x->get<float>(), n, batch->device, batch->x);
     }
-    d["label"] = ToCapsule(batch->label.get<float>(), static_cast<int64_t>(batch->rows),
-                           batch->device, batch);
+    d["label"] = ToCapsule(batch->label->get<float>(), static_cast<int64_t>(batch->rows),
+                           batch->device, batch->label);
     d["rows"] = batch->rows;
     d["dim"] = dim;
-    d["x_ptr"] = reinterpret_cast<uintptr_t>(batch->x.get());
-    d["label_ptr"] = reinterpret_cast<uintptr_t>(batch->label.get());
+    d["x_ptr"] = reinterpret_cast<uintptr_t>(batch->x->get());
+    d["label_ptr"] = reinterpret_cast<uintptr_t>(batch->label->get());
     d["batch"] = py::cast(batch);
     return d;
   }

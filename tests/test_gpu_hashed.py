@@ -190,6 +190,11 @@ def test_fused_batch_reuse(dataset):
     g.before_first()
     c = g.parse_all_hashed(256, seed=4, out=b)
     assert tuple(c["x"].shape) == (want.shape[0], 256)
+    # the reshape reallocated: the earlier tensors keep their own buffers
+    # (each DLPack capsule owns what it exports), still readable, unchanged
+    torch.cuda.synchronize()
+    assert b["x"].data_ptr() == ptr
+    assert torch.equal(b["x"].view(torch.uint8), want)
 
 
 @pytest.mark.parametrize("fmt,junk", [("libsvm", "0 junk 3:1\n1 qid:4 5:1\n"),

@@ -224,3 +224,26 @@ def test_auto_grad_builds_the_transpose_on_a_whole_csr(csr_t):
         a.bias.copy_(m.bias)
     a.loss({k: v for k, v in t.items() if k in ("offset", "index", "value", "label")}).backward()
     torch.testing.assert_close(m.weight.grad, a.weight.grad, rtol=1e-4, atol=1e-6)
+
+
+def test_auto_grad_above_the_transpose_limit_stays_atomic(csr_t):
+    """grad='auto' on a model wider than the counting-sort transpose takes
+    (2^22 + 1 columns): backward keeps the atomic scatter instead of raising,
+    twice (the second-backward rule must not build it either), and the
+    gradient equals grad='atomic'"""
+    import torch
+    from dmlc_core_amd import _dmlc
+    from dmlc_core_amd.models import SparseLogReg
+    t, _ = csr_t
+    wide = _dmlc.csr_transpose_max_features() + 1
+    m = SparseLogReg(wide).cuda()
+    for _ in range(2):
+        m.zero_grad()
+        m.loss(t).backward()
+    assert "transpose" not in t
+    a = SparseLogReg(wide, grad="atomic").cuda()
+    with torch.no_grad():
+        a.weight.copy_(m.weight)
+        a.bias.copy_(m.bias)
+    a.loss({k: v for k, v in t.items() if k in ("offset", "index", "value", "label")}).backward()
+    torch.testing.assert_close(m.weight.grad, a.weight.grad, rtol=1e-4, atol=1e-6)

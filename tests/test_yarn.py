@@ -269,3 +269,34 @@ def test_service_job_blacklists_failed_nodes(rm):
     _RM.script = [st(fail_a), st(fail_a, on_a[0]), st(fail_a, on_a[1])]
     ok, diag = job.wait(poll=0.01, max_attempt=3)
     assert not ok and "blacklisted node nodeA" in diag
+
+
+def test_service_job_does_not_penalise_a_container_placed_before_its_node_was_blacklisted(rm):
+    """worker-0 fails on nodeX and restarts on nodeY; later worker-1 fails on
+    nodeY, which blacklists it.  worker-0's healthy retry on nodeY was placed
+    before that and must not count as a failed attempt (max_attempt 2 would
+    abort the job if it did)"""
+    job = yarn.YarnServiceJob(rm, "j4")
+    job.submit(yarn.service_spec(_args(), {}, "j4"))
+
+    def st(*cs):
+        return {"state": "STARTED", "components": [{"name": "worker", "containers": list(cs)}]}
+    w0_fail = {"id": "c1", "component_instance_name": "worker-0", "state": "FAILED",
+               "bare_host": "nodeX", "diagnostics": "exit 1"}
+    w0_retry = {"id": "c2", "component_instance_name": "worker-0", "state": "READY",
+                "bare_host": "nodeY"}
+    w1_fail = {"id": "c3", "component_instance_name": "worker-1", "state": "FAILED",
+               "bare_host": "nodeY", "diagnostics": "exit 1"}
+    w1_retry = {"id": "c4", "component_instance_name": "worker-1", "state": "READY",
+                "bare_host": "nodeZ"}
+    _RM.script = [st(w0_fail), st(w0_fail, w0_retry), st(w0_fail, w0_retry, w1_fail),
+                  st(w0_fail, w0_retry, w1_fail, w1_retry), {"state": "SUCCEEDED"}]
+    assert job.wait(poll=0.01, max_attempt=2) == (True, "SUCCEEDED")
+    assert job.blacklist == {"nodeX", "nodeY"}
+
+
+def test_submit_without_a_resourcemanager_explains_the_services_path(monkeypatch):
+    """there is no `hadoop jar` mode: --cluster yarn needs YARN_RM_ADDRESS"""
+    monkeypatch.delenv("YARN_RM_ADDRESS", raising=False)
+    with pytest.raises(SystemExit, match="YARN_RM_ADDRESS"):
+        yarn.submit(_args())
