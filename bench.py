@@ -97,6 +97,10 @@ def parse_args():
                     help="HBM replay: first merged chunk (0: no ramp; default: the parser's)")
     ap.add_argument("--replay-chunk-mb", type=float, default=None,
                     help="HBM replay: merged chunk cap (default: the parser's)")
+    ap.add_argument("--no-prelaunch", action="store_true",
+                    help="HBM replay: count + scan in line (no second stream), to price kernels alone")
+    ap.add_argument("--one-pass", action="store_true",
+                    help="HBM replay: one launch per chunk (look-back fill, no count kernel)")
     ap.add_argument("--shape", default="uniform", choices=["uniform", "skewed", "mixed"],
                     help="synthetic row shape (dmlc/synthetic.h): uniform 20-60 tokens of "
                          "0.dddddd; skewed power-law tokens per line (some lines > 8 KiB), "
@@ -319,6 +323,10 @@ def main():
             extra["replay_first_mb"] = args.replay_first_mb
         if args.replay_chunk_mb is not None:
             extra["replay_chunk_mb"] = args.replay_chunk_mb
+        if args.one_pass:
+            extra["one_pass"] = 1
+        if args.no_prelaunch:
+            extra["prelaunch"] = 0
         parser = data.GPUParser(ddir, rank, world, format=args.format, chunk_mb=args.chunk_mb,
                                 read_threads=read_threads, pinned_slots=args.pinned_slots,
                                 device_slots=args.device_slots, device=local_rank,
@@ -383,7 +391,10 @@ def main():
     # per-rank view (rows, bytes, own time, host waits) gathered to every rank
     st = parser.stats() if use_gpu and args.mode != "cache" else {}
     mine = torch.tensor([rank, local["rows"], local["bytes"], elapsed,
-                         st.get("wait_reader_sec", 0.0), st.get("wait_gpu_sec", 0.0)],
+                         st.get("wait_reader_sec", 0.0), st.get("wait_gpu_sec", 0.0),
+                         st.get("zc_pin_budget", 0), st.get("zc_pinned_peak", 0),
+                         st.get("last_fill_sec", 0.0), st.get("last_drain_sec", 0.0),
+                         st.get("last_pass_sec", 0.0)],
                         dtype=torch.float64, device=cdev)
     gathered = [torch.zeros_like(mine) for _ in range(world)]
     if dist is not None:
@@ -392,11 +403,17 @@ def main():
         gathered = [mine]
     per_rank = []
     for g in sorted((x.tolist() for x in gathered), key=lambda v: v[0]):
-        r, rows_r, bytes_r, el_r, wr, wg = g
+        r, rows_r, bytes_r, el_r, wr, wg, pin_b, pin_p, fill_s, drain_s, pass_s = g
         per_rank.append({"rank": int(r), "rows": int(rows_r), "bytes": int(bytes_r),
                          "rows_per_sec": round(rows_r * args.steps / el_r, 1),
                          "input_GBps": round(bytes_r * args.steps / el_r / 1e9, 3),
-                         "wait_reader_sec": round(wr, 4), "wait_gpu_sec": round(wg, 4)})
+                         "wait_reader_sec": round(wr, 4), "wait_gpu_sec": round(wg, 4),
+                         # zero-copy: this rank's share of the host pin budget and
+                         # its peak registered bytes; the last step's pipeline
+                         # fill / drain / pass seconds (host clock)
+                         "zc_pin_budget": int(pin_b), "zc_pinned_peak": int(pin_p),
+                         "last_fill_sec": round(fill_s, 5), "last_drain_sec": round(drain_s, 5),
+                         "last_pass_sec": round(pass_s, 5)})
     elapsed = max(float(x[3]) for x in gathered)  # the slowest rank sets the step time
     # structured per-stage metrics ($DMLC_METRICS_FILE, JSONL, one file per rank
     # with "{rank}" in the path) and their cross-rank reduction

@@ -35,6 +35,8 @@ def task_envs(args, envs: Dict[str, object], role: str, task_id: int, nworker: i
     env = {k: str(v) for k, v in envs.items()}
     env.update({"DMLC_TASK_ID": str(task_id), "DMLC_ROLE": role, "DMLC_JOB_CLUSTER": "local"})
     if role == "worker":
+        # ranks sharing this host (per-host budgets, e.g. the zero-copy pin budget)
+        env["DMLC_LOCAL_WORLD_SIZE"] = str(nworker)
         if args.gpus_per_node:
             local = task_id % args.gpus_per_node
             env["DMLC_LOCAL_RANK"] = str(local)

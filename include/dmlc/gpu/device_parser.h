@@ -52,6 +52,19 @@ struct DeviceParserConfig {
   /*! \brief LibSVM/LibFM: token-parallel kernels with exact per-line fallback */
   bool fast_path{true};
   /*!
+   * \brief ParseAll over HBM-resident text: one launch per chunk (the fill
+   *  counts its own tile and takes its prefix by decoupled look-back) instead
+   *  of count + scan + fill with the next chunk's count prelaunched beside the
+   *  current fill (`?one_pass=1`).  Off by default: measured slower, the fill
+   *  waves serialise count -> look-back -> decode where the separate count
+   *  kernel is hidden behind the previous fill (profiles/r05_one_pass).
+   */
+  bool one_pass{false};
+  /*! \brief counted HBM replay: queue the next chunk's count + scan on a
+   *  second stream beside the current fill (`?prelaunch=0`: in line, for
+   *  pricing each kernel alone) */
+  bool prelaunch{true};
+  /*!
    * \brief zero-copy ingest: mmap the partition and hipHostRegister it so the
    *  DMA engines read the page cache directly (-1 auto with fallback to the
    *  pinned pread ring, 0 off, 1 required)
@@ -101,7 +114,7 @@ struct DeviceParserConfig {
   int shuffle_seed{0};
   /*! \brief apply `?k=v` overrides (chunk_mb, pinned_slots, device_slots,
    *  read_threads, device, format, label_column, weight_column, delimiter,
-   *  fast_path, zero_copy, zc_pin_budget_mb, zc_window_mb, hbm_cache, replay_chunk_mb,
+   *  fast_path, one_pass, prelaunch, zero_copy, zc_pin_budget_mb, zc_window_mb, hbm_cache, replay_chunk_mb,
    *  replay_first_mb,
    *  shuffle_parts, shuffle_seed) */
   void Update(const std::map<std::string, std::string>& args);
@@ -134,8 +147,11 @@ struct DeviceParserStats {
   size_t nnz{0};
   /*! \brief chunks the fast path handed to the exact per-line kernels */
   size_t exact_chunks{0};
-  /*! \brief hashed-batch chunks built in one pass (look-back, no count kernel) */
+  /*! \brief chunks built in one pass (look-back, no count kernel): hashed
+   *  batches, and resident CSR chunks */
   size_t one_pass_chunks{0};
+  /*! \brief one-pass CSR chunks written again (target grown / weight column added) */
+  size_t one_pass_reruns{0};
   /*! \brief seconds the host waited for the reader (pinned ring empty) */
   double wait_reader_sec{0};
   /*! \brief seconds the host waited for GPU results */
@@ -143,6 +159,14 @@ struct DeviceParserStats {
   /*! \brief zero-copy mode active, and the one-time mmap + register cost */
   bool zero_copy{false};
   double register_sec{0};
+  /*! \brief zero-copy: this process's pin budget (the configured one shared
+   *  among the host's ranks, bounded by MemAvailable) and the most bytes it
+   *  has had registered at once */
+  size_t zc_pin_budget{0}, zc_pinned_peak{0};
+  /*! \brief the last ParseAll: its wall time, pipeline fill (start until the
+   *  first chunk is parsed) and drain (the reader's last chunk handed in
+   *  until the pass is done), host clock */
+  double last_pass_sec{0}, last_fill_sec{0}, last_drain_sec{0};
   /*! \brief metadata waits that ended spinning / sleeping / at the bound */
   size_t waits_spun{0}, waits_slept{0}, waits_timed_out{0};
 };

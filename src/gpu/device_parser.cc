@@ -74,6 +74,10 @@ void DeviceParserConfig::Update(const std::map<std::string, std::string>& args) 
       delimiter = v[0];
     } else if (k == "fast_path") {
       fast_path = v != "0" && v != "false";
+    } else if (k == "one_pass") {
+      one_pass = v != "0" && v != "false";
+    } else if (k == "prelaunch") {
+      prelaunch = v != "0" && v != "false";
     } else if (k == "replay_chunk_mb") {
       replay_chunk_bytes = static_cast<size_t>(std::atof(v.c_str()) * (1 << 20));
     } else if (k == "replay_first_mb") {
@@ -214,7 +218,8 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       zc_.reset(new ZeroCopySource());
       const double t0 = GetTime();
       zc_->SetDrain([this]() { copy_->Synchronize(); });
-      if (!zc_->Init(split_.get(), cfg_.chunk_bytes, cfg_.zc_pin_budget, cfg_.zc_window_bytes,
+      stats_.zc_pin_budget = ZeroCopySource::ShardPinBudget(cfg_.zc_pin_budget);
+      if (!zc_->Init(split_.get(), cfg_.chunk_bytes, stats_.zc_pin_budget, cfg_.zc_window_bytes,
                      cfg_.shuffle_parts > 1 ? &all_segs_ : nullptr)) {
         CHECK(cfg_.zero_copy != 1) << "zero_copy=1 but the input cannot be mmap'ed + registered";
         zc_.reset();
@@ -398,15 +403,37 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     out->device_ = device_;
     ResetEpoch();
     merge_replay_ = true;
+    if (cfg_.one_pass && replay_ && cfg_.fast_path && tcfg_.format != TextFormat::kCSV &&
+        !one_pass_off_) {
+      // one pass per resident chunk (no count to hide behind a previous fill,
+      // so no small first chunk): merge up to 2 x replay_chunk_bytes, below
+      // 2 GiB (the exact fallback's 32-bit offsets and the look-back's 31-bit
+      // counts)
+      merge_limit_ = std::min(2 * cfg_.replay_chunk_bytes, (size_t(1) << 31) - (size_t(64) << 20));
+      if (merge_cap_ == 0) merge_cap_ = merge_limit_;
+    }
+    // pipeline fill (start -> first chunk parsed) and drain (last chunk
+    // handed to the pipeline -> pass done), host clock
+    const double t0 = GetTime();
+    double t_first = 0, t_last_in = 0;
     try {
       while (ProcessOne(out, /*append=*/true)) {
+        const double t = GetTime();
+        if (t_first == 0) t_first = t;
+        if (reader_done_ && t_last_in == 0) t_last_in = t;
       }
     } catch (...) {
       merge_replay_ = false;
+      merge_limit_ = 0;
       throw;
     }
     merge_replay_ = false;
+    merge_limit_ = 0;
     FinishEpoch(out);
+    const double t_end = GetTime();
+    stats_.last_pass_sec = t_end - t0;
+    stats_.last_fill_sec = t_first != 0 ? t_first - t0 : 0;
+    stats_.last_drain_sec = t_last_in != 0 ? t_end - t_last_in : 0;
   }
 
   size_t PartitionBytes() const override {
@@ -851,7 +878,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
    *  adopts the set when its chunk is the one prelaunched.
    */
   void PrelaunchCount() {
-    if (!(replay_ && merge_replay_) || pre_.valid || inflight_.empty()) {
+    if (!(replay_ && merge_replay_) || pre_.valid || inflight_.empty() || !cfg_.prelaunch) {
       return;
     }
     const Inflight& nx = inflight_.front();
@@ -928,7 +955,93 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     cursor_ = cur.end_pos;  // only once the chunk is delivered
     stats_.bytes += cur.size;
     stats_.chunks += 1;
+    if (zc_ != nullptr) stats_.zc_pinned_peak = zc_->PeakPinnedBytes();
     return true;
+  }
+
+  /*! \brief outcome of a one-pass chunk: written, needs the counted tile
+   *  path (qid tokens), or needs the exact kernels (irregular text) */
+  enum class OnePass { kDone, kCounted, kExact };
+
+  /*!
+   * \brief one-pass tile parse of a resident chunk (k_tile_fill<kOnePass>):
+   *  look-back instead of C1 + C2, written straight into the target's
+   *  capacity -- a single launch and one host wait per chunk.  Grows the
+   *  target and runs again when the chunk did not fit (or met the first
+   *  weighted row); chunks with letter-started tokens go to the counted path
+   *  (`qid:` data: every later resident chunk too, see ProcessOne).
+   */
+  OnePass OnePassParse(const char* text, size_t nbytes, DeviceCSR<IndexType>* out, size_t row_base,
+                       size_t nnz_base, ChunkPlan* plan) {
+    hipStream_t s = compute_->get();
+    DropPrelaunch();
+    ChunkMeta* dmeta = meta_.get<ChunkMeta>();
+    ChunkMeta* hm = hmap_.get<ChunkMeta>();
+    const bool libfm = tcfg_.format == TextFormat::kLibFM;
+    const size_t tiles = TileCount(nbytes);
+    fstatus_.Reserve(tiles * sizeof(uint64_t));  // zeroed by the launcher, per launch
+    if (hticket_.bytes() == 0) {
+      hticket_.Reserve(sizeof(unsigned long long));
+      DMLC_HIP_CHECK(hipMemsetAsync(hticket_.get(), 0, hticket_.bytes(), s));
+      hticket0_ = 0;
+    }
+    bool first_wait = true;
+    for (;;) {
+      FillTarget<IndexType> tgt;
+      tgt.offset = out->offset();
+      tgt.label = out->label();
+      tgt.weight = out->weight_capacity() >= out->row_capacity() && out->row_capacity() != 0
+                       ? out->weight()
+                       : nullptr;
+      tgt.qid = nullptr;  // qid chunks take the counted path
+      tgt.field = libfm ? out->field() : nullptr;
+      tgt.index = out->index();
+      tgt.value = out->value();
+      tgt.row_base = row_base;
+      tgt.nnz_base = nnz_base;
+      // every row / entry the capacity holds (the row pointer has one slot more)
+      tgt.row_limit = out->row_capacity();
+      tgt.nnz_limit = out->nnz_capacity();
+      if (libfm && tgt.field == nullptr) tgt.nnz_limit = 0;
+      const FillOnePass op{fstatus_.get<uint64_t>(), hticket_.get<unsigned long long>(), hticket0_};
+      hticket0_ += LaunchTileFill<IndexType>(text, nbytes, tcfg_.format, nullptr, tgt,
+                                             slots_.get<MetaPartial>(), dmeta, hm, s, &op);
+      ChunkMeta m = WaitMapped(hm);
+      if (first_wait) {
+        AfterFirstSync();
+        first_wait = false;
+      }
+      // letter-started tokens: `qid:` (the counted path writes the zeroed
+      // qid column; ProcessOne makes that sticky once it finds real ones)
+      // or junk (the counted path sends the chunk on to the exact kernels)
+      if (m.flags & kFlagQid) return OnePass::kCounted;
+      if (m.flags & kFlagIrregular) return OnePass::kExact;
+      if (m.flags & kFlagOverflow) {
+        // grow to the chunk's sizes -- for the whole partition at its density
+        // when this is the pass's first chunk (a new target) -- and run again
+        size_t want_rows = row_base + m.nrows, want_nnz = nnz_base + m.nnz;
+        if (row_base == 0) {
+          const double f = static_cast<double>(PartitionBytes()) / static_cast<double>(nbytes) * 1.05;
+          want_rows = std::max(want_rows, static_cast<size_t>(static_cast<double>(m.nrows) * f) + 1);
+          want_nnz = std::max(want_nnz, static_cast<size_t>(static_cast<double>(m.nnz) * f) + 1);
+        }
+        out->Reserve(want_rows, want_nnz, libfm, s, row_base, nnz_base);
+        stats_.one_pass_reruns += 1;
+        continue;
+      }
+      if ((m.flags & kFlagNeedWeight) && tgt.weight == nullptr) {
+        out->EnableWeight(s);  // earlier rows get 1.0; write this chunk again with it
+        stats_.one_pass_reruns += 1;
+        continue;
+      }
+      m.flags &= ~kFlagNeedWeight;
+      plan->nlines = m.nlines;
+      plan->nrows = m.nrows;
+      plan->nnz = m.nnz;
+      Accumulate(m);
+      stats_.one_pass_chunks += 1;
+      return OnePass::kDone;
+    }
   }
 
   bool ProcessOne(DeviceCSR<IndexType>* out, bool append) {
@@ -939,8 +1052,19 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     const bool more = WithNextChunk([&](const char* text, size_t nbytes) {
       bool done = false;
       if (cfg_.fast_path) {
-        done = csv ? CsvFastParse(text, nbytes, out, row_base, nnz_base, &plan)
-                   : FastParse(text, nbytes, out, row_base, nnz_base, &plan);
+        // resident text (HBM replay) of a regular format: one pass, no count
+        // kernel and no host turnaround between count and fill
+        const OnePass r = cfg_.one_pass && !csv && replay_ && append && !one_pass_off_ && nbytes != 0
+                              ? OnePassParse(text, nbytes, out, row_base, nnz_base, &plan)
+                              : OnePass::kCounted;
+        if (r == OnePass::kDone) {
+          done = true;
+        } else if (r == OnePass::kCounted) {
+          done = csv ? CsvFastParse(text, nbytes, out, row_base, nnz_base, &plan)
+                     : FastParse(text, nbytes, out, row_base, nnz_base, &plan);
+          // qid data: every later resident chunk goes straight to this path
+          if (done && replay_ && (plan.flags & kFlagQid)) one_pass_off_ = true;
+        }
         if (!done) stats_.exact_chunks += 1;
       }
       if (!done) ExactParse(text, nbytes, out, row_base, nnz_base, &plan, cfg_.fast_path);
@@ -1144,6 +1268,10 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   size_t merge_limit_{0};  // merged replay chunk limit (0: replay_chunk_bytes)
   // one-pass hashed batches: look-back words, workgroup tickets, launch tag
   DeviceBuffer hstatus_, hticket_;
+  // one-pass CSR fill: look-back words (zeroed per launch; tickets shared)
+  DeviceBuffer fstatus_;
+  /*! \brief qid data met: resident chunks take the counted tile path */
+  bool one_pass_off_{false};
   unsigned long long hticket0_{0};
   uint32_t htag_{0};
   std::vector<CachedChunk> cached_;

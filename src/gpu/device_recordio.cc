@@ -138,7 +138,8 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
     if (cfg_.zero_copy != 0) {
       zc_.reset(new ZeroCopySource(ZeroCopySource::Cut::kRecordIO));
       zc_->SetDrain([this]() { copy_.Synchronize(); });
-      if (!zc_->Init(split_.get(), cfg_.chunk_bytes)) {
+      if (!zc_->Init(split_.get(), cfg_.chunk_bytes,
+                     ZeroCopySource::ShardPinBudget(size_t(64) << 30))) {
         CHECK_NE(cfg_.zero_copy, 1) << "zero_copy=1 but mmap/hipHostRegister failed";
         zc_.reset();
       }

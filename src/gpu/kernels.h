@@ -174,12 +174,29 @@ void LaunchTileCountScan(const char* text, size_t nbytes, uint64_t* tile_counts,
  *  scanned tile prefixes; merges max index / field and flags into meta and
  *  writes offset[row_base + nrows].  partials needs TileCount(nbytes) slots.
  *  Sets kFlagNeedWeight if a row is weighted and out.weight is null.
+ *
+ *  One pass (one_pass != nullptr; tile_prefix unused, nbytes > 0): no C1 / C2
+ *  -- each wave counts its tile's lines and entries itself (with C1's
+ *  irregular checks) and takes the counts before it by decoupled look-back
+ *  over one_pass->status (zeroed here, in the stream, before the launch).
+ *  The chunk's nlines / nrows / nnz land in meta (and host_meta) with the
+ *  flags.  out.row_limit / nnz_limit are the target's capacities: rows or
+ *  entries past them are not written and set kFlagOverflow (grow the target
+ *  to meta's sizes and run the chunk again; no closing row pointer is
+ *  written).  kFlagQid: the chunk has `qid:` tokens, which only the counted
+ *  path (LaunchTileCountScan first, qid column zeroed) writes -- run it so.
+ *  Returns the workgroups launched: advance ticket0 by it.
  */
+struct FillOnePass {
+  uint64_t* status;            // >= TileCount(nbytes) words
+  unsigned long long* ticket;  // counter, zeroed once
+  unsigned long long ticket0;  // the counter's value before this launch
+};
 template <typename IndexType>
-void LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
-                    const uint64_t* tile_prefix, const FillTarget<IndexType>& out,
-                    MetaPartial* partials, ChunkMeta* meta, ChunkMeta* host_meta,
-                    hipStream_t stream);
+size_t LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
+                      const uint64_t* tile_prefix, const FillTarget<IndexType>& out,
+                      MetaPartial* partials, ChunkMeta* meta, ChunkMeta* host_meta,
+                      hipStream_t stream, const FillOnePass* one_pass = nullptr);
 
 /*!
  * \brief fused tokenize -> hash -> dense rows on the tile parser (config 5):

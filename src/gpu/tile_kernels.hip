@@ -36,8 +36,10 @@
  *     write the chunk's closing row pointer.
  *  Traffic per chunk: text read twice (C1, C3) + the CSR written once.
  */
+#include <dmlc/gpu/hip_utils.h>
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <type_traits>
 
 #include "../data/strtonum.h"
@@ -272,6 +274,53 @@ __device__ __forceinline__ uint64_t lookback_lines(uint64_t* st, size_t tile, ui
   }
   if (lane == 0) {
     __hip_atomic_store(&st[tile], tg | (2ull << 32) | (excl + own), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return excl;
+}
+
+/*!
+ * \brief decoupled look-back over per-tile (lines, entries) pairs -- the one
+ *  pass CSR fill's replacement of C1 + C2.  Word: state (1: this tile's own
+ *  counts, 2: inclusive prefix; 0: not yet -- the array is zeroed by a
+ *  hipMemsetAsync before every launch) << 62 | lines << 31 | entries.  A chunk
+ *  is < 2 GiB, so lines and entries (<= bytes / 2 each) fit 31 bits and the
+ *  packed sums never carry.  The word is the data and the flag at once (one
+ *  8-byte agent-scope store, relaxed agent-scope polls: the granule form of
+ *  cdna_hip_programming.md Guideline 16, R2).  Returns the exclusive prefix.
+ */
+__device__ __forceinline__ uint64_t lookback_fill(uint64_t* st, size_t tile, uint64_t own,
+                                                  int lane) {
+  constexpr uint64_t kVal = (1ull << 62) - 1ull;
+  if (lane == 0) {
+    __hip_atomic_store(&st[tile], ((tile == 0 ? 2ull : 1ull) << 62) | own, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tile == 0) return 0;
+  uint32_t ex_lines = 0, ex_ent = 0;
+  int64_t j = static_cast<int64_t>(tile) - 1;  // the nearest predecessor not summed yet
+  for (;;) {
+    const int64_t k = j - lane;
+    const uint64_t v = k >= 0 ? __hip_atomic_load(&st[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : (2ull << 62);  // before the chunk: inclusive 0
+    const uint32_t state = static_cast<uint32_t>(v >> 62);
+    const uint64_t inc = __ballot(state == 2u);
+    const uint64_t waiting = __ballot(state == 0u);
+    const int first = inc != 0 ? __builtin_ctzll(inc) : dev::kWave - 1;
+    const uint64_t need = first >= dev::kWave - 1 ? ~0ull : ((2ull << first) - 1ull);
+    if ((waiting & need) != 0) {
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    const uint64_t x = lane <= first ? (v & kVal) : 0ull;
+    ex_lines += dev::wave_sum(static_cast<uint32_t>(x >> 31));
+    ex_ent += dev::wave_sum(static_cast<uint32_t>(x & 0x7FFFFFFFull));
+    if (inc != 0) break;
+    j -= dev::kWave;
+  }
+  const uint64_t excl = (static_cast<uint64_t>(ex_lines) << 31) | ex_ent;
+  if (lane == 0) {
+    __hip_atomic_store(&st[tile], (2ull << 62) | (excl + own), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   }
   return excl;
@@ -894,6 +943,8 @@ constexpr int kSteps = static_cast<int>(kTileBytes / kStepBytes);
 constexpr uint32_t kSlotBytes = kStepBytes + 64;           // a step + 64 B of the next
 constexpr uint32_t kStageVecs = 2 * kSlotBytes / 16;       // two slots: step s and s - 1
 constexpr uint32_t kListCap = kDecodeCarry + kStepBytes / 2;  // carried + a step's tokens
+// deferred-token ring: < 64 left after a queue round + 128 from a pair round
+constexpr uint32_t kQueueCap = 256;
 // k_tile_hash: no carried entries; a step of more tokens is listed in two
 // halves.  Sized so that 5 workgroups fit a CU with a 1024-wide f32 row per
 // wave: 4 x (2112 B text + (428 + 64) x 4 B list) + 16 KiB rows + the ticket
@@ -1009,26 +1060,42 @@ __device__ __forceinline__ uint32_t round_slot(int lane) {
   return (static_cast<uint32_t>(lane) & 32u) + k;
 }
 
-template <TextFormat F, typename IndexType>
+/*! \brief the one-pass fill's look-back state (kOnePass) */
+struct FillPass {
+  uint64_t* status;             // per-tile look-back words, zeroed before the launch
+  unsigned long long* ticket;   // workgroup ticket counter
+  unsigned long long ticket0;   // its value at this launch
+  ChunkMeta* meta;              // nlines / nrows / nnz of the chunk (the last tile writes them)
+  uint32_t exp;                 // pricing experiments (DMLC_FILL_EXP; 0 in production):
+                                // 1 no CSR stores, 2 no token decode (outputs are wrong)
+};
+
+template <TextFormat F, typename IndexType, bool kOnePass>
 __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
-    const uint8_t* __restrict__ text, size_t n,
-                                                        size_t ntiles,
-                                                        const uint64_t* __restrict__ prefix,
-                                                        FillTarget<IndexType> out,
-                                                        MetaPartial* __restrict__ partials) {
+    const uint8_t* __restrict__ text, size_t n, size_t ntiles, const uint64_t* __restrict__ prefix,
+    FillTarget<IndexType> out, MetaPartial* __restrict__ partials, FillPass op) {
   __shared__ uint4 s_text[kFillWaves][kStageVecs];
   __shared__ uint32_t s_list[kFillWaves][kListCap + 64];  // + a dummy slot per lane
-  __shared__ uint32_t s_dq[kFillWaves][2][2 * dev::kWave];   // deferred tokens: entry, ordinal
+  __shared__ uint32_t s_dq[kFillWaves][kQueueCap];  // deferred tokens: list index ring
   // wave-uniform in a scalar register: the tile's buffer resource stays scalar
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / dev::kWave);
   const int lane = dev::lane_id();
-  const size_t tile = static_cast<size_t>(blockIdx.x) * kFillWaves + wave;
+  size_t group = blockIdx.x;
+  if constexpr (kOnePass) {
+    // tiles in ticket order: a workgroup looks back only at tiles of
+    // workgroups that started before it (whatever the dispatch order), so
+    // every tile it waits on is resident or done
+    __shared__ uint32_t s_ticket;
+    if (threadIdx.x == 0) s_ticket = static_cast<uint32_t>(atomicAdd(op.ticket, 1ull) - op.ticket0);
+    __syncthreads();
+    group = s_ticket;
+  }
+  const size_t tile = group * kFillWaves + wave;
   if (tile >= ntiles) return;  // whole waves leave; nothing below synchronises waves
   uint4* const st = s_text[wave];
   uint32_t* const sl = s_list[wave];
-  uint32_t* const dq_e = s_dq[wave][0];
-  uint32_t* const dq_i = s_dq[wave][1];
-  uint32_t qn = 0;  // queued tokens
+  uint32_t* const dq = s_dq[wave];
+  uint32_t qh = 0, qn = 0;  // queue head, queued tokens
   const uint32_t slot = round_slot(lane);
   const size_t tile0 = tile * kTileBytes;
 
@@ -1043,11 +1110,61 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
   uint4 a = bload16(trs, loff);
   uint4 b = bload16(trs, loff + 1024);
   uint4 t = make_uint4(0, 0, 0, 0);
-  if (lane < 4) t = bload16(trs, loff + kStepBytes);
+  if (!kOnePass && lane < 4) t = bload16(trs, loff + kStepBytes);
   uint32_t carry_pc = tile0 == 0 ? static_cast<uint32_t>('\n') : text[tile0 - 1];
-  const uint64_t pre = prefix[tile];
-  const uint64_t line_base = pre >> 32;
-  const uint64_t tok_base = pre & 0xffffffffull;
+  uint64_t line_base, tok_base;
+  unsigned count_flags = 0;  // one pass: what C1 would have flagged for this tile
+  if constexpr (kOnePass) {
+    // C1 in the fill: the tile's 8 KiB in flight at once (the steps below
+    // re-read 2 KiB at a time, from L2), line / entry starts and the
+    // irregular checks counted, then the look-back for the tiles before it
+    uint4 v[kCountLoads];
+    v[0] = a;
+    v[1] = b;
+#pragma unroll
+    for (int j = 2; j < kCountLoads; ++j) v[j] = bload16(trs, loff + j * 1024);
+    if (lane < 4) t = v[2];  // step 0's tail (the 64 B after it) is already here
+    uint32_t lines = 0, toks = 0, qtoks = 0;
+    bool bad = false;
+    auto count_tile = [&](auto full) {
+#pragma unroll
+      for (int j = 0; j < kCountLoads; ++j) {
+        const uint32_t left = dev::lane_shr1(v[j].w >> 24);
+        const uint32_t wrap = j == 0 ? carry_pc : dev::lane63(v[j - 1].w >> 24);
+        const uint32_t pc = lane == 0 ? wrap : left;
+        bad |= count16<decltype(full)::value>(v[j], pc, tile0 + j * 1024 + lane * 16, n, &lines,
+                                              &toks, &qtoks);
+      }
+    };
+    if (tile0 + kTileBytes <= n) {  // wave-uniform: every tile but a chunk's last
+      count_tile(std::true_type{});
+    } else {
+      count_tile(std::false_type{});
+    }
+    lines = dev::wave_sum(lines);
+    const uint32_t ent = dev::wave_sum(toks - qtoks);  // letter tokens are no entries
+    qtoks = dev::wave_sum(qtoks);
+    count_flags = (__any(bad) ? kFlagIrregular : 0u) | (qtoks != 0 ? kFlagQid : 0u);
+    const uint64_t own = (static_cast<uint64_t>(lines) << 31) | ent;
+    const uint64_t excl = lookback_fill(op.status, tile, own, lane);
+    line_base = excl >> 31;
+    tok_base = excl & 0x7FFFFFFFull;
+    if (tile + 1 == ntiles && lane == 0) {
+      // the chunk's sizes (k_tile_finish, stream-ordered, adds the flags and
+      // maxima, writes the closing row pointer and publishes the meta)
+      ChunkMeta m;
+      m.nlines = m.nrows = line_base + lines;
+      m.nnz = tok_base + ent - (line_base + lines);
+      m.max_index = m.max_field = 0;
+      m.flags = 0;
+      m.pad = 0;
+      *op.meta = m;
+    }
+  } else {
+    const uint64_t pre = prefix[tile];
+    line_base = pre >> 32;
+    tok_base = pre & 0xffffffffull;
+  }
   // token k = tok_base + i of line l = line_base + lcnt - 1 goes to nnz
   // position C + (i - lcnt); its row is R + lcnt - 1 (as k_tile_scan defines)
   const uint64_t C = out.nnz_base + tok_base - line_base;
@@ -1079,6 +1196,8 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
   using MaxT = typename std::conditional<sizeof(IndexType) == 4, uint32_t, uint64_t>::type;
   MaxT mx_index = 0, mx_field = 0;
   bool any_value = false, any_weight = false, irregular = false, neg = false, need_w = false;
+  bool over = false;
+  uint32_t sink = 0;  // pricing experiments only
 
 #pragma unroll 1
   for (int s = 0; s < kSteps; ++s) {
@@ -1197,7 +1316,21 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
       const bool nnz_ok = rel < nnz_room;
       bool field_ok = true;
       if (F == TextFormat::kLibFM) field_ok = is_label || t.r >= 2;
-      irregular |= active & (is_label ? !row_ok : (!nnz_ok | !field_ok));
+      // past the target's rows / entries: with sizes from C1 + C2 that is a
+      // C1 / C3 disagreement (irregular); one pass writes into the capacity
+      // the host has and asks for more (kFlagOverflow: grow, run again)
+      const bool room_ok = is_label ? row_ok : nnz_ok;
+      irregular |= active & !is_label & !field_ok;
+      if constexpr (kOnePass) {
+        over |= active & !room_ok;
+      } else {
+        irregular |= active & !room_ok;
+      }
+      if (op.exp & 1u) {
+        // pricing: everything but the stores (the values stay live)
+        sink ^= (active ? __float_as_uint(t.f0) ^ t.u0 ^ t.u1 : 0u) + static_cast<uint32_t>(i);
+        return;
+      }
       if (active & is_label & row_ok) {
         lab_at[lc] = t.f0;
         off_at[lc] = C + 1 + (static_cast<int64_t>(i) - static_cast<int64_t>(lc));
@@ -1232,14 +1365,47 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
       neg |= active && bad;
     };
     // tokens the register-window decoder declines (exponents, long fractions,
-    // anything for the generic parser) are queued and decoded 64 at a time in
-    // rounds of their own, so a round with one such token does not pay the
-    // long decoder for all 64 lanes; the queue is drained before the slots it
-    // points into are restaged (by the end of every step).  One loop, one
-    // emit site: list rounds and queue rounds share the code after decode.
+    // anything for the generic parser) are queued (their list index, in a
+    // ring) and decoded 64 at a time in rounds of their own, so a round with
+    // one such token does not pay the long decoder for all 64 lanes; the
+    // queue is drained before the slots it points into are restaged (by the
+    // end of every step).  While 128 listed tokens remain a round decodes two
+    // per lane (tok::decode2: two independent dependency chains per lane).
+    auto enqueue = [&](bool defer, uint32_t li) {
+      const uint64_t dm = __ballot(defer);
+      if (dm != 0) {
+        const uint32_t rank = static_cast<uint32_t>(__popcll(dm & ((1ull << lane) - 1ull)));
+        if (defer) dq[(qh + qn + rank) & (kQueueCap - 1)] = li;
+        qn += static_cast<uint32_t>(__popcll(dm));
+      }
+    };
     for (uint32_t r0 = 0;;) {
       const bool qround = qn >= static_cast<uint32_t>(dev::kWave) || (r0 >= ndec && qn != 0);
       if (!qround && r0 >= ndec) break;
+      if (!qround && r0 + 2 * dev::kWave <= ndec) {  // wave-uniform: a pair round
+        const uint32_t la = r0 + slot, lb = la + dev::kWave;
+        const uint32_t ea = sl[la], eb = sl[lb];
+        tok::Token ta, tb;
+        ta.u0_hi = ta.u1_hi = tb.u0_hi = tb.u1_hi = 0;
+        ta.u1 = tb.u1 = 0;
+        bool oka, okb;
+        if (op.exp & 2u) {  // pricing: no decode
+          ta.u0 = ea;
+          tb.u0 = eb;
+          ta.f0 = ta.f1 = tb.f0 = tb.f1 = 1.0f;
+          ta.r = tb.r = 2;
+          oka = okb = true;
+        } else {
+          tok::decode2<F>(st, ea & 0x1FFFu, eb & 0x1FFFu, ((ea >> 13) & 1u) != 0,
+                          ((eb >> 13) & 1u) != 0, &ta, &tb, &oka, &okb);
+        }
+        enqueue(!oka, la);
+        enqueue(!okb, lb);
+        emit(oka, ea, tok0 + la, ta, false);
+        emit(okb, eb, tok0 + lb, tb, false);
+        r0 += 2 * dev::kWave;
+        continue;
+      }
       bool active;
       uint32_t e, i;
       tok::Token t;
@@ -1254,35 +1420,18 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
         const bool is_label = active && ((e >> 13) & 1u) != 0;
         // 0 in idle lanes: they decode harmless bytes
         const bool ok = tok::decode<F>(st, e & 0x1FFFu, is_label, &t);
-        const bool defer = active & !ok;
-        const uint64_t dm = __ballot(defer);
-        if (dm != 0) {
-          const uint32_t rank = static_cast<uint32_t>(__popcll(dm & ((1ull << lane) - 1ull)));
-          if (defer) {
-            dq_e[qn + rank] = e;
-            dq_i[qn + rank] = i;
-          }
-          qn += static_cast<uint32_t>(__popcll(dm));
-        }
+        enqueue(active & !ok, li);
         active = active & ok;
         r0 += dev::kWave;
       } else {
         dev::wave_sync();  // queue entries visible
         const uint32_t cnt = qn < static_cast<uint32_t>(dev::kWave) ? qn : dev::kWave;
         active = slot < cnt;
-        e = active ? dq_e[slot] : 0u;
-        i = active ? dq_i[slot] : 0u;
-        // the rest (< 64) moves to the front (read, sync, write)
-        const uint32_t keep = qn - cnt;
-        const bool mv = lane < static_cast<int>(keep);
-        const uint32_t me = mv ? dq_e[dev::kWave + lane] : 0u;
-        const uint32_t mi = mv ? dq_i[dev::kWave + lane] : 0u;
-        dev::wave_sync();
-        if (mv) {
-          dq_e[lane] = me;
-          dq_i[lane] = mi;
-        }
-        qn = keep;
+        const uint32_t li = active ? dq[(qh + slot) & (kQueueCap - 1)] : 0u;
+        qh += cnt;
+        qn -= cnt;
+        e = active ? sl[li] : 0u;
+        i = tok0 + li;
         const bool is_label = active && ((e >> 13) & 1u) != 0;
         const uint32_t off = e & 0x1FFFu;
         bool ok = false;
@@ -1319,12 +1468,14 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
     lcnt += nline;
     dev::wave_sync();  // every lane is done with this step's text and list
   }
-  unsigned fl = 0;
+  unsigned fl = count_flags;
+  if (sink == 0x9E3779B9u) fl |= kFlagIrregular;  // keeps a pricing run's values live
   if (any_value) fl |= kFlagValue;
   if (any_weight) fl |= kFlagWeight;
   if (irregular) fl |= kFlagIrregular;
   if (neg) fl |= kFlagNegIndex;
   if (need_w) fl |= kFlagNeedWeight;
+  if (over) fl |= kFlagOverflow;
   if (F == TextFormat::kLibFM) fl |= kFlagField;
   const unsigned long long mi = dev::wave_max(static_cast<unsigned long long>(mx_index));
   const unsigned long long mf = dev::wave_max(static_cast<unsigned long long>(mx_field));
@@ -1780,7 +1931,10 @@ __global__ __launch_bounds__(kFinishThreads) void k_tile_finish(
     meta->max_index = s_mi[0];
     meta->max_field = s_mf[0];
     meta->flags |= s_fl[0];
-    if (offset != nullptr) offset[row_base + meta->nrows] = nnz_base + meta->nnz;
+    // (an overflowed one-pass fill's rows reach past the target: no row pointer)
+    if (offset != nullptr && !(meta->flags & kFlagOverflow)) {
+      offset[row_base + meta->nrows] = nnz_base + meta->nnz;
+    }
     if (host_meta != nullptr) publish_host_meta(host_meta, *meta);
   }
 }
@@ -1900,23 +2054,46 @@ size_t TileScratchWords(size_t ntiles) {
 size_t TileScratchSlots(size_t ntiles) { return ntiles + kFinishGroups; }
 
 template <typename IndexType>
-void LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
-                    const uint64_t* tile_prefix, const FillTarget<IndexType>& out,
-                    MetaPartial* partials, ChunkMeta* meta, ChunkMeta* host_meta,
-                    hipStream_t stream) {
+size_t LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
+                      const uint64_t* tile_prefix, const FillTarget<IndexType>& out,
+                      MetaPartial* partials, ChunkMeta* meta, ChunkMeta* host_meta,
+                      hipStream_t stream, const FillOnePass* one_pass) {
   const size_t ntiles = TileCount(nbytes);
   const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
+  const size_t groups = (ntiles + kFillWaves - 1) / kFillWaves;
+  static const uint32_t exp = [] {
+    const char* v = std::getenv("DMLC_FILL_EXP");
+    return v != nullptr ? static_cast<uint32_t>(std::atoi(v)) : 0u;
+  }();
+  FillPass op{nullptr, nullptr, 0ull, meta, exp};
+  if (one_pass != nullptr) {
+    op.status = one_pass->status;
+    op.ticket = one_pass->ticket;
+    op.ticket0 = one_pass->ticket0;
+    // every look-back word starts "not yet" (cdna_hip_programming.md G16:
+    // zero every polled word before every launch)
+    DMLC_HIP_CHECK(hipMemsetAsync(op.status, 0, ntiles * sizeof(uint64_t), stream));
+  }
   if (ntiles != 0) {
-    const dim3 grid(static_cast<unsigned>((ntiles + kFillWaves - 1) / kFillWaves));
+    const dim3 grid(static_cast<unsigned>(groups));
+#define DMLC_TILE_FILL(FMT, ONE)                                                                \
+  hipLaunchKernelGGL((k_tile_fill<FMT, IndexType, ONE>), grid, dim3(kThreads), 0, stream, t, nbytes, \
+                     ntiles, tile_prefix, out, partials, op)
     if (format == TextFormat::kLibFM) {
-      hipLaunchKernelGGL((k_tile_fill<TextFormat::kLibFM, IndexType>), grid, dim3(kThreads), 0,
-                         stream, t, nbytes, ntiles, tile_prefix, out, partials);
+      if (one_pass != nullptr) {
+        DMLC_TILE_FILL(TextFormat::kLibFM, true);
+      } else {
+        DMLC_TILE_FILL(TextFormat::kLibFM, false);
+      }
+    } else if (one_pass != nullptr) {
+      DMLC_TILE_FILL(TextFormat::kLibSVM, true);
     } else {
-      hipLaunchKernelGGL((k_tile_fill<TextFormat::kLibSVM, IndexType>), grid, dim3(kThreads), 0,
-                         stream, t, nbytes, ntiles, tile_prefix, out, partials);
+      DMLC_TILE_FILL(TextFormat::kLibSVM, false);
     }
+#undef DMLC_TILE_FILL
   }
   LaunchFinish(partials, ntiles, meta, host_meta, out.offset, out.row_base, out.nnz_base, stream);
+  return ntiles != 0 ? groups : 0;
 }
 
 template <typename IndexType>
@@ -1976,12 +2153,12 @@ template size_t LaunchTileHashed<uint64_t>(const char*, size_t, TextFormat, cons
                                            float*, MetaPartial*, ChunkMeta*, ChunkMeta*,
                                            hipStream_t, const HashOnePass*);
 
-template void LaunchTileFill<uint32_t>(const char*, size_t, TextFormat, const uint64_t*,
-                                       const FillTarget<uint32_t>&, MetaPartial*, ChunkMeta*,
-                                       ChunkMeta*, hipStream_t);
-template void LaunchTileFill<uint64_t>(const char*, size_t, TextFormat, const uint64_t*,
-                                       const FillTarget<uint64_t>&, MetaPartial*, ChunkMeta*,
-                                       ChunkMeta*, hipStream_t);
+template size_t LaunchTileFill<uint32_t>(const char*, size_t, TextFormat, const uint64_t*,
+                                         const FillTarget<uint32_t>&, MetaPartial*, ChunkMeta*,
+                                         ChunkMeta*, hipStream_t, const FillOnePass*);
+template size_t LaunchTileFill<uint64_t>(const char*, size_t, TextFormat, const uint64_t*,
+                                         const FillTarget<uint64_t>&, MetaPartial*, ChunkMeta*,
+                                         ChunkMeta*, hipStream_t, const FillOnePass*);
 
 }  // namespace gpu
 }  // namespace dmlc

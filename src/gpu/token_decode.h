@@ -79,12 +79,43 @@ __device__ __forceinline__ uint32_t lead_digits(uint32_t g, uint32_t* val) {
   return k;
 }
 
-/*! \brief RN(1 / 10^k) and 10^k in float, k = 0..7 (branch-free selects) */
+/*!
+ * \brief the value and digit count of a run split in two 4-byte groups:
+ *  (k0, v0) the first group's lead_digits, (k1, v1) the second's, which
+ *  counts only when the first is full.  The empty asm pins the second group
+ *  as computed: left alone, hipcc sinks it into an exec-masked branch (an
+ *  s_and_saveexec / s_cbranch_execz / exec restore per number, and no
+ *  interleaving of independent numbers across it).  Both factors are below
+ *  2^24: a full-rate v_mul_u32_u24, not the quarter-rate v_mul_lo_u32.
+ */
+__device__ __forceinline__ uint32_t join_groups(uint32_t k0, uint32_t v0, uint32_t k1, uint32_t v1,
+                                                uint32_t* k) {
+  // (an explicit v_mul_u32_u24: from __umul24 of operands it can bound,
+  // hipcc emits the quarter-rate v_mul_lo_u32)
+  uint32_t x;
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(x) : "v"(v0), "v"(pow10_u(k1)));
+  x += v1;
+  asm("" : "+v"(x));
+  const bool full = k0 == 4;
+  *k = full ? 4u + k1 : k0;
+  return full ? x : v0;
+}
+
+/*!
+ * \brief RN(1 / 10^k) and 10^k in float, k = 0..7: a three-level select on
+ *  the bits of k.  Each level is pinned by an empty asm -- written as a
+ *  plain ternary chain, hipcc lowers the lookup to nested exec-masked
+ *  branches (s_and_saveexec / s_xor / s_cbranch per level, every number).
+ */
 __device__ __forceinline__ void pow10f(uint32_t k, float* p, float* inv) {
   *p = static_cast<float>(pow10_u(k));
-  const float i_lo = k == 0 ? 1.0f : (k == 1 ? 0.1f : (k == 2 ? 0.01f : 0.001f));
-  const float i_hi = k == 4 ? 1e-4f : (k == 5 ? 1e-5f : (k == 6 ? 1e-6f : 1e-7f));
-  *inv = k < 4 ? i_lo : i_hi;
+  const bool b0 = (k & 1u) != 0, b1 = (k & 2u) != 0, b2 = (k & 4u) != 0;
+  float a0 = b0 ? 0.1f : 1.0f, a1 = b0 ? 0.001f : 0.01f;
+  float a2 = b0 ? 1e-5f : 1e-4f, a3 = b0 ? 1e-7f : 1e-6f;
+  asm("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3));
+  float c0 = b1 ? a1 : a0, c1 = b1 ? a3 : a2;
+  asm("" : "+v"(c0), "+v"(c1));
+  *inv = b2 ? c1 : c0;
 }
 
 /*!
@@ -125,8 +156,8 @@ __device__ __forceinline__ Num parse_num_g(uint4 g, uint32_t a) {
   uint32_t v0, v1;
   const uint32_t k0 = lead_digits(h0, &v0);
   const uint32_t k1 = lead_digits(h1, &v1);
-  const uint32_t k = k0 == 4 ? 4u + k1 : k0;
-  const uint32_t iv = k0 == 4 ? v0 * pow10_u(k1) + v1 : v0;
+  uint32_t k;
+  const uint32_t iv = join_groups(k0, v0, k1, v1, &k);
   const uint32_t tw = k < 4 ? h0 : (k < 8 ? h1 : h2);
   const uint32_t term = (tw >> (8u * (k & 3u))) & 0xFFu;
   // fraction digits: 8 bytes at fs = k + 1 (1..9) of h0..h3
@@ -140,8 +171,8 @@ __device__ __forceinline__ Num parse_num_g(uint4 g, uint32_t a) {
   uint32_t w0, w1;
   const uint32_t f0 = lead_digits(lo, &w0);
   const uint32_t f1 = lead_digits(hi, &w1);
-  const uint32_t nf = f0 == 4 ? 4u + f1 : f0;
-  const uint32_t fv = f0 == 4 ? w0 * pow10_u(f1) + w1 : w0;
+  uint32_t nf;
+  const uint32_t fv = join_groups(f0, w0, f1, w1, &nf);
   const uint32_t fw = nf < 4 ? lo : hi;
   const uint32_t fterm = nf < 8 ? (fw >> (8u * (nf & 3u))) & 0xFFu : 0x30u;
   const bool dot = term == '.';
@@ -184,8 +215,8 @@ __device__ __forceinline__ Num parse_int(const uint4* lds, uint32_t a) {
   uint32_t v0, v1;
   const uint32_t k0 = lead_digits(h0, &v0);
   const uint32_t k1 = lead_digits(h1, &v1);
-  const uint32_t k = k0 == 4 ? 4u + k1 : k0;
-  const uint32_t iv = k0 == 4 ? v0 * pow10_u(k1) + v1 : v0;
+  uint32_t k;
+  const uint32_t iv = join_groups(k0, v0, k1, v1, &k);
   const uint32_t tw = k < 4 ? h0 : (k < 8 ? h1 : h2);
   const uint32_t term = (tw >> (8u * (k & 3u))) & 0xFFu;
   const bool dot = term == '.';
@@ -213,6 +244,33 @@ struct Token {
   int r;                  // values parsed (ParsePair / ParseTriple convention)
 };
 
+/*! \brief the token shape from its decoded numbers (decode's last stage):
+ *  n1 the first number, n2 the one after its ':' (if any), n3 the one after
+ *  n2's ':' (LibFM) */
+template <TextFormat F>
+__device__ __forceinline__ bool assemble(const Num& n1, const Num& n2, const Num& n3,
+                                         bool is_label, Token* t) {
+  const bool c1 = n1.term == ':';
+  // label f[:f] (either format) or LibSVM feature u[:f]
+  const bool first = is_label ? n1.ok_float : n1.ok_uint;
+  const bool pair_ok = first & (c1 ? (n2.ok_float & is_end(n2.term)) : is_end(n1.term));
+  t->u0 = n1.ival;
+  t->f1 = n2.fval;
+  if (F == TextFormat::kLibSVM) {
+    t->f0 = is_label ? n1.fval : n2.fval;
+    t->r = c1 ? 2 : 1;
+    return pair_ok;
+  }
+  // LibFM feature field:index[:value]
+  const bool c2 = n2.term == ':';
+  const bool triple_ok =
+      c1 & n1.ok_uint & n2.ok_uint & (c2 ? (n3.ok_float & is_end(n3.term)) : is_end(n2.term));
+  t->u1 = n2.ival;
+  t->f0 = is_label ? n1.fval : n3.fval;
+  t->r = is_label ? (c1 ? 2 : 1) : (c2 ? 3 : 2);
+  return is_label ? pair_ok : triple_ok;
+}
+
 /*!
  * \brief decode a label `f[:f]`, LibSVM feature `u[:f]` or LibFM feature
  *  `u:u[:f]` starting at LDS byte a, branch-free: the numbers are decoded
@@ -227,33 +285,59 @@ __device__ __forceinline__ bool decode(const uint4* lds, uint32_t a, bool is_lab
   Num n1 = parse_int(lds, a);
   if (__any(is_label & (n1.term == '.'))) n1 = parse_num(lds, a);
   const bool c1 = n1.term == ':';
-  Num n2;
+  Num n2, n3;
   if (F == TextFormat::kLibSVM) {
     n2 = parse_num(lds, n1.end + (c1 ? 1u : 0u));  // the value (or the label's weight)
+    n3 = n2;
   } else {
     // LibFM: the index, or the label's weight
     n2 = parse_int(lds, n1.end + (c1 ? 1u : 0u));
     if (__any(is_label & c1 & (n2.term == '.'))) n2 = parse_num(lds, n1.end + (c1 ? 1u : 0u));
+    const bool c2 = n2.term == ':';
+    n3 = parse_num(lds, n2.end + (c2 ? 1u : 0u));
   }
-  // label f[:f] (either format) or LibSVM feature u[:f]
-  const bool first = is_label ? n1.ok_float : n1.ok_uint;
-  const bool pair_ok = first & (c1 ? (n2.ok_float & is_end(n2.term)) : is_end(n1.term));
-  t->u0 = n1.ival;
-  t->f1 = n2.fval;
+  return assemble<F>(n1, n2, n3, is_label, t);
+}
+
+/*!
+ * \brief decode() of two tokens per lane (a decode "pair round": lanes take
+ *  token i and token i + 64 of the list).  The same instructions as two
+ *  decode() calls, but the two tokens' LDS window reads and number decodes
+ *  are independent chains inside the same basic blocks -- the wave-uniform
+ *  label-fraction branches are shared -- so the compiler interleaves them and
+ *  each LDS round trip is paid once per pair.  Identical results.
+ */
+template <TextFormat F>
+__device__ __forceinline__ void decode2(const uint4* lds, uint32_t a0, uint32_t a1, bool lab0,
+                                        bool lab1, Token* t0, Token* t1, bool* ok0, bool* ok1) {
+  Num n1a = parse_int(lds, a0);
+  Num n1b = parse_int(lds, a1);
+  if (__any((lab0 & (n1a.term == '.')) | (lab1 & (n1b.term == '.')))) {
+    // (parse_num equals parse_int on tokens without a fraction)
+    n1a = parse_num(lds, a0);
+    n1b = parse_num(lds, a1);
+  }
+  const uint32_t s2a = n1a.end + (n1a.term == ':' ? 1u : 0u);
+  const uint32_t s2b = n1b.end + (n1b.term == ':' ? 1u : 0u);
+  Num n2a, n2b, n3a, n3b;
   if (F == TextFormat::kLibSVM) {
-    t->f0 = is_label ? n1.fval : n2.fval;
-    t->r = c1 ? 2 : 1;
-    return pair_ok;
+    n2a = parse_num(lds, s2a);
+    n2b = parse_num(lds, s2b);
+    n3a = n2a;
+    n3b = n2b;
+  } else {
+    n2a = parse_int(lds, s2a);
+    n2b = parse_int(lds, s2b);
+    if (__any((lab0 & (n1a.term == ':') & (n2a.term == '.')) |
+              (lab1 & (n1b.term == ':') & (n2b.term == '.')))) {
+      n2a = parse_num(lds, s2a);
+      n2b = parse_num(lds, s2b);
+    }
+    n3a = parse_num(lds, n2a.end + (n2a.term == ':' ? 1u : 0u));
+    n3b = parse_num(lds, n2b.end + (n2b.term == ':' ? 1u : 0u));
   }
-  // LibFM feature field:index[:value]
-  const bool c2 = n2.term == ':';
-  const Num n3 = parse_num(lds, n2.end + (c2 ? 1u : 0u));
-  const bool triple_ok =
-      c1 & n1.ok_uint & n2.ok_uint & (c2 ? (n3.ok_float & is_end(n3.term)) : is_end(n2.term));
-  t->u1 = n2.ival;
-  t->f0 = is_label ? n1.fval : n3.fval;
-  t->r = is_label ? (c1 ? 2 : 1) : (c2 ? 3 : 2);
-  return is_label ? pair_ok : triple_ok;
+  *ok0 = assemble<F>(n1a, n2a, n3a, lab0, t0);
+  *ok1 = assemble<F>(n1b, n2b, n3b, lab1, t1);
 }
 
 /*! \brief the dword starting at byte 4q (q <= 7) of a 32-byte window g0|g1 */
@@ -304,8 +388,8 @@ __device__ __forceinline__ ExtNum parse_num_ext(const uint4* lds, uint32_t a, ui
   uint32_t v0, v1;
   const uint32_t k0 = lead_digits(win_word(g0, g1, s), &v0);
   const uint32_t k1 = lead_digits(win_word(g0, g1, s + 4), &v1);
-  const uint32_t k = k0 == 4 ? 4u + k1 : k0;
-  const uint32_t iv = k0 == 4 ? v0 * pow10_u(k1) + v1 : v0;
+  uint32_t k;
+  const uint32_t iv = join_groups(k0, v0, k1, v1, &k);
   uint32_t pos = s + k;
   const bool dot = win_byte(g0, g1, pos) == '.';
   // fraction digits, four 4-byte groups (<= 16 digits)

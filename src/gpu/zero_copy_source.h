@@ -5,15 +5,21 @@
  *  H2D DMA reads the page cache directly -- no CPU memcpy into pinned slots
  *  (measured: 87.0M rows/s vs 55.3M with the pread ring, profiles/r01_zero_copy).
  *
+ * The partition is mapped and registered in windows of `window_bytes`; the
+ * next window is prepared (mmap + MAP_POPULATE + hipHostRegister) on a
+ * background thread while the current one is consumed, and the first window
+ * of a pass is small (4 chunks), so the first chunk's DMA starts after one
+ * small registration instead of after the whole shard was read and pinned.
  * Two modes:
- *  - eager: a partition of at most `pin_budget` bytes is mapped and registered
- *    once, up front (registration is paid once per parser, not per epoch);
- *  - windowed: larger partitions (a 288 GB shard per GPU) are mapped and
- *    registered in sliding windows of `window_bytes`; the next window is
- *    prepared on a background thread while the current one is consumed, and at
- *    most two are pinned at once (plus the one being prefetched).  A window is
- *    released only after the owner's drain callback (the copy stream's
+ *  - retained: a partition of at most `pin_budget` bytes keeps every window
+ *    pinned once registered (registration is paid once per parser, not per
+ *    epoch; later epochs find every window mapped);
+ *  - windowed: larger partitions (a 288 GB shard per GPU) keep at most two
+ *    windows pinned (plus the one being prefetched).  A window is released
+ *    only after the owner's drain callback (the copy stream's
  *    synchronisation) has run, so no DMA still reads it.
+ * `pin_budget` is per process; ShardPinBudget() divides the configured budget
+ * among the ranks of a host and bounds it by the host's available memory.
  *
  * Chunks never cross a file boundary and end on a record boundary (a record
  * longer than chunk_bytes makes its chunk longer):
@@ -34,11 +40,14 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <functional>
 #include <future>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include "../io/filesys.h"
@@ -59,8 +68,6 @@ class ZeroCopySource {
     JoinPending();
     for (auto& w : windows_) Unmap(&w);
     windows_.clear();
-    for (auto& m : eager_) Unmap(&m);
-    eager_.clear();
     for (int fd : fds_) {
       if (fd >= 0) ::close(fd);
     }
@@ -71,7 +78,7 @@ class ZeroCopySource {
   /*!
    * \brief prepare the partition; false (nothing left mapped) when it cannot be
    *  mmap'ed + registered
-   * \param pin_budget partitions up to this size are pinned whole (eager)
+   * \param pin_budget partitions up to this size keep every window pinned (retained)
    * \param window_bytes window size of the windowed mode
    */
   bool Init(io::InputSplitBase* split, size_t chunk_bytes, size_t pin_budget = 64UL << 30,
@@ -89,23 +96,14 @@ class ZeroCopySource {
       const int fd = split->filesystem()->OpenRawFd(split->files()[seg.file_index].path);
       if (fd < 0) return Fail();
       fds_.push_back(fd);
-      segs_.push_back(Seg{fds_.size() - 1, seg.begin, seg.end - seg.begin, nullptr, i});
+      segs_.push_back(Seg{fds_.size() - 1, seg.begin, seg.end - seg.begin, i});
     }
     windowed_ = PartitionBytes() > pin_budget;
-    if (windowed_) {
-      // probe once: a file that cannot be mapped + registered fails here
-      if (!segs_.empty()) {
-        Mapping probe;
-        if (!MapRange(segs_[0], 0, std::min(segs_[0].size, page_), &probe)) return Fail();
-        Unmap(&probe);
-      }
-      return true;
-    }
-    for (auto& s : segs_) {
-      Mapping m;
-      if (!MapRange(s, 0, s.size, &m)) return Fail();
-      s.eager = m.data;
-      eager_.push_back(m);
+    // probe once: a file that cannot be mapped + registered fails here
+    if (!segs_.empty()) {
+      Mapping probe;
+      if (!MapRange(segs_[0], 0, std::min(segs_[0].size, page_), &probe)) return Fail();
+      Unmap(&probe);
     }
     all_ = segs_;
     return true;
@@ -117,12 +115,7 @@ class ZeroCopySource {
    */
   void Reorder(const std::vector<size_t>& order) {
     if (all_.empty() && !segs_.empty()) all_ = segs_;
-    if (windowed_) {
-      JoinPending();
-      if (!windows_.empty() && drain_) drain_();
-      for (auto& w : windows_) Unmap(&w);
-      windows_.clear();
-    }
+    Rewind();
     std::vector<Seg> next;
     for (size_t want : order) {
       for (const Seg& s : all_) {
@@ -151,16 +144,9 @@ class ZeroCopySource {
     const size_t remain = s.size - off_;
     size_t want = std::min(chunk_bytes_, remain);
     for (;;) {
-      const char* b = nullptr;
-      size_t avail = 0;  // bytes of the segment visible from b
-      if (!windowed_) {
-        b = s.eager + off_;
-        avail = remain;
-      } else {
-        const Mapping* w = Window(seg_, off_, want);
-        b = w->data + (off_ - w->seg_off);
-        avail = w->seg_off + w->len - off_;
-      }
+      const Mapping* w = Window(s.init_index, off_, want);
+      const char* b = w->data + (off_ - w->seg_off);
+      const size_t avail = w->seg_off + w->len - off_;  // bytes of the segment visible from b
       size_t len = want;
       if (off_ + len < s.size) {
         len = cut_ == Cut::kLine ? CutLine(b, len, avail) : CutRecord(b, len, avail);
@@ -187,12 +173,7 @@ class ZeroCopySource {
   }
   /*! \brief continue from a Tell() cursor */
   void Seek(size_t pos) {
-    if (windowed_) {
-      JoinPending();
-      if (!windows_.empty() && drain_) drain_();
-      for (auto& w : windows_) Unmap(&w);
-      windows_.clear();
-    }
+    Rewind();
     seg_ = 0;
     off_ = pos;
     while (seg_ < segs_.size() && off_ >= segs_[seg_].size) {
@@ -208,10 +189,46 @@ class ZeroCopySource {
   }
   /*! \brief bytes currently registered with HIP (for stats and tests) */
   size_t PinnedBytes() const {
-    size_t n = 0;
-    for (const auto& m : eager_) n += m.map_len;
-    for (const auto& w : windows_) n += w.map_len;
-    return n;
+    std::lock_guard<std::mutex> lk(pinned_mu_);
+    return pinned_;
+  }
+  /*! \brief the most bytes registered at once so far */
+  size_t PeakPinnedBytes() const {
+    std::lock_guard<std::mutex> lk(pinned_mu_);
+    return peak_pinned_;
+  }
+  /*!
+   * \brief the zero-copy pin budget of one process: the configured per-host
+   *  budget divided among the ranks on this host (DMLC_LOCAL_WORLD_SIZE from
+   *  the dmlc launchers, LOCAL_WORLD_SIZE from torchrun) and bounded by half
+   *  of the host's MemAvailable shared the same way -- 8 ranks must not lock
+   *  8 x the budget, nor more memory than the host has free.
+   */
+  static size_t ShardPinBudget(size_t configured) {
+    size_t local = 1;
+    for (const char* k : {"DMLC_LOCAL_WORLD_SIZE", "LOCAL_WORLD_SIZE"}) {
+      const char* v = std::getenv(k);
+      if (v != nullptr && std::atoi(v) > 0) {
+        local = static_cast<size_t>(std::atoi(v));
+        break;
+      }
+    }
+    size_t budget = configured / local;
+    const size_t avail = MemAvailableBytes();
+    if (avail != 0) budget = std::min(budget, avail / 2 / local);
+    return budget;
+  }
+  /*! \brief MemAvailable of /proc/meminfo (0 when unknown) */
+  static size_t MemAvailableBytes() {
+    std::FILE* f = std::fopen("/proc/meminfo", "r");
+    if (f == nullptr) return 0;
+    char line[256];
+    size_t kb = 0;
+    while (std::fgets(line, sizeof(line), f) != nullptr) {
+      if (std::sscanf(line, "MemAvailable: %zu kB", &kb) == 1) break;
+    }
+    std::fclose(f);
+    return kb * 1024;
   }
 
  private:
@@ -219,8 +236,7 @@ class ZeroCopySource {
     size_t fd_index;
     size_t file_begin;  // first byte of the segment in its file
     size_t size;
-    const char* eager;  // eager mode: mapped segment start
-    size_t init_index;  // position in the Init segment list
+    size_t init_index;  // position in the Init segment list (window key)
   };
   struct Mapping {
     void* map{nullptr};
@@ -247,30 +263,60 @@ class ZeroCopySource {
       return false;
     }
     m->registered = true;
+    {
+      std::lock_guard<std::mutex> lk(pinned_mu_);
+      pinned_ += m->map_len;
+      peak_pinned_ = std::max(peak_pinned_, pinned_);
+    }
     m->data = static_cast<const char*>(m->map) + (file_off - map_off);
     m->seg_off = seg_off;
     m->len = len;
     return true;
   }
-  static void Unmap(Mapping* m) {
+  void Unmap(Mapping* m) {
     if (m->map == nullptr) return;
-    if (m->registered) (void)hipHostUnregister(m->map);
+    if (m->registered) {
+      (void)hipHostUnregister(m->map);
+      std::lock_guard<std::mutex> lk(pinned_mu_);
+      pinned_ -= m->map_len;
+    }
     munmap(m->map, m->map_len);
     m->map = nullptr;
   }
+  /*! \brief finish the background registration; retained mode keeps its window */
   void JoinPending() {
-    if (pending_.valid()) {
-      Mapping m = pending_.get();
+    if (!pending_.valid()) return;
+    Mapping m = pending_.get();
+    if (!windowed_ && m.map != nullptr) {
+      windows_.push_back(m);
+    } else {
       Unmap(&m);
     }
   }
-  /*! \brief the window of segment si holding [off, off + want), mapped on demand */
+  /*! \brief a new pass (Seek / Reorder): windowed mode releases its windows
+   *  (after the drain), retained mode keeps them */
+  void Rewind() {
+    JoinPending();
+    if (!windowed_) return;
+    if (!windows_.empty() && drain_) drain_();
+    for (auto& w : windows_) Unmap(&w);
+    windows_.clear();
+  }
+  /*! \brief the Init-list segment with key si */
+  const Seg& SegByKey(size_t si) const {
+    for (const Seg& s : all_) {
+      if (s.init_index == si) return s;
+    }
+    LOG(FATAL) << "zero-copy: no segment " << si;
+    return all_[0];
+  }
+  /*! \brief the window of segment si (Init index) holding [off, off + want),
+   *  mapped on demand */
   const Mapping* Window(size_t si, size_t off, size_t want) {
     for (const auto& w : windows_) {
       if (w.seg_index == si && off >= w.seg_off && off + want <= w.seg_off + w.len) return &w;
     }
-    const Seg& s = segs_[si];
-    const size_t len = std::min(s.size - off, std::max(window_bytes_, want));
+    const Seg& s = SegByKey(si);
     Mapping m;
     bool have = false;
     if (pending_.valid()) {
@@ -279,16 +325,25 @@ class ZeroCopySource {
           off + want <= p.seg_off + p.len) {
         m = p;
         have = true;
+      } else if (!windowed_ && p.map != nullptr) {
+        windows_.push_back(p);  // retained: another part of the shard, kept
+        for (const auto& w : windows_) {
+          if (w.seg_index == si && off >= w.seg_off && off + want <= w.seg_off + w.len) return &w;
+        }
       } else {
         Unmap(&p);
       }
     }
     if (!have) {
+      // mapped synchronously (the pass's first window, or a record longer
+      // than the window): small, so the pipeline starts after little I/O
+      const size_t first = std::max(4 * chunk_bytes_, want);
+      const size_t len = std::min(s.size - off, std::min(std::max(window_bytes_, want), first));
       CHECK(MapRange(s, off, len, &m)) << "zero-copy: cannot map + register a window";
       m.seg_index = si;
     }
-    // at most two windows pinned: release the oldest once its DMAs are done
-    if (windows_.size() >= 2) {
+    // windowed: at most two windows pinned, the oldest released once its DMAs are done
+    if (windowed_ && windows_.size() >= 2) {
       if (drain_) drain_();
       Unmap(&windows_.front());
       windows_.pop_front();
@@ -300,11 +355,18 @@ class ZeroCopySource {
     if (m.seg_off + m.len < s.size) Prefetch(si, m.seg_off + m.len - overlap);
     return &windows_.back();
   }
-  /*! \brief map + register the window after this one on a background thread */
+  /*! \brief map + register the window after this one on a background thread
+   *  (nothing to do when a retained window already covers it) */
   void Prefetch(size_t si, size_t off) {
-    if (si >= segs_.size() || off >= segs_[si].size) return;
-    const Seg s = segs_[si];
-    const size_t len = std::min(s.size - off, window_bytes_);
+    const Seg& seg = SegByKey(si);
+    if (off >= seg.size) return;
+    const size_t len = std::min(seg.size - off, window_bytes_);
+    for (const auto& w : windows_) {
+      if (w.seg_index == si && off >= w.seg_off && off + 2 * chunk_bytes_ <= w.seg_off + w.len) {
+        return;
+      }
+    }
+    const Seg s = seg;
     pending_ = std::async(std::launch::async, [this, s, si, off, len]() {
       Mapping m;
       if (!MapRange(s, off, len, &m)) m.map = nullptr;
@@ -342,8 +404,6 @@ class ZeroCopySource {
     return avail;
   }
   bool Fail() {
-    for (auto& m : eager_) Unmap(&m);
-    eager_.clear();
     for (int fd : fds_) {
       if (fd >= 0) ::close(fd);
     }
@@ -358,8 +418,9 @@ class ZeroCopySource {
   std::vector<int> fds_;
   std::vector<Seg> segs_;
   std::vector<Seg> all_;  // the Init list (Reorder's source)
-  std::vector<Mapping> eager_;
   std::deque<Mapping> windows_;
+  mutable std::mutex pinned_mu_;  // MapRange runs on the prefetch thread too
+  size_t pinned_{0}, peak_pinned_{0};
   std::future<Mapping> pending_;
   std::function<void()> drain_;
   size_t seg_{0}, off_{0};

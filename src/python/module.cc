@@ -459,10 +459,16 @@ class PyDeviceParser {
     d["nnz"] = s.nnz;
     d["exact_chunks"] = s.exact_chunks;
     d["one_pass_chunks"] = s.one_pass_chunks;
+    d["one_pass_reruns"] = s.one_pass_reruns;
     d["wait_reader_sec"] = s.wait_reader_sec;
     d["wait_gpu_sec"] = s.wait_gpu_sec;
     d["zero_copy"] = s.zero_copy;
     d["register_sec"] = s.register_sec;
+    d["zc_pin_budget"] = s.zc_pin_budget;
+    d["zc_pinned_peak"] = s.zc_pinned_peak;
+    d["last_pass_sec"] = s.last_pass_sec;
+    d["last_fill_sec"] = s.last_fill_sec;
+    d["last_drain_sec"] = s.last_drain_sec;
     d["waits_spun"] = s.waits_spun;
     d["waits_slept"] = s.waits_slept;
     d["waits_timed_out"] = s.waits_timed_out;

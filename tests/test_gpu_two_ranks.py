@@ -62,3 +62,33 @@ def test_bench_share_gpu_two_ranks(tmp_path, mode):
     assert sum(r["rows"] for r in out["per_rank"]) == 120000
     probe = out["allreduce_busbw_GBps"]
     assert probe["backend"] == "gloo" and probe["4MB"] > 0 and probe["256MB"] > 0
+
+
+@pytest.mark.timeout(330)
+def test_bench_share_gpu_eight_ranks(tmp_path):
+    """The world-8 rehearsal on one GPU: bench.py --gpus 8 --share-gpu starts
+    8 tracker ranks on GPU 0 (gloo control plane), the shape of the driver's
+    8-GPU SCALE run.  Per-rank rows sum to the dataset, the all-reduce probe
+    reports, and the zero-copy pin budget is shared: every rank's budget is
+    the host budget / 8 (or less, by MemAvailable) and no rank pinned more
+    than its budget -- 8 ranks never lock 8 x the host budget."""
+    env = dict(os.environ, PYTHONPATH=ROOT, DMLC_HEARTBEAT_PERIOD="1")
+    cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "8", "--share-gpu",
+           "--steps", "2", "--warmup", "1", "--rows", "400000",
+           "--data-dir", str(tmp_path / "bench")]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-5000:]
+    out = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][-1])
+    assert out["n_gpus"] == 8 and out["config"]["rows"] == 400000
+    ranks = out["per_rank"]
+    assert sorted(r["rank"] for r in ranks) == list(range(8))
+    assert sum(r["rows"] for r in ranks) == 400000
+    assert all(r["rows"] > 0 for r in ranks)
+    probe = out["allreduce_busbw_GBps"]
+    assert probe["backend"] == "gloo" and probe["4MB"] > 0
+    host_budget = 64 << 30  # DeviceParserConfig::zc_pin_budget
+    for r in ranks:
+        assert 0 < r["zc_pin_budget"] <= host_budget // 8
+        assert 0 < r["zc_pinned_peak"] <= r["zc_pin_budget"]
+        assert r["last_pass_sec"] > 0 and 0 < r["last_fill_sec"] <= r["last_pass_sec"]
+    assert sum(r["zc_pinned_peak"] for r in ranks) <= host_budget

@@ -176,8 +176,8 @@ WORKER = textwrap.dedent("""
 """)
 
 
-def _submit(args, timeout=240):
-    env = dict(os.environ, PYTHONPATH=ROOT)
+def _submit(args, timeout=240, **extra_env):
+    env = dict(os.environ, PYTHONPATH=ROOT, **extra_env)
     return subprocess.run([sys.executable, "-m", "dmlc_core_amd.parallel.launch.submit", *args],
                           capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
 
@@ -253,7 +253,7 @@ def test_gloo_process_group_via_torch_env(tmp_path):
     ("sge", "qsub -cwd -t 1-4"),
     ("mesos", "mesos-execute"),
     ("kubernetes", "amd.com/gpu"),
-    ("yarn", "org.apache.hadoop.yarn.dmlc.Client"),
+    ("yarn", '"number_of_containers": 4'),  # the Services spec (no hadoop jar mode)
     ("local", "DMLC_LOCAL_RANK=1"),
 ])
 def test_backend_dry_run(cluster, needle, tmp_path):
@@ -261,7 +261,8 @@ def test_backend_dry_run(cluster, needle, tmp_path):
             "--env", "FOO=bar", "echo", "hi"]
     if cluster == "mesos":
         args = ["--mesos-master", "m:5050"] + args
-    p = _submit(args, timeout=120)
+    rm = {"YARN_RM_ADDRESS": "http://rm.invalid:8088"} if cluster == "yarn" else {}
+    p = _submit(args, timeout=120, **rm)
     assert p.returncode == 0, p.stderr[-2000:]
     assert needle in p.stdout
     assert "FOO" in p.stdout
