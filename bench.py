@@ -285,10 +285,13 @@ def main():
     if use_gpu and args.format == "recordio":
         from dmlc_core_amd import io as dio
 
+        rextra = {} if args.replay_chunk_mb is None else {"replay_chunk_mb": args.replay_chunk_mb}
+        if args.one_pass:
+            rextra["one_pass"] = 1
         parser = dio.GPURecordIO(ddir, rank, world, chunk_mb=args.chunk_mb,
                                  device_slots=args.device_slots, pinned_slots=args.pinned_slots,
                                  zero_copy=args.zero_copy, device=local_rank,
-                                 hbm_cache=int(args.mode == "hbm"))
+                                 hbm_cache=int(args.mode == "hbm"), **rextra)
 
         def step():
             parser.before_first()

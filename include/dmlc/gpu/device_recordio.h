@@ -45,6 +45,15 @@ struct DeviceRecordIOConfig {
   bool hbm_cache{false};
   size_t replay_chunk_bytes{1UL << 30};
   /*!
+   * \brief ReadAll over the HBM cache decodes each merged chunk in ONE launch
+   *  (R1 inside the fill, decoupled look-back; the text is read once) instead
+   *  of count + scan + fill with the next chunk's count prelaunched beside
+   *  the current fill (`?one_pass=1`).  Off by default: the look-back costs
+   *  the fill waves 338 us per GiB, the prelaunched count hides behind the
+   *  fill (profiles/r05_recordio)
+   */
+  bool one_pass{false};
+  /*!
    * \brief indexed RecordIO (reference "indexed_recordio" InputSplit): the
    *  index file ("key offset" lines); shards by record count; with shuffle,
    *  every epoch visits the shard's records in the std::mt19937(111 + seed)
@@ -58,8 +67,8 @@ struct DeviceRecordIOConfig {
   double wait_spin_us{50};
   /*!
    * \brief apply `?k=v` overrides: chunk_mb, chunk_bytes, device, zero_copy,
-   *  device_slots, pinned_slots, hbm_cache, replay_chunk_mb, index, shuffle,
-   *  seed, wait_spin_us
+   *  device_slots, pinned_slots, hbm_cache, replay_chunk_mb, one_pass, index,
+   *  shuffle, seed, wait_spin_us
    */
   void Update(const std::map<std::string, std::string>& args);
 };
@@ -83,6 +92,10 @@ struct DeviceRecordIOStats {
   double wait_gpu_sec{0};
   /*! \brief chunks decoded from the HBM-resident copy (hbm_cache / indexed) */
   size_t replayed_chunks{0};
+  /*! \brief of those, chunks decoded in one launch (look-back, no count kernel) */
+  size_t one_pass_chunks{0};
+  /*! \brief one-pass chunks decoded again after growing the output */
+  size_t one_pass_reruns{0};
 };
 
 class DeviceRecordIOReader {

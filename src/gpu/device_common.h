@@ -228,6 +228,56 @@ __device__ __forceinline__ void block_store_partial(unsigned long long mi, unsig
 }
 
 /*!
+ * \brief decoupled look-back over per-tile count pairs -- the one-pass
+ *  kernels' replacement of a count kernel + scan.  Word: state (1: this tile's
+ *  own counts, 2: inclusive prefix; 0: not yet -- the array is zeroed by a
+ *  hipMemsetAsync before every launch) << 62 | hi << kLoBits | lo; the caller
+ *  guarantees that every prefix of hi fits 62 - kLoBits bits and of lo
+ *  kLoBits (no carries between the packed fields).  The word is the data and
+ *  the flag at once (one 8-byte agent-scope store, relaxed agent-scope polls:
+ *  the granule form of cdna_hip_programming.md Guideline 16, R2).  Tiles run
+ *  in ticket order, so every tile waited on is resident or done.  Returns the
+ *  exclusive prefix (packed the same way).
+ */
+template <int kLoBits>
+__device__ __forceinline__ uint64_t lookback_pairs(uint64_t* st, size_t tile, uint64_t own, int lane) {
+  constexpr uint64_t kVal = (1ull << 62) - 1ull;
+  constexpr uint64_t kLo = (1ull << kLoBits) - 1ull;
+  if (lane == 0) {
+    __hip_atomic_store(&st[tile], ((tile == 0 ? 2ull : 1ull) << 62) | own, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tile == 0) return 0;
+  uint32_t ex_hi = 0, ex_lo = 0;
+  int64_t j = static_cast<int64_t>(tile) - 1;  // the nearest predecessor not summed yet
+  for (;;) {
+    const int64_t k = j - lane;
+    const uint64_t v = k >= 0 ? __hip_atomic_load(&st[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : (2ull << 62);  // before the chunk: inclusive 0
+    const uint32_t state = static_cast<uint32_t>(v >> 62);
+    const uint64_t inc = __ballot(state == 2u);
+    const uint64_t waiting = __ballot(state == 0u);
+    const int first = inc != 0 ? __builtin_ctzll(inc) : kWave - 1;
+    const uint64_t need = first >= kWave - 1 ? ~0ull : ((2ull << first) - 1ull);
+    if ((waiting & need) != 0) {
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    const uint64_t x = lane <= first ? (v & kVal) : 0ull;
+    ex_hi += wave_sum(static_cast<uint32_t>(x >> kLoBits));
+    ex_lo += wave_sum(static_cast<uint32_t>(x & kLo));
+    if (inc != 0) break;
+    j -= kWave;
+  }
+  const uint64_t excl = (static_cast<uint64_t>(ex_hi) << kLoBits) | ex_lo;
+  if (lane == 0) {
+    __hip_atomic_store(&st[tile], (2ull << 62) | (excl + own), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return excl;
+}
+
+/*!
  * \brief 16-bit mask of the bytes of a 16-byte vector equal to `c`
  *  (exact SWAR zero-byte test per 32-bit word).
  */

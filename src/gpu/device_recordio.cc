@@ -67,6 +67,8 @@ void DeviceRecordIOConfig::Update(const std::map<std::string, std::string>& args
       hbm_cache = flag(v);
     } else if (k == "replay_chunk_mb") {
       replay_chunk_bytes = mb(v);
+    } else if (k == "one_pass") {
+      one_pass = flag(v);
     } else if (k == "index") {
       index_uri = v;
     } else if (k == "shuffle") {
@@ -441,10 +443,63 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
     CHECK_EQ(e & kRecErrBadPart, 0U) << "RecordIO: malformed record (bad multi-part chain or header)";
   }
 
+  /*!
+   * \brief one launch for an HBM-resident piece of ReadAll: the fill counts
+   *  its own tiles (look-back), writes into output sized by the piece's bound
+   *  (nwords / 2 records, its bytes) -- no count kernel, no second read of
+   *  the text, one host wait
+   */
+  void DecodeOnePass(const Piece& p) {
+    hipStream_t st = compute_.get();
+    DropPrelaunch();
+    const size_t nwords = p.bytes / 4;
+    const size_t tiles = RecordIOTiles(nwords);
+    partials_.Reserve(TileScratchSlots(tiles) * sizeof(MetaPartial));
+    status_.Reserve(tiles * sizeof(uint64_t));
+    if (ticket_.bytes() == 0) {
+      ticket_.Reserve(sizeof(unsigned long long));
+      DMLC_HIP_CHECK(hipMemsetAsync(ticket_.get(), 0, ticket_.bytes(), st));
+      ticket0_ = 0;
+    }
+    ChunkMeta* dmeta = meta_.get<ChunkMeta>();
+    ChunkMeta* hm = hmap_.get<ChunkMeta>();
+    ChunkMeta done;
+    for (;;) {
+      // into the capacity the resident output has (an earlier epoch sized it)
+      uint64_t* off = res_off_.get<uint64_t>();
+      uint8_t* dat = res_data_.get<uint8_t>();
+      const size_t rec_cap = res_off_.bytes() / sizeof(uint64_t);
+      const RecordIOOnePass op{status_.get<uint64_t>(), ticket_.get<unsigned long long>(),
+                               ticket0_, dmeta, rec_cap > 0 ? rec_cap - 1 : 0, res_data_.bytes()};
+      ticket0_ += LaunchRecordIOTileFill(p.words, nwords, nullptr, off, resident_rows_, dat,
+                                         resident_bytes_, partials_.get<MetaPartial>(), st, &op);
+      LaunchTileFinish(partials_.get<MetaPartial>(), tiles, dmeta, hm, off, resident_rows_,
+                       resident_bytes_, st);
+      done = WaitMeta();
+      CheckErrors(done.flags);
+      if (!(done.flags & kFlagOverflow)) break;
+      GrowResident(done.nrows, done.nnz);  // did not fit: grow, run the piece again
+      stats_.one_pass_reruns += 1;
+    }
+    busy_ = 0;
+    resident_rows_ += done.nrows;
+    resident_bytes_ += done.nnz;
+    stats_.bytes += p.bytes;
+    stats_.chunks += 1;
+    stats_.records += done.nrows;
+    stats_.one_pass_chunks += 1;
+  }
+
   void Decode(Piece p, bool resident) {
     ScopedRange range("recordio_chunk");
     busy_ = 1;
     hipStream_t st = compute_.get();
+    if (resident && cfg_.one_pass && p.slot < 0 && p.host == nullptr && indexed_ == nullptr &&
+        replay_ && p.bytes != 0) {
+      DecodeOnePass(p);
+      FillPipeline();
+      return;
+    }
     if (p.slot >= 0) DMLC_HIP_CHECK(hipStreamWaitEvent(st, slots_[p.slot]->copied.get(), 0));
     const size_t nwords = p.bytes / 4;
     const size_t tiles = RecordIOTiles(nwords);
@@ -588,6 +643,9 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
   } pre_;
   HostWaitStats waits_;
   DeviceBuffer out_off_, out_data_, res_off_, res_data_;
+  // one-pass replays: look-back words (zeroed per launch), workgroup tickets
+  DeviceBuffer status_, ticket_;
+  unsigned long long ticket0_{0};
   size_t resident_rows_{0}, resident_bytes_{0};
   DeviceRecordBatch batch_, resident_;
   DeviceRecordIOStats stats_;

@@ -289,9 +289,28 @@ void LaunchRecordIOTileCount(const uint32_t* words, size_t nwords, uint64_t* til
  *  MetaPartial per tile (error bits), folded by LaunchTileFinish, which also
  *  writes the closing offset.
  */
-void LaunchRecordIOTileFill(const uint32_t* words, size_t nwords, const uint64_t* tile_prefix,
-                            uint64_t* offset, uint64_t rec_base, uint8_t* data, uint64_t byte_base,
-                            MetaPartial* partials, hipStream_t stream);
+/*!
+ *  One pass (one_pass != nullptr; tile_prefix unused, nwords > 0): R1 runs
+ *  inside the fill (decoupled look-back over one_pass->status, zeroed here
+ *  before the launch); the chunk's records / bytes land in one_pass->meta
+ *  (nrows / nnz), for LaunchTileFinish.  Records at or past rec_cap (offset
+ *  slots; the closing one needs one more) and bytes past byte_cap are not
+ *  written and set kFlagOverflow: grow to rec_base + nrows / byte_base + nnz
+ *  and run the chunk again.  Returns the workgroups launched (advance
+ *  ticket0 by it).
+ */
+struct RecordIOOnePass {
+  uint64_t* status;            // >= RecordIOTiles(nwords) words
+  unsigned long long* ticket;  // counter, zeroed once
+  unsigned long long ticket0;  // the counter's value before this launch
+  ChunkMeta* meta;
+  uint64_t rec_cap;            // offset slots - 1
+  uint64_t byte_cap;           // data bytes
+};
+size_t LaunchRecordIOTileFill(const uint32_t* words, size_t nwords, const uint64_t* tile_prefix,
+                              uint64_t* offset, uint64_t rec_base, uint8_t* data,
+                              uint64_t byte_base, MetaPartial* partials, hipStream_t stream,
+                              const RecordIOOnePass* one_pass = nullptr);
 /*!
  * \brief R3: gather nrec whole records (src + src_off[k], len[k] bytes, 4-byte
  *  multiples) to dst + dst_off[k]

@@ -28,11 +28,18 @@
  *      that follows it (a continuation must follow a first / middle part,
  *      a head must follow a whole / last part).
  *   C4 (tile_kernels.hip): error bits folded, closing offset, published.
+ *   One pass (HBM-resident replays): R2 with R1 inside -- each wave counts
+ *      its tile from the words it already holds and takes the tiles before it
+ *      by decoupled look-back, so a replayed chunk is one launch that reads
+ *      the text once (the payload copies read the LDS-staged tile).
  *   R3 k_rec_gather: device gather of whole records (header included) into a
  *      contiguous batch -- the shuffled indexed-RecordIO epochs gather their
  *      batches from the HBM-resident partition with it.
  */
+#include <dmlc/gpu/hip_utils.h>
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 
 #include "./device_common.h"
 #include "./kernels.h"
@@ -176,35 +183,25 @@ __device__ __forceinline__ void lane_copy(const uint32_t* __restrict__ src, uint
   }
 }
 
-/*! \brief the whole wave copies len bytes of words src to byte address dst */
-__device__ __forceinline__ void wave_copy(const uint32_t* __restrict__ src, uint32_t len,
-                                          uint8_t* __restrict__ dst, int lane) {
-  const uintptr_t da = reinterpret_cast<uintptr_t>(dst);
-  const uintptr_t sa = reinterpret_cast<uintptr_t>(src);
-  uint32_t done = 0;
-  if ((da & 15U) == 0 && (sa & 15U) == 0) {
-    const uint32_t n16 = len / 16;
-    for (uint32_t c = lane; c < n16; c += kWave) {
-      reinterpret_cast<uint4*>(dst)[c] = reinterpret_cast<const uint4*>(src)[c];
-    }
-    done = n16 * 16;
-  } else if ((da & 3U) == 0) {
-    const uint32_t n4 = len / 4;
-    for (uint32_t c = lane; c < n4; c += kWave) reinterpret_cast<uint32_t*>(dst)[c] = src[c];
-    done = n4 * 4;
-  }
-  // the rest byte by byte (a misaligned destination, or the tail)
-  for (uint32_t b = done + lane; b < len; b += kWave) {
-    dst[b] = static_cast<uint8_t>(src[b / 4] >> (8 * (b & 3U)));
-  }
-}
-
 struct BigPart {
   uint32_t word;  // chunk word index of the header
   uint32_t len;
   uint64_t dst;   // output byte position (chunk-relative, after the re-inserted magic)
 };
 
+/*! \brief the one-pass fill's look-back state (kOnePass) */
+struct RecPass {
+  uint64_t* status;            // per-tile look-back words, zeroed before the launch
+  unsigned long long* ticket;  // workgroup ticket counter
+  unsigned long long ticket0;  // its value at this launch
+  ChunkMeta* meta;             // records / bytes of the chunk (the last tile writes them)
+  uint64_t rec_cap, byte_cap;  // offset / data capacity: records / bytes past them are not
+                               // written and set kFlagOverflow (grow, run again)
+  uint32_t exp;                // pricing experiments (DMLC_REC_EXP; 0 in production): 1 no
+                               // look-back wait (wrong positions), 2 no payload copies
+};
+
+template <bool kOnePass>
 __global__ __launch_bounds__(kThreads) void k_rec_tile_fill(const uint32_t* __restrict__ w,
                                                             size_t n, size_t ntiles,
                                                             const uint64_t* __restrict__ prefix,
@@ -212,14 +209,27 @@ __global__ __launch_bounds__(kThreads) void k_rec_tile_fill(const uint32_t* __re
                                                             uint64_t rec_base,
                                                             uint8_t* __restrict__ data,
                                                             uint64_t byte_base,
-                                                            MetaPartial* __restrict__ partials) {
+                                                            MetaPartial* __restrict__ partials,
+                                                            RecPass op) {
   __shared__ BigPart s_big[kWaves][kBigCap];
   // the tile's words (+ the one after it): a part's successor check reads its
-  // header from here instead of a dependent global load per part
+  // header from here instead of a dependent global load per part, and the
+  // payload copies read their source from here (the text is read from
+  // memory once)
   __shared__ uint4 s_tw[kWaves][kTileWords / 4 + 1];
   const int lane = lane_id();
   const int wave = threadIdx.x / kWave;
-  const size_t tile = static_cast<size_t>(blockIdx.x) * kWaves + wave;
+  size_t group = blockIdx.x;
+  if constexpr (kOnePass) {
+    // tiles in ticket order: a workgroup looks back only at tiles of
+    // workgroups that started before it, so every tile it waits on is
+    // resident or done
+    __shared__ uint32_t s_ticket;
+    if (threadIdx.x == 0) s_ticket = static_cast<uint32_t>(atomicAdd(op.ticket, 1ull) - op.ticket0);
+    __syncthreads();
+    group = s_ticket;
+  }
+  const size_t tile = group * kWaves + wave;
   if (tile >= ntiles) return;  // whole waves leave; nothing below synchronises waves
   BigPart* big = s_big[wave];
   const size_t base = tile * kTileWords;
@@ -235,11 +245,41 @@ __global__ __launch_bounds__(kThreads) void k_rec_tile_fill(const uint32_t* __re
     const size_t r = q - base;
     return r <= kTileWords ? tw[r] : w[q];
   };
-  const uint64_t pre = prefix[tile];
+  uint64_t pre;
+  uint32_t err = 0;
+  if constexpr (kOnePass) {
+    // R1 in the fill: the tile's (heads, bytes) from the registers it already
+    // holds, then the look-back for the tiles before it (heads < 2^30 and
+    // bytes < 2^32 in a chunk < 4 GiB: a 30 / 32-bit pair)
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < kLoads; ++j) {
+      c += quad_counts(t.q[j], t.after[j], base + j * 256 + lane * 4, n, &err);
+    }
+    if (tile == 0 && lane == 0 && n != 0 && !(t.q[0].x == kMagic && n > 1 && cflag_of(t.q[0].y) <= 1))
+      err |= kRecErrBadPart;  // a chunk starts at a record head
+    c = wave_sum_2x32(c);
+    if (op.exp & 1u) {
+      pre = static_cast<uint64_t>(tile) * c;  // pricing: positions without the look-back
+    } else {
+      pre = lookback_pairs<32>(op.status, tile, c, lane);
+    }
+    if (tile + 1 == ntiles && lane == 0) {
+      ChunkMeta m;
+      m.nlines = m.nrows = (pre + c) >> 32;
+      m.nnz = (pre + c) & 0xffffffffull;
+      m.max_index = m.max_field = 0;
+      m.flags = 0;
+      m.pad = 0;
+      *op.meta = m;  // k_tile_finish (stream-ordered) adds the error bits, publishes
+    }
+  } else {
+    pre = prefix[tile];
+  }
   uint64_t rec = pre >> 32;            // records before this 1 KiB sub-tile (chunk-relative)
   uint64_t pos = pre & 0xffffffffull;  // output bytes before it
   uint8_t* const out = data + byte_base;
-  uint32_t err = 0;
+  bool over = false;
   uint32_t nbig = 0;
 #pragma unroll
   for (int j = 0; j < kLoads; ++j) {
@@ -277,16 +317,22 @@ __global__ __launch_bounds__(kThreads) void k_rec_tile_fill(const uint32_t* __re
           err |= (ends_record == next_continues || next > 3) ? kRecErrBadPart : 0u;
         }
       }
+      // one pass writes into the capacity it was given (counted: sized exactly)
+      const bool fits = !kOnePass || (rec_base + r < op.rec_cap &&
+                                      byte_base + p + len + 4 <= op.byte_cap);
+      over |= !fits;
       if (cf <= 1) {
-        offset[rec_base + r] = byte_base + p;
+        if (fits) offset[rec_base + r] = byte_base + p;
         ++r;
       } else {
         // the reader re-inserts the escaped magic in front of a continuation
+        if (fits) {
 #pragma unroll
-        for (int b = 0; b < 4; ++b) out[p + b] = static_cast<uint8_t>(kMagic >> (8 * b));
+          for (int b = 0; b < 4; ++b) out[p + b] = static_cast<uint8_t>(kMagic >> (8 * b));
+        }
         p += 4;
       }
-      const bool whole = i + 2 + (static_cast<size_t>(len) + 3) / 4 <= n;  // else: truncated
+      const bool whole = fits && i + 2 + (static_cast<size_t>(len) + 3) / 4 <= n;  // else: truncated
       if (whole && len <= kSmallPart) {
         lane_copy(w + i + 2, len, out + p);
       } else if (whole) {
@@ -307,49 +353,49 @@ __global__ __launch_bounds__(kThreads) void k_rec_tile_fill(const uint32_t* __re
     pos += tot & 0xffffffffull;
   }
   wave_sync();  // the list is visible to every lane
-  // parts up to 1 KiB into 16-byte-aligned destinations (the common shape):
-  // kBatch parts per round, every lane's loads of all of them issued before
-  // any store, so a round waits for one memory latency instead of one per
-  // part; anything else takes the generic wave copy
-  constexpr uint32_t kBatch = 4;
-  for (uint32_t e0 = 0; e0 < nbig; e0 += kBatch) {
-    uint32_t v[kBatch][4];
-    BigPart bp[kBatch];
-    bool fast[kBatch];
-#pragma unroll
-    for (uint32_t q = 0; q < kBatch; ++q) {
-      fast[q] = false;
-      if (e0 + q < nbig) {
-        bp[q] = big[e0 + q];
-        fast[q] = bp[q].len <= 1024 && ((reinterpret_cast<uintptr_t>(out + bp[q].dst) & 15U) == 0);
-        const uint32_t b0 = static_cast<uint32_t>(lane) * 16;
-        if (fast[q] && b0 < bp[q].len) {
-          const uint32_t* src = w + bp[q].word + 2 + lane * 4;
-          const uint32_t nw = (bp[q].len - b0 + 3) / 4;  // words of this lane (<= 4)
-#pragma unroll
-          for (uint32_t k = 0; k < 4; ++k) v[q][k] = k < nw ? src[k] : 0u;
-        }
+  // the listed parts (> 64 B), two at a time: half-wave h copies part e0 + h.
+  // Destinations are any byte offset (a continuation's re-inserted magic
+  // shifts every later part by 4, odd payload lengths by anything), so each
+  // part is written as its head bytes up to the first 16-byte boundary, whole
+  // aligned 16-byte blocks (one dwordx4 store per lane) and its tail bytes;
+  // a block's 16 source bytes are five payload words funnel-shifted into
+  // place, read from the LDS-staged tile (or from memory past the tile).
+  const int hl = lane & 31;
+  for (uint32_t e0 = 0; e0 < ((op.exp & 2u) ? 0u : nbig); e0 += 2) {
+    const uint32_t e = e0 + static_cast<uint32_t>(lane >> 5);
+    if (e < nbig) {
+      const BigPart bp = big[e];
+      uint8_t* const d = out + bp.dst;
+      const uint32_t head = (16u - static_cast<uint32_t>(reinterpret_cast<uintptr_t>(d) & 15u)) & 15u;
+      const uint32_t h = head < bp.len ? head : bp.len;
+      const uint32_t nblk = (bp.len - h) / 16;
+      const uint32_t tail = bp.len - h - nblk * 16;
+      const size_t pw = static_cast<size_t>(bp.word) + 2;  // chunk word of payload byte 0
+      // payload word j: staged when inside the tile (+1), else from memory
+      auto pword = [&](uint32_t j) {
+        const size_t q = pw + j;
+        return q - base <= kTileWords ? tw[q - base] : w[q];
+      };
+      auto pbyte = [&](uint32_t o) { return static_cast<uint8_t>(pword(o >> 2) >> (8 * (o & 3u))); };
+      for (uint32_t b = static_cast<uint32_t>(hl); b < nblk; b += 32) {
+        const uint32_t o = h + 16 * b;  // payload byte of the block's first byte
+        const uint32_t j = o >> 2, r = o & 3u;
+        const uint32_t w0 = pword(j), w1 = pword(j + 1), w2 = pword(j + 2), w3 = pword(j + 3);
+        // (the fifth word only when the block is not word-aligned: it may lie
+        // past the payload's last word, so it is not read otherwise)
+        const uint32_t w4 = r != 0 ? pword(j + 4) : 0u;
+        *reinterpret_cast<uint4*>(d + o) =
+            make_uint4(__builtin_amdgcn_alignbyte(w1, w0, r), __builtin_amdgcn_alignbyte(w2, w1, r),
+                       __builtin_amdgcn_alignbyte(w3, w2, r), __builtin_amdgcn_alignbyte(w4, w3, r));
       }
-    }
-#pragma unroll
-    for (uint32_t q = 0; q < kBatch; ++q) {
-      if (e0 + q >= nbig) break;
-      if (!fast[q]) {
-        wave_copy(w + bp[q].word + 2, bp[q].len, out + bp[q].dst, lane);
-        continue;
-      }
-      const uint32_t b0 = static_cast<uint32_t>(lane) * 16;
-      if (b0 >= bp[q].len) continue;
-      uint8_t* d = out + bp[q].dst + b0;
-      const uint32_t m = bp[q].len - b0;
-      if (m >= 16) {
-        *reinterpret_cast<uint4*>(d) = make_uint4(v[q][0], v[q][1], v[q][2], v[q][3]);
-      } else {
-        for (uint32_t k = 0; k < m; ++k) d[k] = static_cast<uint8_t>(v[q][k >> 2] >> (8 * (k & 3U)));
+      if (static_cast<uint32_t>(hl) < h) d[hl] = pbyte(static_cast<uint32_t>(hl));
+      if (static_cast<uint32_t>(hl) < tail) {
+        const uint32_t o = h + nblk * 16 + static_cast<uint32_t>(hl);
+        d[o] = pbyte(o);
       }
     }
   }
-  err = wave_or(err);
+  err = wave_or(err | (over ? kFlagOverflow : 0u));
   if (lane == 0) {
     MetaPartial mp;
     mp.max_index = 0;
@@ -403,14 +449,30 @@ void LaunchRecordIOTileCount(const uint32_t* words, size_t nwords, uint64_t* til
                      stream, words, nwords, tiles, tile_counts, tile_flags);
 }
 
-void LaunchRecordIOTileFill(const uint32_t* words, size_t nwords, const uint64_t* tile_prefix,
-                            uint64_t* offset, uint64_t rec_base, uint8_t* data, uint64_t byte_base,
-                            MetaPartial* partials, hipStream_t stream) {
+size_t LaunchRecordIOTileFill(const uint32_t* words, size_t nwords, const uint64_t* tile_prefix,
+                              uint64_t* offset, uint64_t rec_base, uint8_t* data,
+                              uint64_t byte_base, MetaPartial* partials, hipStream_t stream,
+                              const RecordIOOnePass* one_pass) {
   const size_t tiles = RecordIOTiles(nwords);
-  if (tiles == 0) return;
-  hipLaunchKernelGGL(k_rec_tile_fill, dim3((tiles + kWaves - 1) / kWaves), dim3(kThreads), 0,
-                     stream, words, nwords, tiles, tile_prefix, offset, rec_base, data, byte_base,
-                     partials);
+  if (tiles == 0) return 0;
+  const size_t groups = (tiles + kWaves - 1) / kWaves;
+  static const uint32_t exp = [] {
+    const char* v = std::getenv("DMLC_REC_EXP");
+    return v != nullptr ? static_cast<uint32_t>(std::atoi(v)) : 0u;
+  }();
+  RecPass op{nullptr, nullptr, 0ull, nullptr, 0ull, 0ull, exp};
+  if (one_pass != nullptr) {
+    op = RecPass{one_pass->status, one_pass->ticket, one_pass->ticket0, one_pass->meta,
+                 one_pass->rec_cap, one_pass->byte_cap, exp};
+    // every look-back word starts "not yet" (zeroed before every launch)
+    DMLC_HIP_CHECK(hipMemsetAsync(op.status, 0, tiles * sizeof(uint64_t), stream));
+    hipLaunchKernelGGL(k_rec_tile_fill<true>, dim3(groups), dim3(kThreads), 0, stream, words,
+                       nwords, tiles, tile_prefix, offset, rec_base, data, byte_base, partials, op);
+  } else {
+    hipLaunchKernelGGL(k_rec_tile_fill<false>, dim3(groups), dim3(kThreads), 0, stream, words,
+                       nwords, tiles, tile_prefix, offset, rec_base, data, byte_base, partials, op);
+  }
+  return groups;
 }
 
 void LaunchRecordIOGather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len,

@@ -280,53 +280,6 @@ __device__ __forceinline__ uint64_t lookback_lines(uint64_t* st, size_t tile, ui
 }
 
 /*!
- * \brief decoupled look-back over per-tile (lines, entries) pairs -- the one
- *  pass CSR fill's replacement of C1 + C2.  Word: state (1: this tile's own
- *  counts, 2: inclusive prefix; 0: not yet -- the array is zeroed by a
- *  hipMemsetAsync before every launch) << 62 | lines << 31 | entries.  A chunk
- *  is < 2 GiB, so lines and entries (<= bytes / 2 each) fit 31 bits and the
- *  packed sums never carry.  The word is the data and the flag at once (one
- *  8-byte agent-scope store, relaxed agent-scope polls: the granule form of
- *  cdna_hip_programming.md Guideline 16, R2).  Returns the exclusive prefix.
- */
-__device__ __forceinline__ uint64_t lookback_fill(uint64_t* st, size_t tile, uint64_t own,
-                                                  int lane) {
-  constexpr uint64_t kVal = (1ull << 62) - 1ull;
-  if (lane == 0) {
-    __hip_atomic_store(&st[tile], ((tile == 0 ? 2ull : 1ull) << 62) | own, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (tile == 0) return 0;
-  uint32_t ex_lines = 0, ex_ent = 0;
-  int64_t j = static_cast<int64_t>(tile) - 1;  // the nearest predecessor not summed yet
-  for (;;) {
-    const int64_t k = j - lane;
-    const uint64_t v = k >= 0 ? __hip_atomic_load(&st[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                              : (2ull << 62);  // before the chunk: inclusive 0
-    const uint32_t state = static_cast<uint32_t>(v >> 62);
-    const uint64_t inc = __ballot(state == 2u);
-    const uint64_t waiting = __ballot(state == 0u);
-    const int first = inc != 0 ? __builtin_ctzll(inc) : dev::kWave - 1;
-    const uint64_t need = first >= dev::kWave - 1 ? ~0ull : ((2ull << first) - 1ull);
-    if ((waiting & need) != 0) {
-      __builtin_amdgcn_s_sleep(1);
-      continue;
-    }
-    const uint64_t x = lane <= first ? (v & kVal) : 0ull;
-    ex_lines += dev::wave_sum(static_cast<uint32_t>(x >> 31));
-    ex_ent += dev::wave_sum(static_cast<uint32_t>(x & 0x7FFFFFFFull));
-    if (inc != 0) break;
-    j -= dev::kWave;
-  }
-  const uint64_t excl = (static_cast<uint64_t>(ex_lines) << 31) | ex_ent;
-  if (lane == 0) {
-    __hip_atomic_store(&st[tile], (2ull << 62) | (excl + own), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  }
-  return excl;
-}
-
-/*!
  * \brief C1: one wave per 8 KiB tile, 8 x 16 B loads per lane all in flight,
  *  wave-level reductions only (no LDS, no barrier).
  */
@@ -1146,7 +1099,9 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
     qtoks = dev::wave_sum(qtoks);
     count_flags = (__any(bad) ? kFlagIrregular : 0u) | (qtoks != 0 ? kFlagQid : 0u);
     const uint64_t own = (static_cast<uint64_t>(lines) << 31) | ent;
-    const uint64_t excl = lookback_fill(op.status, tile, own, lane);
+    // (lines, entries) as a 31 / 31-bit pair: a chunk is < 2 GiB, so both are
+    // <= bytes / 2 and the packed sums never carry
+    const uint64_t excl = dev::lookback_pairs<31>(op.status, tile, own, lane);
     line_base = excl >> 31;
     tok_base = excl & 0x7FFFFFFFull;
     if (tile + 1 == ntiles && lane == 0) {

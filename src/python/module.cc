@@ -628,6 +628,8 @@ class PyDeviceRecordIO {
     d["wait_reader_sec"] = s.wait_reader_sec;
     d["wait_gpu_sec"] = s.wait_gpu_sec;
     d["replayed_chunks"] = s.replayed_chunks;
+    d["one_pass_chunks"] = s.one_pass_chunks;
+    d["one_pass_reruns"] = s.one_pass_reruns;
     return d;
   }
   uintptr_t Stream() const { return reinterpret_cast<uintptr_t>(reader_->stream()); }

@@ -174,6 +174,7 @@ def test_gpu_recordio_hbm_cache_replay(tmp_path, zero_copy):
         r.read_all()
         assert io.split_records(*r.resident_to_host()) == recs, e
     assert r.stats()["replayed_chunks"] > 0
+
     # streaming from the cache too, with the first epoch's batch sizes (the
     # resident read_all merges cached chunks; Next() must not)
     r.before_first()
@@ -222,3 +223,42 @@ def test_gpu_recordio_rejects_corrupt_chain(tmp_path):
     r = io.GPURecordIO(str(p), zero_copy=0)
     with pytest.raises(Exception, match="malformed record"):
         r.read_all()
+
+
+def test_gpu_recordio_one_pass_overflow_rerun(tmp_path):
+    """one_pass=1 after a streamed first epoch: the first read_all finds no
+    resident output yet, its piece overflows, grows the output and runs again"""
+    p = tmp_path / "v.rec"
+    recs = _records(2500, 17)
+    _write(p, recs)
+    r = io.GPURecordIO(str(p), 0, 1, chunk_bytes=16 * 1024, hbm_cache=1, one_pass=1)
+    assert sum(1 for _ in r.iter_host()) > 1  # epoch 1 streams, fills the cache
+    for _ in range(2):
+        r.before_first()
+        r.read_all()
+        assert io.split_records(*r.resident_to_host()) == recs
+    assert r.stats()["one_pass_chunks"] > 0 and r.stats()["one_pass_reruns"] >= 1
+
+
+@pytest.mark.parametrize("replay_mb", [0.05, 1])
+def test_gpu_recordio_one_pass_replay(tmp_path, replay_mb):
+    """read_all over the HBM cache decodes each merged piece in one launch
+    (R1 inside the fill, look-back, payload copied from the LDS-staged tile):
+    multi-part records, escaped magic words, empty and tiny records, records
+    straddling tiles -- every epoch equals the CPU reader and the counted
+    path (one_pass=0)"""
+    p = tmp_path / "o.rec"
+    recs = _records(4000, 13, max_len=3000)
+    _write(p, recs)
+    outs = {}
+    for one in (1, 0):
+        r = io.GPURecordIO(str(p), 0, 1, chunk_bytes=16 * 1024, hbm_cache=1,
+                           replay_chunk_mb=replay_mb, one_pass=one)
+        for e in range(3):
+            if e:
+                r.before_first()
+            r.read_all()
+            got = io.split_records(*r.resident_to_host())
+            assert got == recs, (one, e)
+        outs[one] = r.stats()
+    assert outs[1]["one_pass_chunks"] > 0 and outs[0]["one_pass_chunks"] == 0
