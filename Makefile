@@ -131,8 +131,14 @@ $(BUILD)/dmlc_bench_split_cpu: tools/dmlc_bench_split_cpu.cc $(LIB) $(HEADERS)
 	$(CXX) $(CXXFLAGS_BASE) $< -o $@ -L$(LIBDIR) -ldmlc -Wl,-rpath,$(abspath $(LIBDIR)) \
 	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64
 
+$(BUILD)/dmlc_bench_read: tools/dmlc_bench_read.cc $(LIB) $(HEADERS)
+	@mkdir -p $(BUILD)
+	$(CXX) $(CXXFLAGS_BASE) $< -o $@ -L$(LIBDIR) -ldmlc -Wl,-rpath,$(abspath $(LIBDIR)) \
+	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64
+
 tools: $(BUILD)/dmlc_parameter_example $(BUILD)/dmlc_gen $(BUILD)/dmlc_bench_cpu $(BUILD)/dmlc_recordio_dist $(BUILD)/dmlc_fs \
-  $(BUILD)/dmlc_recordio $(BUILD)/dmlc_gpu_api_check $(BUILD)/dmlc_objserver $(BUILD)/dmlc_bench_split_cpu
+  $(BUILD)/dmlc_recordio $(BUILD)/dmlc_gpu_api_check $(BUILD)/dmlc_objserver $(BUILD)/dmlc_bench_split_cpu \
+  $(BUILD)/dmlc_bench_read
 
 # same-host baseline ("re-measure on the MI355X host's CPU"): the
 # reference's own sources, read in place from REF (never copied into this

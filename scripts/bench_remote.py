@@ -30,11 +30,13 @@ def main():
     ap.add_argument("--epochs", type=int, default=3)
     ap.add_argument("--threads", default="8,16,32", help="read_threads values for s3://")
     ap.add_argument("--data", default="/tmp/dmlc_remote_bench")
+    ap.add_argument("--reader-threads", default="8,16,32,64",
+                    help="read_threads values for the reader-alone runs (tools/dmlc_bench_read)")
     args = ap.parse_args()
 
     import torch
 
-    from dmlc_core_amd import data
+    from dmlc_core_amd import _dmlc, data
 
     bucket = os.path.join(args.data, "bench", "train")
     os.makedirs(bucket, exist_ok=True)
@@ -52,11 +54,25 @@ def main():
         port = int(srv.stdout.readline().split()[1])
         os.environ.update({"S3_ENDPOINT": f"http://127.0.0.1:{port}", "S3_ACCESS_KEY_ID": "bench",
                            "S3_SECRET_ACCESS_KEY": "bench", "S3_REGION": "us-east-1"})
+        # the host stage alone (ShardReader.Fill into a 64 MiB buffer, no GPU):
+        # what the ring's reader can deliver, natively received and via libcurl
+        out_reader = []
+        for native in ("1", "0"):
+            for t in [x for x in args.reader_threads.split(",") if x]:
+                env = dict(os.environ, DMLC_HTTP_NATIVE=native)
+                p = subprocess.run([os.path.join(ROOT, "build", "dmlc_bench_read"), "s3://bench/train/",
+                                    t, "64", str(args.epochs)], capture_output=True, text=True,
+                                   env=env, timeout=600)
+                rec = json.loads(p.stdout.strip().splitlines()[-1])
+                rec["native"] = native == "1"
+                out_reader.append(rec)
+                print(json.dumps(rec), file=sys.stderr, flush=True)
         runs = [("local", bucket + "/", 8)]
         runs += [("s3", "s3://bench/train/", int(t)) for t in args.threads.split(",") if t]
         runs.append(("http_one_file", f"http://127.0.0.1:{port}/bench/train/part-000.libsvm", 16))
         out = {"rows": args.rows, "files": args.files, "bytes": nbytes, "epochs": args.epochs,
-               "server": "tools/dmlc_objserver (loopback, sendfile)", "runs": []}
+               "server": "tools/dmlc_objserver (loopback, sendfile)", "reader_alone": out_reader,
+               "runs": []}
         for name, uri, threads in runs:
             gp = data.GPUParser(uri, format="libsvm", read_threads=threads)
             csr = data.DeviceCSR()
@@ -83,7 +99,7 @@ def main():
                        (s1["wait_reader_sec"] - s0["wait_reader_sec"]) / args.epochs, 4),
                    "wait_gpu_sec_per_epoch": round(
                        (s1["wait_gpu_sec"] - s0["wait_gpu_sec"]) / args.epochs, 4),
-                   "zero_copy": s1.get("zero_copy")}
+                   "zero_copy": s1.get("zero_copy"), "http": _dmlc.http_stats()}
             out["runs"].append(rec)
             print(json.dumps(rec), file=sys.stderr, flush=True)
         print(json.dumps(out), flush=True)

@@ -7,9 +7,18 @@
 #include <dlfcn.h>
 #include <dmlc/fault.h>
 #include <dmlc/logging.h>
+#include <errno.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+#include <sys/time.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <ctime>
 #include <thread>
@@ -136,11 +145,226 @@ size_t OnHeader(char* data, size_t size, size_t nmemb, void* user) {
   return n;
 }
 
+// ------------------------------------------------------------------------
+// Plain-http GETs received straight into the caller's memory.  libcurl reads
+// the socket into its own 16 KiB buffer and hands it to OnWrite, which copies
+// it into req.out (the pinned ring slot): two copies of every byte, ~30 GB/s
+// of loopback per host in round 3 (profiles/r03_remote).  Here the body is
+// recv()ed with MSG_WAITALL directly into req.out -- the kernel's socket copy
+// is the only one.  Keep-alive connections are per thread (one per pool
+// worker).  Anything unusual (https, a non-2xx status, chunked or
+// length-less bodies, a transport error) closes the connection and the
+// request goes to libcurl instead, so the fast path never changes semantics.
+
+struct NativeConn {
+  std::string authority;  // host[:port] the socket is connected to
+  int fd{-1};
+  ~NativeConn() { Close(); }
+  void Close() {
+    if (fd >= 0) ::close(fd);
+    fd = -1;
+  }
+};
+
+NativeConn& ThreadConn() {
+  thread_local NativeConn c;
+  return c;
+}
+
+bool NativeEnabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("DMLC_HTTP_NATIVE");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
+std::atomic<uint64_t> g_native_gets{0}, g_native_fallbacks{0};
+
+int ConnectTo(const std::string& host, const std::string& port, long timeout_sec) {
+  addrinfo hints{};
+  hints.ai_family = AF_UNSPEC;
+  hints.ai_socktype = SOCK_STREAM;
+  addrinfo* res = nullptr;
+  if (::getaddrinfo(host.c_str(), port.c_str(), &hints, &res) != 0) return -1;
+  int fd = -1;
+  for (addrinfo* a = res; a != nullptr; a = a->ai_next) {
+    fd = ::socket(a->ai_family, a->ai_socktype | SOCK_CLOEXEC, a->ai_protocol);
+    if (fd < 0) continue;
+    if (::connect(fd, a->ai_addr, a->ai_addrlen) == 0) break;
+    ::close(fd);
+    fd = -1;
+  }
+  ::freeaddrinfo(res);
+  if (fd < 0) return -1;
+  const int one = 1;
+  ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  timeval tv{timeout_sec, 0};
+  ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  ::setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+  return fd;
+}
+
+bool SendAll(int fd, const char* p, size_t n) {
+  while (n > 0) {
+    const ssize_t k = ::send(fd, p, n, MSG_NOSIGNAL);
+    if (k <= 0) {
+      if (k < 0 && errno == EINTR) continue;
+      return false;
+    }
+    p += k;
+    n -= static_cast<size_t>(k);
+  }
+  return true;
+}
+
+/*! \brief recv exactly n bytes (MSG_WAITALL: one syscall for the whole body on loopback) */
+bool RecvAll(int fd, char* p, size_t n) {
+  while (n > 0) {
+    const ssize_t k = ::recv(fd, p, n, MSG_WAITALL);
+    if (k <= 0) {
+      if (k < 0 && errno == EINTR) continue;
+      return false;
+    }
+    p += k;
+    n -= static_cast<size_t>(k);
+  }
+  return true;
+}
+
+/*!
+ * \brief one GET on the thread's keep-alive connection into req.out.
+ * \return true if `resp` holds the outcome; false = use libcurl (the
+ *  connection is closed, nothing of `resp` is kept)
+ */
+bool NativeGet(const HttpRequest& req, HttpResponse* resp) {
+  static const std::string kScheme = "http://";
+  if (req.url.compare(0, kScheme.size(), kScheme) != 0) return false;
+  const size_t slash = req.url.find('/', kScheme.size());
+  const std::string authority =
+      req.url.substr(kScheme.size(), slash == std::string::npos ? std::string::npos
+                                                                  : slash - kScheme.size());
+  const std::string target = slash == std::string::npos ? "/" : req.url.substr(slash);
+  if (authority.empty() || authority.find('@') != std::string::npos ||
+      authority.front() == '[') {
+    return false;  // userinfo / IPv6 literals: libcurl
+  }
+  const size_t colon = authority.rfind(':');
+  const std::string host = authority.substr(0, colon);
+  const std::string port = colon == std::string::npos ? "80" : authority.substr(colon + 1);
+
+  std::string head = "GET " + target + " HTTP/1.1\r\nHost: " + authority + "\r\n";
+  for (const auto& h : req.headers) head += h + "\r\n";
+  head += "\r\n";
+
+  NativeConn& c = ThreadConn();
+  if (c.fd >= 0 && c.authority != authority) c.Close();
+  char hdr[16384];
+  size_t have = 0, hend = std::string::npos;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    const bool reused = c.fd >= 0;
+    if (!reused) {
+      c.fd = ConnectTo(host, port, req.timeout_sec);
+      if (c.fd < 0) return false;
+      c.authority = authority;
+    }
+    have = 0;
+    bool ok = SendAll(c.fd, head.data(), head.size());
+    while (ok && hend == std::string::npos) {
+      const ssize_t k = ::recv(c.fd, hdr + have, sizeof(hdr) - have, 0);
+      if (k < 0 && errno == EINTR) continue;
+      if (k <= 0) {
+        ok = false;
+        break;
+      }
+      have += static_cast<size_t>(k);
+      const char* e = static_cast<const char*>(memmem(hdr, have, "\r\n\r\n", 4));
+      if (e != nullptr) hend = static_cast<size_t>(e - hdr) + 4;
+      else if (have == sizeof(hdr)) ok = false;  // oversized header block
+    }
+    if (ok) break;
+    c.Close();
+    // a reused keep-alive connection the server has since closed: one fresh try
+    if (!reused || have != 0) return false;
+  }
+  if (hend == std::string::npos) return false;
+
+  // status line + headers
+  HttpResponse r;
+  const std::string block(hdr, hend);
+  size_t eol = block.find("\r\n");
+  const std::string status_line = block.substr(0, eol);
+  if (status_line.compare(0, 5, "HTTP/") != 0) {
+    c.Close();
+    return false;
+  }
+  const bool http10 = status_line.compare(0, 8, "HTTP/1.0") == 0;
+  const size_t sp = status_line.find(' ');
+  r.status = sp == std::string::npos ? 0 : std::strtol(status_line.c_str() + sp + 1, nullptr, 10);
+  for (size_t p = eol + 2; p < hend - 2;) {
+    const size_t e = block.find("\r\n", p);
+    const std::string line = block.substr(p, e - p);
+    p = e + 2;
+    const size_t col = line.find(':');
+    if (col == std::string::npos) continue;
+    std::string k = line.substr(0, col);
+    std::transform(k.begin(), k.end(), k.begin(), ::tolower);
+    const size_t b = line.find_first_not_of(" \t", col + 1);
+    r.headers[k] = b == std::string::npos ? "" : line.substr(b);
+  }
+  auto conn = r.headers.find("connection");
+  std::string conn_v = conn == r.headers.end() ? "" : conn->second;
+  std::transform(conn_v.begin(), conn_v.end(), conn_v.begin(), ::tolower);
+  const bool close_after = conn_v == "close" || (http10 && conn_v != "keep-alive");
+  auto cl = r.headers.find("content-length");
+  if ((r.status != 200 && r.status != 206) || cl == r.headers.end() ||
+      r.headers.count("transfer-encoding") != 0) {
+    c.Close();  // errors, redirects, chunked bodies: libcurl re-issues the request
+    return false;
+  }
+  const size_t len = std::strtoull(cl->second.c_str(), nullptr, 10);
+  const size_t into = std::min(len, req.out_cap);
+  const size_t early = std::min(have - hend, len);  // body bytes that came with the headers
+  const size_t early_in = std::min(early, into);
+  std::memcpy(req.out, hdr + hend, early_in);
+  if (early > early_in) r.body.append(hdr + hend + early_in, early - early_in);
+  bool ok = RecvAll(c.fd, req.out + early_in, into - early_in);
+  bool drop = close_after;
+  if (ok && len > std::max(early, into)) {
+    // overflow beyond out_cap (e.g. a server that ignored Range): keep a
+    // little for diagnostics; a large rest is not drained, the socket closes
+    const size_t rest = len - std::max(early, into);
+    if (rest <= (64u << 10)) {
+      const size_t at = r.body.size();
+      r.body.resize(at + rest);
+      ok = RecvAll(c.fd, &r.body[at], rest);
+    } else {
+      drop = true;
+    }
+  }
+  if (!ok || drop) c.Close();
+  if (!ok) return false;
+  r.out_written = into;
+  *resp = std::move(r);
+  return true;
+}
+
 }  // namespace
 
 bool Http::Available() { return Curl().ok(); }
 
+uint64_t Http::NativeGets() { return g_native_gets.load(); }
+uint64_t Http::NativeFallbacks() { return g_native_fallbacks.load(); }
+
 HttpResponse Http::Perform(const HttpRequest& req) {
+  if (req.method == "GET" && req.out != nullptr && req.out_cap != 0 && NativeEnabled()) {
+    HttpResponse r;
+    if (NativeGet(req, &r)) {
+      g_native_gets.fetch_add(1, std::memory_order_relaxed);
+      return r;
+    }
+    g_native_fallbacks.fetch_add(1, std::memory_order_relaxed);
+  }
   CurlApi& c = Curl();
   CHECK(c.ok()) << "HTTP filesystems need libcurl: " << c.error;
   HttpResponse resp;
@@ -230,8 +454,10 @@ size_t RangedReadStream::Read(void* ptr, size_t size) {
       total += k;
       continue;
     }
-    if (size >= block_) {
-      // large read: straight into the caller's memory
+    if (size >= std::min(block_, kDirectRead)) {
+      // large read (a shard reader's piece): one exact ranged GET straight
+      // into the caller's memory -- never a block_-sized read-ahead GET and
+      // a copy out of it
       const size_t k = std::min(size, avail_file);
       FetchRetry(pos_, k, out);
       out += k;

@@ -7,6 +7,9 @@
  * at run time), so libdmlc has no link-time dependency and the remote
  * backends fail with a clear error when libcurl is absent.  Each thread keeps
  * one easy handle, so keep-alive connections are reused across requests.
+ * Plain-http GETs into caller memory (the ranged reads of the shard reader)
+ * bypass libcurl: the body is recv()ed straight into the destination (see
+ * NativeGet in http.cc), libcurl handles everything else.
  *
  * Retry policy follows the reference: reads reconnect up to 50 times with a
  * 100 ms pause (`src/io/s3_filesys.cc:318-342`), writes retry 3 times
@@ -60,15 +63,25 @@ class Http {
    *  sleeping `pause_ms` between attempts
    */
   static HttpResponse PerformRetry(const HttpRequest& req, int retries, int pause_ms = 100);
+  /*!
+   * \brief process-wide counts of GETs into caller memory served by the
+   *  native plain-http receive path (body recv()ed straight into req.out) and
+   *  of those it handed to libcurl (https, non-2xx, chunked, transport error).
+   *  DMLC_HTTP_NATIVE=0 sends everything to libcurl.
+   */
+  static uint64_t NativeGets();
+  static uint64_t NativeFallbacks();
 };
 
 /*!
- * \brief SeekStream over ranged GETs: reads of at least `block` bytes go
- *  straight into the caller's buffer, smaller ones are served from a
- *  read-ahead buffer of `block` bytes.
+ * \brief SeekStream over ranged GETs: reads of at least min(`block`,
+ *  kDirectRead) bytes go straight into the caller's buffer as one exact
+ *  ranged GET, smaller ones are served from a read-ahead buffer of `block`
+ *  bytes.
  */
 class RangedReadStream : public SeekStream {
  public:
+  static constexpr size_t kDirectRead = 256UL << 10;
   /*! \brief fetch [offset, offset+len) into dst; returns bytes written (0 = failure) */
   using Fetcher = std::function<size_t(size_t offset, size_t len, char* dst)>;
   RangedReadStream(size_t file_size, Fetcher fetch, size_t block = 8UL << 20)

@@ -10,6 +10,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 namespace dmlc {
@@ -89,7 +90,15 @@ void ReadPool::Run(const std::vector<std::function<void()>>& jobs) {
 
 // --------------------------------------------------------------- reader
 namespace {
-constexpr size_t kRemotePiece = 8UL << 20;
+// smallest ranged GET of a remote Fill (DMLC_REMOTE_MIN_PIECE_KB overrides)
+size_t RemoteMinPiece() {
+  static const size_t v = [] {
+    const char* e = std::getenv("DMLC_REMOTE_MIN_PIECE_KB");
+    const size_t kb = e != nullptr ? std::strtoull(e, nullptr, 10) : 1024;
+    return std::max<size_t>(kb, 64) << 10;
+  }();
+  return v;
+}
 
 void PreadFull(int fd, char* dst, size_t len, size_t off) {
   while (len != 0) {
@@ -228,12 +237,16 @@ size_t ShardReader::Fill(char* buf, size_t cap) {
       }
     } else {
       // remote filesystem: parallel ranged GETs, one stream per piece (size
-      // known from the listing, so no HEAD per piece).  Pieces of >= 8 MiB
-      // amortise request latency; the pool size bounds connections in flight.
+      // known from the listing, so no HEAD per piece).  One piece per pool
+      // worker, so every connection is busy for the whole Fill (round 3 had
+      // an 8 MiB floor: a 64 MiB slot kept 8 connections busy whatever the
+      // pool size, profiles/r03_remote); the floor bounds request overhead.
       FileSystem* fs = split_->filesystem();
       const URI path = split_->files()[s.file].path;
       const size_t fsize = split_->files()[s.file].size;
-      const size_t piece = std::max(kRemotePiece, (n + pool_->size() - 1) / std::max(1, pool_->size()));
+      const size_t piece =
+          std::max(RemoteMinPiece(),
+                   ((n + pool_->size() - 1) / std::max(1, pool_->size()) + 65535) & ~size_t(65535));
       for (size_t o = 0; o < n; o += piece) {
         const size_t len = std::min(piece, n - o);
         char* dst = buf + pos + o;

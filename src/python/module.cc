@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "../gpu/kernels.h"
+#include "../io/http.h"
 #include "../io/line_split.h"
 #include "../io/recordio_split.h"
 #include "../io/shard_reader.h"
@@ -942,6 +943,15 @@ PYBIND11_MODULE(_dmlc, m) {
       },
       py::arg("uri"), py::arg("part") = 0, py::arg("nparts") = 1, py::arg("type") = "text",
       py::arg("nthread") = 8, py::arg("chunk_bytes") = 64UL << 20);
+  m.def(
+      "http_stats",
+      []() {
+        py::dict d;
+        d["native_gets"] = io::Http::NativeGets();
+        d["native_fallbacks"] = io::Http::NativeFallbacks();
+        return d;
+      },
+      "process-wide counts of ranged GETs received natively / handed to libcurl");
   m.def("fault_configure", &fault::Configure, py::arg("spec"),
         "arm DMLC_FAULT_INJECT-style faults (\"\" disarms); resets pass counters");
   m.def("fault_count", &fault::Count, py::arg("point"));

@@ -297,6 +297,7 @@ class AzureHandler(_Base):
 # --------------------------------------------------------------------------- HTTP
 class PlainHandler(_Base):
     store: Dict[str, bytes] = {}
+    chunked = False  # answer GETs with Transfer-Encoding: chunked bodies
 
     def do_HEAD(self):
         data = self.store.get(self.path)
@@ -306,6 +307,16 @@ class PlainHandler(_Base):
         data = self.store.get(self.path)
         if data is None:
             self._send(404)
+        elif self.chunked:
+            b, e = _range(self.headers.get("Range"), len(data)) or (0, len(data) - 1)
+            body = data[b:e + 1]
+            self.send_response(206)
+            self.send_header("Transfer-Encoding", "chunked")
+            self.end_headers()
+            for i in range(0, len(body), 65536):
+                part = body[i:i + 65536]
+                self.wfile.write(b"%x\r\n" % len(part) + part + b"\r\n")
+            self.wfile.write(b"0\r\n\r\n")
         else:
             self._serve_object(data, self.headers.get("Range"))
 

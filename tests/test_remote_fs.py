@@ -171,6 +171,33 @@ def test_http_ranged_reads():
         srv.shutdown()
 
 
+def test_http_native_receive_and_libcurl_fallback():
+    """Ranged GETs into caller memory are received natively (the body recv()ed
+    straight into the destination, no libcurl buffer); a response the native
+    path does not take (chunked transfer encoding) goes to libcurl and the
+    bytes are the same."""
+    srv = mock_remote.serve(mock_remote.PlainHandler)
+    try:
+        payload = _blob((3 << 20) + 777, seed=4)
+        mock_remote.PlainHandler.store["/files/n.bin"] = payload
+        url = f"http://127.0.0.1:{srv.server_address[1]}/files/n.bin"
+        s0 = _dmlc.http_stats()
+        assert _read_all(url, chunk=1 << 20) == payload
+        s1 = _dmlc.http_stats()
+        if os.environ.get("DMLC_HTTP_NATIVE", "1") != "0":
+            assert s1["native_gets"] - s0["native_gets"] >= 4
+        assert s1["native_fallbacks"] == s0["native_fallbacks"]
+        mock_remote.PlainHandler.chunked = True
+        assert _read_all(url, chunk=1 << 20) == payload
+        s2 = _dmlc.http_stats()
+        assert s2["native_gets"] == s1["native_gets"]
+        if os.environ.get("DMLC_HTTP_NATIVE", "1") != "0":
+            assert s2["native_fallbacks"] - s1["native_fallbacks"] >= 4
+    finally:
+        mock_remote.PlainHandler.chunked = False
+        srv.shutdown()
+
+
 def test_hdfs_fails_loudly_without_libhdfs():
     with pytest.raises(_dmlc.DMLCError, match="libhdfs"):
         io.Stream("hdfs://namenode:8020/x", "r")
