@@ -10,13 +10,34 @@ optional ``value`` float32 [nnz], optional ``field``).
 """
 from __future__ import annotations
 
-from typing import Dict
+from typing import Dict, Optional
 
 import torch
 
 from .. import _dmlc
 
-__all__ = ["spmv", "spmv_t", "hashed_dense", "SpMVFunction", "csr_spmv", "transpose"]
+__all__ = ["spmv", "spmv_t", "hashed_dense", "SpMVFunction", "csr_spmv", "transpose",
+           "release_workspace"]
+
+# persistent transpose scratch per (device, stream), grow-only: a rebuild (a
+# further shard, a refreshed batch) allocates no multi-GB scratch again
+_WORKSPACE: Dict = {}
+
+
+def _workspace(nbytes: int, dev) -> torch.Tensor:
+    key = (dev.index, _stream())
+    ws = _WORKSPACE.get(key)
+    if ws is None or ws.numel() < nbytes:
+        _WORKSPACE.pop(key, None)  # free the smaller one first
+        ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+        _WORKSPACE[key] = ws
+    return ws
+
+
+def release_workspace() -> None:
+    """Free the persistent scratch of :func:`transpose` (it is kept between
+    calls so that later builds allocate only their outputs)."""
+    _WORKSPACE.clear()
 
 
 def _ptr(t) -> int:
@@ -84,7 +105,7 @@ def hashed_dense(csr: Dict, dim: int, seed: int = 0, fp8: bool = True,
     return out
 
 
-def transpose(csr: Dict, num_features: int) -> Dict:
+def transpose(csr: Dict, num_features: int, out: Optional[Dict] = None) -> Dict:
     """The CSR's transpose (CSC / inverted index) on the device, as a
     CSR-shaped dict whose rows are the features: ``offset`` int64
     [num_features + 1], ``index`` int32 row ids (ascending within every
@@ -99,7 +120,12 @@ def transpose(csr: Dict, num_features: int) -> Dict:
     runs ~17x below the contiguous atomic rate when 64 lanes hit 64 different
     rows (MI355X_MICROARCH.md, Global float atomics).  Feature ids must be
     < num_features <= ``_dmlc.csr_transpose_max_features()`` (2^22); an id
-    outside raises."""
+    outside raises.
+
+    The sort's scratch (~10 bytes per entry) is a persistent per-device,
+    per-stream workspace (:func:`release_workspace` frees it).  ``out``: a
+    previous result of the same shape to overwrite instead of allocating
+    the outputs (its ``index`` / ``value`` need at least nnz entries)."""
     _check(csr)
     offset, index, value = csr["offset"], csr["index"], csr.get("value")
     nrows, dev = offset.numel() - 1, index.device
@@ -111,11 +137,19 @@ def transpose(csr: Dict, num_features: int) -> Dict:
     # (one device read for both ends)
     lo, hi = (int(v) for v in off[[0, -1]].tolist()) if nrows > 0 else (0, 0)
     nnz = hi - lo
-    col_ptr = torch.empty(num_features + 1, dtype=torch.int64, device=dev)
-    rows = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
-    vals = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev) if value is not None else None
-    scratch = torch.empty(_dmlc.csr_transpose_scratch_bytes(nnz, num_features), dtype=torch.uint8,
-                          device=dev)
+    if out is not None:
+        col_ptr, rows, vals = out["offset"], out["index"], out.get("value")
+        if (col_ptr.numel() != num_features + 1 or rows.numel() < nnz
+                or (value is not None and (vals is None or vals.numel() < nnz))):
+            raise ValueError("transpose: out= does not fit this CSR")
+        if value is None:
+            vals = None
+    else:
+        col_ptr = torch.empty(num_features + 1, dtype=torch.int64, device=dev)
+        rows = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
+        vals = (torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
+                if value is not None else None)
+    scratch = _workspace(_dmlc.csr_transpose_scratch_bytes(nnz, num_features), dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     _dmlc.csr_transpose(_ptr(offset), nrows, lo, nnz, _ptr(index), _ptr(value), int(num_features),
                         _ptr(col_ptr), _ptr(rows), _ptr(vals), _ptr(scratch), _ptr(err), _stream(),

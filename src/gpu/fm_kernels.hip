@@ -28,6 +28,7 @@
  * F3 k_fm_reduce + F4 k_fm_grads: the partials summed in a fixed order and
  *   turned into dw, dV on the device (no torch reduction over the partials).
  */
+#include <dmlc/logging.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -465,6 +466,284 @@ __global__ __launch_bounds__(256) void k_fm_prep(const float* __restrict__ w,
   q[k] = acc;
 }
 
+/*!
+ * F5.  The whole step over one read of the batch.  Workgroup = W = dim / 128
+ * waves over rows [blockIdx.x * rows_per_block, ...); wave w owns features
+ * [128 w, 128 w + 128) for both halves of the step.  Per 32-row tile, with
+ * the tile's X fragment (F1's and F2's lane layout are the same: lane (col, h)
+ * holds 64 bytes of row col) loaded once:
+ *   P1  the previous tile's G^T X (F2, from s_gt / s_g), then this tile's
+ *       x.[w | V] block products (F1, [w | V] in LDS) and x^2.q;
+ *       the 32 x 18 partial sums go to s_part.            barrier
+ *   P2  16 threads per row sum the W partials of its 18 columns, form y, the
+ *       loss and g, and write G^T = [g, g sx xV] (bf16) and g.   barrier
+ * The next tile's X is loaded one tile ahead (two register buffers).
+ * Loss partials and dbias partials (sum g) per workgroup go to lpart.
+ */
+/*! \brief ds_swizzle in bit mode: lane ^ xor_mask within 32 (no address VGPR) */
+template <int kXor>
+__device__ __forceinline__ float swz_xor(float v) {
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), (kXor << 10) | 0x1F));
+}
+/*! \brief lane (lane & ~15) + kLane of the lane's 16-lane group */
+template <int kLane>
+__device__ __forceinline__ float swz_group(float v) {
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x10 | (kLane << 5)));
+}
+
+template <int W>
+__global__ __launch_bounds__(64 * W) void k_fm_fused(
+    const uint8_t* __restrict__ x, int64_t rows, const __bf16* __restrict__ wt,
+    const float* __restrict__ q, const float* __restrict__ bias, float sx,
+    const float* __restrict__ label, const float* __restrict__ weight, int loss, float inv_n,
+    int64_t rows_per_block, float* __restrict__ y, float* __restrict__ part,
+    float* __restrict__ lpart) {
+  // every shape is compile-time (dim = 128 W), so each LDS access is one base
+  // register + an immediate offset: no per-address registers to keep live
+  constexpr int D = 128 * W;
+  constexpr int kLdw = D + 8;
+  constexpr int P = W + 1;  // odd stride of the partials: conflict-free column writes
+  constexpr int kThreads = 64 * W;
+  __shared__ __attribute__((aligned(16))) __bf16 s_wt[kFmCols * kLdw];  // F1's [17][D + 8]
+  __shared__ __attribute__((aligned(16))) float s_q[D];
+  __shared__ float s_part[32 * 18 * P];                                // [row][column][wave]
+  __shared__ __attribute__((aligned(16))) __bf16 s_gt[32 * 40];        // G^T [column][row]
+  __shared__ __attribute__((aligned(16))) float s_g[32];
+  __shared__ float s_red[2 * W];
+  const int tid = threadIdx.x;
+  const int lane = lane_id();
+  const int h = lane >> 5, col = lane & 31;
+  const int wave = tid / kWave;
+  for (int i = tid; i < kFmCols * D / 8; i += kThreads) {
+    const int c = i / (D / 8), k8 = i % (D / 8);
+    *reinterpret_cast<uint4*>(s_wt + c * kLdw + 8 * k8) =
+        reinterpret_cast<const uint4*>(wt + static_cast<size_t>(c) * D)[k8];
+  }
+  for (int i = tid; i < D / 4; i += kThreads) {
+    reinterpret_cast<float4*>(s_q)[i] = reinterpret_cast<const float4*>(q)[i];
+  }
+  for (int i = tid; i < 32 * 40; i += kThreads) s_gt[i] = static_cast<__bf16>(0.0f);
+  if (tid < 32) s_g[tid] = 0.0f;
+  const int kbase = 128 * wave + 64 * h;
+  // F2's identity B fragments
+  bf16x8 eye[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool one = h == (col >> 4) && s == ((col >> 3) & 1) && j == (col & 7);
+      eye[s][j] = static_cast<__bf16>(one ? 1.0f : 0.0f);
+    }
+  }
+  const float b0 = *bias;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  const int64_t r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
+  const int64_t rlast = r1 > r0 ? r1 - 1 : r0;
+  auto load_x = [&](int64_t t, uint4 (&v)[4]) {
+    const int64_t r = t + col;
+    const bool ok = r < r1;
+    const int64_t rc = r < rlast ? r : rlast;
+    const uint4* p = reinterpret_cast<const uint4*>(x + rc * D + kbase);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint4 u = p[i];
+      v[i] = ok ? u : make_uint4(0, 0, 0, 0);
+    }
+  };
+  // labels / weights of a tile: lane l holds row (l & 31), loaded a tile ahead
+  auto load_lw = [&](int64_t t, float* lab, float* wgt) {
+    const int64_t r = t + col;
+    const int64_t rc = r < rlast ? r : rlast;
+    const float l = label[rc];
+    const float w = weight != nullptr ? weight[rc] : 1.0f;
+    *lab = l;
+    *wgt = w;
+  };
+  f32x16 acc[4] = {};
+  float tacc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  float lsum = 0.0f, gsum = 0.0f;
+  // F2 on one tile's X fragment with the G^T of s_gt / s_g
+  auto backward = [&](const uint4 (&xw)[4]) {
+    bf16x8 ga[2];
+    const uint2* gt_row = reinterpret_cast<const uint2*>(s_gt + col * 40);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint2 lo = gt_row[4 * s + h], hi = gt_row[4 * s + 2 + h];
+      ga[s] = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+    }
+    float gr[16];
+#pragma unroll
+    for (int r4 = 0; r4 < 4; ++r4) {
+      const float4 g4 = *reinterpret_cast<const float4*>(s_g + 8 * r4 + 4 * h);
+      gr[4 * r4 + 0] = g4.x;
+      gr[4 * r4 + 1] = g4.y;
+      gr[4 * r4 + 2] = g4.z;
+      gr[4 * r4 + 3] = g4.w;
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      f32x16 tt = {};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        tt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            fp8x8_bf16(word(xw, 2 * (2 * b + s)), word(xw, 2 * (2 * b + s) + 1)), eye[s], tt, 0, 0,
+            0);
+      }
+      float ta = 0.0f;
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) ta += tt[reg] * tt[reg] * gr[reg];
+      tacc[b] += ta;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 tb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) tb[j] = static_cast<__bf16>(tt[8 * s + j]);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[s], tb, acc[b], 0, 0, 0);
+      }
+      // one feature block's transpose live at a time (else the scheduler
+      // interleaves all four and the kernel spills its accumulators)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  float lab_n = 0.0f, wgt_n = 1.0f;
+  load_lw(r0, &lab_n, &wgt_n);
+  __syncthreads();  // s_wt, s_q, s_gt, s_g
+  // xp: the previous tile's X (its backward runs first), xn: this tile's,
+  // loaded one tile ahead; after the backward xp takes a copy of xn and xn
+  // the next tile's load (in flight for a whole tile)
+  uint4 xp[4], xn[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) xp[i] = make_uint4(0, 0, 0, 0);
+  load_x(r0, xn);
+  for (int64_t t0 = r0; t0 < r1; t0 += 32) {
+    const float lab_t = lab_n, wgt_t = wgt_n;
+    load_lw(t0 + 32, &lab_n, &wgt_n);
+    // ---- P1
+    if (t0 != r0) backward(xp);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xp[i] = xn[i];
+    load_x(t0 + 32, xn);
+    __builtin_amdgcn_sched_barrier(0);
+    const uint4 (&xc)[4] = xp;
+    f32x16 fa = {};
+    f32x2 x2q2 = {0.0f, 0.0f};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t lo = word(xc, 2 * i), hi = word(xc, 2 * i + 1);
+      float f[8];
+      fp8x8(lo, hi, f);
+      const float4 q0 = *reinterpret_cast<const float4*>(s_q + kbase + 8 * i);
+      const float4 q1 = *reinterpret_cast<const float4*>(s_q + kbase + 8 * i + 4);
+      f32x2 sq[4] = {{f[0], f[1]}, {f[2], f[3]}, {f[4], f[5]}, {f[6], f[7]}};
+      const f32x2 qq[4] = {{q0.x, q0.y}, {q0.z, q0.w}, {q1.x, q1.y}, {q1.z, q1.w}};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) x2q2 = __builtin_elementwise_fma(sq[k] * sq[k], qq[k], x2q2);
+      const bf16x8 b = col < kFmCols
+                           ? *reinterpret_cast<const bf16x8*>(s_wt + col * kLdw + kbase + 8 * i)
+                           : bf16x8{};
+      fa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fp8x8_bf16(lo, hi), b, fa, 0, 0, 0);
+    }
+    float x2q = x2q2[0] + x2q2[1];
+    x2q += __shfl_xor(x2q, 32, kWave);
+    if (col < kFmCols) {
+      float* pw = s_part + (4 * h * 18 + col) * P + wave;
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        // accumulator row m = (reg & 3) + 8 (reg >> 2) + 4 h (C/D map)
+        pw[((reg & 3) + 8 * (reg >> 2)) * 18 * P] = fa[reg];
+      }
+    }
+    if (h == 0) s_part[(col * 18 + 17) * P + wave] = x2q;
+    __syncthreads();
+    // ---- P2: 16 threads per row; row rr = tid / 16 (+ 4 W per pass)
+    const int k = tid & 15;
+#pragma unroll
+    for (int pass = 0; pass < 32 / (4 * W); ++pass) {
+      const int rr = (tid >> 4) + pass * 4 * W;
+      const float* p0 = s_part + (rr * 18 + k) * P;
+      float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+      for (int w2 = 0; w2 < W; ++w2) s0 += p0[w2];
+      if (k < 2) {
+#pragma unroll
+        for (int w2 = 0; w2 < W; ++w2) s1 += p0[16 * P + w2];
+      }
+      // lane k: column k (0 = x.w, 1..15 = xV_1..15); lane 0 also column 16
+      // (xV_16), lane 1 column 17 (x^2.q)
+      float sq = (k >= 1 ? s0 * s0 : 0.0f) + (k == 0 ? s1 * s1 : 0.0f);
+      sq += swz_xor<1>(sq);
+      sq += swz_xor<2>(sq);
+      sq += swz_xor<4>(sq);
+      sq += swz_xor<8>(sq);
+      const float lin = swz_group<0>(s0);
+      const float xq = swz_group<1>(s1);
+      const float yv = b0 + sx * lin + 0.5f * sx * sx * (sq - xq);
+      const int64_t row = t0 + rr;
+      const bool valid = row < r1;
+      const float lab = __shfl(lab_t, rr, kWave);
+      const float wg = __shfl(wgt_t, rr, kWave);
+      float l, g;
+      if (loss == kFmSquared) {
+        const float d = yv - lab;
+        l = d * d;
+        g = 2.0f * d;
+      } else {
+        const float e = __expf(-fabsf(yv));
+        l = fmaxf(yv, 0.0f) - yv * lab + log1pf(e);
+        const float sig = yv >= 0.0f ? 1.0f / (1.0f + e) : e / (1.0f + e);
+        g = sig - lab;
+      }
+      g = valid ? g * wg * inv_n : 0.0f;
+      s_gt[k * 40 + rr] = static_cast<__bf16>(k == 0 ? g : g * sx * s0);
+      if (k == 0) {
+        s_gt[16 * 40 + rr] = static_cast<__bf16>(g * sx * s1);
+        s_g[rr] = g;
+        if (valid) {
+          lsum += wg * l;
+          gsum += g;
+          if (y != nullptr) y[row] = yv;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  backward(xp);  // the last tile
+  // ---- partials
+  float* out = part + static_cast<size_t>(blockIdx.x) * (kFmCols + 1) * D;
+  const int fbase = 128 * wave;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int feat = fbase + 64 * (col >> 4) + 16 * b + 8 * ((col >> 3) & 1) + (col & 7);
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int c = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (c < kFmCols) out[static_cast<size_t>(c) * D + feat] = acc[b][reg];
+    }
+    const float tt = tacc[b] + __shfl_xor(tacc[b], 32, kWave);
+    if (h == 0) out[static_cast<size_t>(kFmCols) * D + feat] = tt;
+  }
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    lsum += __shfl_xor(lsum, d, kWave);
+    gsum += __shfl_xor(gsum, d, kWave);
+  }
+  if (lane == 0) {
+    s_red[2 * wave] = lsum;
+    s_red[2 * wave + 1] = gsum;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float a = 0.0f, c = 0.0f;
+#pragma unroll
+    for (int w2 = 0; w2 < W; ++w2) {
+      a += s_red[2 * w2];
+      c += s_red[2 * w2 + 1];
+    }
+    lpart[2 * blockIdx.x] = a;
+    lpart[2 * blockIdx.x + 1] = c;
+  }
+}
+
 }  // namespace
 
 void LaunchFmPrep(const float* w, const float* v, int dim, void* wt_bf16, float* q,
@@ -497,6 +776,23 @@ void LaunchFmForward(const uint8_t* x, int64_t rows, int dim, const void* wt_bf1
   const int grid = static_cast<int>(want < cap ? want : cap);
   hipLaunchKernelGGL(k_fm_fwd, dim3(grid), dim3(kFwdThreads), FmForwardSharedBytes(dim), stream, x,
                      rows, dim, reinterpret_cast<const __bf16*>(wt_bf16), q, bias, sx, y, xv);
+}
+
+
+void LaunchFmFused(const uint8_t* x, int64_t rows, int dim, const void* wt_bf16, const float* q,
+                   const float* bias, float sx, const float* label, const float* weight,
+                   int loss, float inv_n, int nblocks, float* y, float* part, float* lpart,
+                   hipStream_t stream) {
+  if (nblocks == 0) return;
+  const int64_t per = (((rows + nblocks - 1) / nblocks) + 31) / 32 * 32;
+  const int w = dim / 128;
+  auto kernel = w == 8 ? k_fm_fused<8> : w == 4 ? k_fm_fused<4> : w == 2 ? k_fm_fused<2>
+                                                                         : k_fm_fused<1>;
+  CHECK(dim % 128 == 0 && (w == 1 || w == 2 || w == 4 || w == 8))
+      << "fused HashedFM step: dim must be 128, 256, 512 or 1024 (got " << dim << ")";
+  hipLaunchKernelGGL(kernel, dim3(nblocks), dim3(64 * w), 0, stream, x, rows,
+                     reinterpret_cast<const __bf16*>(wt_bf16), q, bias, sx, label, weight, loss,
+                     inv_n, per, y, part, lpart);
 }
 
 void LaunchFmBackward(const uint8_t* x, int64_t rows, int dim, const float* g, const float* xv,

@@ -375,14 +375,32 @@ void LaunchFmForward(const uint8_t* x, int64_t rows, int dim, const void* wt_bf1
  */
 void LaunchFmBackward(const uint8_t* x, int64_t rows, int dim, const float* g, const float* xv,
                       int nblocks, float* part, hipStream_t stream);
-/*! \brief sum the LaunchFmBackward partials (z: [kFmCols + 1][dim] scratch)
- *  and write dw [dim] and dV [dim][kFmRank] (v: [dim][kFmRank] f32) */
 /*! \brief [w | V]^T in bf16 ([kFmCols][dim]) and q = rowsum(V^2) for LaunchFmForward
  *  (w: [dim] f32, v: [dim][kFmRank] f32) */
 void LaunchFmPrep(const float* w, const float* v, int dim, void* wt_bf16, float* q,
                   hipStream_t stream);
+/*! \brief sum the LaunchFmBackward partials (z: [kFmCols + 1][dim] scratch)
+ *  and write dw [dim] and dV [dim][kFmRank] (v: [dim][kFmRank] f32) */
 void LaunchFmReduceGrads(const float* part, int nblocks, int dim, const float* v, float sx,
                          float* z, float* gw, float* gv, hipStream_t stream);
+/*! \brief losses of the fused HashedFM step */
+enum FmLoss : int { kFmLogistic = 0, kFmSquared = 1 };
+/*! \brief largest dim of LaunchFmFused (one wave per 128 features, 8 waves) */
+constexpr int kFmFusedMaxDim = 1024;
+/*!
+ * \brief F5: forward, loss and backward of one HashedFM step in one pass over
+ *  the fp8 batch.  Per 32-row tile: F1's products (split over the
+ *  workgroup's waves by feature block, summed through LDS), y, the loss and
+ *  g = dloss/dy for the tile's labels (mean over `rows`: g is scaled by
+ *  inv_n), then F2's G^T X products from the same registers.  Writes y
+ *  (optional), part[nblocks][18][dim] as LaunchFmBackward, and
+ *  lpart[nblocks][2] = (sum of weighted losses, sum of g) per block.
+ *  dim: multiple of 128, <= kFmFusedMaxDim.  weight may be null.
+ */
+void LaunchFmFused(const uint8_t* x, int64_t rows, int dim, const void* wt_bf16, const float* q,
+                   const float* bias, float sx, const float* label, const float* weight,
+                   int loss, float inv_n, int nblocks, float* y, float* part, float* lpart,
+                   hipStream_t stream);
 
 /*! \brief K10: dst_offset[i] = src_offset[i] - src_base + dst_base for i<=nrows */
 void LaunchOffsetRebase(const uint64_t* src_offset, size_t nrows, uint64_t src_base,

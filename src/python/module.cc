@@ -803,6 +803,25 @@ PYBIND11_MODULE(_dmlc, m) {
       },
       py::arg("part"), py::arg("nblocks"), py::arg("dim"), py::arg("v"), py::arg("sx"),
       py::arg("z"), py::arg("gw"), py::arg("gv"), py::arg("stream"));
+  m.def(
+      "fm_fused",
+      [stream_of](uintptr_t x, int64_t rows, int dim, uintptr_t wt, uintptr_t q, uintptr_t bias,
+                  float sx, uintptr_t label, uintptr_t weight, int loss, float inv_n, int nblocks,
+                  uintptr_t y, uintptr_t part, uintptr_t lpart, uintptr_t stream) {
+        CHECK(dim == 128 || dim == 256 || dim == 512 || dim == 1024)
+            << "fused HashedFM step: dim must be 128, 256, 512 or 1024 (got " << dim << ")";
+        CHECK(loss == gpu::kFmLogistic || loss == gpu::kFmSquared) << "unknown loss " << loss;
+        gpu::LaunchFmFused(reinterpret_cast<const uint8_t*>(x), rows, dim,
+                           reinterpret_cast<const void*>(wt), reinterpret_cast<const float*>(q),
+                           reinterpret_cast<const float*>(bias), sx,
+                           reinterpret_cast<const float*>(label),
+                           reinterpret_cast<const float*>(weight), loss, inv_n, nblocks,
+                           reinterpret_cast<float*>(y), reinterpret_cast<float*>(part),
+                           reinterpret_cast<float*>(lpart), stream_of(stream));
+      },
+      py::arg("x"), py::arg("rows"), py::arg("dim"), py::arg("wt"), py::arg("q"), py::arg("bias"),
+      py::arg("sx"), py::arg("label"), py::arg("weight"), py::arg("loss"), py::arg("inv_n"),
+      py::arg("nblocks"), py::arg("y"), py::arg("part"), py::arg("lpart"), py::arg("stream"));
   m.attr("fm_rank") = gpu::kFmRank;
   m.def("shuffle_parts_order", &InputSplitShuffle::VisitOrder, py::arg("part"), py::arg("nparts"),
         py::arg("num_shuffle_parts"), py::arg("seed"), py::arg("epoch"),

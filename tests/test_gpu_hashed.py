@@ -273,6 +273,83 @@ def test_fm_kernels_match_fp32(dim, rows):
         assert err < 2e-2, err
 
 
+@pytest.mark.parametrize("dim,rows,kind,weighted", [
+    (128, 37, "logistic", False), (256, 1000, "squared", True), (512, 3001, "logistic", True),
+    (1024, 4133, "logistic", False), (1024, 70000, "squared", False)])
+def test_fm_fused_step_matches_two_pass(dim, rows, kind, weighted):
+    """F5 (forward + loss + backward in one pass over the batch) against the
+    two-pass path (F1, torch loss, F2) and the fp32 reference: the same loss
+    and logits (f32 epilogues), gradients within the bf16-G bound of
+    test_fm_kernels_match_fp32."""
+    torch.manual_seed(dim + rows)
+    dev = "cuda"
+    x8 = (torch.randn(rows, dim, device=dev) * 2).to(torch.float8_e4m3fn)
+    x8[:, ::5] = 0
+    scale = 0.5
+    label = (torch.rand(rows, device=dev) > 0.5).float()
+    weight = torch.rand(rows, device=dev) + 0.5 if weighted else None
+    model = HashedFM(dim=dim, rank=16).to(dev)
+    with torch.no_grad():
+        model.w.normal_(0, 0.05)
+        model.v.normal_(0, 0.05)
+        model.bias.fill_(0.1)
+    fused = model.loss(x8, label, scale=scale, loss=kind, weight=weight)
+    assert model.gemm == "hip_mfma_bf16_fused"
+    fused.backward()
+    got = [p.grad.clone() for p in (model.w, model.v, model.bias)]
+    logits = model.last_logits.clone()
+    model.zero_grad()
+    y = model(x8, scale=scale)
+    if kind == "logistic":
+        ref = torch.nn.functional.binary_cross_entropy_with_logits(y, label, weight=weight)
+    else:
+        e = (y - label) ** 2
+        ref = (e * weight).mean() if weighted else e.mean()
+    ref.backward()
+    want = [p.grad.clone() for p in (model.w, model.v, model.bias)]
+    torch.testing.assert_close(logits, y.detach(), rtol=1e-5, atol=1e-5)
+    assert abs(fused.item() - ref.item()) <= 1e-5 * abs(ref.item()) + 1e-6
+    for g, w in zip(got, want):
+        err = (g - w).abs().max().item() / (w.abs().max().item() + 1e-9)
+        assert err < 1e-2, err
+    # and against fp32 autograd of the same model
+    x = x8.float() / scale
+    w32 = model.w.detach().clone().requires_grad_(True)
+    v32 = model.v.detach().clone().requires_grad_(True)
+    b32 = model.bias.detach().clone().requires_grad_(True)
+    y32 = HashedFM.reference(x, w32, v32, b32)
+    if kind == "logistic":
+        l32 = torch.nn.functional.binary_cross_entropy_with_logits(y32, label, weight=weight)
+    else:
+        e = (y32 - label) ** 2
+        l32 = (e * weight).mean() if weighted else e.mean()
+    l32.backward()
+    for g, w in zip(got, (w32.grad, v32.grad, b32.grad)):
+        err = (g - w).abs().max().item() / (w.abs().max().item() + 1e-9)
+        assert err < 2e-2, err
+
+
+def test_fm_fused_step_trains():
+    """A few SGD steps of the fused path lower the loss (the gradient signs
+    and the mean scaling are right end to end)."""
+    torch.manual_seed(0)
+    dev = "cuda"
+    rows, dim = 8192, 256
+    x8 = (torch.randn(rows, dim, device=dev)).to(torch.float8_e4m3fn)
+    truth = torch.randn(dim, device=dev) * 0.3
+    label = ((x8.float() @ truth) > 0).float()
+    model = HashedFM(dim=dim, rank=16).to(dev)
+    opt = torch.optim.SGD(model.parameters(), lr=0.5)
+    losses = []
+    for _ in range(20):
+        opt.zero_grad()
+        loss = model.loss(x8, label)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert losses[-1] < 0.8 * losses[0], losses
+
+
 @pytest.mark.parametrize("fmt", ["libsvm", "libfm"])
 def test_one_pass_hashed_matches_counted(tmp_path, fmt):
     """A replayed pass into a reused batch runs one kernel per chunk (line

@@ -108,6 +108,31 @@ def test_transpose_and_gather_gradient_match(csr_t):
     torch.testing.assert_close(grads["transpose"], grads["atomic"], rtol=1e-4, atol=1e-6)
 
 
+def test_transpose_workspace_is_persistent_and_out_reuses(csr_t):
+    """The sort's scratch is kept between builds (no multi-GB allocation per
+    build); out= overwrites a previous result; both give the same CSC as a
+    fresh build, and release_workspace() frees the scratch."""
+    import torch
+    t, csr = csr_t
+    nfeat = int(csr.max_index) + 1
+    a = ops.transpose(t, nfeat)
+    ws = [w.data_ptr() for w in ops._WORKSPACE.values()]
+    assert ws
+    b = ops.transpose(t, nfeat)
+    assert [w.data_ptr() for w in ops._WORKSPACE.values()] == ws
+    for k in ("offset", "index", "value"):
+        torch.testing.assert_close(a[k], b[k], rtol=0, atol=0)
+    junk = {k: torch.full_like(v, 7) for k, v in a.items()}
+    c = ops.transpose(t, nfeat, out=junk)
+    assert c["index"].data_ptr() == junk["index"].data_ptr()
+    for k in ("offset", "index", "value"):
+        torch.testing.assert_close(a[k], c[k], rtol=0, atol=0)
+    with pytest.raises(ValueError, match="out= does not fit"):
+        ops.transpose(t, nfeat + 1, out=junk)
+    ops.release_workspace()
+    assert not ops._WORKSPACE
+
+
 def test_transpose_of_a_row_slice_and_auto_mode(csr_t):
     """A batch that is a row slice of a larger CSR (offsets not starting at 0,
     full index / value arrays -- examples/train_sparse_logreg.py) transposes to
