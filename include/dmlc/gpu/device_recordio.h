@@ -54,6 +54,12 @@ struct DeviceRecordIOConfig {
    */
   bool one_pass{false};
   /*!
+   * \brief R1c, the chain count (headers only, one read per part) instead of
+   *  R1 (every word): -1 auto (once decoded chunks show >= 128 and <= 4096
+   *  bytes per record on average), 0 never, 1 always (`?chain_count=`)
+   */
+  int chain_count{-1};
+  /*!
    * \brief indexed RecordIO (reference "indexed_recordio" InputSplit): the
    *  index file ("key offset" lines); shards by record count; with shuffle,
    *  every epoch visits the shard's records in the std::mt19937(111 + seed)
@@ -67,8 +73,8 @@ struct DeviceRecordIOConfig {
   double wait_spin_us{50};
   /*!
    * \brief apply `?k=v` overrides: chunk_mb, chunk_bytes, device, zero_copy,
-   *  device_slots, pinned_slots, hbm_cache, replay_chunk_mb, one_pass, index,
-   *  shuffle, seed, wait_spin_us
+   *  device_slots, pinned_slots, hbm_cache, replay_chunk_mb, one_pass,
+   *  chain_count, index, shuffle, seed, wait_spin_us
    */
   void Update(const std::map<std::string, std::string>& args);
 };
@@ -96,6 +102,8 @@ struct DeviceRecordIOStats {
   size_t one_pass_chunks{0};
   /*! \brief one-pass chunks decoded again after growing the output */
   size_t one_pass_reruns{0};
+  /*! \brief chunks counted by following part chains (R1c) */
+  size_t chain_counts{0};
 };
 
 class DeviceRecordIOReader {

@@ -69,6 +69,8 @@ void DeviceRecordIOConfig::Update(const std::map<std::string, std::string>& args
       replay_chunk_bytes = mb(v);
     } else if (k == "one_pass") {
       one_pass = flag(v);
+    } else if (k == "chain_count") {
+      chain_count = (v == "auto" || v == "-1") ? -1 : (flag(v) ? 1 : 0);
     } else if (k == "index") {
       index_uri = v;
     } else if (k == "shuffle") {
@@ -516,8 +518,7 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
       DropPrelaunch();
       tcounts_.Reserve(TileScratchWords(tiles) * sizeof(uint64_t));
       tflags_.Reserve(TileScratchWords(tiles) * sizeof(uint32_t));
-      LaunchRecordIOTileCount(p.words, nwords, tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(),
-                              st);
+      LaunchCount(p.words, nwords, tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(), st);
       LaunchTileScanRaw(tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(), tiles,
                         meta_.get<ChunkMeta>(), hmap_.get<ChunkMeta>(), st);
     }
@@ -545,8 +546,12 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
       off = out_off_.get<uint64_t>();
       dat = out_data_.get<uint8_t>();
     }
+    // the fill's guards: writes inside the output, tile totals equal to the count's
+    const RecordIOCaps caps{dmeta,
+                            (resident ? res_off_.bytes() : out_off_.bytes()) / sizeof(uint64_t) - 1,
+                            resident ? res_data_.bytes() : out_data_.bytes()};
     LaunchRecordIOTileFill(p.words, nwords, tcounts_.get<uint64_t>(), off, rec_base, dat, byte_base,
-                           partials_.get<MetaPartial>(), st);
+                           partials_.get<MetaPartial>(), st, nullptr, &caps);
     LaunchTileFinish(partials_.get<MetaPartial>(), tiles, dmeta, hm, off, rec_base, byte_base, st);
     if (resident) PrelaunchCount();
     const ChunkMeta done = WaitMeta();
@@ -581,14 +586,33 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
     const size_t tiles = RecordIOTiles(nwords);
     tcounts_next_.Reserve(TileScratchWords(tiles) * sizeof(uint64_t));
     tflags_next_.Reserve(TileScratchWords(tiles) * sizeof(uint32_t));
-    LaunchRecordIOTileCount(nx.words, nwords, tcounts_next_.get<uint64_t>(),
-                            tflags_next_.get<uint32_t>(), count_.get());
+    LaunchCount(nx.words, nwords, tcounts_next_.get<uint64_t>(), tflags_next_.get<uint32_t>(),
+                count_.get());
     LaunchTileScanRaw(tcounts_next_.get<uint64_t>(), tflags_next_.get<uint32_t>(), tiles,
                       meta_next_.get<ChunkMeta>(), hmap_next_.get<ChunkMeta>(), count_.get());
     pre_done_.Record(count_.get());
     pre_.valid = true;
     pre_.words = nx.words;
     pre_.bytes = nx.bytes;
+  }
+
+  /*!
+   * \brief R1 or, for chunks of large enough records, R1c (headers only):
+   *  auto decides from the records decoded so far (the first chunk: R1)
+   */
+  void LaunchCount(const uint32_t* words, size_t nwords, uint64_t* counts, uint32_t* flags,
+                   hipStream_t st) {
+    bool chain = cfg_.chain_count == 1;
+    if (cfg_.chain_count < 0 && stats_.records != 0) {
+      const size_t per = stats_.bytes / stats_.records;
+      chain = per >= 128 && per <= 4096;
+    }
+    if (chain) {
+      LaunchRecordIOTileCountChain(words, nwords, counts, flags, st);
+      stats_.chain_counts += 1;
+    } else {
+      LaunchRecordIOTileCount(words, nwords, counts, flags, st);
+    }
   }
 
   /*! \brief retire a prelaunched count nobody adopts (its flag re-armed) */

@@ -307,10 +307,30 @@ struct RecordIOOnePass {
   uint64_t rec_cap;            // offset slots - 1
   uint64_t byte_cap;           // data bytes
 };
+/*!
+ * \brief counted fill's guards: writes past (rec_cap offset slots, byte_cap
+ *  data bytes) are dropped, and each tile checks that its parts end at the
+ *  next tile's prefix (the last one: meta's totals); either miss is
+ *  kRecErrBadPart (a count that disagrees with the fill's header view)
+ */
+struct RecordIOCaps {
+  ChunkMeta* meta;
+  uint64_t rec_cap;
+  uint64_t byte_cap;
+};
 size_t LaunchRecordIOTileFill(const uint32_t* words, size_t nwords, const uint64_t* tile_prefix,
                               uint64_t* offset, uint64_t rec_base, uint8_t* data,
                               uint64_t byte_base, MetaPartial* partials, hipStream_t stream,
-                              const RecordIOOnePass* one_pass = nullptr);
+                              const RecordIOOnePass* one_pass = nullptr,
+                              const RecordIOCaps* caps = nullptr);
+/*!
+ * \brief R1c: LaunchRecordIOTileCount's per-tile counts by following part
+ *  chains (one 8-byte read per part after each tile's first-header search):
+ *  the same counts on a well-formed chunk for ~2 % of its reads at 512-byte
+ *  records; latency-bound, for chunks of parts >= ~128 bytes
+ */
+void LaunchRecordIOTileCountChain(const uint32_t* words, size_t nwords, uint64_t* tile_counts,
+                                  uint32_t* tile_flags, hipStream_t stream);
 /*!
  * \brief R3: gather nrec whole records (src + src_off[k], len[k] bytes, 4-byte
  *  multiples) to dst + dst_off[k]

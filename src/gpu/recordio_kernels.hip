@@ -163,6 +163,68 @@ __global__ __launch_bounds__(kThreads) void k_rec_tile_count(const uint32_t* __r
   }
 }
 
+/*!
+ * \brief R1c: the same (heads << 32 | bytes) per tile as R1 from the part
+ *  headers alone.  Lane per tile: the first aligned magic at or after the
+ *  tile start is a part header (the writer escapes aligned magics inside
+ *  payloads), and each header gives the next (h + 2 + ceil(len / 4) words),
+ *  so a tile costs its first-header search plus one 8-byte read per part
+ *  instead of reading every word: 512-byte records read ~2 % of the chunk.
+ *  Latency-bound (one dependent read per part), so the host takes it for
+ *  parts of >= 128 bytes on average.  A chain that does not land on a magic
+ *  word is an error (R1 would count a different set of headers); the fill
+ *  checks its own tile totals against the prefix, so an R1c / R2 mismatch is
+ *  an error too, never a misplaced write.
+ */
+__global__ __launch_bounds__(kThreads) void k_rec_tile_count_chain(const uint32_t* __restrict__ w,
+                                                                   size_t n, size_t ntiles,
+                                                                   uint64_t* __restrict__ counts,
+                                                                   uint32_t* __restrict__ flags) {
+  const size_t tile = static_cast<size_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (tile >= ntiles) return;
+  const size_t base = tile * kTileWords;
+  const size_t end = base + kTileWords < n ? base + kTileWords : n;
+  // the first header: 16 words (4 loads in flight) per step
+  size_t h = end;
+  for (size_t i = base; i < end && h == end; i += 16) {
+    uint4 q[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[k] = load_quad(w, n, i + 4 * k);
+#pragma unroll
+    for (int k = 3; k >= 0; --k) {
+      const uint32_t m = header_bits(q[k], i + 4 * k, n);
+      if (m != 0) h = i + 4 * k + static_cast<uint32_t>(__ffs(m) - 1);
+    }
+    if (h > end) h = end;
+  }
+  uint32_t heads = 0, bytes = 0, err = 0;
+  // a chunk starts at a record head
+  if (tile == 0 && n != 0 && h != 0) err |= kRecErrBadPart;
+  while (h < end) {  // h + 1 < n: a header (search) or checked below
+    const uint32_t magic = w[h], lrec = w[h + 1];
+    if (magic != kMagic) {
+      err |= kRecErrBadPart;
+      break;
+    }
+    const uint32_t cf = cflag_of(lrec), len = len_of(lrec);
+    if (tile == 0 && h == 0 && cf > 1) err |= kRecErrBadPart;
+    heads += cf <= 1 ? 1u : 0u;
+    bytes += len + (cf >= 2 ? 4u : 0u);
+    if (cf > 3) err |= kRecErrBadPart;
+    const size_t q = h + 2 + (static_cast<size_t>(len) + 3) / 4;
+    if (q > n) {
+      err |= kRecErrTruncated;
+      break;
+    }
+    // a successor inside the tile must be a full header (R1 counts no
+    // header in the chunk's last word; the fill flags that chain)
+    if (q < end && q + 1 >= n) break;
+    h = q;
+  }
+  counts[tile] = (static_cast<uint64_t>(heads) << 32) | bytes;
+  flags[tile] = err;
+}
+
 /*! \brief copy len payload bytes of words src to byte address dst (one lane) */
 __device__ __forceinline__ void lane_copy(const uint32_t* __restrict__ src, uint32_t len,
                                           uint8_t* __restrict__ dst) {
@@ -317,9 +379,9 @@ __global__ __launch_bounds__(kThreads) void k_rec_tile_fill(const uint32_t* __re
           err |= (ends_record == next_continues || next > 3) ? kRecErrBadPart : 0u;
         }
       }
-      // one pass writes into the capacity it was given (counted: sized exactly)
-      const bool fits = !kOnePass || (rec_base + r < op.rec_cap &&
-                                      byte_base + p + len + 4 <= op.byte_cap);
+      // writes stay inside the capacity given (one pass: overflow -> grow ->
+      // rerun; counted: sized exactly, so a miss is a count / fill mismatch)
+      const bool fits = rec_base + r < op.rec_cap && byte_base + p + len + 4 <= op.byte_cap;
       over |= !fits;
       if (cf <= 1) {
         if (fits) offset[rec_base + r] = byte_base + p;
@@ -395,6 +457,18 @@ __global__ __launch_bounds__(kThreads) void k_rec_tile_fill(const uint32_t* __re
       }
     }
   }
+  if constexpr (!kOnePass) {
+    // the tile's own parts must end where the count said the next tile
+    // starts (R1c follows chains; R2 sees every aligned magic)
+    if (op.meta != nullptr && lane == 0) {
+      const uint64_t want = tile + 1 < ntiles ? prefix[tile + 1]
+                                              : ((static_cast<uint64_t>(op.meta->nrows) << 32) |
+                                                 op.meta->nnz);
+      if (((rec << 32) | pos) != want) err |= kRecErrBadPart;
+    }
+    if (over) err |= kRecErrBadPart;
+    over = false;
+  }
   err = wave_or(err | (over ? kFlagOverflow : 0u));
   if (lane == 0) {
     MetaPartial mp;
@@ -449,10 +523,18 @@ void LaunchRecordIOTileCount(const uint32_t* words, size_t nwords, uint64_t* til
                      stream, words, nwords, tiles, tile_counts, tile_flags);
 }
 
+void LaunchRecordIOTileCountChain(const uint32_t* words, size_t nwords, uint64_t* tile_counts,
+                                  uint32_t* tile_flags, hipStream_t stream) {
+  const size_t tiles = RecordIOTiles(nwords);
+  if (tiles == 0) return;
+  hipLaunchKernelGGL(k_rec_tile_count_chain, dim3((tiles + kThreads - 1) / kThreads),
+                     dim3(kThreads), 0, stream, words, nwords, tiles, tile_counts, tile_flags);
+}
+
 size_t LaunchRecordIOTileFill(const uint32_t* words, size_t nwords, const uint64_t* tile_prefix,
                               uint64_t* offset, uint64_t rec_base, uint8_t* data,
                               uint64_t byte_base, MetaPartial* partials, hipStream_t stream,
-                              const RecordIOOnePass* one_pass) {
+                              const RecordIOOnePass* one_pass, const RecordIOCaps* caps) {
   const size_t tiles = RecordIOTiles(nwords);
   if (tiles == 0) return 0;
   const size_t groups = (tiles + kWaves - 1) / kWaves;
@@ -460,7 +542,12 @@ size_t LaunchRecordIOTileFill(const uint32_t* words, size_t nwords, const uint64
     const char* v = std::getenv("DMLC_REC_EXP");
     return v != nullptr ? static_cast<uint32_t>(std::atoi(v)) : 0u;
   }();
-  RecPass op{nullptr, nullptr, 0ull, nullptr, 0ull, 0ull, exp};
+  RecPass op{nullptr, nullptr, 0ull, nullptr, ~0ull, ~0ull, exp};
+  if (caps != nullptr) {
+    op.meta = caps->meta;
+    op.rec_cap = caps->rec_cap;
+    op.byte_cap = caps->byte_cap;
+  }
   if (one_pass != nullptr) {
     op = RecPass{one_pass->status, one_pass->ticket, one_pass->ticket0, one_pass->meta,
                  one_pass->rec_cap, one_pass->byte_cap, exp};

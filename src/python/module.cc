@@ -631,6 +631,7 @@ class PyDeviceRecordIO {
     d["replayed_chunks"] = s.replayed_chunks;
     d["one_pass_chunks"] = s.one_pass_chunks;
     d["one_pass_reruns"] = s.one_pass_reruns;
+    d["chain_counts"] = s.chain_counts;
     return d;
   }
   uintptr_t Stream() const { return reinterpret_cast<uintptr_t>(reader_->stream()); }

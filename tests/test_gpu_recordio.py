@@ -262,3 +262,60 @@ def test_gpu_recordio_one_pass_replay(tmp_path, replay_mb):
             assert got == recs, (one, e)
         outs[one] = r.stats()
     assert outs[1]["one_pass_chunks"] > 0 and outs[0]["one_pass_chunks"] == 0
+
+
+@pytest.mark.parametrize("max_len", [700, 20000])
+@pytest.mark.parametrize("chunk_kb", [4, 64, 1024])
+def test_gpu_recordio_chain_count_equals_cpu(tmp_path, max_len, chunk_kb):
+    """R1c (counts from part headers alone, chain_count=1) decodes every
+    shard exactly like the CPU reader: multi-part records, escaped magic
+    words, empty / tiny records, records longer than a tile (tiles without a
+    header)."""
+    p = tmp_path / "h.rec"
+    recs = _records(1500, 19, max_len=max_len)
+    _write(p, recs)
+    for nparts in (1, 3):
+        got = []
+        for part in range(nparts):
+            r = io.GPURecordIO(str(p), part, nparts, chunk_bytes=chunk_kb * 1024, chain_count=1)
+            r.read_all()
+            mine = io.split_records(*r.resident_to_host())
+            assert mine == _cpu(p, part, nparts)
+            assert r.stats()["chain_counts"] > 0
+            got += mine
+        assert got == recs
+
+
+def test_gpu_recordio_chain_count_auto_on_replay(tmp_path):
+    """chain_count auto: the first chunk uses R1, later ones (records of
+    >= 128 B on average) R1c, including the prelaunched replay counts"""
+    p = tmp_path / "a.rec"
+    rng = random.Random(3)
+    recs = [bytes(rng.getrandbits(8) for _ in range(rng.randint(200, 900))) for _ in range(3000)]
+    _write(p, recs)
+    r = io.GPURecordIO(str(p), 0, 1, chunk_bytes=64 * 1024, hbm_cache=1, replay_chunk_mb=0.2)
+    for e in range(3):
+        if e:
+            r.before_first()
+        r.read_all()
+        assert io.split_records(*r.resident_to_host()) == recs, e
+    assert r.stats()["chain_counts"] > 0
+
+
+def test_gpu_recordio_chain_count_rejects_unescaped_header(tmp_path):
+    """A payload holding an unescaped part header that ends exactly where the
+    payload ends (a writer that skipped the escaping): the chain count and
+    the fill see different headers, and the tile check turns that into an
+    error instead of a silently different record list."""
+    p = tmp_path / "u.rec"
+    recs = [b"a" * 24, b"x" * 64, b"b" * 20]
+    _write(p, recs)
+    raw = bytearray(open(p, "rb").read())
+    pos = raw.find(b"x" * 64)
+    assert pos > 0 and pos % 4 == 0
+    raw[pos:pos + 4] = MAGIC
+    raw[pos + 4:pos + 8] = (56).to_bytes(4, "little")  # a whole record of 56 bytes
+    open(p, "wb").write(bytes(raw))
+    r = io.GPURecordIO(str(p), zero_copy=0, chain_count=1)
+    with pytest.raises(Exception, match="malformed record"):
+        r.read_all()
