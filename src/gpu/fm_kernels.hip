@@ -472,12 +472,15 @@ __global__ __launch_bounds__(256) void k_fm_prep(const float* __restrict__ w,
  * [128 w, 128 w + 128) for both halves of the step.  Per 32-row tile, with
  * the tile's X fragment (F1's and F2's lane layout are the same: lane (col, h)
  * holds 64 bytes of row col) loaded once:
- *   P1  the previous tile's G^T X (F2, from s_gt / s_g), then this tile's
- *       x.[w | V] block products (F1, [w | V] in LDS) and x^2.q;
- *       the 32 x 18 partial sums go to s_part.            barrier
+ *   P1  G^T X of the tile two back (F2, its X fragment kept in LDS, G^T
+ *       from s_gt / s_g), then this tile's x.[w | V] block products (F1,
+ *       [w | V] in LDS) and x^2.q; the 32 x 18 partial sums go to s_part.
+ *                                                          barrier
  *   P2  16 threads per row sum the W partials of its 18 columns, form y, the
- *       loss and g, and write G^T = [g, g sx xV] (bf16) and g.   barrier
- * The next tile's X is loaded one tile ahead (two register buffers).
+ *       loss and g, and write G^T = [g, g sx xV] (bf16) and g.
+ * Partials, G^T and X are double-buffered by tile parity, so one barrier per
+ * tile orders everything (the loop's comment); the next tile's X is loaded
+ * one tile ahead.
  * Loss partials and dbias partials (sum g) per workgroup go to lpart.
  */
 /*! \brief ds_swizzle in bit mode: lane ^ xor_mask within 32 (no address VGPR) */
@@ -506,9 +509,13 @@ __global__ __launch_bounds__(64 * W) void k_fm_fused(
   constexpr int kThreads = 64 * W;
   __shared__ __attribute__((aligned(16))) __bf16 s_wt[kFmCols * kLdw];  // F1's [17][D + 8]
   __shared__ __attribute__((aligned(16))) float s_q[D];
-  __shared__ float s_part[32 * 18 * P];                                // [row][column][wave]
-  __shared__ __attribute__((aligned(16))) __bf16 s_gt[32 * 40];        // G^T [column][row]
-  __shared__ __attribute__((aligned(16))) float s_g[32];
+  // double-buffered by tile parity: one barrier per tile (see the loop)
+  __shared__ float s_part[2][32 * 18 * P];                             // [row][column][wave]
+  __shared__ __attribute__((aligned(16))) __bf16 s_gt[2][32 * 40];     // G^T [column][row]
+  __shared__ __attribute__((aligned(16))) float s_g[2][32];
+  // each wave's X fragment of a tile, kept two tiles for its backward
+  // (lane-interleaved: conflict-free 16-byte accesses)
+  __shared__ uint4 s_x[2][W * 4 * 64];
   __shared__ float s_red[2 * W];
   const int tid = threadIdx.x;
   const int lane = lane_id();
@@ -522,8 +529,8 @@ __global__ __launch_bounds__(64 * W) void k_fm_fused(
   for (int i = tid; i < D / 4; i += kThreads) {
     reinterpret_cast<float4*>(s_q)[i] = reinterpret_cast<const float4*>(q)[i];
   }
-  for (int i = tid; i < 32 * 40; i += kThreads) s_gt[i] = static_cast<__bf16>(0.0f);
-  if (tid < 32) s_g[tid] = 0.0f;
+  for (int i = tid; i < 2 * 32 * 40; i += kThreads) (&s_gt[0][0])[i] = static_cast<__bf16>(0.0f);
+  if (tid < 64) (&s_g[0][0])[tid] = 0.0f;
   const int kbase = 128 * wave + 64 * h;
   // F2's identity B fragments
   bf16x8 eye[2];
@@ -562,10 +569,13 @@ __global__ __launch_bounds__(64 * W) void k_fm_fused(
   f32x16 acc[4] = {};
   float tacc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   float lsum = 0.0f, gsum = 0.0f;
-  // F2 on one tile's X fragment with the G^T of s_gt / s_g
-  auto backward = [&](const uint4 (&xw)[4]) {
+  // F2 on the tile of parity bf: its X fragment from s_x, G^T from s_gt / s_g
+  auto backward = [&](int bf) {
+    uint4 xw[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xw[i] = s_x[bf][(wave * 4 + i) * 64 + lane];
     bf16x8 ga[2];
-    const uint2* gt_row = reinterpret_cast<const uint2*>(s_gt + col * 40);
+    const uint2* gt_row = reinterpret_cast<const uint2*>(s_gt[bf] + col * 40);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const uint2 lo = gt_row[4 * s + h], hi = gt_row[4 * s + 2 + h];
@@ -574,7 +584,7 @@ __global__ __launch_bounds__(64 * W) void k_fm_fused(
     float gr[16];
 #pragma unroll
     for (int r4 = 0; r4 < 4; ++r4) {
-      const float4 g4 = *reinterpret_cast<const float4*>(s_g + 8 * r4 + 4 * h);
+      const float4 g4 = *reinterpret_cast<const float4*>(s_g[bf] + 8 * r4 + 4 * h);
       gr[4 * r4 + 0] = g4.x;
       gr[4 * r4 + 1] = g4.y;
       gr[4 * r4 + 2] = g4.z;
@@ -608,23 +618,30 @@ __global__ __launch_bounds__(64 * W) void k_fm_fused(
   float lab_n = 0.0f, wgt_n = 1.0f;
   load_lw(r0, &lab_n, &wgt_n);
   __syncthreads();  // s_wt, s_q, s_gt, s_g
-  // xp: the previous tile's X (its backward runs first), xn: this tile's,
-  // loaded one tile ahead; after the backward xp takes a copy of xn and xn
-  // the next tile's load (in flight for a whole tile)
-  uint4 xp[4], xn[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) xp[i] = make_uint4(0, 0, 0, 0);
+  // Tile j (parity bf = j & 1):
+  //   backward of tile j - 2 (its X in s_x[bf], its G^T in s_gt[bf]: written
+  //   by P2(j - 2), which every thread finished before barrier j - 1);
+  //   X(j) from registers into s_x[bf], X(j + 1) in flight; forward of j ->
+  //   s_part[bf];  barrier j;  P2(j): s_part[bf] -> s_gt[bf], s_g[bf].
+  // s_part[bf] is next written by forward(j + 2), after barrier j + 1, which
+  // every thread reaches only after its P2(j): one barrier per tile, and a
+  // wave done with P2 runs on into the next tile's products
+  uint4 xn[4];
   load_x(r0, xn);
-  for (int64_t t0 = r0; t0 < r1; t0 += 32) {
+  int j = 0;
+  for (int64_t t0 = r0; t0 < r1; t0 += 32, ++j) {
+    const int bf = j & 1;
     const float lab_t = lab_n, wgt_t = wgt_n;
     load_lw(t0 + 32, &lab_n, &wgt_n);
-    // ---- P1
-    if (t0 != r0) backward(xp);
+    if (j >= 2) backward(bf);
+    uint4 xc[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) xp[i] = xn[i];
+    for (int i = 0; i < 4; ++i) {
+      xc[i] = xn[i];
+      s_x[bf][(wave * 4 + i) * 64 + lane] = xc[i];
+    }
     load_x(t0 + 32, xn);
     __builtin_amdgcn_sched_barrier(0);
-    const uint4 (&xc)[4] = xp;
     f32x16 fa = {};
     f32x2 x2q2 = {0.0f, 0.0f};
 #pragma unroll
@@ -645,22 +662,23 @@ __global__ __launch_bounds__(64 * W) void k_fm_fused(
     }
     float x2q = x2q2[0] + x2q2[1];
     x2q += __shfl_xor(x2q, 32, kWave);
+    float* const sp = s_part[bf];
     if (col < kFmCols) {
-      float* pw = s_part + (4 * h * 18 + col) * P + wave;
+      float* pw = sp + (4 * h * 18 + col) * P + wave;
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
         // accumulator row m = (reg & 3) + 8 (reg >> 2) + 4 h (C/D map)
         pw[((reg & 3) + 8 * (reg >> 2)) * 18 * P] = fa[reg];
       }
     }
-    if (h == 0) s_part[(col * 18 + 17) * P + wave] = x2q;
+    if (h == 0) sp[(col * 18 + 17) * P + wave] = x2q;
     __syncthreads();
     // ---- P2: 16 threads per row; row rr = tid / 16 (+ 4 W per pass)
     const int k = tid & 15;
 #pragma unroll
     for (int pass = 0; pass < 32 / (4 * W); ++pass) {
       const int rr = (tid >> 4) + pass * 4 * W;
-      const float* p0 = s_part + (rr * 18 + k) * P;
+      const float* p0 = sp + (rr * 18 + k) * P;
       float s0 = 0.0f, s1 = 0.0f;
 #pragma unroll
       for (int w2 = 0; w2 < W; ++w2) s0 += p0[w2];
@@ -694,10 +712,10 @@ __global__ __launch_bounds__(64 * W) void k_fm_fused(
         g = sig - lab;
       }
       g = valid ? g * wg * inv_n : 0.0f;
-      s_gt[k * 40 + rr] = static_cast<__bf16>(k == 0 ? g : g * sx * s0);
+      s_gt[bf][k * 40 + rr] = static_cast<__bf16>(k == 0 ? g : g * sx * s0);
       if (k == 0) {
-        s_gt[16 * 40 + rr] = static_cast<__bf16>(g * sx * s1);
-        s_g[rr] = g;
+        s_gt[bf][16 * 40 + rr] = static_cast<__bf16>(g * sx * s1);
+        s_g[bf][rr] = g;
         if (valid) {
           lsum += wg * l;
           gsum += g;
@@ -705,9 +723,11 @@ __global__ __launch_bounds__(64 * W) void k_fm_fused(
         }
       }
     }
-    __syncthreads();
   }
-  backward(xp);  // the last tile
+  // the last two tiles' backward, after every thread's last P2
+  __syncthreads();
+  if (j >= 2) backward(j & 1);
+  if (j >= 1) backward((j - 1) & 1);
   // ---- partials
   float* out = part + static_cast<size_t>(blockIdx.x) * (kFmCols + 1) * D;
   const int fbase = 128 * wave;

@@ -381,7 +381,9 @@ __global__ __launch_bounds__(kThreads) void k_rec_tile_fill(const uint32_t* __re
       }
       // writes stay inside the capacity given (one pass: overflow -> grow ->
       // rerun; counted: sized exactly, so a miss is a count / fill mismatch)
-      const bool fits = rec_base + r < op.rec_cap && byte_base + p + len + 4 <= op.byte_cap;
+      // (a head takes an offset slot, a continuation its re-inserted magic)
+      const bool fits = (cf >= 2 || rec_base + r < op.rec_cap) &&
+                        byte_base + p + len + (cf >= 2 ? 4u : 0u) <= op.byte_cap;
       over |= !fits;
       if (cf <= 1) {
         if (fits) offset[rec_base + r] = byte_base + p;

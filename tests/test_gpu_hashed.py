@@ -307,8 +307,11 @@ def test_fm_fused_step_matches_two_pass(dim, rows, kind, weighted):
         ref = (e * weight).mean() if weighted else e.mean()
     ref.backward()
     want = [p.grad.clone() for p in (model.w, model.v, model.bias)]
-    torch.testing.assert_close(logits, y.detach(), rtol=1e-5, atol=1e-5)
-    assert abs(fused.item() - ref.item()) <= 1e-5 * abs(ref.item()) + 1e-6
+    # the same f32 epilogue over partial sums added in another order (the
+    # fused step splits K over the workgroup's waves): the F1 test's bound
+    tol = y.detach().abs().max().item()
+    assert (logits - y.detach()).abs().max().item() <= 1e-4 * tol + 1e-5
+    assert abs(fused.item() - ref.item()) <= 1e-4 * abs(ref.item()) + 1e-6
     for g, w in zip(got, want):
         err = (g - w).abs().max().item() / (w.abs().max().item() + 1e-9)
         assert err < 1e-2, err
