@@ -403,107 +403,89 @@ __global__ __launch_bounds__(kThreads) void k_csv_tile_fill(const uint8_t* __res
     wave_sync();
     // pricing experiments (DMLC_CSV_EXP, 0 in production): 4 skips the rounds
     const uint32_t nlist = (exp & 4u) ? 0u : (nf < kListCap ? nf : kListCap);
-    // pair rounds: lane takes fields r0 + lane and r0 + 64 + lane, both fast
-    // decodes branch-free in the same blocks (independent chains interleave);
-    // the rare generic fields and the stores follow
-    const uint8_t* rb = reinterpret_cast<const uint8_t*>(ring);
-    struct Fast {
-      uint32_t row_t, col, ent, off;
-      float v;
-      bool last, generic;
-    };
-    auto fast = [&](uint32_t k, bool ok) {
-      const uint2 en = ok ? list[k] : make_uint2(0u, 0u);  // (a lane past the list: offset 0)
-      Fast f;
-      f.off = en.x & 0xFFFFu;
-      f.row_t = en.x >> 16;
-      f.col = en.y & 0xFFFFu;
-      f.ent = en.y >> 16;
-      const uint32_t off = f.off;
-      // one LDS read per field: the 16 bytes from the field start serve the
-      // number, its first byte and (usually) the byte after its delimiter
-      const uint4 g16 = tok::ext16(ring, off);
-      const uint32_t c0 = g16.x & 0xFFu;
-      // a field ended by a delimiter is still the row's last one when the
-      // line ends right after that delimiter (no empty trailing field)
-      const uint64_t glo = (static_cast<uint64_t>(g16.y) << 32) | g16.x;
-      const uint64_t ghi = (static_cast<uint64_t>(g16.w) << 32) | g16.z;
-      auto eol_at = [=](uint32_t o) {
-        const uint32_t i = o - off;  // a 64-bit shift, not an indexed array (scratch)
-        const uint64_t h = i < 8u ? glo : ghi;
-        const uint32_t c = i < 16u ? static_cast<uint32_t>((h >> (8u * (i & 7u))) & 0xFFu) : rb[o];
-        return c == '\n' || c == '\r' || c == 0;
-      };
-      if (exp & 1u) {  // pricing: no number decode
-        f.v = static_cast<float>(c0);
-        f.last = eol_at(off + 8);
-        f.generic = false;
-        return f;
-      }
-      const bool empty = c0 == delim || c0 == '\n' || c0 == '\r' || c0 == 0;
-      const tok::Num x = tok::parse_num_g(g16, off);
-      const bool t_eol = x.term == '\n' || x.term == '\r' || x.term == 0;
-      const uint32_t probe = empty ? off + 1 : x.end + 1;
-      const bool after_eol = eol_at(probe);
-      f.v = empty ? 0.0f : x.fval;
-      f.last = empty ? (c0 != delim || after_eol) : (t_eol || after_eol);
-      f.generic = !empty && !(x.ok_float && (x.term == delim || t_eol));
-      return f;
-    };
-    auto generic = [&](Fast* f) {
-      const size_t gpos = tile0 + s * kStep + (f->off - slot * 16u);
-      const GenericField g = generic_field(reinterpret_cast<const char*>(text) + gpos,
-                                           reinterpret_cast<const char*>(text) + n,
-                                           static_cast<char>(delim));
-      f->v = g.v;
-      f->last = g.last;
-    };
-    auto store = [&](const Fast& f) {
-      const uint32_t col = f.col;
-      const float v = f.v;
-      const uint64_t row = R + f.row_t;
-      const uint64_t e = C + f.ent;
-      if (exp & 2u) {  // pricing: no stores (a value sink the compiler keeps)
-        mx = __float_as_uint(v) == 0x7FC00001u ? mx + 1 : mx;
-      } else if (row >= out.row_limit) {
-        irregular = true;
-      } else {
-        if (static_cast<int>(col) == cfg.label_col) {
-          out.label[row] = v;
-        } else if (static_cast<int>(col) == cfg.weight_col) {
-          out.weight[row] = v;
-        } else if (e < out.nnz_limit) {
-          uint32_t idx = col;
-          idx -= (cfg.label_col >= 0 && col > static_cast<uint32_t>(cfg.label_col)) ? 1u : 0u;
-          idx -= (cfg.weight_col >= 0 && col > static_cast<uint32_t>(cfg.weight_col)) ? 1u : 0u;
-          out.index[e] = static_cast<IndexType>(idx);
-          out.value[e] = v;
-          mx = idx > mx ? idx : mx;
-          any_value = true;
+    for (uint32_t r0 = 0; r0 < nlist; r0 += kWave) {
+      const uint32_t k = r0 + lane;
+      if (k < nlist) {
+        const uint2 en = list[k];
+        const uint32_t off = en.x & 0xFFFFu;
+        const uint32_t row_t = en.x >> 16;
+        const uint32_t col = en.y & 0xFFFFu;
+        const uint32_t ent = en.y >> 16;
+        const uint8_t* rb = reinterpret_cast<const uint8_t*>(ring);
+        // one LDS read per field: the 16 bytes from the field start serve the
+        // number, its first byte and (usually) the byte after its delimiter
+        const uint4 g16 = tok::ext16(ring, off);
+        const uint32_t c0 = g16.x & 0xFFu;
+        // a field ended by a delimiter is still the row's last one when the
+        // line ends right after that delimiter (no empty trailing field)
+        const uint64_t glo = (static_cast<uint64_t>(g16.y) << 32) | g16.x;
+        const uint64_t ghi = (static_cast<uint64_t>(g16.w) << 32) | g16.z;
+        auto eol_at = [=](uint32_t o) {
+          const uint32_t i = o - off;  // a 64-bit shift, not an indexed array (scratch)
+          const uint64_t h = i < 8u ? glo : ghi;
+          const uint32_t c = i < 16u ? static_cast<uint32_t>((h >> (8u * (i & 7u))) & 0xFFu) : rb[o];
+          return c == '\n' || c == '\r' || c == 0;
+        };
+        float v;
+        bool last;
+        if (exp & 1u) {  // pricing: no number decode
+          v = static_cast<float>(c0);
+          last = eol_at(off + 8);
+        } else if (c0 == delim || c0 == '\n' || c0 == '\r' || c0 == 0) {
+          v = 0.0f;  // empty field
+          last = c0 != delim || eol_at(off + 1);
         } else {
+          const tok::Num x = tok::parse_num_g(g16, off);
+          const bool t_eol = x.term == '\n' || x.term == '\r' || x.term == 0;
+          // (the window is dead before the generic call below)
+          const bool last_fast = t_eol || eol_at(x.end + 1);
+          if (x.ok_float && (x.term == delim || t_eol)) {
+            v = x.fval;
+            last = last_fast;
+          } else {
+            const size_t gpos = tile0 + s * kStep + (off - slot * 16u);
+            const GenericField g = generic_field(reinterpret_cast<const char*>(text) + gpos,
+                                                 reinterpret_cast<const char*>(text) + n,
+                                                 static_cast<char>(delim));
+            v = g.v;
+            last = g.last;
+          }
+        }
+        const uint64_t row = R + row_t;
+        const uint64_t e = C + ent;
+        if (exp & 2u) {  // pricing: no stores (a value sink the compiler keeps)
+          mx = __float_as_uint(v) == 0x7FC00001u ? mx + 1 : mx;
+        } else if (row >= out.row_limit) {
           irregular = true;
-        }
-        if (col == 0) {
-          out.offset[row] = e;
-          if (cfg.label_col < 0) out.label[row] = 0.0f;
-        }
-        if (f.last) {
-          // a short row: no label / weight field
-          if (cfg.label_col >= 0 && col < static_cast<uint32_t>(cfg.label_col)) out.label[row] = 0.0f;
-          if (cfg.has_weight && (cfg.weight_col < 0 || col < static_cast<uint32_t>(cfg.weight_col))) {
-            out.weight[row] = 1.0f;
+        } else {
+          if (static_cast<int>(col) == cfg.label_col) {
+            out.label[row] = v;
+          } else if (static_cast<int>(col) == cfg.weight_col) {
+            out.weight[row] = v;
+          } else if (e < out.nnz_limit) {
+            uint32_t idx = col;
+            idx -= (cfg.label_col >= 0 && col > static_cast<uint32_t>(cfg.label_col)) ? 1u : 0u;
+            idx -= (cfg.weight_col >= 0 && col > static_cast<uint32_t>(cfg.weight_col)) ? 1u : 0u;
+            out.index[e] = static_cast<IndexType>(idx);
+            out.value[e] = v;
+            mx = idx > mx ? idx : mx;
+            any_value = true;
+          } else {
+            irregular = true;
+          }
+          if (col == 0) {
+            out.offset[row] = e;
+            if (cfg.label_col < 0) out.label[row] = 0.0f;
+          }
+          if (last) {
+            // a short row: no label / weight field
+            if (cfg.label_col >= 0 && col < static_cast<uint32_t>(cfg.label_col)) out.label[row] = 0.0f;
+            if (cfg.has_weight && (cfg.weight_col < 0 || col < static_cast<uint32_t>(cfg.weight_col))) {
+              out.weight[row] = 1.0f;
+            }
           }
         }
       }
-    };
-    for (uint32_t r0 = 0; r0 < nlist; r0 += 2 * kWave) {
-      const uint32_t k0 = r0 + lane, k1 = k0 + kWave;
-      const bool ok0 = k0 < nlist, ok1 = k1 < nlist;
-      Fast f0 = fast(k0, ok0), f1 = fast(k1, ok1);
-      if (ok0 && f0.generic) generic(&f0);
-      if (ok1 && f1.generic) generic(&f1);
-      if (ok0) store(f0);
-      if (ok1) store(f1);
     }
     if (w.done) break;
     wave_sync();  // the next prefetch overwrites this step's slot

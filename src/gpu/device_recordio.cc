@@ -165,7 +165,9 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
   }
 
   void BeforeFirst() override {
-    Drain();
+    // a replay keeps the next epoch's prelaunched first count (the arena
+    // stays); anything else retires it
+    Drain(/*keep_prelaunch=*/cache_complete_ && indexed_ == nullptr);
     exhausted_ = false;
     resident_rows_ = resident_bytes_ = 0;
     if (indexed_ != nullptr) {
@@ -208,6 +210,7 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
     while (NextPiece(&p)) Decode(p, true);
     merge_replay_ = false;
     compute_.Synchronize();
+    PrelaunchNextEpoch();
     resident_.size = resident_rows_;
     resident_.bytes = resident_bytes_;
     resident_.offset = res_off_.get<uint64_t>();
@@ -412,10 +415,10 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
     return true;
   }
 
-  void Drain() {
+  void Drain(bool keep_prelaunch = false) {
     copy_.Synchronize();
     compute_.Synchronize();
-    DropPrelaunch();
+    if (!keep_prelaunch) DropPrelaunch();
     for (auto& p : ready_) {
       if (p.host != nullptr) iter_.Recycle(&p.host);
     }
@@ -579,21 +582,50 @@ class DeviceRecordIOImpl : public DeviceRecordIOReader {
    *  used by the piece before the current one, which is complete.
    */
   void PrelaunchCount() {
-    if (!replay_ || indexed_ != nullptr || pre_.valid || ready_.empty()) return;
+    if (!replay_ || indexed_ != nullptr || pre_.valid) return;
+    if (ready_.empty()) {
+      // the epoch's last piece is decoding: count the next epoch's first
+      // one beside it (ReadAll over the cache replays the same pieces)
+      if (exhausted_ && merge_replay_) PrelaunchNextEpoch();
+      return;
+    }
     const Piece& nx = ready_.front();
     if (nx.slot >= 0 || nx.host != nullptr) return;  // not an arena-resident piece
-    const size_t nwords = nx.bytes / 4;
+    PrelaunchFor(nx.words, nx.bytes);
+  }
+
+  /*!
+   * \brief at the end of a ReadAll over the HBM cache: the next epoch's
+   *  first piece (the same merge from the first cached chunk) is counted
+   *  now, on count_, so the next ReadAll's first fill does not wait for its
+   *  count.  A next pass that starts with another piece (Next() batches)
+   *  drops it unused.
+   */
+  void PrelaunchNextEpoch() {
+    if (!replay_ || indexed_ != nullptr || pre_.valid || cached_.empty()) return;
+    size_t off = cached_[0].first, n = cached_[0].second;
+    for (size_t i = 1; i < cached_.size() && cached_[i].first == off + n &&
+                       n + cached_[i].second <= cfg_.replay_chunk_bytes;
+         ++i) {
+      n += cached_[i].second;
+    }
+    if (n == 0) return;
+    PrelaunchFor(reinterpret_cast<const uint32_t*>(arena_.get<char>() + off), n);
+  }
+
+  void PrelaunchFor(const uint32_t* words, size_t bytes) {
+    const size_t nwords = bytes / 4;
     const size_t tiles = RecordIOTiles(nwords);
     tcounts_next_.Reserve(TileScratchWords(tiles) * sizeof(uint64_t));
     tflags_next_.Reserve(TileScratchWords(tiles) * sizeof(uint32_t));
-    LaunchCount(nx.words, nwords, tcounts_next_.get<uint64_t>(), tflags_next_.get<uint32_t>(),
+    LaunchCount(words, nwords, tcounts_next_.get<uint64_t>(), tflags_next_.get<uint32_t>(),
                 count_.get());
     LaunchTileScanRaw(tcounts_next_.get<uint64_t>(), tflags_next_.get<uint32_t>(), tiles,
                       meta_next_.get<ChunkMeta>(), hmap_next_.get<ChunkMeta>(), count_.get());
     pre_done_.Record(count_.get());
     pre_.valid = true;
-    pre_.words = nx.words;
-    pre_.bytes = nx.bytes;
+    pre_.words = words;
+    pre_.bytes = bytes;
   }
 
   /*!
