@@ -22,15 +22,18 @@
  *      binary search over 64 row ends -- then leaves in bucket runs, so one
  *      store instruction touches a few lines / pages instead of 64 (the
  *      direct scatter was bound by partial lines and TLB misses: 16 ms at
- *      400 M entries).  Writes (low key u16, row u32, value f32).
+ *      400 M entries).  Writes the low key (u16) and the (row, value) pair
+ *      (8 bytes; the row alone without values).  The next sub-tile's
+ *      entries load while this one is sorted.
  *   T4a k_lowkey_hist  one workgroup per (bucket, segment) of the bucket: LDS
  *      histogram of the L low keys -> H[bucket][segment][L].
  *   T4b k_lowkey_scan  one workgroup per bucket: column totals over segments,
  *      exclusive scan over the bucket's columns -> col_ptr, and per-segment
  *      starting cursors (in place in H).
  *   T4c k_lowkey_scatter  one wave per (bucket, segment): cursors in LDS,
- *      the segment's entries in order, ranks by ballots over the low-key
- *      bits -> row / value at their final CSC position.
+ *      the segment's entries in order (8 groups of 64 loaded a batch ahead),
+ *      ranks by ballots over the low-key bits -> row / value at their final
+ *      CSC position.
  *  Traffic for 400 M entries: keys read 3x + (row, value) written and read
  *  once through the intermediate arrays, ~17 GB, no global atomics.
  */
@@ -108,11 +111,26 @@ __global__ __launch_bounds__(kThreads) void k_bucket_hist(const IndexType* __res
   const uint64_t e0 = static_cast<uint64_t>(blockIdx.x) * kBlockElems;
   const uint64_t e1 = e0 + kBlockElems < nnz ? e0 + kBlockElems : nnz;
   bool bad = false;
-  for (uint64_t e = e0 + threadIdx.x; e < e1; e += kThreads) {
-    const IndexType c = index[e];
+  auto add = [&](IndexType c) {
     bad |= static_cast<uint64_t>(c) >= num_features;
     atomicAdd(&hist[column(c, num_features) >> kLowBits], 1u);
+  };
+  uint64_t e = e0 + threadIdx.x;
+  if (sizeof(IndexType) == 4 && (reinterpret_cast<uintptr_t>(index + e0) & 15u) == 0) {
+    // four ids per 16-byte load (kBlockElems is a multiple of 4): a quarter
+    // of the load instructions of the one-id-per-lane walk
+    const uint64_t n4 = (e1 - e0) / 4;
+    const uint4* q = reinterpret_cast<const uint4*>(index + e0);
+    for (uint64_t i = threadIdx.x; i < n4; i += kThreads) {
+      const uint4 v = q[i];
+      add(static_cast<IndexType>(v.x));
+      add(static_cast<IndexType>(v.y));
+      add(static_cast<IndexType>(v.z));
+      add(static_cast<IndexType>(v.w));
+    }
+    e = e0 + n4 * 4 + threadIdx.x;
   }
+  for (; e < e1; e += kThreads) add(index[e]);
   if (__any(bad) && dev::lane_id() == 0) atomicOr(error, 1u);
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < nbuckets; b += kThreads) {
@@ -134,7 +152,7 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
     const IndexType* __restrict__ index, const float* __restrict__ value, uint64_t nnz,
     uint64_t num_features, uint32_t nbuckets, int bucket_bits, const uint64_t* __restrict__ G,
     size_t nblocks, const uint32_t* __restrict__ chunk_row,
-    uint16_t* __restrict__ t_key, uint32_t* __restrict__ t_row, float* __restrict__ t_val) {
+    uint16_t* __restrict__ t_key, uint32_t* __restrict__ t_row, uint2* __restrict__ t_rv) {
   // the sub-tile, sorted by (bucket, position) in LDS before it leaves
   __shared__ uint32_t s_col[kSubElems];
   __shared__ uint32_t s_row[kSubElems];
@@ -156,9 +174,27 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
   __syncthreads();
   const uint64_t blk0 = static_cast<uint64_t>(blockIdx.x) * kBlockElems;
   const uint64_t blk1 = blk0 + kBlockElems < nnz ? blk0 + kBlockElems : nnz;
+  // the next sub-tile's entries (and its chunk's first row) are loaded while
+  // this one is sorted: a wave waits for memory once per block, not once per
+  // sub-tile (round 4: 71 % of the cycles waiting)
+  IndexType ci[kPerLane];
+  float vi[kPerLane];
+  uint32_t nwb = 0;
+  auto fetch = [&](uint64_t s0n) {
+    const uint64_t c0n = s0n + static_cast<uint64_t>(w) * kChunk;
+    const uint64_t c1n = c0n + kChunk < blk1 ? c0n + kChunk : blk1;
+#pragma unroll
+    for (int i = 0; i < kPerLane; ++i) {
+      const uint64_t e = c0n + static_cast<uint64_t>(i) * dev::kWave + lane;
+      ci[i] = e < c1n ? index[e] : IndexType(0);
+      vi[i] = (e < c1n && value != nullptr) ? value[e] : 0.0f;
+    }
+    nwb = c0n < c1n ? chunk_row[c0n / kChunk] : 0u;
+  };
+  fetch(blk0);
   for (uint64_t s0 = blk0; s0 < blk1; s0 += kSubElems) {
     const uint32_t nsub = static_cast<uint32_t>(blk1 - s0 < kSubElems ? blk1 - s0 : kSubElems);
-    // ---- this wave's chunk: kPerLane coalesced groups, all loads in flight
+    // ---- this wave's chunk: kPerLane coalesced groups (loaded a sub-tile ago)
     const uint64_t c0 = s0 + static_cast<uint64_t>(w) * kChunk;
     const uint64_t c1 = c0 + kChunk < blk1 ? c0 + kChunk : blk1;
     uint32_t col[kPerLane];
@@ -166,16 +202,17 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
 #pragma unroll
     for (int i = 0; i < kPerLane; ++i) {
       const uint64_t e = c0 + static_cast<uint64_t>(i) * dev::kWave + lane;
-      col[i] = e < c1 ? column(index[e], num_features) : 0u;
-      v[i] = (e < c1 && value != nullptr) ? value[e] : 0.0f;
+      col[i] = e < c1 ? column(ci[i], num_features) : 0u;
+      v[i] = vi[i];
     }
     // the row window of the rank phase below, in flight during count + scan
-    uint32_t wbase = c0 < c1 ? chunk_row[c0 / kChunk] : 0u;
+    uint32_t wbase = nwb;
     auto window = [&](uint32_t wb) {
       const size_t ri = static_cast<size_t>(wb) + 1 + lane;
       return ri <= nrows ? offset[ri] - base : ~0ull;
     };
     uint64_t wend = window(wbase);
+    if (s0 + kSubElems < blk1) fetch(s0 + kSubElems);
     // ---- count per bucket: lanes of a group with equal buckets from ballots
     // over the bucket bits (no atomics); each group's rank among its equal
     // buckets and their number stay in registers for the rank phase
@@ -282,8 +319,13 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
       const uint32_t b = c >> kLowBits;
       const uint64_t p = static_cast<uint64_t>(gcur[b]) + (j - lstart[b]);
       t_key[p] = static_cast<uint16_t>(c & (kLow - 1u));
-      t_row[p] = s_row[j];
-      if (value != nullptr) t_val[p] = s_val[j];
+      // (row, value) as one 8-byte pair: two store streams per sub-tile
+      // instead of three, one load per entry in T4c
+      if (value != nullptr) {
+        t_rv[p] = make_uint2(s_row[j], __float_as_uint(s_val[j]));
+      } else {
+        t_row[p] = s_row[j];
+      }
     }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < nbuckets; b += kThreads) {
@@ -340,28 +382,45 @@ __global__ __launch_bounds__(kThreads) void k_lowkey_hist(const uint16_t* __rest
   for (uint32_t c = threadIdx.x; c < kLow; c += kThreads) out[c] = hist[c];
 }
 
-/*! \brief per bucket: column totals over segments -> col_ptr; per-segment cursors in H */
+/*! \brief per bucket: column totals over segments -> col_ptr; per-segment
+ *  cursors in H.  Thread t walks columns t, t + 256, ... so every H access of
+ *  a segment row is one coalesced 1 KiB line run (round 4 walked 16
+ *  consecutive columns per thread: 64-byte-strided lanes, 354 us); the scan
+ *  over the bucket's columns runs on the LDS copy of the totals. */
 __global__ __launch_bounds__(kThreads) void k_lowkey_scan(uint32_t* __restrict__ H,
                                                           const uint64_t* __restrict__ bstart,
                                                           uint64_t num_features,
                                                           uint64_t* __restrict__ col_ptr) {
+  __shared__ uint32_t s_tot[kLow];  // column totals, then exclusive column starts (u32)
   __shared__ uint64_t swave[kWaves];
-  constexpr uint32_t kPer = kLow / kThreads;  // columns per thread, contiguous
+  constexpr uint32_t kPer = kLow / kThreads;  // columns per thread
   const uint32_t b = blockIdx.x;
   uint32_t* Hb = H + static_cast<size_t>(b) * kSegments * kLow;
+  // 1. per column: the segments' counts -> offsets inside the column (in H)
+  //    and the column total (coalesced: consecutive threads, consecutive columns)
+#pragma unroll 4
+  for (uint32_t i = 0; i < kPer; ++i) {
+    const uint32_t c = i * kThreads + threadIdx.x;
+    uint32_t h[kSegments];
+#pragma unroll
+    for (int s = 0; s < kSegments; ++s) h[s] = Hb[static_cast<size_t>(s) * kLow + c];
+    uint32_t acc = 0;
+#pragma unroll
+    for (int s = 0; s < kSegments; ++s) {
+      Hb[static_cast<size_t>(s) * kLow + c] = acc;
+      acc += h[s];
+    }
+    s_tot[c] = acc;
+  }
+  __syncthreads();
+  // 2. exclusive scan of the 4096 totals: thread t owns columns 16 t .. 16 t + 15
   const uint32_t c0 = threadIdx.x * kPer;
   uint32_t tot[kPer];
   uint64_t sum = 0;
 #pragma unroll
   for (uint32_t i = 0; i < kPer; ++i) {
-    uint32_t acc = 0;
-    for (int s = 0; s < kSegments; ++s) {
-      const uint32_t h = Hb[static_cast<size_t>(s) * kLow + c0 + i];
-      Hb[static_cast<size_t>(s) * kLow + c0 + i] = acc;  // offset inside the column
-      acc += h;
-    }
-    tot[i] = acc;
-    sum += acc;
+    tot[i] = s_tot[c0 + i];
+    sum += tot[i];
   }
   uint64_t wtot;
   const uint64_t wx = dev::wave_excl_scan(sum, &wtot);
@@ -371,22 +430,30 @@ __global__ __launch_bounds__(kThreads) void k_lowkey_scan(uint32_t* __restrict__
   uint64_t before = wx;
   for (int q = 0; q < w; ++q) before += swave[q];
   const uint64_t base = bstart[b];
-  uint64_t x = base + before;
+  uint64_t x = before;  // relative to the bucket base (< 2^32: nnz < 2^32)
 #pragma unroll
   for (uint32_t i = 0; i < kPer; ++i) {
     const uint64_t c = static_cast<uint64_t>(b) * kLow + c0 + i;
-    if (c < num_features) col_ptr[c] = x;
-    // cursors become absolute CSC positions (u32 offsets from the bucket base)
-    for (int s = 0; s < kSegments; ++s) {
-      Hb[static_cast<size_t>(s) * kLow + c0 + i] += static_cast<uint32_t>(x - base);
-    }
+    if (c < num_features) col_ptr[c] = base + x;
+    s_tot[c0 + i] = static_cast<uint32_t>(x);
     x += tot[i];
+  }
+  __syncthreads();
+  // 3. cursors become absolute CSC positions (u32 offsets from the bucket base)
+#pragma unroll 4
+  for (uint32_t i = 0; i < kPer; ++i) {
+    const uint32_t c = i * kThreads + threadIdx.x;
+    const uint32_t start = s_tot[c];
+#pragma unroll
+    for (int s = 0; s < kSegments; ++s) Hb[static_cast<size_t>(s) * kLow + c] += start;
   }
 }
 
+constexpr int kScatterDepth = 8;  // T4c: 64-entry groups per batch (loads a batch ahead)
+
 __global__ __launch_bounds__(dev::kWave) void k_lowkey_scatter(
     const uint16_t* __restrict__ t_key, const uint32_t* __restrict__ t_row,
-    const float* __restrict__ t_val, const uint64_t* __restrict__ bstart,
+    const uint2* __restrict__ t_rv, const uint64_t* __restrict__ bstart,
     const uint32_t* __restrict__ H, uint32_t* __restrict__ row_out, float* __restrict__ val_out) {
   __shared__ uint32_t cur[kLow];
   const uint32_t b = blockIdx.x / kSegments;
@@ -398,34 +465,71 @@ __global__ __launch_bounds__(dev::kWave) void k_lowkey_scatter(
   uint64_t e0, e1;
   segment(bstart, b, s, &e0, &e1);
   const uint64_t base = bstart[b];
-  // the next group's loads are in flight while this group is ranked / stored
-  auto load = [&](uint64_t e, uint32_t* k, uint32_t* row, float* v) {
-    const bool ok = e < e1;
-    *k = ok ? t_key[e] : 0u;
-    *row = ok ? t_row[e] : 0u;
-    *v = (ok && val_out != nullptr) ? t_val[e] : 0.0f;
+  const uint64_t below = lanes_below();
+  // The segment walks in batches of kScatterDepth groups of 64 consecutive
+  // entries (group j of a batch: entries + 64 j + lane, so groups stay in
+  // entry order).  A batch's loads are issued a whole batch ahead, into the
+  // other register set: a wave keeps 8 x 64 entries in flight instead of one
+  // group (the round-4 kernel waited out the memory latency every 64
+  // entries, at 10 waves per CU -- 72 % of its cycles waiting)
+  struct Batch {
+    uint32_t k[kScatterDepth], r[kScatterDepth];
+    float v[kScatterDepth];
   };
-  uint32_t nk, nrow;
-  float nv;
-  load(e0 + lane, &nk, &nrow, &nv);
-  for (uint64_t g = e0; g < e1; g += dev::kWave) {
-    const uint64_t e = g + lane;
-    const bool valid = e < e1;
-    const uint32_t k = nk, row = nrow;
-    const float v = nv;
-    load(e + dev::kWave, &nk, &nrow, &nv);
-    const uint64_t m = match_lanes(k, kLowBits, valid);
-    const uint32_t rank = static_cast<uint32_t>(__popcll(m & lanes_below()));
-    const uint32_t n = static_cast<uint32_t>(__popcll(m));
-    const uint32_t before = valid ? cur[k] : 0u;
-    dev::wave_sync();
-    if (valid) {
-      const uint64_t pos = base + before + rank;
-      row_out[pos] = row;
-      if (val_out != nullptr) val_out[pos] = v;
-      if (rank + 1 == n) cur[k] = before + n;
+  auto load = [&](uint64_t at, Batch* x) {
+#pragma unroll
+    for (int j = 0; j < kScatterDepth; ++j) {
+      const uint64_t e = at + static_cast<uint64_t>(j) * dev::kWave + lane;
+      const bool ok = e < e1;
+      x->k[j] = ok ? t_key[e] : 0u;
+      if (val_out != nullptr) {
+        const uint2 rv = ok ? t_rv[e] : make_uint2(0u, 0u);
+        x->r[j] = rv.x;
+        x->v[j] = __uint_as_float(rv.y);
+      } else {
+        x->r[j] = ok ? t_row[e] : 0u;
+        x->v[j] = 0.0f;
+      }
     }
-    dev::wave_sync();
+  };
+  auto process = [&](uint64_t at, const Batch& x) {
+    // the ranks need no LDS: every group's ballots first, then the cursor
+    // updates group by group (the only dependent chain)
+    uint32_t rk[kScatterDepth];
+#pragma unroll
+    for (int j = 0; j < kScatterDepth; ++j) {
+      const bool valid = at + static_cast<uint64_t>(j) * dev::kWave + lane < e1;
+      const uint64_t m = match_lanes(x.k[j], kLowBits, valid);
+      rk[j] = static_cast<uint32_t>(__popcll(m & below)) |
+              (static_cast<uint32_t>(__popcll(m)) << 8);
+    }
+#pragma unroll
+    for (int j = 0; j < kScatterDepth; ++j) {
+      const uint64_t g = at + static_cast<uint64_t>(j) * dev::kWave;
+      if (g >= e1) break;  // wave-uniform
+      const bool valid = g + lane < e1;
+      const uint32_t k = x.k[j];
+      const uint32_t rank = rk[j] & 0xFFu, n = rk[j] >> 8;
+      const uint32_t before = valid ? cur[k] : 0u;
+      dev::wave_sync();
+      if (valid) {
+        const uint64_t pos = base + before + rank;
+        row_out[pos] = x.r[j];
+        if (val_out != nullptr) val_out[pos] = x.v[j];
+        if (rank + 1 == n) cur[k] = before + n;
+      }
+      dev::wave_sync();
+    }
+  };
+  constexpr uint64_t kBatch = static_cast<uint64_t>(kScatterDepth) * dev::kWave;
+  Batch A, B;
+  load(e0, &A);
+  for (uint64_t at = e0; at < e1; at += 2 * kBatch) {
+    load(at + kBatch, &B);
+    process(at, A);
+    if (at + kBatch >= e1) break;
+    load(at + 2 * kBatch, &A);
+    process(at + kBatch, B);
   }
 }
 
@@ -504,8 +608,9 @@ void LaunchCSRTranspose(const uint64_t* offset, size_t nrows, uint64_t base, uin
   const TransposePlan p = Plan(nnz, num_features);
   char* sc = static_cast<char*>(scratch);
   uint16_t* t_key = reinterpret_cast<uint16_t*>(sc + p.key_off);
+  // rows alone, or (row, value) pairs over the row + value regions (>= 8 nnz bytes)
   uint32_t* t_row = reinterpret_cast<uint32_t*>(sc + p.row_off);
-  float* t_val = value != nullptr ? reinterpret_cast<float*>(sc + p.val_off) : nullptr;
+  uint2* t_rv = reinterpret_cast<uint2*>(sc + p.row_off);
   uint64_t* G = reinterpret_cast<uint64_t*>(sc + p.g_off);
   uint64_t* partials = reinterpret_cast<uint64_t*>(sc + p.partials_off);
   uint32_t* H = reinterpret_cast<uint32_t*>(sc + p.h_off);
@@ -528,7 +633,7 @@ void LaunchCSRTranspose(const uint64_t* offset, size_t nrows, uint64_t base, uin
                        0, stream, offset, nrows, base, nnz, chunk_row);
     hipLaunchKernelGGL(k_bucket_scatter<IndexType>, dim3(p.nblocks), dim3(kThreads), 0, stream,
                        offset, nrows, base, idx, val, nnz, num_features, p.nbuckets,
-                       p.bucket_bits, G, p.nblocks, chunk_row, t_key, t_row, t_val);
+                       p.bucket_bits, G, p.nblocks, chunk_row, t_key, t_row, t_rv);
   }
   // T4
   const unsigned nseg = p.nbuckets * kSegments;
@@ -536,7 +641,7 @@ void LaunchCSRTranspose(const uint64_t* offset, size_t nrows, uint64_t base, uin
   hipLaunchKernelGGL(k_lowkey_scan, dim3(p.nbuckets), dim3(kThreads), 0, stream, H, bstart,
                      num_features, col_ptr);
   hipLaunchKernelGGL(k_lowkey_scatter, dim3(nseg), dim3(dev::kWave), 0, stream, t_key, t_row,
-                     t_val, bstart, H, row_out, val_out);
+                     t_rv, bstart, H, row_out, val_out);
   hipLaunchKernelGGL(k_transpose_close, dim3(1), dim3(1), 0, stream, bstart, p.nbuckets,
                      num_features, col_ptr);
 }
