@@ -8,6 +8,9 @@
 #   nodecode       alone, DMLC_FILL_EXP=2: the fill without its token decode
 #   neither        alone, DMLC_FILL_EXP=3
 #   onepass        --one-pass: look-back fill, no count kernel
+# The DMLC_FILL_EXP experiments exist only in a pricing build of the kernels
+# (production kernels hold no experiment flags):
+#   make clean && make HIPFLAGS_EXTRA=-DDMLC_FILL_PRICING all
 # usage (through gpurun): bash scripts/fill_pricing.sh OUTDIR [format]
 set -o pipefail
 root="${GRAFT_REPO_ROOT:-$(pwd)}"

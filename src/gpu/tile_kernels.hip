@@ -1023,6 +1023,18 @@ struct FillPass {
                                 // 1 no CSR stores, 2 no token decode (outputs are wrong)
 };
 
+/*! \brief the pricing experiments of a DMLC_FILL_PRICING build (scripts/
+ *  fill_pricing.sh); a constant 0 otherwise, so production kernels hold no
+ *  experiment flags in scalar registers (the fill is at the SGPR limit) */
+__device__ __forceinline__ uint32_t fill_exp(const FillPass& op) {
+#ifdef DMLC_FILL_PRICING
+  return op.exp;
+#else
+  (void)op;
+  return 0u;
+#endif
+}
+
 template <TextFormat F, typename IndexType, bool kOnePass>
 __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
     const uint8_t* __restrict__ text, size_t n, size_t ntiles, const uint64_t* __restrict__ prefix,
@@ -1281,7 +1293,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
       } else {
         irregular |= active & !room_ok;
       }
-      if (op.exp & 1u) {
+      if (fill_exp(op) & 1u) {
         // pricing: everything but the stores (the values stay live)
         sink ^= (active ? __float_as_uint(t.f0) ^ t.u0 ^ t.u1 : 0u) + static_cast<uint32_t>(i);
         return;
@@ -1344,7 +1356,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
         ta.u0_hi = ta.u1_hi = tb.u0_hi = tb.u1_hi = 0;
         ta.u1 = tb.u1 = 0;
         bool oka, okb;
-        if (op.exp & 2u) {  // pricing: no decode
+        if (fill_exp(op) & 2u) {  // pricing: no decode
           ta.u0 = ea;
           tb.u0 = eb;
           ta.f0 = ta.f1 = tb.f0 = tb.f1 = 1.0f;
