@@ -178,12 +178,17 @@ __global__ __launch_bounds__(kThreads) void k_rec_tile_count(const uint32_t* __r
  */
 __global__ __launch_bounds__(kThreads) void k_rec_tile_count_chain(const uint32_t* __restrict__ w,
                                                                    size_t n, size_t ntiles,
+                                                                   uint32_t per_lane,
                                                                    uint64_t* __restrict__ counts,
                                                                    uint32_t* __restrict__ flags) {
-  const size_t tile = static_cast<size_t>(blockIdx.x) * kThreads + threadIdx.x;
-  if (tile >= ntiles) return;
-  const size_t base = tile * kTileWords;
-  const size_t end = base + kTileWords < n ? base + kTileWords : n;
+  // a lane takes per_lane consecutive tiles: one first-header search, then the
+  // chain runs on across its tiles (the header after a tile's last part is
+  // the next tile's first), counts binned by the tile of each header
+  const size_t t0 = (static_cast<size_t>(blockIdx.x) * kThreads + threadIdx.x) * per_lane;
+  if (t0 >= ntiles) return;
+  const size_t t1 = t0 + per_lane < ntiles ? t0 + per_lane : ntiles;
+  const size_t base = t0 * kTileWords;
+  const size_t end = t1 * kTileWords < n ? t1 * kTileWords : n;
   // the first header: 16 words (4 loads in flight) per step
   size_t h = end;
   for (size_t i = base; i < end && h == end; i += 16) {
@@ -197,17 +202,26 @@ __global__ __launch_bounds__(kThreads) void k_rec_tile_count_chain(const uint32_
     }
     if (h > end) h = end;
   }
+  size_t tile = t0;  // the tile being binned
   uint32_t heads = 0, bytes = 0, err = 0;
+  auto emit_to = [&](size_t upto) {  // close tiles [tile, upto)
+    for (; tile < upto; ++tile) {
+      counts[tile] = (static_cast<uint64_t>(heads) << 32) | bytes;
+      flags[tile] = err;
+      heads = bytes = err = 0;
+    }
+  };
   // a chunk starts at a record head
-  if (tile == 0 && n != 0 && h != 0) err |= kRecErrBadPart;
+  if (t0 == 0 && n != 0 && h != 0) err |= kRecErrBadPart;
   while (h < end) {  // h + 1 < n: a header (search) or checked below
+    emit_to(h / kTileWords);
     const uint32_t magic = w[h], lrec = w[h + 1];
     if (magic != kMagic) {
       err |= kRecErrBadPart;
       break;
     }
     const uint32_t cf = cflag_of(lrec), len = len_of(lrec);
-    if (tile == 0 && h == 0 && cf > 1) err |= kRecErrBadPart;
+    if (h == 0 && cf > 1) err |= kRecErrBadPart;
     heads += cf <= 1 ? 1u : 0u;
     bytes += len + (cf >= 2 ? 4u : 0u);
     if (cf > 3) err |= kRecErrBadPart;
@@ -216,13 +230,12 @@ __global__ __launch_bounds__(kThreads) void k_rec_tile_count_chain(const uint32_
       err |= kRecErrTruncated;
       break;
     }
-    // a successor inside the tile must be a full header (R1 counts no
+    // a successor inside the range must be a full header (R1 counts no
     // header in the chunk's last word; the fill flags that chain)
     if (q < end && q + 1 >= n) break;
     h = q;
   }
-  counts[tile] = (static_cast<uint64_t>(heads) << 32) | bytes;
-  flags[tile] = err;
+  emit_to(t1);
 }
 
 /*! \brief copy len payload bytes of words src to byte address dst (one lane) */
@@ -529,8 +542,21 @@ void LaunchRecordIOTileCountChain(const uint32_t* words, size_t nwords, uint64_t
                                   uint32_t* tile_flags, hipStream_t stream) {
   const size_t tiles = RecordIOTiles(nwords);
   if (tiles == 0) return;
-  hipLaunchKernelGGL(k_rec_tile_count_chain, dim3((tiles + kThreads - 1) / kThreads),
-                     dim3(kThreads), 0, stream, words, nwords, tiles, tile_counts, tile_flags);
+  // large pieces (counted beside a fill): up to 8 tiles per lane, so the
+  // latency-bound chain waves hold few CU slots; small ones: a lane per tile
+  // (DMLC_REC_CHAIN_TILES forces a tiles-per-lane value: the tests' small
+  // chunks exercise the multi-tile walk with it)
+  static const size_t forced = [] {
+    const char* v = std::getenv("DMLC_REC_CHAIN_TILES");
+    return v != nullptr ? static_cast<size_t>(std::atoi(v)) : size_t(0);
+  }();
+  const size_t per = forced != 0 ? forced
+                     : tiles >= 8 * 16384 ? 8
+                     : (tiles >= 4 * 16384 ? 4 : (tiles >= 2 * 16384 ? 2 : 1));
+  const size_t lanes = (tiles + per - 1) / per;
+  hipLaunchKernelGGL(k_rec_tile_count_chain, dim3((lanes + kThreads - 1) / kThreads),
+                     dim3(kThreads), 0, stream, words, nwords, tiles, static_cast<uint32_t>(per),
+                     tile_counts, tile_flags);
 }
 
 size_t LaunchRecordIOTileFill(const uint32_t* words, size_t nwords, const uint64_t* tile_prefix,

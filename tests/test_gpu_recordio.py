@@ -286,6 +286,36 @@ def test_gpu_recordio_chain_count_equals_cpu(tmp_path, max_len, chunk_kb):
         assert got == recs
 
 
+def test_gpu_recordio_chain_count_multi_tile_lanes(tmp_path):
+    """R1c with several consecutive tiles per lane (the layout of large
+    pieces; forced here by DMLC_REC_CHAIN_TILES=3 in a subprocess, since the
+    setting is read once): the chain runs on across a lane's tiles, the
+    counts binned per tile equal R1's -- every shard equals the CPU reader."""
+    import json
+    import subprocess
+    import sys
+    p = tmp_path / "m.rec"
+    recs = _records(2500, 23, max_len=9000)
+    _write(p, recs)
+    code = (
+        "import json, sys\n"
+        "from dmlc_core_amd import io\n"
+        "out = []\n"
+        "for part in range(2):\n"
+        "    r = io.GPURecordIO(sys.argv[1], part, 2, chunk_bytes=256 * 1024, chain_count=1)\n"
+        "    r.read_all()\n"
+        "    out.append([x.hex() for x in io.split_records(*r.resident_to_host())])\n"
+        "    assert r.stats()['chain_counts'] > 0\n"
+        "print(json.dumps(out))\n")
+    env = dict(os.environ, DMLC_REC_CHAIN_TILES="3")
+    res = subprocess.run([sys.executable, "-c", code, str(p)], capture_output=True, text=True,
+                         env=env, timeout=120)
+    assert res.returncode == 0, res.stderr[-3000:]
+    got = json.loads(res.stdout.strip().splitlines()[-1])
+    for part in range(2):
+        assert [bytes.fromhex(x) for x in got[part]] == _cpu(p, part, 2)
+
+
 def test_gpu_recordio_chain_count_auto_on_replay(tmp_path):
     """chain_count auto: the first chunk uses R1, later ones (records of
     >= 128 B on average) R1c, including the prelaunched replay counts"""
