@@ -48,13 +48,29 @@ def _index64(csr: Dict) -> bool:
     return csr["index"].element_size() == 8
 
 
-def _check(csr: Dict):
+def _paired(csr: Dict) -> bool:
+    """index / value are the interleaved (int32 index, float32 value) pair
+    views :func:`transpose` returns: value's storage is index's shifted by one
+    4-byte word, both with stride 2"""
+    idx, val = csr["index"], csr.get("value")
+    return (val is not None and idx.element_size() == 4 and idx.dim() == 1 and val.dim() == 1
+            and idx.stride(0) == 2 and val.stride(0) == 2 and idx.numel() == val.numel()
+            and val.data_ptr() == idx.data_ptr() + 4 and idx.data_ptr() % 8 == 0)
+
+
+def _check(csr: Dict, pairs: bool = False):
+    """device CSR arrays the kernels can take: contiguous, or (``pairs``: the
+    SpMV) the interleaved pair views of a transpose"""
+    if pairs and _paired(csr) and csr["offset"].is_cuda and csr["offset"].is_contiguous():
+        return
     for k in ("offset", "index"):
         t = csr[k]
         if not t.is_cuda or not t.is_contiguous():
             raise ValueError(f"csr[{k!r}] must be a contiguous device tensor")
     if csr.get("value") is not None and csr["value"].dtype != torch.float32:
         raise ValueError("csr['value'] must be float32")
+    if csr.get("value") is not None and not csr["value"].is_contiguous():
+        raise ValueError("csr['value'] must be contiguous")
 
 
 def _stream() -> int:
@@ -62,8 +78,9 @@ def _stream() -> int:
 
 
 def spmv(csr: Dict, w: torch.Tensor, bias: float = 0.0) -> torch.Tensor:
-    """y[r] = sum_j value[j] * w[index[j]] + bias  (K11, 16 lanes per row)."""
-    _check(csr)
+    """y[r] = sum_j value[j] * w[index[j]] + bias  (K11, 16 lanes per row).
+    Takes contiguous arrays or a transpose's interleaved (index, value) pairs."""
+    _check(csr, pairs=True)
     assert w.dtype == torch.float32 and w.is_cuda and w.is_contiguous()
     nrows = csr["offset"].numel() - 1
     y = torch.empty(nrows, dtype=torch.float32, device=w.device)
@@ -109,7 +126,12 @@ def transpose(csr: Dict, num_features: int, out: Optional[Dict] = None) -> Dict:
     """The CSR's transpose (CSC / inverted index) on the device, as a
     CSR-shaped dict whose rows are the features: ``offset`` int64
     [num_features + 1], ``index`` int32 row ids (ascending within every
-    column), ``value`` (or None).
+    column), ``value`` (or None).  With values, ``index`` and ``value`` are
+    the two columns of one interleaved [nnz, 2] buffer (``pairs``: int32 row,
+    float32 bits), so each is a stride-2 view: the column scatter writes one
+    8-byte pair per entry instead of a 4-byte store into each of two arrays,
+    and :func:`spmv` reads the pairs directly (``.contiguous()`` gives
+    separate copies).
 
     Built by the hand-written stable two-level counting sort of
     src/gpu/transpose_kernels.hip (bucket histogram -> scan -> stable bucket
@@ -137,6 +159,7 @@ def transpose(csr: Dict, num_features: int, out: Optional[Dict] = None) -> Dict:
     # (one device read for both ends)
     lo, hi = (int(v) for v in off[[0, -1]].tolist()) if nrows > 0 else (0, 0)
     nnz = hi - lo
+    pairs = None
     if out is not None:
         col_ptr, rows, vals = out["offset"], out["index"], out.get("value")
         if (col_ptr.numel() != num_features + 1 or rows.numel() < nnz
@@ -144,11 +167,18 @@ def transpose(csr: Dict, num_features: int, out: Optional[Dict] = None) -> Dict:
             raise ValueError("transpose: out= does not fit this CSR")
         if value is None:
             vals = None
+        elif _paired(out):
+            pairs = out.get("pairs")
+        elif not (rows.is_contiguous() and vals.is_contiguous()):
+            raise ValueError("transpose: out= index / value must be contiguous or a transpose's pairs")
     else:
         col_ptr = torch.empty(num_features + 1, dtype=torch.int64, device=dev)
-        rows = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
-        vals = (torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
-                if value is not None else None)
+        if value is not None:
+            pairs = torch.empty((max(nnz, 1), 2), dtype=torch.int32, device=dev)
+            rows, vals = pairs[:, 0], pairs.view(torch.float32)[:, 1]
+        else:
+            rows = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
+            vals = None
     scratch = _workspace(_dmlc.csr_transpose_scratch_bytes(nnz, num_features), dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     _dmlc.csr_transpose(_ptr(offset), nrows, lo, nnz, _ptr(index), _ptr(value), int(num_features),
@@ -156,8 +186,11 @@ def transpose(csr: Dict, num_features: int, out: Optional[Dict] = None) -> Dict:
                         _index64(csr))
     if int(err.item()) != 0:
         raise ValueError(f"transpose: a feature id is >= num_features ({num_features})")
-    return {"offset": col_ptr, "index": rows[:nnz],
-            "value": vals[:nnz] if vals is not None else None}
+    res = {"offset": col_ptr, "index": rows[:nnz],
+           "value": vals[:nnz] if vals is not None else None}
+    if pairs is not None:
+        res["pairs"] = pairs
+    return res
 
 
 def _source_key(csr: Dict, num_features: int):

@@ -18,6 +18,10 @@
  * `column - excluded columns before it`), the ordinals where it goes:
  *   S1 k_csv_tile_count : (rows << 32 | entries) per tile + irregular flag,
  *                         straight from global memory (no LDS);
+ *   S1p k_csv_tile_count_pos (label / weight column <= 0): the same counts by
+ *                         position -- line ends and delimiters only, 8 loads
+ *                         in flight, no walk; the fill adds its tile's head
+ *                         fields and does S1's checks;
  *   C2 (tile_kernels.hip, raw scan), then
  *   S2 k_csv_tile_fill  : the same walk over a two-step LDS ring (one step
  *                         prefetched, so a number's 16-byte window never
@@ -59,6 +63,7 @@ struct CsvCfg {
   int has_weight;   // weight_column >= 0 (every row gets a weight)
   int zero_excl;    // label / weight columns equal to 0 (excluded field per row)
   uint32_t delim;
+  int pos;          // positional tile counts (S1p; label / weight at most column 0)
 };
 
 /*! \brief bit 7 of every byte of x equal to the byte in c4 (exact SWAR test) */
@@ -123,6 +128,7 @@ struct Walk {
   uint32_t carry_eol, carry_delim;  // last byte of the previous step
   uint32_t col_carry;               // fields since the last row start
   uint32_t rows, fields, excl;      // owned so far
+  uint32_t pre;                     // field starts of the tile before its first row start
   bool started, done, bad;
 };
 
@@ -172,6 +178,7 @@ __device__ __forceinline__ Slice step_slice(uint4 g, uint32_t s, uint32_t nrem, 
   w->carry_delim = lane63(last_d);
   // ownership: from the first row start in the tile to the first one after it
   uint32_t own = 0xFFFFu;
+  const bool was_started = w->started;
   const uint64_t any_ls = __ballot(lm != 0);
   const int first_lane = any_ls != 0 ? __builtin_ctzll(any_ls) : 0;
   const uint32_t first_lm = __builtin_amdgcn_readlane(lm, first_lane);  // (first_lane: uniform)
@@ -196,6 +203,9 @@ __device__ __forceinline__ Slice step_slice(uint4 g, uint32_t s, uint32_t nrem, 
     }
   }
   if (s * kStep + kStep >= nrem) w->done = true;  // the chunk ends in this step
+  // (S1p) the tile's field starts before its first row start: the rest of
+  // the previous tile's last row (wave-uniform: only until the walk starts)
+  if (s < kTileSteps && !was_started) w->pre += wave_sum(static_cast<uint32_t>(__popc(fm & ~own)));
   fm &= own;
   lm &= own;
   w->bad |= __any(bad && own != 0);
@@ -299,6 +309,69 @@ __global__ __launch_bounds__(kThreads) void k_csv_tile_count(const uint8_t* __re
   }
 }
 
+/*!
+ * \brief S1p: positional tile counts -- the row starts and entries whose
+ *  first byte lies in the tile (not the rows the tile owns), for a label /
+ *  weight column of at most 0 (one excluded field per row, no columns
+ *  needed).  A wave reads its 8 KiB with all 8 loads in flight and tests only
+ *  line ends and delimiters: no ownership walk, no scans, no extension.  The
+ *  fill adds the field starts before its first row start (Walk::pre) and
+ *  flags what S1 flagged (control bytes, > kListCap fields per step, rows
+ *  past the extension) itself, so a chunk is checked once.
+ */
+__global__ __launch_bounds__(kThreads) void k_csv_tile_count_pos(const uint8_t* __restrict__ text,
+                                                                 size_t n, size_t ntiles,
+                                                                 CsvCfg cfg,
+                                                                 uint64_t* __restrict__ counts,
+                                                                 uint32_t* __restrict__ flags) {
+  constexpr int kLoads = static_cast<int>(kTileBytes / 1024);
+  const int lane = lane_id();
+  const size_t tile = static_cast<size_t>(blockIdx.x) * kWaves + threadIdx.x / kWave;
+  if (tile >= ntiles) return;  // whole waves leave; nothing below synchronises waves
+  const size_t tile0 = tile * kTileBytes;
+  uint4 v[kLoads];
+#pragma unroll
+  for (int j = 0; j < kLoads; ++j) v[j] = load16_clip(text, tile0 + j * 1024 + 16u * lane, n);
+  uint32_t pe = 1u, pd = 0u;  // the byte before the tile: a line end / delimiter
+  if (tile0 != 0) {
+    const uint32_t c = text[tile0 - 1];
+    pe = (c == '\n' || c == '\r') ? 1u : 0u;
+    pd = c == cfg.delim ? 1u : 0u;
+  }
+  const uint32_t delim4 = cfg.delim * 0x01010101u;
+  uint32_t rows = 0, fields = 0;
+#pragma unroll
+  for (int j = 0; j < kLoads; ++j) {
+    const uint32_t w4[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+    uint32_t he[4], hd[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      // line ends, and the zeros past the chunk (no field starts there)
+      he[k] = hb_eq(w4[k], 0x0A0A0A0Au) | hb_eq(w4[k], 0x0D0D0D0Du) | hb_eq(w4[k], 0u);
+      hd[k] = hb_eq(w4[k], delim4);
+    }
+    const uint32_t e = mask16(he[0], he[1], he[2], he[3]);
+    const uint32_t d = mask16(hd[0], hd[1], hd[2], hd[3]);
+    const uint32_t last_e = (e >> 15) & 1u, last_d = (d >> 15) & 1u;
+    // the byte before each lane's 16: lane - 1's last, lane 0 the previous load's lane 63
+    const uint32_t up_e = lane_shr1(last_e), up_d = lane_shr1(last_d);
+    const uint32_t le = lane == 0 ? pe : up_e, ld = lane == 0 ? pd : up_d;
+    pe = lane63(last_e);
+    pd = lane63(last_d);
+    const uint32_t lm = ~e & ((e << 1) | le) & 0xFFFFu;
+    const uint32_t fm = lm | (((d << 1) | ld) & ~e & 0xFFFFu);
+    rows += static_cast<uint32_t>(__popc(lm));
+    fields += static_cast<uint32_t>(__popc(fm));
+  }
+  const uint64_t c = wave_sum_2x32((static_cast<uint64_t>(rows) << 32) | fields);
+  if (lane == 0) {
+    const uint32_t r = static_cast<uint32_t>(c >> 32);
+    counts[tile] = (c & 0xFFFFFFFF00000000ull) |
+                   (static_cast<uint32_t>(c) - r * static_cast<uint32_t>(cfg.zero_excl));
+    flags[tile] = 0u;
+  }
+}
+
 /*! \brief StrToFloat of the field at global position q (the generic path);
  *  returned by value -- an out-pointer into the caller's frame would put it on
  *  the stack (a scratch store + load per field round) */
@@ -342,6 +415,7 @@ __global__ __launch_bounds__(kThreads) void k_csv_tile_fill(const uint8_t* __res
   if (tile0 != 0) {
     const uint32_t c = text[tile0 - 1];
     w.carry_eol = (c == '\n' || c == '\r') ? 1u : 0u;
+    w.carry_delim = c == cfg.delim ? 1u : 0u;
   }
   const uint32_t delim = cfg.delim;
   uint64_t mx = 0;
@@ -452,7 +526,9 @@ __global__ __launch_bounds__(kThreads) void k_csv_tile_fill(const uint8_t* __res
           }
         }
         const uint64_t row = R + row_t;
-        const uint64_t e = C + ent;
+        // S1p: the prefix counts entries by position; the tile's own start
+        // after the rest of the previous tile's last row
+        const uint64_t e = C + ent + (cfg.pos ? w.pre : 0u);
         if (exp & 2u) {  // pricing: no stores (a value sink the compiler keeps)
           mx = __float_as_uint(v) == 0x7FC00001u ? mx + 1 : mx;
         } else if (row >= out.row_limit) {
@@ -490,6 +566,9 @@ __global__ __launch_bounds__(kThreads) void k_csv_tile_fill(const uint8_t* __res
     if (w.done) break;
     wave_sync();  // the next prefetch overwrites this step's slot
   }
+  // rows run past the extension while the chunk goes on: exact kernels (S1
+  // flags it too; S1p leaves it to the fill)
+  if (!w.done && tile0 + kTileBytes + kExt < n) irregular = true;
   unsigned fl = 0;
   if (irregular || w.bad) fl |= kFlagIrregular;
   if (any_value) fl |= kFlagValue;
@@ -515,6 +594,13 @@ CsvCfg MakeCfg(int label_column, int weight_column, char delimiter) {
   c.has_weight = weight_column >= 0 ? 1 : 0;
   c.zero_excl = (c.label_col == 0 ? 1 : 0) + (c.weight_col == 0 ? 1 : 0);
   c.delim = static_cast<uint8_t>(delimiter);
+  // positional counts whenever no column numbers are needed
+  // (DMLC_CSV_POSCOUNT=0: the owning-tile count S1 for every chunk)
+  static const bool pos_ok = [] {
+    const char* v = std::getenv("DMLC_CSV_POSCOUNT");
+    return v == nullptr || std::atoi(v) != 0;
+  }();
+  c.pos = pos_ok && c.label_col <= 0 && c.weight_col <= 0 ? 1 : 0;
   return c;
 }
 
@@ -525,9 +611,11 @@ void LaunchCsvTileCount(const char* text, size_t nbytes, int label_column, int w
                         hipStream_t stream) {
   const size_t ntiles = TileCount(nbytes);
   if (ntiles == 0) return;
-  hipLaunchKernelGGL(k_csv_tile_count, dim3((ntiles + kWaves - 1) / kWaves), dim3(kThreads), 0,
-                     stream, reinterpret_cast<const uint8_t*>(text), nbytes, ntiles,
-                     MakeCfg(label_column, weight_column, delimiter), tile_counts, tile_flags);
+  const CsvCfg cfg = MakeCfg(label_column, weight_column, delimiter);
+  hipLaunchKernelGGL(cfg.pos ? k_csv_tile_count_pos : k_csv_tile_count,
+                     dim3((ntiles + kWaves - 1) / kWaves), dim3(kThreads), 0, stream,
+                     reinterpret_cast<const uint8_t*>(text), nbytes, ntiles, cfg, tile_counts,
+                     tile_flags);
 }
 
 template <typename IndexType>

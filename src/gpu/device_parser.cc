@@ -798,7 +798,8 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
    * \brief CSV on the tile pipeline (csv_kernels.hip): lane-per-row count ->
    *  raw scan -> fill -> finish, both size read-outs through mapped pinned
    *  memory; false when the chunk must take the exact path (rows longer than
-   *  the tile extension, control bytes).
+   *  the tile extension, control bytes), found by the count (S1) or, with
+   *  positional counts (S1p), by the fill.
    */
   bool CsvFastParse(const char* text, size_t nbytes, DeviceCSR<IndexType>* out, size_t row_base,
                     size_t nnz_base, ChunkPlan* plan) {
@@ -822,8 +823,9 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
                      s);
     PrelaunchCount();
     const ChunkMeta m = WaitMapped(hm);
-    CHECK(!(m.flags & kFlagIrregular))
-        << "internal error: CSV fill pass disagreed with the count pass";
+    // with positional counts (S1p) the fill is where control bytes, crowded
+    // steps and over-long rows are found: the exact kernels rewrite the chunk
+    if (m.flags & kFlagIrregular) return false;
     Accumulate(m);
     return true;
   }

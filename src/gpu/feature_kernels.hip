@@ -12,6 +12,7 @@
  * K9 accumulates one row per wave in LDS (ds_add_f32) and converts pairs of
  * f32 to fp8 with the gfx950 v_cvt_pk_fp8_f32 instruction.
  */
+#include <dmlc/logging.h>
 #include <hip/hip_runtime.h>
 
 #include "./device_common.h"
@@ -54,6 +55,28 @@ __global__ __launch_bounds__(kThreads) void k_spmv(const uint64_t* __restrict__ 
     for (uint64_t j = b + g; j < e; j += kGroup) {
       const float v = value != nullptr ? value[j] : 1.0f;
       acc += v * w[index[j]];
+    }
+#pragma unroll
+    for (int d = kGroup / 2; d >= 1; d >>= 1) acc += __shfl_xor(acc, d, kGroup);
+    if (g == 0) y[r] = acc + bias;
+  }
+}
+
+/*! \brief k_spmv over interleaved (u32 index, f32 value) pairs (the paired
+ *  transpose output): one 8-byte load per entry */
+__global__ __launch_bounds__(kThreads) void k_spmv_pairs(const uint64_t* __restrict__ offset,
+                                                         const uint2* __restrict__ iv,
+                                                         size_t nrows, const float* __restrict__ w,
+                                                         float bias, float* __restrict__ y) {
+  const size_t ngroups = static_cast<size_t>(gridDim.x) * (kThreads / kGroup);
+  const int g = threadIdx.x % kGroup;
+  for (size_t r = blockIdx.x * static_cast<size_t>(kThreads / kGroup) + threadIdx.x / kGroup;
+       r < nrows; r += ngroups) {
+    const uint64_t b = offset[r], e = offset[r + 1];
+    float acc = 0.0f;
+    for (uint64_t j = b + g; j < e; j += kGroup) {
+      const uint2 p = iv[j];
+      acc += __uint_as_float(p.y) * w[p.x];
     }
 #pragma unroll
     for (int d = kGroup / 2; d >= 1; d >>= 1) acc += __shfl_xor(acc, d, kGroup);
@@ -212,6 +235,14 @@ template <typename IndexType>
 void LaunchCSRSpMV(const uint64_t* offset, const IndexType* index, const float* value,
                    size_t nrows, const float* w, float bias, float* y, hipStream_t stream) {
   if (nrows == 0) return;
+  // interleaved (index, value) pairs: value is the float after a u32 index
+  if (sizeof(IndexType) == 4 && value != nullptr &&
+      value == reinterpret_cast<const float*>(index) + 1) {
+    CHECK_EQ(reinterpret_cast<uintptr_t>(index) & 7u, 0u) << "spmv: pairs not 8-byte aligned";
+    hipLaunchKernelGGL(k_spmv_pairs, dim3(GridFor(nrows, kThreads / kGroup)), dim3(kThreads), 0,
+                       stream, offset, reinterpret_cast<const uint2*>(index), nrows, w, bias, y);
+    return;
+  }
   hipLaunchKernelGGL(k_spmv<IndexType>, dim3(GridFor(nrows, kThreads / kGroup)), dim3(kThreads),
                      0, stream, offset, index, value, nrows, w, bias, y);
 }

@@ -254,6 +254,10 @@ void LaunchTileFinish(MetaPartial* partials, size_t nslots, ChunkMeta* meta, Chu
  * \brief S1: per 8 KiB tile (rows starting in it << 32 | their entries) and
  *  kFlagIrregular (a row running > 4 KiB past its tile, control bytes); scan
  *  them with LaunchTileScanRaw.  tile_counts / tile_flags: TileScratchWords.
+ *  With label / weight columns of at most 0 the counts are positional (S1p:
+ *  row starts and entries whose first byte is in the tile, no flags) and the
+ *  fill flags irregular chunks; LaunchCsvTileFill takes the same columns, so
+ *  both pick the same mode.
  */
 void LaunchCsvTileCount(const char* text, size_t nbytes, int label_column, int weight_column,
                         char delimiter, uint64_t* tile_counts, uint32_t* tile_flags,
@@ -366,7 +370,8 @@ void LaunchTextHashed(const char* text, size_t nbytes, const uint32_t* line_star
                       TextFormat format, const uint64_t* line_info, uint64_t row_base, int dim,
                       float scale, uint32_t seed, bool fp8, void* out, float* labels,
                       MetaPartial* partials, ChunkMeta* meta, hipStream_t stream);
-/*! \brief K11: y[r] = sum_j value * w[index] (+ bias), row per wave */
+/*! \brief K11: y[r] = sum_j value * w[index] (+ bias), 16 lanes per row; value ==
+ *  (float*)index + 1 (u32 indices): interleaved (index, value) pairs */
 template <typename IndexType>
 void LaunchCSRSpMV(const uint64_t* offset, const IndexType* index, const float* value,
                    size_t nrows, const float* w, float bias, float* y, hipStream_t stream);
@@ -436,7 +441,9 @@ void LaunchPageRebase(uint64_t* offset, size_t nrows, const uint64_t* page_row_e
  * \brief CSR -> CSC (transpose_kernels.hip): rows [0, nrows) of a CSR whose
  *  entries are [base, base + nnz) of index / value; writes col_ptr
  *  [num_features + 1] (u64, from 0), row_out [nnz] (u32 row ids, ascending
- *  within each column) and val_out [nnz] (when value != null).  Feature ids
+ *  within each column) and val_out [nnz] (when value != null).  With
+ *  val_out == (float*)row_out + 1 (row_out 8-byte aligned) the output is
+ *  interleaved (row, value) pairs, one 8-byte store per entry.  Feature ids
  *  >= num_features are clamped and set *error (device u32) to 1.
  *  num_features <= CSRTransposeMaxFeatures(); scratch of
  *  CSRTransposeScratchBytes(nnz, num_features) bytes (256-byte aligned).

@@ -451,6 +451,10 @@ __global__ __launch_bounds__(kThreads) void k_lowkey_scan(uint32_t* __restrict__
 
 constexpr int kScatterDepth = 8;  // T4c: 64-entry groups per batch (loads a batch ahead)
 
+// kPair: the output is interleaved (row, value) pairs -- one 8-byte store per
+// entry instead of a 4-byte store into each of two arrays (T4c is bound by
+// the output lines its scattered stores touch)
+template <bool kPair>
 __global__ __launch_bounds__(dev::kWave) void k_lowkey_scatter(
     const uint16_t* __restrict__ t_key, const uint32_t* __restrict__ t_row,
     const uint2* __restrict__ t_rv, const uint64_t* __restrict__ bstart,
@@ -514,8 +518,12 @@ __global__ __launch_bounds__(dev::kWave) void k_lowkey_scatter(
       dev::wave_sync();
       if (valid) {
         const uint64_t pos = base + before + rank;
-        row_out[pos] = x.r[j];
-        if (val_out != nullptr) val_out[pos] = x.v[j];
+        if constexpr (kPair) {
+          reinterpret_cast<uint2*>(row_out)[pos] = make_uint2(x.r[j], __float_as_uint(x.v[j]));
+        } else {
+          row_out[pos] = x.r[j];
+          if (val_out != nullptr) val_out[pos] = x.v[j];
+        }
         if (rank + 1 == n) cur[k] = before + n;
       }
       dev::wave_sync();
@@ -640,8 +648,16 @@ void LaunchCSRTranspose(const uint64_t* offset, size_t nrows, uint64_t base, uin
   hipLaunchKernelGGL(k_lowkey_hist, dim3(nseg), dim3(kThreads), 0, stream, t_key, bstart, H);
   hipLaunchKernelGGL(k_lowkey_scan, dim3(p.nbuckets), dim3(kThreads), 0, stream, H, bstart,
                      num_features, col_ptr);
-  hipLaunchKernelGGL(k_lowkey_scatter, dim3(nseg), dim3(dev::kWave), 0, stream, t_key, t_row,
-                     t_rv, bstart, H, row_out, val_out);
+  // (row, value) pairs when val_out is the float after row_out (8-byte aligned)
+  const bool paired = val_out != nullptr && val_out == reinterpret_cast<float*>(row_out) + 1;
+  if (paired) {
+    CHECK_EQ(reinterpret_cast<uintptr_t>(row_out) & 7u, 0u) << "transpose: pair output not 8-byte aligned";
+    hipLaunchKernelGGL(k_lowkey_scatter<true>, dim3(nseg), dim3(dev::kWave), 0, stream, t_key,
+                       t_row, t_rv, bstart, H, row_out, val_out);
+  } else {
+    hipLaunchKernelGGL(k_lowkey_scatter<false>, dim3(nseg), dim3(dev::kWave), 0, stream, t_key,
+                       t_row, t_rv, bstart, H, row_out, val_out);
+  }
   hipLaunchKernelGGL(k_transpose_close, dim3(1), dim3(1), 0, stream, bstart, p.nbuckets,
                      num_features, col_ptr);
 }

@@ -129,6 +129,12 @@ def test_transpose_workspace_is_persistent_and_out_reuses(csr_t):
         torch.testing.assert_close(a[k], c[k], rtol=0, atol=0)
     with pytest.raises(ValueError, match="out= does not fit"):
         ops.transpose(t, nfeat + 1, out=junk)
+    # a previous (paired) result as out=: the pairs are overwritten in place
+    a["pairs"].fill_(7)
+    d = ops.transpose(t, nfeat, out=a)
+    assert d["pairs"].data_ptr() == a["pairs"].data_ptr()
+    for k in ("offset", "index", "value"):
+        torch.testing.assert_close(b[k], d[k], rtol=0, atol=0)
     ops.release_workspace()
     assert not ops._WORKSPACE
 
@@ -223,6 +229,32 @@ def test_transpose_kernel_is_a_stable_csc(tmp_path, nfeat, rows, index64):
     np.testing.assert_array_equal(tt["offset"].cpu().numpy(), ptr)
     np.testing.assert_array_equal(tt["index"].cpu().numpy(), r)
     np.testing.assert_array_equal(tt["value"].cpu().numpy(), v)
+    # values: index / value are the columns of one interleaved pair buffer
+    assert tt["index"].stride(0) == 2 and tt["value"].stride(0) == 2
+    assert tt["value"].data_ptr() == tt["index"].data_ptr() + 4
+    assert tt["pairs"].shape[1] == 2
+
+
+def test_spmv_over_pairs_matches_separate_arrays(csr_t):
+    """K11 over a transpose's interleaved (index, value) pairs equals K11 over
+    contiguous copies of the same arrays and the fp32 dense reference; other
+    ops reject the strided views"""
+    import torch
+    t, csr = csr_t
+    nfeat = int(csr.max_index) + 1
+    tt = ops.transpose(t, nfeat)
+    assert ops._paired(tt)
+    sep = {"offset": tt["offset"], "index": tt["index"].contiguous(),
+           "value": tt["value"].contiguous()}
+    assert not ops._paired(sep)
+    d = torch.randn(csr.rows, device="cuda")
+    g_pairs = ops.spmv(tt, d, 0.5)
+    g_sep = ops.spmv(sep, d, 0.5)
+    torch.testing.assert_close(g_pairs, g_sep, rtol=0, atol=0)
+    x = dense_ref(t, nfeat)
+    torch.testing.assert_close(g_pairs.cpu(), x.t() @ d.cpu() + 0.5, rtol=1e-4, atol=1e-4)
+    with pytest.raises(ValueError, match="contiguous"):
+        ops.spmv_t(tt, torch.randn(nfeat, device="cuda"), csr.rows)
 
 
 def test_transpose_rejects_out_of_range_ids(csr_t):
