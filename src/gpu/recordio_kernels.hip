@@ -103,38 +103,21 @@ struct TileQuads {
   uint32_t after[kLoads];
 };
 
-/*! \brief the tile's loads as issued (the fill prefetches the next tile's) */
-struct TileLoads {
-  uint4 q[kLoads];
-  uint32_t tail;  // the word after the tile
-};
-
-__device__ __forceinline__ void issue_tile(const uint32_t* __restrict__ w, size_t n, size_t base,
-                                           int lane, TileLoads* l) {
-#pragma unroll
-  for (int j = 0; j < kLoads; ++j) l->q[j] = load_quad(w, n, base + j * 256 + lane * 4);
-  const size_t past = base + kTileWords;
-  l->tail = past < n ? w[past] : 0u;
-}
-
-__device__ __forceinline__ void finish_tile(const TileLoads& l, int lane, TileQuads* t) {
-#pragma unroll
-  for (int j = 0; j < kLoads; ++j) {
-    t->q[j] = l.q[j];
-    const uint32_t right = lane_shl1(l.q[j].x);
-    // every lane runs the cross-lane ops (under a lane condition they would
-    // read an inactive lane)
-    const uint32_t next0 = __builtin_amdgcn_readlane(l.q[j + 1 < kLoads ? j + 1 : j].x, 0);
-    const uint32_t wrap = j + 1 < kLoads ? next0 : l.tail;
-    t->after[j] = lane == kWave - 1 ? wrap : right;
-  }
-}
-
 __device__ __forceinline__ void load_tile(const uint32_t* __restrict__ w, size_t n, size_t base,
                                           int lane, TileQuads* t) {
-  TileLoads l;
-  issue_tile(w, n, base, lane, &l);
-  finish_tile(l, lane, t);
+#pragma unroll
+  for (int j = 0; j < kLoads; ++j) t->q[j] = load_quad(w, n, base + j * 256 + lane * 4);
+  const size_t past = base + kTileWords;
+  const uint32_t tail = past < n ? w[past] : 0u;
+#pragma unroll
+  for (int j = 0; j < kLoads; ++j) {
+    const uint32_t right = lane_shl1(t->q[j].x);
+    // every lane runs the cross-lane ops (under a lane condition they would
+    // read an inactive lane)
+    const uint32_t next0 = __builtin_amdgcn_readlane(t->q[j + 1 < kLoads ? j + 1 : j].x, 0);
+    const uint32_t wrap = j + 1 < kLoads ? next0 : tail;
+    t->after[j] = lane == kWave - 1 ? wrap : right;
+  }
 }
 
 /*! \brief (heads << 32 | bytes) and error bits of the parts headed in one quad */
@@ -293,13 +276,8 @@ struct RecPass {
                                // look-back wait (wrong positions), 2 no payload copies
 };
 
-// kPf (counted mode): 0 a wave per tile; 1 persistent, the next tile's loads
-// issued once this tile is staged in LDS; 2 persistent, issued after the
-// header walk (the long-part copies run under them).  4 waves per SIMD (the
-// LDS allows 4 workgroups per CU): kPf 1 holds the prefetch beside the walk
-template <bool kOnePass, int kPf>
-__global__ __launch_bounds__(kThreads)
-__attribute__((amdgpu_waves_per_eu(4))) void k_rec_tile_fill(const uint32_t* __restrict__ w,
+template <bool kOnePass>
+__global__ __launch_bounds__(kThreads) void k_rec_tile_fill(const uint32_t* __restrict__ w,
                                                             size_t n, size_t ntiles,
                                                             const uint64_t* __restrict__ prefix,
                                                             uint64_t* __restrict__ offset,
@@ -326,216 +304,195 @@ __attribute__((amdgpu_waves_per_eu(4))) void k_rec_tile_fill(const uint32_t* __r
     __syncthreads();
     group = s_ticket;
   }
-  size_t tile = group * kWaves + wave;
+  const size_t tile = group * kWaves + wave;
   if (tile >= ntiles) return;  // whole waves leave; nothing below synchronises waves
-  constexpr bool kPersist = !kOnePass && kPf != 0;
-  // persistent (counted mode): workgroups step over the tiles by the grid, a
-  // wave's next tile loads while it walks / copies this one
-  const size_t stride = static_cast<size_t>(gridDim.x) * kWaves;
   BigPart* big = s_big[wave];
+  const size_t base = tile * kTileWords;
+  TileQuads t;
+  load_tile(w, n, base, lane, &t);
   uint32_t* const tw = reinterpret_cast<uint32_t*>(s_tw[wave]);
-  TileLoads ld;
-  issue_tile(w, n, tile * kTileWords, lane, &ld);
-  for (;;) {
-    const size_t base = tile * kTileWords;
-    const size_t next = tile + stride;
-    TileQuads t;
-    finish_tile(ld, lane, &t);
-    if constexpr (kPersist) wave_sync();  // the last tile's copies are done with the LDS
 #pragma unroll
-    for (int j = 0; j < kLoads; ++j) s_tw[wave][j * 64 + lane] = t.q[j];
-    if (lane == kWave - 1) tw[kTileWords] = t.after[kLoads - 1];
-    wave_sync();
-    if constexpr (kPersist && kPf == 1) {
-      if (next < ntiles) issue_tile(w, n, next * kTileWords, lane, &ld);
-    }
-    // word q of the chunk (q < n): staged when inside the tile (+1), else global
-    auto word_at = [&](size_t q) {
-      const size_t r = q - base;
-      return r <= kTileWords ? tw[r] : w[q];
-    };
-    uint64_t pre;
-    uint32_t err = 0;
-    if constexpr (kOnePass) {
-      // R1 in the fill: the tile's (heads, bytes) from the registers it already
-      // holds, then the look-back for the tiles before it (heads < 2^30 and
-      // bytes < 2^32 in a chunk < 4 GiB: a 30 / 32-bit pair)
-      uint64_t c = 0;
-#pragma unroll
-      for (int j = 0; j < kLoads; ++j) {
-        c += quad_counts(t.q[j], t.after[j], base + j * 256 + lane * 4, n, &err);
-      }
-      if (tile == 0 && lane == 0 && n != 0 && !(t.q[0].x == kMagic && n > 1 && cflag_of(t.q[0].y) <= 1))
-        err |= kRecErrBadPart;  // a chunk starts at a record head
-      c = wave_sum_2x32(c);
-      if (op.exp & 1u) {
-        pre = static_cast<uint64_t>(tile) * c;  // pricing: positions without the look-back
-      } else {
-        pre = lookback_pairs<32>(op.status, tile, c, lane);
-      }
-      if (tile + 1 == ntiles && lane == 0) {
-        ChunkMeta m;
-        m.nlines = m.nrows = (pre + c) >> 32;
-        m.nnz = (pre + c) & 0xffffffffull;
-        m.max_index = m.max_field = 0;
-        m.flags = 0;
-        m.pad = 0;
-        *op.meta = m;  // k_tile_finish (stream-ordered) adds the error bits, publishes
-      }
-    } else {
-      pre = prefix[tile];
-    }
-    uint64_t rec = pre >> 32;            // records before this 1 KiB sub-tile (chunk-relative)
-    uint64_t pos = pre & 0xffffffffull;  // output bytes before it
-    uint8_t* const out = data + byte_base;
-    bool over = false;
-    uint32_t nbig = 0;
+  for (int j = 0; j < kLoads; ++j) s_tw[wave][j * 64 + lane] = t.q[j];
+  if (lane == kWave - 1) tw[kTileWords] = t.after[kLoads - 1];
+  wave_sync();
+  // word q of the chunk (q < n): staged when inside the tile (+1), else global
+  auto word_at = [&](size_t q) {
+    const size_t r = q - base;
+    return r <= kTileWords ? tw[r] : w[q];
+  };
+  uint64_t pre;
+  uint32_t err = 0;
+  if constexpr (kOnePass) {
+    // R1 in the fill: the tile's (heads, bytes) from the registers it already
+    // holds, then the look-back for the tiles before it (heads < 2^30 and
+    // bytes < 2^32 in a chunk < 4 GiB: a 30 / 32-bit pair)
+    uint64_t c = 0;
 #pragma unroll
     for (int j = 0; j < kLoads; ++j) {
-      const size_t i0 = base + j * 256 + lane * 4;
-      // kPf 1: the quads come back from LDS (their registers hold the next tile)
-      const uint4 qj = kPf == 1 ? s_tw[wave][j * 64 + lane] : t.q[j];
-      const uint32_t aj = kPf == 1 ? tw[j * 256 + lane * 4 + 4] : t.after[j];
-      uint32_t unused = 0;
-      const uint64_t c = quad_counts(qj, aj, i0, n, &unused);
-      uint64_t tot;
-      const uint64_t before = wave_excl_scan_2x32(c, &tot);  // heads << 32 | bytes
-      uint64_t r = rec + (before >> 32);
-      uint64_t p = pos + (before & 0xffffffffull);
-      // parts of more than 64 B are > 16 words apart: at most one per quad
-      bool has_big = false;
-      BigPart mine{0, 0, 0};
-      uint32_t m = header_bits(qj, i0, n);
-      while (m != 0) {
-        const uint32_t k = static_cast<uint32_t>(__ffs(m) - 1);
-        m &= m - 1;
-        const uint32_t lrec = lrec_at(qj, k, aj);
-        const uint32_t cf = cflag_of(lrec), len = len_of(lrec);
-        const size_t i = i0 + k;
-        {
-          // the part that follows: a continuation must follow a first / middle
-          // part, a head a whole / last part (read from the staged words)
-          const size_t q = i + 2 + (static_cast<size_t>(len) + 3) / 4;
-          const bool ends_record = cf == 0 || cf == 3;
-          if (q > n) {
-            err |= kRecErrTruncated;
-          } else if (q == n) {
-            err |= ends_record ? 0u : kRecErrTruncated;
-          } else if (q + 1 >= n || word_at(q) != kMagic) {
-            err |= kRecErrBadPart;
-          } else {
-            const uint32_t next = cflag_of(word_at(q + 1));
-            const bool next_continues = next == 2 || next == 3;
-            err |= (ends_record == next_continues || next > 3) ? kRecErrBadPart : 0u;
-          }
-        }
-        // writes stay inside the capacity given (one pass: overflow -> grow ->
-        // rerun; counted: sized exactly, so a miss is a count / fill mismatch)
-        // (a head takes an offset slot, a continuation its re-inserted magic)
-        const bool fits = (cf >= 2 || rec_base + r < op.rec_cap) &&
-                          byte_base + p + len + (cf >= 2 ? 4u : 0u) <= op.byte_cap;
-        over |= !fits;
-        if (cf <= 1) {
-          if (fits) offset[rec_base + r] = byte_base + p;
-          ++r;
-        } else {
-          // the reader re-inserts the escaped magic in front of a continuation
-          if (fits) {
+      c += quad_counts(t.q[j], t.after[j], base + j * 256 + lane * 4, n, &err);
+    }
+    if (tile == 0 && lane == 0 && n != 0 && !(t.q[0].x == kMagic && n > 1 && cflag_of(t.q[0].y) <= 1))
+      err |= kRecErrBadPart;  // a chunk starts at a record head
+    c = wave_sum_2x32(c);
+    if (op.exp & 1u) {
+      pre = static_cast<uint64_t>(tile) * c;  // pricing: positions without the look-back
+    } else {
+      pre = lookback_pairs<32>(op.status, tile, c, lane);
+    }
+    if (tile + 1 == ntiles && lane == 0) {
+      ChunkMeta m;
+      m.nlines = m.nrows = (pre + c) >> 32;
+      m.nnz = (pre + c) & 0xffffffffull;
+      m.max_index = m.max_field = 0;
+      m.flags = 0;
+      m.pad = 0;
+      *op.meta = m;  // k_tile_finish (stream-ordered) adds the error bits, publishes
+    }
+  } else {
+    pre = prefix[tile];
+  }
+  uint64_t rec = pre >> 32;            // records before this 1 KiB sub-tile (chunk-relative)
+  uint64_t pos = pre & 0xffffffffull;  // output bytes before it
+  uint8_t* const out = data + byte_base;
+  bool over = false;
+  uint32_t nbig = 0;
 #pragma unroll
-            for (int b = 0; b < 4; ++b) out[p + b] = static_cast<uint8_t>(kMagic >> (8 * b));
-          }
-          p += 4;
-        }
-        const bool whole = fits && i + 2 + (static_cast<size_t>(len) + 3) / 4 <= n;  // else: truncated
-        if (whole && len <= kSmallPart) {
-          lane_copy(w + i + 2, len, out + p);
-        } else if (whole) {
-          has_big = true;
-          mine = BigPart{static_cast<uint32_t>(i), len, p};
-        }
-        p += len;
-      }
-      const uint64_t bigs = __ballot(has_big);
-      if (has_big) {
-        const uint32_t slot = nbig + __builtin_amdgcn_mbcnt_hi(
-                                         static_cast<uint32_t>(bigs >> 32),
-                                         __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bigs), 0u));
-        big[slot] = mine;
-      }
-      nbig += static_cast<uint32_t>(__popcll(bigs));
-      rec += tot >> 32;
-      pos += tot & 0xffffffffull;
-    }
-    if constexpr (kPersist && kPf == 2) {
-      if (next < ntiles) issue_tile(w, n, next * kTileWords, lane, &ld);
-    }
-    wave_sync();  // the list is visible to every lane
-    // the listed parts (> 64 B), two at a time: half-wave h copies part e0 + h.
-    // Destinations are any byte offset (a continuation's re-inserted magic
-    // shifts every later part by 4, odd payload lengths by anything), so each
-    // part is written as its head bytes up to the first 16-byte boundary, whole
-    // aligned 16-byte blocks (one dwordx4 store per lane) and its tail bytes;
-    // a block's 16 source bytes are five payload words funnel-shifted into
-    // place, read from the LDS-staged tile (or from memory past the tile).
-    const int hl = lane & 31;
-    for (uint32_t e0 = 0; e0 < ((op.exp & 2u) ? 0u : nbig); e0 += 2) {
-      const uint32_t e = e0 + static_cast<uint32_t>(lane >> 5);
-      if (e < nbig) {
-        const BigPart bp = big[e];
-        uint8_t* const d = out + bp.dst;
-        const uint32_t head = (16u - static_cast<uint32_t>(reinterpret_cast<uintptr_t>(d) & 15u)) & 15u;
-        const uint32_t h = head < bp.len ? head : bp.len;
-        const uint32_t nblk = (bp.len - h) / 16;
-        const uint32_t tail = bp.len - h - nblk * 16;
-        const size_t pw = static_cast<size_t>(bp.word) + 2;  // chunk word of payload byte 0
-        // payload word j: staged when inside the tile (+1), else from memory
-        auto pword = [&](uint32_t j) {
-          const size_t q = pw + j;
-          return q - base <= kTileWords ? tw[q - base] : w[q];
-        };
-        auto pbyte = [&](uint32_t o) { return static_cast<uint8_t>(pword(o >> 2) >> (8 * (o & 3u))); };
-        for (uint32_t b = static_cast<uint32_t>(hl); b < nblk; b += 32) {
-          const uint32_t o = h + 16 * b;  // payload byte of the block's first byte
-          const uint32_t j = o >> 2, r = o & 3u;
-          const uint32_t w0 = pword(j), w1 = pword(j + 1), w2 = pword(j + 2), w3 = pword(j + 3);
-          // (the fifth word only when the block is not word-aligned: it may lie
-          // past the payload's last word, so it is not read otherwise)
-          const uint32_t w4 = r != 0 ? pword(j + 4) : 0u;
-          *reinterpret_cast<uint4*>(d + o) =
-              make_uint4(__builtin_amdgcn_alignbyte(w1, w0, r), __builtin_amdgcn_alignbyte(w2, w1, r),
-                         __builtin_amdgcn_alignbyte(w3, w2, r), __builtin_amdgcn_alignbyte(w4, w3, r));
-        }
-        if (static_cast<uint32_t>(hl) < h) d[hl] = pbyte(static_cast<uint32_t>(hl));
-        if (static_cast<uint32_t>(hl) < tail) {
-          const uint32_t o = h + nblk * 16 + static_cast<uint32_t>(hl);
-          d[o] = pbyte(o);
+  for (int j = 0; j < kLoads; ++j) {
+    const size_t i0 = base + j * 256 + lane * 4;
+    uint32_t unused = 0;
+    const uint64_t c = quad_counts(t.q[j], t.after[j], i0, n, &unused);
+    uint64_t tot;
+    const uint64_t before = wave_excl_scan_2x32(c, &tot);  // heads << 32 | bytes
+    uint64_t r = rec + (before >> 32);
+    uint64_t p = pos + (before & 0xffffffffull);
+    // parts of more than 64 B are > 16 words apart: at most one per quad
+    bool has_big = false;
+    BigPart mine{0, 0, 0};
+    uint32_t m = header_bits(t.q[j], i0, n);
+    while (m != 0) {
+      const uint32_t k = static_cast<uint32_t>(__ffs(m) - 1);
+      m &= m - 1;
+      const uint32_t lrec = lrec_at(t.q[j], k, t.after[j]);
+      const uint32_t cf = cflag_of(lrec), len = len_of(lrec);
+      const size_t i = i0 + k;
+      {
+        // the part that follows: a continuation must follow a first / middle
+        // part, a head a whole / last part (read from the staged words)
+        const size_t q = i + 2 + (static_cast<size_t>(len) + 3) / 4;
+        const bool ends_record = cf == 0 || cf == 3;
+        if (q > n) {
+          err |= kRecErrTruncated;
+        } else if (q == n) {
+          err |= ends_record ? 0u : kRecErrTruncated;
+        } else if (q + 1 >= n || word_at(q) != kMagic) {
+          err |= kRecErrBadPart;
+        } else {
+          const uint32_t next = cflag_of(word_at(q + 1));
+          const bool next_continues = next == 2 || next == 3;
+          err |= (ends_record == next_continues || next > 3) ? kRecErrBadPart : 0u;
         }
       }
-    }
-    if constexpr (!kOnePass) {
-      // the tile's own parts must end where the count said the next tile
-      // starts (R1c follows chains; R2 sees every aligned magic)
-      if (op.meta != nullptr && lane == 0) {
-        const uint64_t want = tile + 1 < ntiles ? prefix[tile + 1]
-                                                : ((static_cast<uint64_t>(op.meta->nrows) << 32) |
-                                                   op.meta->nnz);
-        if (((rec << 32) | pos) != want) err |= kRecErrBadPart;
+      // writes stay inside the capacity given (one pass: overflow -> grow ->
+      // rerun; counted: sized exactly, so a miss is a count / fill mismatch)
+      // (a head takes an offset slot, a continuation its re-inserted magic)
+      const bool fits = (cf >= 2 || rec_base + r < op.rec_cap) &&
+                        byte_base + p + len + (cf >= 2 ? 4u : 0u) <= op.byte_cap;
+      over |= !fits;
+      if (cf <= 1) {
+        if (fits) offset[rec_base + r] = byte_base + p;
+        ++r;
+      } else {
+        // the reader re-inserts the escaped magic in front of a continuation
+        if (fits) {
+#pragma unroll
+          for (int b = 0; b < 4; ++b) out[p + b] = static_cast<uint8_t>(kMagic >> (8 * b));
+        }
+        p += 4;
       }
-      if (over) err |= kRecErrBadPart;
-      over = false;
+      const bool whole = fits && i + 2 + (static_cast<size_t>(len) + 3) / 4 <= n;  // else: truncated
+      if (whole && len <= kSmallPart) {
+        lane_copy(w + i + 2, len, out + p);
+      } else if (whole) {
+        has_big = true;
+        mine = BigPart{static_cast<uint32_t>(i), len, p};
+      }
+      p += len;
     }
-    err = wave_or(err | (over ? kFlagOverflow : 0u));
-    if (lane == 0) {
-      MetaPartial mp;
-      mp.max_index = 0;
-      mp.max_field = 0;
-      mp.flags = err;
-      mp.pad = 0;
-      partials[tile] = mp;
+    const uint64_t bigs = __ballot(has_big);
+    if (has_big) {
+      const uint32_t slot = nbig + __builtin_amdgcn_mbcnt_hi(
+                                       static_cast<uint32_t>(bigs >> 32),
+                                       __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bigs), 0u));
+      big[slot] = mine;
     }
-    if (!kPersist || next >= ntiles) break;
-    tile = next;
-  }  // for tiles
+    nbig += static_cast<uint32_t>(__popcll(bigs));
+    rec += tot >> 32;
+    pos += tot & 0xffffffffull;
+  }
+  wave_sync();  // the list is visible to every lane
+  // the listed parts (> 64 B), two at a time: half-wave h copies part e0 + h.
+  // Destinations are any byte offset (a continuation's re-inserted magic
+  // shifts every later part by 4, odd payload lengths by anything), so each
+  // part is written as its head bytes up to the first 16-byte boundary, whole
+  // aligned 16-byte blocks (one dwordx4 store per lane) and its tail bytes;
+  // a block's 16 source bytes are five payload words funnel-shifted into
+  // place, read from the LDS-staged tile (or from memory past the tile).
+  const int hl = lane & 31;
+  for (uint32_t e0 = 0; e0 < ((op.exp & 2u) ? 0u : nbig); e0 += 2) {
+    const uint32_t e = e0 + static_cast<uint32_t>(lane >> 5);
+    if (e < nbig) {
+      const BigPart bp = big[e];
+      uint8_t* const d = out + bp.dst;
+      const uint32_t head = (16u - static_cast<uint32_t>(reinterpret_cast<uintptr_t>(d) & 15u)) & 15u;
+      const uint32_t h = head < bp.len ? head : bp.len;
+      const uint32_t nblk = (bp.len - h) / 16;
+      const uint32_t tail = bp.len - h - nblk * 16;
+      const size_t pw = static_cast<size_t>(bp.word) + 2;  // chunk word of payload byte 0
+      // payload word j: staged when inside the tile (+1), else from memory
+      auto pword = [&](uint32_t j) {
+        const size_t q = pw + j;
+        return q - base <= kTileWords ? tw[q - base] : w[q];
+      };
+      auto pbyte = [&](uint32_t o) { return static_cast<uint8_t>(pword(o >> 2) >> (8 * (o & 3u))); };
+      for (uint32_t b = static_cast<uint32_t>(hl); b < nblk; b += 32) {
+        const uint32_t o = h + 16 * b;  // payload byte of the block's first byte
+        const uint32_t j = o >> 2, r = o & 3u;
+        const uint32_t w0 = pword(j), w1 = pword(j + 1), w2 = pword(j + 2), w3 = pword(j + 3);
+        // (the fifth word only when the block is not word-aligned: it may lie
+        // past the payload's last word, so it is not read otherwise)
+        const uint32_t w4 = r != 0 ? pword(j + 4) : 0u;
+        *reinterpret_cast<uint4*>(d + o) =
+            make_uint4(__builtin_amdgcn_alignbyte(w1, w0, r), __builtin_amdgcn_alignbyte(w2, w1, r),
+                       __builtin_amdgcn_alignbyte(w3, w2, r), __builtin_amdgcn_alignbyte(w4, w3, r));
+      }
+      if (static_cast<uint32_t>(hl) < h) d[hl] = pbyte(static_cast<uint32_t>(hl));
+      if (static_cast<uint32_t>(hl) < tail) {
+        const uint32_t o = h + nblk * 16 + static_cast<uint32_t>(hl);
+        d[o] = pbyte(o);
+      }
+    }
+  }
+  if constexpr (!kOnePass) {
+    // the tile's own parts must end where the count said the next tile
+    // starts (R1c follows chains; R2 sees every aligned magic)
+    if (op.meta != nullptr && lane == 0) {
+      const uint64_t want = tile + 1 < ntiles ? prefix[tile + 1]
+                                              : ((static_cast<uint64_t>(op.meta->nrows) << 32) |
+                                                 op.meta->nnz);
+      if (((rec << 32) | pos) != want) err |= kRecErrBadPart;
+    }
+    if (over) err |= kRecErrBadPart;
+    over = false;
+  }
+  err = wave_or(err | (over ? kFlagOverflow : 0u));
+  if (lane == 0) {
+    MetaPartial mp;
+    mp.max_index = 0;
+    mp.max_field = 0;
+    mp.flags = err;
+    mp.pad = 0;
+    partials[tile] = mp;
+  }
 }
 
 /*!
@@ -624,35 +581,13 @@ size_t LaunchRecordIOTileFill(const uint32_t* words, size_t nwords, const uint64
                  one_pass->rec_cap, one_pass->byte_cap, exp};
     // every look-back word starts "not yet" (zeroed before every launch)
     DMLC_HIP_CHECK(hipMemsetAsync(op.status, 0, tiles * sizeof(uint64_t), stream));
-    hipLaunchKernelGGL((k_rec_tile_fill<true, 0>), dim3(groups), dim3(kThreads), 0, stream, words,
-                       nwords, tiles, tile_prefix, offset, rec_base, data, byte_base, partials, op);
-    return groups;
-  }
-  static const int pf = [] {
-    const char* v = std::getenv("DMLC_REC_FILL_PF");
-    return v != nullptr ? std::atoi(v) : 2;
-  }();
-  if (pf == 0) {
-    hipLaunchKernelGGL((k_rec_tile_fill<false, 0>), dim3(groups), dim3(kThreads), 0, stream, words,
-                       nwords, tiles, tile_prefix, offset, rec_base, data, byte_base, partials, op);
-    return groups;
-  }
-  // persistent: as many workgroups as are resident at once (LDS: 4 per CU)
-  static const size_t resident = [] {
-    int dev = 0, cus = 0;
-    DMLC_HIP_CHECK(hipGetDevice(&dev));
-    DMLC_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    return static_cast<size_t>(cus > 0 ? cus : 256) * 4;
-  }();
-  const size_t grid = groups < resident ? groups : resident;
-  if (pf == 1) {
-    hipLaunchKernelGGL((k_rec_tile_fill<false, 1>), dim3(grid), dim3(kThreads), 0, stream, words,
+    hipLaunchKernelGGL(k_rec_tile_fill<true>, dim3(groups), dim3(kThreads), 0, stream, words,
                        nwords, tiles, tile_prefix, offset, rec_base, data, byte_base, partials, op);
   } else {
-    hipLaunchKernelGGL((k_rec_tile_fill<false, 2>), dim3(grid), dim3(kThreads), 0, stream, words,
+    hipLaunchKernelGGL(k_rec_tile_fill<false>, dim3(groups), dim3(kThreads), 0, stream, words,
                        nwords, tiles, tile_prefix, offset, rec_base, data, byte_base, partials, op);
   }
-  return grid;
+  return groups;
 }
 
 void LaunchRecordIOGather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len,

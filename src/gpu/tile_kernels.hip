@@ -994,12 +994,6 @@ __device__ __forceinline__ void list_slice(uint32_t* sl, uint32_t tm, uint32_t l
  *  quads, where lane-ordered slots put tokens 256 B apart into one group
  */
 __device__ __forceinline__ uint32_t round_slot(int lane) {
-#ifndef DMLC_SLOT_B128
-  // the decoders read their windows as five ds_read_b32 ({0-31}, {32-63},
-  // bank = dword mod 32): 32 consecutive tokens span ~120 dwords (~4-way
-  // conflicts); every other token spans ~240 at ~7.5-dword spacing
-  return 2u * (static_cast<uint32_t>(lane) & 31u) + (static_cast<uint32_t>(lane) >> 5);
-#endif
   // rank within its group + 16 * group, for lanes 0..31 (4 bits per entry)
   const uint32_t l = static_cast<uint32_t>(lane) & 31u;
   uint32_t k;

@@ -41,6 +41,8 @@
 #include <dmlc/logging.h>
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "./device_common.h"
 #include "./kernels.h"
 
@@ -650,13 +652,19 @@ void LaunchCSRTranspose(const uint64_t* offset, size_t nrows, uint64_t base, uin
                      num_features, col_ptr);
   // (row, value) pairs when val_out is the float after row_out (8-byte aligned)
   const bool paired = val_out != nullptr && val_out == reinterpret_cast<float*>(row_out) + 1;
+  // pricing: extra LDS per T4c wave throttles how many run at once (the
+  // columns they keep open -- their write frontier -- shrink with them)
+  static const size_t t4c_lds = [] {
+    const char* v = std::getenv("DMLC_T4C_LDS");
+    return v != nullptr ? static_cast<size_t>(std::atoi(v)) : size_t(0);
+  }();
   if (paired) {
     CHECK_EQ(reinterpret_cast<uintptr_t>(row_out) & 7u, 0u) << "transpose: pair output not 8-byte aligned";
-    hipLaunchKernelGGL(k_lowkey_scatter<true>, dim3(nseg), dim3(dev::kWave), 0, stream, t_key,
-                       t_row, t_rv, bstart, H, row_out, val_out);
+    hipLaunchKernelGGL(k_lowkey_scatter<true>, dim3(nseg), dim3(dev::kWave), t4c_lds, stream,
+                       t_key, t_row, t_rv, bstart, H, row_out, val_out);
   } else {
-    hipLaunchKernelGGL(k_lowkey_scatter<false>, dim3(nseg), dim3(dev::kWave), 0, stream, t_key,
-                       t_row, t_rv, bstart, H, row_out, val_out);
+    hipLaunchKernelGGL(k_lowkey_scatter<false>, dim3(nseg), dim3(dev::kWave), t4c_lds, stream,
+                       t_key, t_row, t_rv, bstart, H, row_out, val_out);
   }
   hipLaunchKernelGGL(k_transpose_close, dim3(1), dim3(1), 0, stream, bstart, p.nbuckets,
                      num_features, col_ptr);
