@@ -8,8 +8,9 @@
  *  include/dmlc/data.h:143-157 (Row::SDot) -- the transpose turns X^T d into
  *  the same gather over columns.
  *
- *  Column c = (bucket c >> kLowBits, low key c & (L - 1)), L = 4096 columns per
- *  bucket, at most kMaxBuckets buckets (so feature ids < 2^22):
+ *  Column c = (bucket c >> kB, low key c & (L - 1)), L = 2^kB columns per
+ *  bucket (kB = 10 .. 12, LowBits: the narrowest that keeps at most
+ *  kMaxBuckets buckets, so feature ids < 2^22):
  *   T1 k_bucket_hist  one workgroup per block of kBlockElems entries (in CSR
  *      order): LDS histogram of buckets -> G[bucket][block].
  *   T2 exclusive scan of G (bucket-major): where each (bucket, block) run
@@ -52,8 +53,9 @@ namespace gpu {
 namespace {
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / dev::kWave;
-constexpr int kLowBits = 12;
-constexpr uint32_t kLow = 1u << kLowBits;  // columns per bucket
+constexpr int kMinLowBits = 10;  // columns per bucket: 2^kB, kB = 10 .. 12 (LowBits)
+constexpr int kMaxLowBits = 12;
+constexpr int kDefaultLowBits = 12;  // the narrowest width tried by default
 constexpr uint32_t kMaxBuckets = 1024;
 constexpr uint32_t kSubElems = 3072;        // T3 sub-tile, sorted in LDS (3 workgroups / CU)
 constexpr size_t kBlockElems = 10 * kSubElems;  // T1 / T3 block (per workgroup)
@@ -100,7 +102,7 @@ __device__ __forceinline__ uint32_t row_of(const uint64_t* __restrict__ offset, 
   return static_cast<uint32_t>(lo);
 }
 
-template <typename IndexType>
+template <typename IndexType, int kB>
 __global__ __launch_bounds__(kThreads) void k_bucket_hist(const IndexType* __restrict__ index,
                                                           uint64_t nnz, uint64_t num_features,
                                                           uint32_t nbuckets,
@@ -115,7 +117,7 @@ __global__ __launch_bounds__(kThreads) void k_bucket_hist(const IndexType* __res
   bool bad = false;
   auto add = [&](IndexType c) {
     bad |= static_cast<uint64_t>(c) >= num_features;
-    atomicAdd(&hist[column(c, num_features) >> kLowBits], 1u);
+    atomicAdd(&hist[column(c, num_features) >> kB], 1u);
   };
   uint64_t e = e0 + threadIdx.x;
   if (sizeof(IndexType) == 4 && (reinterpret_cast<uintptr_t>(index + e0) & 15u) == 0) {
@@ -148,7 +150,7 @@ __global__ void k_chunk_rows(const uint64_t* __restrict__ offset, size_t nrows, 
   if (c * kChunk < nnz) chunk_row[c] = row_of(offset, nrows, base, c * kChunk);
 }
 
-template <typename IndexType>
+template <typename IndexType, int kB>
 __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
     const uint64_t* __restrict__ offset, size_t nrows, uint64_t base,
     const IndexType* __restrict__ index, const float* __restrict__ value, uint64_t nnz,
@@ -222,7 +224,7 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
 #pragma unroll
     for (int i = 0; i < kPerLane; ++i) {
       const bool valid = c0 + static_cast<uint64_t>(i) * dev::kWave + lane < c1;
-      const uint32_t bk = col[i] >> kLowBits;
+      const uint32_t bk = col[i] >> kB;
       const uint64_t m = match_lanes(bk, bucket_bits, valid);
       const uint32_t rank = static_cast<uint32_t>(__popcll(m & below));
       const uint32_t n = static_cast<uint32_t>(__popcll(m));
@@ -300,7 +302,7 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
         wbase += dev::kWave;  // more than 64 row ends before some entry (empty rows)
         wend = window(wbase);
       }
-      const uint32_t bk = col[i] >> kLowBits;
+      const uint32_t bk = col[i] >> kB;
       const uint32_t rank = rk[i] & 0xFFu, n = rk[i] >> 8;
       const uint32_t before = valid ? cnt[w][bk] : 0u;
       dev::wave_sync();  // every lane has read its cursor
@@ -318,9 +320,9 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
     // positions of one bucket's run
     for (uint32_t j = threadIdx.x; j < nsub; j += kThreads) {
       const uint32_t c = s_col[j];
-      const uint32_t b = c >> kLowBits;
+      const uint32_t b = c >> kB;
       const uint64_t p = static_cast<uint64_t>(gcur[b]) + (j - lstart[b]);
-      t_key[p] = static_cast<uint16_t>(c & (kLow - 1u));
+      t_key[p] = static_cast<uint16_t>(c & ((1u << kB) - 1u));
       // (row, value) as one 8-byte pair: two store streams per sub-tile
       // instead of three, one load per entry in T4c
       if (value != nullptr) {
@@ -347,9 +349,11 @@ __device__ __forceinline__ void segment(const uint64_t* __restrict__ bstart, uin
   *end = b0 + n * static_cast<uint64_t>(s + 1) / kSegments;
 }
 
+template <int kB>
 __global__ __launch_bounds__(kThreads) void k_lowkey_hist(const uint16_t* __restrict__ t_key,
                                                           const uint64_t* __restrict__ bstart,
                                                           uint32_t* __restrict__ H) {
+  constexpr uint32_t kLow = 1u << kB;
   // counts need no order: the whole workgroup shares one histogram
   __shared__ uint32_t hist[kLow];
   const uint32_t b = blockIdx.x / kSegments;
@@ -389,10 +393,12 @@ __global__ __launch_bounds__(kThreads) void k_lowkey_hist(const uint16_t* __rest
  *  a segment row is one coalesced 1 KiB line run (round 4 walked 16
  *  consecutive columns per thread: 64-byte-strided lanes, 354 us); the scan
  *  over the bucket's columns runs on the LDS copy of the totals. */
+template <int kB>
 __global__ __launch_bounds__(kThreads) void k_lowkey_scan(uint32_t* __restrict__ H,
                                                           const uint64_t* __restrict__ bstart,
                                                           uint64_t num_features,
                                                           uint64_t* __restrict__ col_ptr) {
+  constexpr uint32_t kLow = 1u << kB;
   __shared__ uint32_t s_tot[kLow];  // column totals, then exclusive column starts (u32)
   __shared__ uint64_t swave[kWaves];
   constexpr uint32_t kPer = kLow / kThreads;  // columns per thread
@@ -456,11 +462,12 @@ constexpr int kScatterDepth = 8;  // T4c: 64-entry groups per batch (loads a bat
 // kPair: the output is interleaved (row, value) pairs -- one 8-byte store per
 // entry instead of a 4-byte store into each of two arrays (T4c is bound by
 // the output lines its scattered stores touch)
-template <bool kPair>
+template <bool kPair, int kB>
 __global__ __launch_bounds__(dev::kWave) void k_lowkey_scatter(
     const uint16_t* __restrict__ t_key, const uint32_t* __restrict__ t_row,
     const uint2* __restrict__ t_rv, const uint64_t* __restrict__ bstart,
     const uint32_t* __restrict__ H, uint32_t* __restrict__ row_out, float* __restrict__ val_out) {
+  constexpr uint32_t kLow = 1u << kB;
   __shared__ uint32_t cur[kLow];
   const uint32_t b = blockIdx.x / kSegments;
   const int s = static_cast<int>(blockIdx.x % kSegments);
@@ -505,7 +512,7 @@ __global__ __launch_bounds__(dev::kWave) void k_lowkey_scatter(
 #pragma unroll
     for (int j = 0; j < kScatterDepth; ++j) {
       const bool valid = at + static_cast<uint64_t>(j) * dev::kWave + lane < e1;
-      const uint64_t m = match_lanes(x.k[j], kLowBits, valid);
+      const uint64_t m = match_lanes(x.k[j], kB, valid);
       rk[j] = static_cast<uint32_t>(__popcll(m & below)) |
               (static_cast<uint32_t>(__popcll(m)) << 8);
     }
@@ -551,6 +558,7 @@ __global__ void k_transpose_close(const uint64_t* __restrict__ bstart, uint32_t 
 size_t AlignUp(size_t n) { return (n + 255) & ~size_t(255); }
 
 struct TransposePlan {
+  int low_bits;  // columns per bucket: 2^low_bits
   uint32_t nbuckets;
   int bucket_bits;
   size_t nblocks;
@@ -558,9 +566,30 @@ struct TransposePlan {
   size_t key_off, row_off, val_off, g_off, partials_off, h_off, chunk_off, total;
 };
 
+/*!
+ * \brief columns per bucket for a feature space: the narrowest of 2^10 ..
+ *  2^12 that keeps the buckets <= kMaxBuckets (DMLC_T_LOWBITS forces a
+ *  width that fits).  Narrower buckets shrink T4c's LDS cursor table (more
+ *  waves per CU) and its ballots, and widen T3's fan-out.
+ */
+int LowBits(uint64_t num_features) {
+  static const int forced = [] {
+    const char* v = std::getenv("DMLC_T_LOWBITS");
+    return v != nullptr ? std::atoi(v) : 0;
+  }();
+  auto fits = [&](int b) { return num_features <= (static_cast<uint64_t>(kMaxBuckets) << b); };
+  if (forced >= kMinLowBits && forced <= kMaxLowBits && fits(forced)) return forced;
+  for (int b = kDefaultLowBits; b < kMaxLowBits; ++b) {
+    if (fits(b)) return b;
+  }
+  return kMaxLowBits;
+}
+
 TransposePlan Plan(uint64_t nnz, uint64_t num_features) {
   TransposePlan p;
-  p.nbuckets = static_cast<uint32_t>((num_features + kLow - 1) / kLow);
+  p.low_bits = LowBits(num_features);
+  const uint64_t low = uint64_t(1) << p.low_bits;
+  p.nbuckets = static_cast<uint32_t>((num_features + low - 1) / low);
   if (p.nbuckets == 0) p.nbuckets = 1;
   p.bucket_bits = 0;
   while ((1u << p.bucket_bits) < p.nbuckets) ++p.bucket_bits;
@@ -568,7 +597,7 @@ TransposePlan Plan(uint64_t nnz, uint64_t num_features) {
   if (p.nblocks == 0) p.nblocks = 1;
   p.g_words = static_cast<size_t>(p.nbuckets) * p.nblocks + 1;  // + the bucket-end sentinel
   p.partials_words = ScanPartials(p.g_words) + 2;
-  p.h_words = static_cast<size_t>(p.nbuckets) * kSegments * kLow;
+  p.h_words = static_cast<size_t>(p.nbuckets) * kSegments * low;
   p.nchunks = (nnz + kChunk - 1) / kChunk;
   size_t off = 0;
   p.key_off = off;
@@ -597,25 +626,13 @@ __global__ void k_bucket_starts(const uint64_t* __restrict__ G, size_t nblocks, 
     bstart[b] = b < nbuckets ? G[static_cast<size_t>(b) * nblocks] : nnz;
   }
 }
-}  // namespace
 
-size_t CSRTransposeScratchBytes(uint64_t nnz, uint64_t num_features) {
-  // + the bucket-start table
-  return Plan(nnz, num_features).total + AlignUp((kMaxBuckets + 1) * sizeof(uint64_t));
-}
-
-uint64_t CSRTransposeMaxFeatures() { return static_cast<uint64_t>(kMaxBuckets) * kLow; }
-
-template <typename IndexType>
-void LaunchCSRTranspose(const uint64_t* offset, size_t nrows, uint64_t base, uint64_t nnz,
-                        const IndexType* index, const float* value, uint64_t num_features,
-                        uint64_t* col_ptr, uint32_t* row_out, float* val_out, void* scratch,
-                        uint32_t* error, hipStream_t stream) {
-  CHECK_GT(num_features, 0U);
-  CHECK_LE(num_features, CSRTransposeMaxFeatures()) << "transpose: num_features above the limit";
-  CHECK_LT(nnz, uint64_t(1) << 32) << "transpose: at most 2^32 - 1 entries";
-  CHECK_LT(nrows, size_t(1) << 32) << "transpose: at most 2^32 - 1 rows";
-  const TransposePlan p = Plan(nnz, num_features);
+/*! \brief T1 .. T4 at 2^kB columns per bucket */
+template <typename IndexType, int kB>
+void RunSort(const TransposePlan& p, const uint64_t* offset, size_t nrows, uint64_t base,
+             uint64_t nnz, const IndexType* index, const float* value, uint64_t num_features,
+             uint64_t* col_ptr, uint32_t* row_out, float* val_out, void* scratch,
+             uint32_t* error, hipStream_t stream) {
   char* sc = static_cast<char*>(scratch);
   uint16_t* t_key = reinterpret_cast<uint16_t*>(sc + p.key_off);
   // rows alone, or (row, value) pairs over the row + value regions (>= 8 nnz bytes)
@@ -631,8 +648,8 @@ void LaunchCSRTranspose(const uint64_t* offset, size_t nrows, uint64_t base, uin
   // T1 + T2
   DMLC_HIP_CHECK(hipMemsetAsync(G, 0, p.g_words * sizeof(uint64_t), stream));
   if (nnz != 0) {
-    hipLaunchKernelGGL(k_bucket_hist<IndexType>, dim3(p.nblocks), dim3(kThreads), 0, stream, idx,
-                       nnz, num_features, p.nbuckets, G, p.nblocks, error);
+    hipLaunchKernelGGL((k_bucket_hist<IndexType, kB>), dim3(p.nblocks), dim3(kThreads), 0, stream,
+                       idx, nnz, num_features, p.nbuckets, G, p.nblocks, error);
   }
   LaunchScanU64(G, p.g_words, partials, partials + p.partials_words - 1, stream);
   hipLaunchKernelGGL(k_bucket_starts, dim3((p.nbuckets + kThreads) / kThreads), dim3(kThreads), 0,
@@ -641,33 +658,61 @@ void LaunchCSRTranspose(const uint64_t* offset, size_t nrows, uint64_t base, uin
   if (nnz != 0) {
     hipLaunchKernelGGL(k_chunk_rows, dim3((p.nchunks + kThreads - 1) / kThreads), dim3(kThreads),
                        0, stream, offset, nrows, base, nnz, chunk_row);
-    hipLaunchKernelGGL(k_bucket_scatter<IndexType>, dim3(p.nblocks), dim3(kThreads), 0, stream,
-                       offset, nrows, base, idx, val, nnz, num_features, p.nbuckets,
+    hipLaunchKernelGGL((k_bucket_scatter<IndexType, kB>), dim3(p.nblocks), dim3(kThreads), 0,
+                       stream, offset, nrows, base, idx, val, nnz, num_features, p.nbuckets,
                        p.bucket_bits, G, p.nblocks, chunk_row, t_key, t_row, t_rv);
   }
   // T4
   const unsigned nseg = p.nbuckets * kSegments;
-  hipLaunchKernelGGL(k_lowkey_hist, dim3(nseg), dim3(kThreads), 0, stream, t_key, bstart, H);
-  hipLaunchKernelGGL(k_lowkey_scan, dim3(p.nbuckets), dim3(kThreads), 0, stream, H, bstart,
+  hipLaunchKernelGGL(k_lowkey_hist<kB>, dim3(nseg), dim3(kThreads), 0, stream, t_key, bstart, H);
+  hipLaunchKernelGGL(k_lowkey_scan<kB>, dim3(p.nbuckets), dim3(kThreads), 0, stream, H, bstart,
                      num_features, col_ptr);
   // (row, value) pairs when val_out is the float after row_out (8-byte aligned)
   const bool paired = val_out != nullptr && val_out == reinterpret_cast<float*>(row_out) + 1;
-  // pricing: extra LDS per T4c wave throttles how many run at once (the
-  // columns they keep open -- their write frontier -- shrink with them)
-  static const size_t t4c_lds = [] {
-    const char* v = std::getenv("DMLC_T4C_LDS");
-    return v != nullptr ? static_cast<size_t>(std::atoi(v)) : size_t(0);
-  }();
   if (paired) {
     CHECK_EQ(reinterpret_cast<uintptr_t>(row_out) & 7u, 0u) << "transpose: pair output not 8-byte aligned";
-    hipLaunchKernelGGL(k_lowkey_scatter<true>, dim3(nseg), dim3(dev::kWave), t4c_lds, stream,
+    hipLaunchKernelGGL((k_lowkey_scatter<true, kB>), dim3(nseg), dim3(dev::kWave), 0, stream,
                        t_key, t_row, t_rv, bstart, H, row_out, val_out);
   } else {
-    hipLaunchKernelGGL(k_lowkey_scatter<false>, dim3(nseg), dim3(dev::kWave), t4c_lds, stream,
+    hipLaunchKernelGGL((k_lowkey_scatter<false, kB>), dim3(nseg), dim3(dev::kWave), 0, stream,
                        t_key, t_row, t_rv, bstart, H, row_out, val_out);
   }
   hipLaunchKernelGGL(k_transpose_close, dim3(1), dim3(1), 0, stream, bstart, p.nbuckets,
                      num_features, col_ptr);
+}
+}  // namespace
+
+size_t CSRTransposeScratchBytes(uint64_t nnz, uint64_t num_features) {
+  // + the bucket-start table
+  return Plan(nnz, num_features).total + AlignUp((kMaxBuckets + 1) * sizeof(uint64_t));
+}
+
+uint64_t CSRTransposeMaxFeatures() { return static_cast<uint64_t>(kMaxBuckets) << kMaxLowBits; }
+
+template <typename IndexType>
+void LaunchCSRTranspose(const uint64_t* offset, size_t nrows, uint64_t base, uint64_t nnz,
+                        const IndexType* index, const float* value, uint64_t num_features,
+                        uint64_t* col_ptr, uint32_t* row_out, float* val_out, void* scratch,
+                        uint32_t* error, hipStream_t stream) {
+  CHECK_GT(num_features, 0U);
+  CHECK_LE(num_features, CSRTransposeMaxFeatures()) << "transpose: num_features above the limit";
+  CHECK_LT(nnz, uint64_t(1) << 32) << "transpose: at most 2^32 - 1 entries";
+  CHECK_LT(nrows, size_t(1) << 32) << "transpose: at most 2^32 - 1 rows";
+  const TransposePlan p = Plan(nnz, num_features);
+  switch (p.low_bits) {
+    case 10:
+      RunSort<IndexType, 10>(p, offset, nrows, base, nnz, index, value, num_features, col_ptr,
+                             row_out, val_out, scratch, error, stream);
+      break;
+    case 11:
+      RunSort<IndexType, 11>(p, offset, nrows, base, nnz, index, value, num_features, col_ptr,
+                             row_out, val_out, scratch, error, stream);
+      break;
+    default:
+      RunSort<IndexType, 12>(p, offset, nrows, base, nnz, index, value, num_features, col_ptr,
+                             row_out, val_out, scratch, error, stream);
+      break;
+  }
 }
 
 template void LaunchCSRTranspose<uint32_t>(const uint64_t*, size_t, uint64_t, uint64_t,
