@@ -55,7 +55,7 @@ constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / dev::kWave;
 constexpr int kMinLowBits = 10;  // columns per bucket: 2^kB, kB = 10 .. 12 (LowBits)
 constexpr int kMaxLowBits = 12;
-constexpr int kDefaultLowBits = 12;  // the narrowest width tried by default
+constexpr int kDefaultLowBits = kMinLowBits;
 constexpr uint32_t kMaxBuckets = 1024;
 constexpr uint32_t kSubElems = 3072;        // T3 sub-tile, sorted in LDS (3 workgroups / CU)
 constexpr size_t kBlockElems = 10 * kSubElems;  // T1 / T3 block (per workgroup)
@@ -457,12 +457,12 @@ __global__ __launch_bounds__(kThreads) void k_lowkey_scan(uint32_t* __restrict__
   }
 }
 
-constexpr int kScatterDepth = 8;  // T4c: 64-entry groups per batch (loads a batch ahead)
 
 // kPair: the output is interleaved (row, value) pairs -- one 8-byte store per
 // entry instead of a 4-byte store into each of two arrays (T4c is bound by
 // the output lines its scattered stores touch)
-template <bool kPair, int kB>
+// kDepth: 64-entry groups per batch (loads a batch ahead; 8: 74 VGPRs -- 4 took 89)
+template <bool kPair, int kB, int kDepth>
 __global__ __launch_bounds__(dev::kWave) void k_lowkey_scatter(
     const uint16_t* __restrict__ t_key, const uint32_t* __restrict__ t_row,
     const uint2* __restrict__ t_rv, const uint64_t* __restrict__ bstart,
@@ -479,19 +479,19 @@ __global__ __launch_bounds__(dev::kWave) void k_lowkey_scatter(
   segment(bstart, b, s, &e0, &e1);
   const uint64_t base = bstart[b];
   const uint64_t below = lanes_below();
-  // The segment walks in batches of kScatterDepth groups of 64 consecutive
+  // The segment walks in batches of kDepth groups of 64 consecutive
   // entries (group j of a batch: entries + 64 j + lane, so groups stay in
   // entry order).  A batch's loads are issued a whole batch ahead, into the
   // other register set: a wave keeps 8 x 64 entries in flight instead of one
   // group (the round-4 kernel waited out the memory latency every 64
   // entries, at 10 waves per CU -- 72 % of its cycles waiting)
   struct Batch {
-    uint32_t k[kScatterDepth], r[kScatterDepth];
-    float v[kScatterDepth];
+    uint32_t k[kDepth], r[kDepth];
+    float v[kDepth];
   };
   auto load = [&](uint64_t at, Batch* x) {
 #pragma unroll
-    for (int j = 0; j < kScatterDepth; ++j) {
+    for (int j = 0; j < kDepth; ++j) {
       const uint64_t e = at + static_cast<uint64_t>(j) * dev::kWave + lane;
       const bool ok = e < e1;
       x->k[j] = ok ? t_key[e] : 0u;
@@ -508,16 +508,16 @@ __global__ __launch_bounds__(dev::kWave) void k_lowkey_scatter(
   auto process = [&](uint64_t at, const Batch& x) {
     // the ranks need no LDS: every group's ballots first, then the cursor
     // updates group by group (the only dependent chain)
-    uint32_t rk[kScatterDepth];
+    uint32_t rk[kDepth];
 #pragma unroll
-    for (int j = 0; j < kScatterDepth; ++j) {
+    for (int j = 0; j < kDepth; ++j) {
       const bool valid = at + static_cast<uint64_t>(j) * dev::kWave + lane < e1;
       const uint64_t m = match_lanes(x.k[j], kB, valid);
       rk[j] = static_cast<uint32_t>(__popcll(m & below)) |
               (static_cast<uint32_t>(__popcll(m)) << 8);
     }
 #pragma unroll
-    for (int j = 0; j < kScatterDepth; ++j) {
+    for (int j = 0; j < kDepth; ++j) {
       const uint64_t g = at + static_cast<uint64_t>(j) * dev::kWave;
       if (g >= e1) break;  // wave-uniform
       const bool valid = g + lane < e1;
@@ -538,7 +538,7 @@ __global__ __launch_bounds__(dev::kWave) void k_lowkey_scatter(
       dev::wave_sync();
     }
   };
-  constexpr uint64_t kBatch = static_cast<uint64_t>(kScatterDepth) * dev::kWave;
+  constexpr uint64_t kBatch = static_cast<uint64_t>(kDepth) * dev::kWave;
   Batch A, B;
   load(e0, &A);
   for (uint64_t at = e0; at < e1; at += 2 * kBatch) {
@@ -671,10 +671,10 @@ void RunSort(const TransposePlan& p, const uint64_t* offset, size_t nrows, uint6
   const bool paired = val_out != nullptr && val_out == reinterpret_cast<float*>(row_out) + 1;
   if (paired) {
     CHECK_EQ(reinterpret_cast<uintptr_t>(row_out) & 7u, 0u) << "transpose: pair output not 8-byte aligned";
-    hipLaunchKernelGGL((k_lowkey_scatter<true, kB>), dim3(nseg), dim3(dev::kWave), 0, stream,
+    hipLaunchKernelGGL((k_lowkey_scatter<true, kB, 8>), dim3(nseg), dim3(dev::kWave), 0, stream,
                        t_key, t_row, t_rv, bstart, H, row_out, val_out);
   } else {
-    hipLaunchKernelGGL((k_lowkey_scatter<false, kB>), dim3(nseg), dim3(dev::kWave), 0, stream,
+    hipLaunchKernelGGL((k_lowkey_scatter<false, kB, 8>), dim3(nseg), dim3(dev::kWave), 0, stream,
                        t_key, t_row, t_rv, bstart, H, row_out, val_out);
   }
   hipLaunchKernelGGL(k_transpose_close, dim3(1), dim3(1), 0, stream, bstart, p.nbuckets,
