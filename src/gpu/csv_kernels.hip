@@ -390,8 +390,10 @@ __device__ __noinline__ GenericField generic_field(const char* q, const char* en
   return r;
 }
 
+// 6 waves per SIMD (the LDS allows 6 workgroups per CU): <= 84 VGPRs
 template <typename IndexType>
-__global__ __launch_bounds__(kThreads) void k_csv_tile_fill(const uint8_t* __restrict__ text,
+__global__ __launch_bounds__(kThreads)
+__attribute__((amdgpu_waves_per_eu(6))) void k_csv_tile_fill(const uint8_t* __restrict__ text,
                                                             size_t n, size_t ntiles, CsvCfg cfg,
                                                             const uint64_t* __restrict__ prefix,
                                                             FillTarget<IndexType> out,
@@ -410,6 +412,19 @@ __global__ __launch_bounds__(kThreads) void k_csv_tile_fill(const uint8_t* __res
   const uint64_t pre = prefix[tile];
   const uint64_t R = out.row_base + (pre >> 32);          // the tile's first row
   const uint64_t C = out.nnz_base + (pre & 0xffffffffull);  // and first entry
+  // outputs addressed from the tile's first row / entry, rooms clamped to
+  // int32 (a tile's rows and entries are < 2^16): 32-bit compares per field
+  // and fewer live 64-bit scalars in the round loop
+  auto room32 = [](uint64_t limit, uint64_t at) {
+    return limit <= at ? 0 : (limit - at > 0x7FFFFFFFull ? 0x7FFFFFFF : static_cast<int32_t>(limit - at));
+  };
+  const int32_t row_room = room32(out.row_limit, R);
+  const int32_t nnz_room = room32(out.nnz_limit, C);
+  float* const lab_at = out.label + R;
+  float* const wgt_at = out.weight + R;  // (used only with has_weight: allocated)
+  uint64_t* const off_at = out.offset + R;
+  IndexType* const idx_at = out.index + C;
+  float* const val_at = out.value + C;
   Walk w{};
   w.carry_eol = 1u;
   if (tile0 != 0) {
@@ -525,39 +540,38 @@ __global__ __launch_bounds__(kThreads) void k_csv_tile_fill(const uint8_t* __res
             last = g.last;
           }
         }
-        const uint64_t row = R + row_t;
         // S1p: the prefix counts entries by position; the tile's own start
-        // after the rest of the previous tile's last row
-        const uint64_t e = C + ent + (cfg.pos ? w.pre : 0u);
+        // after the rest of the previous tile's last row (e: entry in the tile)
+        const uint32_t e = ent + (cfg.pos ? w.pre : 0u);
         if (exp & 2u) {  // pricing: no stores (a value sink the compiler keeps)
           mx = __float_as_uint(v) == 0x7FC00001u ? mx + 1 : mx;
-        } else if (row >= out.row_limit) {
+        } else if (static_cast<int32_t>(row_t) >= row_room) {
           irregular = true;
         } else {
           if (static_cast<int>(col) == cfg.label_col) {
-            out.label[row] = v;
+            lab_at[row_t] = v;
           } else if (static_cast<int>(col) == cfg.weight_col) {
-            out.weight[row] = v;
-          } else if (e < out.nnz_limit) {
+            wgt_at[row_t] = v;
+          } else if (static_cast<int32_t>(e) < nnz_room) {
             uint32_t idx = col;
             idx -= (cfg.label_col >= 0 && col > static_cast<uint32_t>(cfg.label_col)) ? 1u : 0u;
             idx -= (cfg.weight_col >= 0 && col > static_cast<uint32_t>(cfg.weight_col)) ? 1u : 0u;
-            out.index[e] = static_cast<IndexType>(idx);
-            out.value[e] = v;
+            idx_at[e] = static_cast<IndexType>(idx);
+            val_at[e] = v;
             mx = idx > mx ? idx : mx;
             any_value = true;
           } else {
             irregular = true;
           }
           if (col == 0) {
-            out.offset[row] = e;
-            if (cfg.label_col < 0) out.label[row] = 0.0f;
+            off_at[row_t] = C + e;
+            if (cfg.label_col < 0) lab_at[row_t] = 0.0f;
           }
           if (last) {
             // a short row: no label / weight field
-            if (cfg.label_col >= 0 && col < static_cast<uint32_t>(cfg.label_col)) out.label[row] = 0.0f;
+            if (cfg.label_col >= 0 && col < static_cast<uint32_t>(cfg.label_col)) lab_at[row_t] = 0.0f;
             if (cfg.has_weight && (cfg.weight_col < 0 || col < static_cast<uint32_t>(cfg.weight_col))) {
-              out.weight[row] = 1.0f;
+              wgt_at[row_t] = 1.0f;
             }
           }
         }

@@ -11,7 +11,7 @@
  *  Column c = (bucket c >> kB, low key c & (L - 1)), L = 2^kB columns per
  *  bucket (kB = 10 .. 12, LowBits: the narrowest that keeps at most
  *  kMaxBuckets buckets, so feature ids < 2^22):
- *   T1 k_bucket_hist  one workgroup per block of kBlockElems entries (in CSR
+ *   T1 k_bucket_hist  one workgroup per block of BlockSubs() sub-tiles (in CSR
  *      order): LDS histogram of buckets -> G[bucket][block].
  *   T2 exclusive scan of G (bucket-major): where each (bucket, block) run
  *      lands in the bucket-ordered intermediate arrays.
@@ -57,8 +57,8 @@ constexpr int kMinLowBits = 10;  // columns per bucket: 2^kB, kB = 10 .. 12 (Low
 constexpr int kMaxLowBits = 12;
 constexpr int kDefaultLowBits = kMinLowBits;
 constexpr uint32_t kMaxBuckets = 1024;
-constexpr uint32_t kSubElems = 3072;        // T3 sub-tile, sorted in LDS (3 workgroups / CU)
-constexpr size_t kBlockElems = 10 * kSubElems;  // T1 / T3 block (per workgroup)
+constexpr uint32_t kSubElems = 2048;        // T3 sub-tile, sorted in LDS (4 workgroups / CU)
+constexpr int kBlockSubs = 15;  // sub-tiles per T1 / T3 block (a workgroup), BlockSubs()
 constexpr uint32_t kChunk = kSubElems / kWaves;  // entries per wave per sub-tile
 constexpr int kPerLane = kChunk / dev::kWave;
 constexpr int kSegments = 16;              // T4 segments per bucket
@@ -107,13 +107,13 @@ __global__ __launch_bounds__(kThreads) void k_bucket_hist(const IndexType* __res
                                                           uint64_t nnz, uint64_t num_features,
                                                           uint32_t nbuckets,
                                                           uint64_t* __restrict__ G,
-                                                          size_t nblocks,
+                                                          size_t nblocks, uint64_t block_elems,
                                                           uint32_t* __restrict__ error) {
   __shared__ uint32_t hist[kMaxBuckets];
   for (uint32_t b = threadIdx.x; b < nbuckets; b += kThreads) hist[b] = 0;
   __syncthreads();
-  const uint64_t e0 = static_cast<uint64_t>(blockIdx.x) * kBlockElems;
-  const uint64_t e1 = e0 + kBlockElems < nnz ? e0 + kBlockElems : nnz;
+  const uint64_t e0 = static_cast<uint64_t>(blockIdx.x) * block_elems;
+  const uint64_t e1 = e0 + block_elems < nnz ? e0 + block_elems : nnz;
   bool bad = false;
   auto add = [&](IndexType c) {
     bad |= static_cast<uint64_t>(c) >= num_features;
@@ -121,7 +121,7 @@ __global__ __launch_bounds__(kThreads) void k_bucket_hist(const IndexType* __res
   };
   uint64_t e = e0 + threadIdx.x;
   if (sizeof(IndexType) == 4 && (reinterpret_cast<uintptr_t>(index + e0) & 15u) == 0) {
-    // four ids per 16-byte load (kBlockElems is a multiple of 4): a quarter
+    // four ids per 16-byte load (block_elems is a multiple of 4): a quarter
     // of the load instructions of the one-id-per-lane walk
     const uint64_t n4 = (e1 - e0) / 4;
     const uint4* q = reinterpret_cast<const uint4*>(index + e0);
@@ -155,7 +155,7 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
     const uint64_t* __restrict__ offset, size_t nrows, uint64_t base,
     const IndexType* __restrict__ index, const float* __restrict__ value, uint64_t nnz,
     uint64_t num_features, uint32_t nbuckets, int bucket_bits, const uint64_t* __restrict__ G,
-    size_t nblocks, const uint32_t* __restrict__ chunk_row,
+    size_t nblocks, uint64_t block_elems, const uint32_t* __restrict__ chunk_row,
     uint16_t* __restrict__ t_key, uint32_t* __restrict__ t_row, uint2* __restrict__ t_rv) {
   // the sub-tile, sorted by (bucket, position) in LDS before it leaves
   __shared__ uint32_t s_col[kSubElems];
@@ -176,8 +176,8 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
     gcur[b] = static_cast<uint32_t>(G[static_cast<size_t>(b) * nblocks + blockIdx.x]);
   }
   __syncthreads();
-  const uint64_t blk0 = static_cast<uint64_t>(blockIdx.x) * kBlockElems;
-  const uint64_t blk1 = blk0 + kBlockElems < nnz ? blk0 + kBlockElems : nnz;
+  const uint64_t blk0 = static_cast<uint64_t>(blockIdx.x) * block_elems;
+  const uint64_t blk1 = blk0 + block_elems < nnz ? blk0 + block_elems : nnz;
   // the next sub-tile's entries (and its chunk's first row) are loaded while
   // this one is sorted: a wave waits for memory once per block, not once per
   // sub-tile (round 4: 71 % of the cycles waiting)
@@ -559,6 +559,7 @@ size_t AlignUp(size_t n) { return (n + 255) & ~size_t(255); }
 
 struct TransposePlan {
   int low_bits;  // columns per bucket: 2^low_bits
+  uint64_t block_elems;  // entries per T1 / T3 block
   uint32_t nbuckets;
   int bucket_bits;
   size_t nblocks;
@@ -585,6 +586,17 @@ int LowBits(uint64_t num_features) {
   return kMaxLowBits;
 }
 
+/*! \brief sub-tiles per T1 / T3 block (DMLC_T_BLOCK_SUBS overrides, 1 .. 64):
+ *  fewer blocks shrink G (buckets x blocks, written by T1 column by column) */
+int BlockSubs() {
+  static const int subs = [] {
+    const char* v = std::getenv("DMLC_T_BLOCK_SUBS");
+    const int k = v != nullptr ? std::atoi(v) : 0;
+    return k >= 1 && k <= 64 ? k : kBlockSubs;
+  }();
+  return subs;
+}
+
 TransposePlan Plan(uint64_t nnz, uint64_t num_features) {
   TransposePlan p;
   p.low_bits = LowBits(num_features);
@@ -593,7 +605,8 @@ TransposePlan Plan(uint64_t nnz, uint64_t num_features) {
   if (p.nbuckets == 0) p.nbuckets = 1;
   p.bucket_bits = 0;
   while ((1u << p.bucket_bits) < p.nbuckets) ++p.bucket_bits;
-  p.nblocks = (nnz + kBlockElems - 1) / kBlockElems;
+  p.block_elems = static_cast<uint64_t>(BlockSubs()) * kSubElems;
+  p.nblocks = (nnz + p.block_elems - 1) / p.block_elems;
   if (p.nblocks == 0) p.nblocks = 1;
   p.g_words = static_cast<size_t>(p.nbuckets) * p.nblocks + 1;  // + the bucket-end sentinel
   p.partials_words = ScanPartials(p.g_words) + 2;
@@ -649,7 +662,7 @@ void RunSort(const TransposePlan& p, const uint64_t* offset, size_t nrows, uint6
   DMLC_HIP_CHECK(hipMemsetAsync(G, 0, p.g_words * sizeof(uint64_t), stream));
   if (nnz != 0) {
     hipLaunchKernelGGL((k_bucket_hist<IndexType, kB>), dim3(p.nblocks), dim3(kThreads), 0, stream,
-                       idx, nnz, num_features, p.nbuckets, G, p.nblocks, error);
+                       idx, nnz, num_features, p.nbuckets, G, p.nblocks, p.block_elems, error);
   }
   LaunchScanU64(G, p.g_words, partials, partials + p.partials_words - 1, stream);
   hipLaunchKernelGGL(k_bucket_starts, dim3((p.nbuckets + kThreads) / kThreads), dim3(kThreads), 0,
@@ -660,7 +673,8 @@ void RunSort(const TransposePlan& p, const uint64_t* offset, size_t nrows, uint6
                        0, stream, offset, nrows, base, nnz, chunk_row);
     hipLaunchKernelGGL((k_bucket_scatter<IndexType, kB>), dim3(p.nblocks), dim3(kThreads), 0,
                        stream, offset, nrows, base, idx, val, nnz, num_features, p.nbuckets,
-                       p.bucket_bits, G, p.nblocks, chunk_row, t_key, t_row, t_rv);
+                       p.bucket_bits, G, p.nblocks, p.block_elems, chunk_row, t_key, t_row,
+                       t_rv);
   }
   // T4
   const unsigned nseg = p.nbuckets * kSegments;
