@@ -40,10 +40,11 @@ struct DeviceRecordIOConfig {
   /*!
    * \brief keep the partition's bytes resident in HBM after the first epoch
    *  and decode later epochs from there (adjacent chunks merged up to
-   *  replay_chunk_bytes)
+   *  replay_chunk_bytes: 2 GiB, so a resident epoch of ~2 GB pays one scan /
+   *  finish / host turnaround; < 4 GiB for the 32-bit in-chunk byte offsets)
    */
   bool hbm_cache{false};
-  size_t replay_chunk_bytes{1UL << 30};
+  size_t replay_chunk_bytes{2UL << 30};
   /*!
    * \brief ReadAll over the HBM cache decodes each merged chunk in ONE launch
    *  (R1 inside the fill, decoupled look-back; the text is read once) instead

@@ -41,19 +41,6 @@ __device__ __forceinline__ uint32_t lane_shl1(uint32_t x) {
       __builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x130, 0xF, 0xF, false));
 }
 
-/*!
- * \brief p held in VGPRs from here on: for a base pointer used once per row,
- *  not per token, in a kernel at the SGPR limit -- its two SGPRs go to the
- *  hot loop instead of a v_writelane / v_readlane spill
- */
-template <typename T>
-__device__ __forceinline__ T* in_vgprs(T* p) {
-  const uint64_t v = reinterpret_cast<uint64_t>(p);
-  uint32_t lo = static_cast<uint32_t>(v), hi = static_cast<uint32_t>(v >> 32);
-  asm("" : "+v"(lo), "+v"(hi));
-  return reinterpret_cast<T*>((static_cast<uint64_t>(hi) << 32) | lo);
-}
-
 /*! \brief x of lane 63, as a scalar (uniform to the compiler) */
 __device__ __forceinline__ uint32_t lane63(uint32_t x) {
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), 63));

@@ -1147,12 +1147,10 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
   IndexType* const idx_at = out.index + C;
   float* const val_at = out.value + C;
   IndexType* const fld_at = out.field != nullptr ? out.field + C : nullptr;
-  // per-row outputs (a store per line, not per token): VGPR bases, so the
-  // kernel's SGPRs serve the token loop
-  float* const lab_at = dev::in_vgprs(out.label + R - 1);
-  uint64_t* const off_at = dev::in_vgprs(out.offset + R - 1);
-  float* const wgt_at = out.weight != nullptr ? dev::in_vgprs(out.weight + R - 1) : nullptr;
-  uint64_t* const qid_at = out.qid != nullptr ? dev::in_vgprs(out.qid + R - 1) : nullptr;
+  float* const lab_at = out.label + R - 1;
+  uint64_t* const off_at = out.offset + R - 1;
+  float* const wgt_at = out.weight != nullptr ? out.weight + R - 1 : nullptr;
+  uint64_t* const qid_at = out.qid != nullptr ? out.qid + R - 1 : nullptr;
   // the count pass saw 'q' token starts in this chunk (the host then enables
   // the qid column): only such chunks look for `qid:` tokens
   const bool qid_chunk = F == TextFormat::kLibSVM && out.qid != nullptr;
