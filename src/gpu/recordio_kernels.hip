@@ -16,7 +16,7 @@
  * of (record heads, output bytes) every part knows where its bytes go,
  * without walking chains:
  *
- *   R1 k_rec_tile_count: one wave per 2048-word (8 KiB) tile, 8 coalesced
+ *   R1 k_rec_tile_count: one wave per 1024-word (4 KiB) tile, 4 coalesced
  *      16 B loads per lane in flight; (heads << 32 | bytes) per tile and
  *      error bits (a part running past the chunk, a bad cflag).
  *   C2 (tile_kernels.hip, raw mode): exclusive scan, totals published.
@@ -53,13 +53,13 @@ using namespace dev;  // NOLINT(build/namespaces)
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr uint32_t kMagic = 0xced7230aU;
-constexpr size_t kTileWords = 2048;  // 8 loads x 64 lanes x 4 words
+constexpr size_t kTileWords = 1024;  // 4 loads x 64 lanes x 4 words
 constexpr int kLoads = static_cast<int>(kTileWords / 256);
 constexpr uint32_t kSmallPart = 64;  // bytes copied lane-by-lane
 // parts > 64 B whose header lies in a tile: headers >= 19 words apart (2 + 17),
-// so at most 108 in 2048 words.  112 keeps the fill at 40 KiB of LDS per
-// workgroup: 4 workgroups per CU (kTileWords / 16 = 128 made it 3)
-constexpr int kBigCap = 112;
+// so at most 54 in 1024 words.  4 KiB tiles keep the fill at 20 KiB of LDS
+// and 68 VGPRs per wave: 7 waves per SIMD (8 KiB tiles: 40 KiB, 88 VGPRs, 4)
+constexpr int kBigCap = 56;
 static_assert(kBigCap * 19 >= static_cast<int>(kTileWords) + 19, "kBigCap too small");
 
 __device__ __forceinline__ uint32_t cflag_of(uint32_t lrec) { return lrec >> 29; }
@@ -542,7 +542,7 @@ void LaunchRecordIOTileCountChain(const uint32_t* words, size_t nwords, uint64_t
                                   uint32_t* tile_flags, hipStream_t stream) {
   const size_t tiles = RecordIOTiles(nwords);
   if (tiles == 0) return;
-  // large pieces (counted beside a fill): up to 8 tiles per lane, so the
+  // large pieces (counted beside a fill): up to 16 tiles per lane, so the
   // latency-bound chain waves hold few CU slots; small ones: a lane per tile
   // (DMLC_REC_CHAIN_TILES forces a tiles-per-lane value: the tests' small
   // chunks exercise the multi-tile walk with it)
@@ -550,9 +550,10 @@ void LaunchRecordIOTileCountChain(const uint32_t* words, size_t nwords, uint64_t
     const char* v = std::getenv("DMLC_REC_CHAIN_TILES");
     return v != nullptr ? static_cast<size_t>(std::atoi(v)) : size_t(0);
   }();
-  const size_t per = forced != 0 ? forced
-                     : tiles >= 8 * 16384 ? 8
-                     : (tiles >= 4 * 16384 ? 4 : (tiles >= 2 * 16384 ? 2 : 1));
+  // (64 KiB of text per lane on pieces of >= 1 GiB)
+  size_t per = 1;
+  while (per < 16 && tiles >= per * 2 * 16384) per *= 2;
+  if (forced != 0) per = forced;
   const size_t lanes = (tiles + per - 1) / per;
   hipLaunchKernelGGL(k_rec_tile_count_chain, dim3((lanes + kThreads - 1) / kThreads),
                      dim3(kThreads), 0, stream, words, nwords, tiles, static_cast<uint32_t>(per),
