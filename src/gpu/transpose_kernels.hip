@@ -74,6 +74,7 @@ __device__ __forceinline__ uint32_t column(IndexType c, uint64_t num_features) {
 /*! \brief lanes of this wave whose `key` (low `bits` bits) equals mine, among `valid` */
 __device__ __forceinline__ uint64_t match_lanes(uint32_t key, int bits, bool valid) {
   uint64_t m = __ballot(valid);
+#pragma unroll 1
   for (int i = 0; i < bits; ++i) {
     const bool b = (key >> i) & 1u;
     const uint64_t v = __ballot(b);
@@ -515,6 +516,10 @@ __global__ __launch_bounds__(dev::kWave) void k_lowkey_scatter(
       const uint64_t m = match_lanes(x.k[j], kB, valid);
       rk[j] = static_cast<uint32_t>(__popcll(m & below)) |
               (static_cast<uint32_t>(__popcll(m)) << 8);
+      // one group's ballots at a time: interleaved, the kB ballots of all
+      // kDepth groups (64-bit SGPR pairs) overflowed the SGPRs into hundreds
+      // of v_writelane / v_readlane spills
+      __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int j = 0; j < kDepth; ++j) {
