@@ -169,6 +169,7 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
   __shared__ uint16_t lstart[kMaxBuckets + 2];
   __shared__ uint32_t gcur[kMaxBuckets];
   __shared__ uint32_t swave[kWaves];
+  __shared__ uint32_t s_ends[kWaves][dev::kWave];  // row ends per group position
   const int w = threadIdx.x / dev::kWave;
   const int lane = dev::lane_id();
   const uint64_t below = lanes_below();
@@ -270,9 +271,12 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
     // ---- rank every group into the LDS sub-tile.  Rows: lane i holds the end
     // of row wbase + i (one coalesced load of 64 row ends, from the chunk's
     // first row); an entry's row is wbase + the number of those ends at or
-    // before it (a binary search over the lanes).  The window only moves
-    // forward (rows are monotone in entry order), reloaded when a group runs
-    // past its 64 rows -- not a dependent global load per group
+    // before it: each end is counted at its position in the group (an LDS
+    // add; empty rows stack on one position) and a DPP scan over the
+    // positions gives every entry its count -- two LDS trips per group
+    // instead of a chain of six bpermutes (a binary search over the lanes).
+    // The window only moves forward (rows are monotone in entry order),
+    // reloaded when a group runs past its 64 rows
 #pragma unroll
     for (int i = 0; i < kPerLane; ++i) {
       const uint64_t g = c0 + static_cast<uint64_t>(i) * dev::kWave;
@@ -287,14 +291,14 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
         const uint32_t rel = wend <= g ? 0u
                              : wend - g >= 0xFFFFFFFFull ? 0xFFFFFFFFu
                                                          : static_cast<uint32_t>(wend - g);
-        uint32_t n = 0;  // lanes [0, n) have rel <= pos
-#pragma unroll
-        for (uint32_t step = 32; step >= 1; step >>= 1) {
-          const uint32_t probe = __shfl(rel, static_cast<int>(n + step - 1), dev::kWave);
-          if (probe <= pos) n += step;
-        }
-        const uint32_t last = __shfl(rel, dev::kWave - 1, dev::kWave);
-        if (n == dev::kWave - 1 && last <= pos) n = dev::kWave;
+        uint32_t* const ends = s_ends[w];
+        ends[lane] = 0u;
+        dev::wave_sync();
+        if (rel < static_cast<uint32_t>(dev::kWave)) atomicAdd(&ends[rel], 1u);
+        dev::wave_sync();
+        // ends at or before position pos (64: the whole window ends before it)
+        const uint32_t n = dev::wave_incl_scan_u32(ends[pos]);
+        dev::wave_sync();  // every lane has read its count before the next reset
         if (!found && n < static_cast<uint32_t>(dev::kWave)) {
           row = wbase + n;
           found = true;

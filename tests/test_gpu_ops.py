@@ -257,6 +257,30 @@ def test_spmv_over_pairs_matches_separate_arrays(csr_t):
         ops.spmv_t(tt, torch.randn(nfeat, device="cuda"), csr.rows)
 
 
+def test_transpose_with_long_runs_of_empty_rows():
+    """rows found for entries after > 64 empty rows (the T3 row window moves
+    on past them) and after rows that end exactly at group boundaries: the
+    CSC equals numpy's stable argsort"""
+    import torch
+    rng = np.random.default_rng(11)
+    lens = rng.integers(1, 9, size=5000)
+    lens[100:400] = 0          # 300 empty rows in a row
+    lens[1000:1065] = 0        # exactly 65
+    lens[2000:2064] = 0        # exactly 64
+    lens[3000] = 64            # a row of exactly one 64-entry group
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    nfeat = 3000
+    idx = rng.integers(0, nfeat, size=int(off[-1])).astype(np.int32)
+    val = rng.standard_normal(int(off[-1])).astype(np.float32)
+    t = {"offset": torch.from_numpy(off).cuda(), "index": torch.from_numpy(idx).cuda(),
+         "value": torch.from_numpy(val).cuda()}
+    tt = ops.transpose(t, nfeat)
+    ptr, r, v = _ref_transpose(t, nfeat)
+    np.testing.assert_array_equal(tt["offset"].cpu().numpy(), ptr)
+    np.testing.assert_array_equal(tt["index"].cpu().numpy(), r)
+    np.testing.assert_array_equal(tt["value"].cpu().numpy(), v)
+
+
 def test_transpose_rejects_out_of_range_ids(csr_t):
     t, csr = csr_t
     with pytest.raises(ValueError, match="num_features"):
