@@ -73,6 +73,18 @@ def _check(csr: Dict, pairs: bool = False):
         raise ValueError("csr['value'] must be contiguous")
 
 
+def _unpair(csr: Dict) -> Dict:
+    """a transpose's interleaved (index, value) pair views as separate
+    contiguous arrays, for the kernels that take only contiguous CSR arrays
+    (any other dict is returned as it is)"""
+    if not _paired(csr):
+        return csr
+    out = dict(csr)
+    out["index"], out["value"] = csr["index"].contiguous(), csr["value"].contiguous()
+    out.pop("pairs", None)
+    return out
+
+
 def _stream() -> int:
     return int(torch.cuda.current_stream().cuda_stream)
 
@@ -90,7 +102,9 @@ def spmv(csr: Dict, w: torch.Tensor, bias: float = 0.0) -> torch.Tensor:
 
 
 def spmv_t(csr: Dict, d: torch.Tensor, num_features: int) -> torch.Tensor:
-    """g[index[j]] += value[j] * d[row(j)]  (transposed K11, f32 atomics)."""
+    """g[index[j]] += value[j] * d[row(j)]  (transposed K11, f32 atomics).
+    A transpose's pair views are unpaired into contiguous copies first."""
+    csr = _unpair(csr)
     _check(csr)
     assert d.dtype == torch.float32 and d.is_cuda and d.is_contiguous()
     g = torch.zeros(num_features, dtype=torch.float32, device=d.device)
@@ -107,6 +121,7 @@ def hashed_dense(csr: Dict, dim: int, seed: int = 0, fp8: bool = True,
     Returns float8_e4m3fn [rows, dim] (gfx950 OCP fp8, hardware conversion)
     when ``fp8`` else float32.  LibFM fields are folded into the hash key.
     """
+    csr = _unpair(csr)
     _check(csr)
     nrows = csr["offset"].numel() - 1
     dev = csr["index"].device
@@ -147,7 +162,9 @@ def transpose(csr: Dict, num_features: int, out: Optional[Dict] = None) -> Dict:
     The sort's scratch (~10 bytes per entry) is a persistent per-device,
     per-stream workspace (:func:`release_workspace` frees it).  ``out``: a
     previous result of the same shape to overwrite instead of allocating
-    the outputs (its ``index`` / ``value`` need at least nnz entries)."""
+    the outputs (its ``index`` / ``value`` need at least nnz entries).  The
+    input may itself be a transpose (its pair views are unpaired first)."""
+    csr = _unpair(csr)
     _check(csr)
     offset, index, value = csr["offset"], csr["index"], csr.get("value")
     nrows, dev = offset.numel() - 1, index.device

@@ -77,6 +77,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--kube-server-image", default="rocm/pytorch", type=str)
     p.add_argument("--kube-worker-template", default=None, type=str)
     p.add_argument("--kube-server-template", default=None, type=str)
+    p.add_argument("--kube-pod-per-rank", default=False, type=_bool,
+                   help="kubernetes + --gpus-per-node: one pod (1 GPU) per rank instead of "
+                        "one pod per node running --gpus-per-node ranks")
     # MI355X additions
     p.add_argument("--gpus-per-node", default=0, type=int,
                    help="bind one process per GPU (DMLC_LOCAL_RANK = local index)")

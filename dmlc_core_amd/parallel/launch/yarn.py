@@ -6,10 +6,13 @@ The reference submits through its own Java ApplicationMaster
 backend needs no JVM and no jar: the ResourceManager's YARN Services REST API
 (``$YARN_RM_ADDRESS``, Hadoop >= 3.1) runs the containers and the AM's
 per-task policy runs here, in `YarnServiceJob.wait`.  One component per
-  role, one container per task, ``yarn.amd.com/gpu``-style GPU resources when
-  ``--gpus-per-node`` is set.  `YarnServiceJob.wait` applies the dmlc
+  role, one container per task; with ``--gpus-per-node`` every worker container asks for one
+  ``amd.com/gpu`` (one process per GPU) and binds local rank 0.  Each
+  container exports its own ``DMLC_TASK_ID`` / ``DMLC_WORKER_ID`` (or
+  ``DMLC_SERVER_ID``) from the service's ``${COMPONENT_ID}`` and
+  ``DMLC_NODE_HOST``.  `YarnServiceJob.wait` applies the dmlc
   ApplicationMaster's policy to the containers the service reports
-  (`yarn_am.py`): a memory-limit kill aborts the job, other failures are
+  (simulated end to end in `tests/yarn_am_sim.py`): a memory-limit kill aborts the job, other failures are
   retried by YARN up to DMLC_MAX_ATTEMPT, and more than that aborts.
   The node of every failed container is blacklisted (the service AM is asked
   to with ``yarn.service.node-blacklist.threshold`` = 1, and a task re-placed
@@ -116,10 +119,22 @@ def service_spec(args, envs: Dict[str, object], name: str,
         if n <= 0:
             continue
         res = {"cpus": int(cores), "memory": str(_mb(mem))}
-        if role == "worker" and getattr(args, "gpus_per_node", 0):
-            res["additional"] = {"amd.com/gpu": {"value": int(args.gpus_per_node)}}
+        gpu = role == "worker" and bool(getattr(args, "gpus_per_node", 0))
+        if gpu:
+            # one rank per container, so one GPU per container (YARN isolates
+            # it: the container sees it as device 0); --gpus-per-node only
+            # says that GPU workers are wanted, never N GPUs for one rank
+            res["additional"] = {"amd.com/gpu": {"value": 1}}
+        # per-container identity, as the dmlc AM gives each launch
+        # (reference ApplicationMaster.java:443-446): the service expands
+        # ${COMPONENT_ID} to the instance index (0..n-1) in the launch command;
+        # servers follow the workers in task-id space, like the tracker's ranks
+        base = 0 if role == "worker" else int(args.num_workers)
+        ident = (f"export DMLC_TASK_ID=$(( ${{COMPONENT_ID}} + {base} )) "
+                 f"DMLC_{role.upper()}_ID=${{COMPONENT_ID}} DMLC_NODE_HOST=$(hostname -f); "
+                 + ("export DMLC_LOCAL_RANK=0 LOCAL_RANK=0 LOCAL_WORLD_SIZE=1; " if gpu else ""))
         comps.append({
-            "name": role, "number_of_containers": int(n), "launch_command": cmd,
+            "name": role, "number_of_containers": int(n), "launch_command": ident + cmd,
             "resource": res, "restart_policy": "ON_FAILURE",
             "configuration": {
                 "env": dict(env, DMLC_ROLE=role),

@@ -267,7 +267,7 @@ __global__ __launch_bounds__(kBwdThreads) void k_fm_bwd(const uint8_t* __restric
   // loads are issued unconditionally (a clamped row, the value zeroed past
   // the block's rows): every tile issues the same memory ops, so the wait for
   // a load counts only the ops issued after it
-  const int64_t rlast = r1 > r0 ? r1 - 1 : r0;
+  const int64_t rlast = r1 > r0 ? r1 - 1 : rows - 1;  // in the batch for an empty block too
   auto load_g = [&](int64_t t, float* gv, float2* v) {
     const int64_t r = t + grow;
     const bool ok = threadIdx.x < 256 && r < r1;
@@ -545,7 +545,11 @@ __global__ __launch_bounds__(64 * W) void k_fm_fused(
   const float b0 = *bias;
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
   const int64_t r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
-  const int64_t rlast = r1 > r0 ? r1 - 1 : r0;
+  // the clamp row of the unconditional loads: inside the batch even for a
+  // block that starts at or past the last row (rows_per_block is rounded up to
+  // 32, so trailing blocks can be empty); such a block loads row rows - 1,
+  // zeroes it and writes zero partials
+  const int64_t rlast = r1 > r0 ? r1 - 1 : rows - 1;
   auto load_x = [&](int64_t t, uint4 (&v)[4]) {
     const int64_t r = t + col;
     const bool ok = r < r1;
@@ -804,6 +808,7 @@ void LaunchFmFused(const uint8_t* x, int64_t rows, int dim, const void* wt_bf16,
                    int loss, float inv_n, int nblocks, float* y, float* part, float* lpart,
                    hipStream_t stream) {
   if (nblocks == 0) return;
+  CHECK_GT(rows, 0) << "fused HashedFM step: empty batch";
   const int64_t per = (((rows + nblocks - 1) / nblocks) + 31) / 32 * 32;
   const int w = dim / 128;
   auto kernel = w == 8 ? k_fm_fused<8> : w == 4 ? k_fm_fused<4> : w == 2 ? k_fm_fused<2>

@@ -8,9 +8,11 @@
 #include <dmlc/fault.h>
 #include <dmlc/logging.h>
 #include <errno.h>
+#include <fcntl.h>
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <poll.h>
 #include <sys/socket.h>
 #include <sys/time.h>
 #include <unistd.h>
@@ -21,6 +23,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <ctime>
+#include <mutex>
+#include <set>
 #include <thread>
 
 namespace dmlc {
@@ -154,7 +158,10 @@ size_t OnHeader(char* data, size_t size, size_t nmemb, void* user) {
 // is the only one.  Keep-alive connections are per thread (one per pool
 // worker).  Anything unusual (https, a non-2xx status, chunked or
 // length-less bodies, a transport error) closes the connection and the
-// request goes to libcurl instead, so the fast path never changes semantics.
+// request goes to libcurl instead.  Hosts libcurl would reach through a proxy
+// (http_proxy / all_proxy minus no_proxy) never take the native path, the
+// connect waits at most libcurl's 30 s, and an authority whose direct connect
+// failed is remembered, so later requests go straight to libcurl.
 
 struct NativeConn {
   std::string authority;  // host[:port] the socket is connected to
@@ -181,6 +188,91 @@ bool NativeEnabled() {
 
 std::atomic<uint64_t> g_native_gets{0}, g_native_fallbacks{0};
 
+/*! \brief libcurl's connect timeout (Perform sets the same 30 s) */
+constexpr int kConnectTimeoutMs = 30000;
+
+std::string LowerEnv(const char* a, const char* b) {
+  const char* v = std::getenv(a);
+  if (v == nullptr || *v == '\0') v = std::getenv(b);
+  std::string s = v == nullptr ? "" : v;
+  std::transform(s.begin(), s.end(), s.begin(), ::tolower);
+  return s;
+}
+
+/*!
+ * \brief true if libcurl would send a plain-http request to `host` through a
+ *  proxy: http_proxy / all_proxy set (either case) and the host not excluded
+ *  by no_proxy ("*", an exact name, or a domain suffix with or without the
+ *  leading dot).  The native path then stays off: it only speaks to origin
+ *  servers directly.
+ */
+bool ProxyApplies(const std::string& host) {
+  const char* hp = std::getenv("http_proxy");  // curl reads only lowercase http_proxy
+  const std::string proxy = hp != nullptr && *hp != '\0' ? std::string(hp)
+                                                           : LowerEnv("all_proxy", "ALL_PROXY");
+  if (proxy.empty()) return false;
+  std::string h = host;
+  std::transform(h.begin(), h.end(), h.begin(), ::tolower);
+  const std::string np = LowerEnv("no_proxy", "NO_PROXY");
+  size_t at = 0;
+  while (at <= np.size()) {
+    size_t e = np.find(',', at);
+    if (e == std::string::npos) e = np.size();
+    std::string d = np.substr(at, e - at);
+    at = e + 1;
+    d.erase(0, d.find_first_not_of(" \t"));
+    const size_t z = d.find_last_not_of(" \t");
+    d.erase(z == std::string::npos ? 0 : z + 1);
+    const size_t c = d.rfind(':');  // "host:port" entries: the host part
+    if (c != std::string::npos && d.find(']') == std::string::npos) d.erase(c);
+    if (d.empty()) continue;
+    if (d == "*") return false;
+    if (d.front() == '.') d.erase(0, 1);
+    if (h == d) return false;
+    if (h.size() > d.size() && h.compare(h.size() - d.size(), d.size(), d) == 0 &&
+        h[h.size() - d.size() - 1] == '.') {
+      return false;
+    }
+  }
+  return true;
+}
+
+/*!
+ * \brief authorities whose direct connect failed once: later requests go to
+ *  libcurl at once instead of paying the connect timeout again per request
+ */
+std::mutex g_unreachable_mu;
+std::set<std::string> g_unreachable;
+
+bool KnownUnreachable(const std::string& authority) {
+  std::lock_guard<std::mutex> lk(g_unreachable_mu);
+  return g_unreachable.count(authority) != 0;
+}
+
+void MarkUnreachable(const std::string& authority) {
+  std::lock_guard<std::mutex> lk(g_unreachable_mu);
+  g_unreachable.insert(authority);
+}
+
+/*! \brief connect with a bounded wait (non-blocking connect + poll) */
+bool ConnectWithin(int fd, const sockaddr* addr, socklen_t len, int timeout_ms) {
+  const int fl = ::fcntl(fd, F_GETFL, 0);
+  if (fl < 0 || ::fcntl(fd, F_SETFL, fl | O_NONBLOCK) < 0) return false;
+  int rc = ::connect(fd, addr, len);
+  if (rc != 0) {
+    if (errno != EINPROGRESS) return false;
+    pollfd p{fd, POLLOUT, 0};
+    do {
+      rc = ::poll(&p, 1, timeout_ms);
+    } while (rc < 0 && errno == EINTR);
+    if (rc <= 0) return false;  // timed out
+    int err = 0;
+    socklen_t el = sizeof(err);
+    if (::getsockopt(fd, SOL_SOCKET, SO_ERROR, &err, &el) != 0 || err != 0) return false;
+  }
+  return ::fcntl(fd, F_SETFL, fl) == 0;  // blocking again for MSG_WAITALL receives
+}
+
 int ConnectTo(const std::string& host, const std::string& port, long timeout_sec) {
   addrinfo hints{};
   hints.ai_family = AF_UNSPEC;
@@ -191,7 +283,7 @@ int ConnectTo(const std::string& host, const std::string& port, long timeout_sec
   for (addrinfo* a = res; a != nullptr; a = a->ai_next) {
     fd = ::socket(a->ai_family, a->ai_socktype | SOCK_CLOEXEC, a->ai_protocol);
     if (fd < 0) continue;
-    if (::connect(fd, a->ai_addr, a->ai_addrlen) == 0) break;
+    if (ConnectWithin(fd, a->ai_addr, a->ai_addrlen, kConnectTimeoutMs)) break;
     ::close(fd);
     fd = -1;
   }
@@ -252,6 +344,8 @@ bool NativeGet(const HttpRequest& req, HttpResponse* resp) {
   const size_t colon = authority.rfind(':');
   const std::string host = authority.substr(0, colon);
   const std::string port = colon == std::string::npos ? "80" : authority.substr(colon + 1);
+  // a proxied host, or one whose direct connect already failed: libcurl
+  if (ProxyApplies(host) || KnownUnreachable(authority)) return false;
 
   std::string head = "GET " + target + " HTTP/1.1\r\nHost: " + authority + "\r\n";
   for (const auto& h : req.headers) head += h + "\r\n";
@@ -265,7 +359,10 @@ bool NativeGet(const HttpRequest& req, HttpResponse* resp) {
     const bool reused = c.fd >= 0;
     if (!reused) {
       c.fd = ConnectTo(host, port, req.timeout_sec);
-      if (c.fd < 0) return false;
+      if (c.fd < 0) {
+        MarkUnreachable(authority);
+        return false;
+      }
       c.authority = authority;
     }
     have = 0;

@@ -298,13 +298,20 @@ class AzureHandler(_Base):
 class PlainHandler(_Base):
     store: Dict[str, bytes] = {}
     chunked = False  # answer GETs with Transfer-Encoding: chunked bodies
+    proxied = 0  # requests that came in proxy form (absolute URL as the target)
+
+    def _key(self):
+        if self.path.startswith("http://"):  # a forward-proxy request to this same server
+            type(self).proxied += 1
+            return urllib.parse.urlsplit(self.path).path
+        return self.path
 
     def do_HEAD(self):
-        data = self.store.get(self.path)
+        data = self.store.get(self._key())
         self._send(404) if data is None else self._send(200, b"", {"Content-Length": str(len(data))})
 
     def do_GET(self):
-        data = self.store.get(self.path)
+        data = self.store.get(self._key())
         if data is None:
             self._send(404)
         elif self.chunked:

@@ -332,6 +332,37 @@ def test_fm_fused_step_matches_two_pass(dim, rows, kind, weighted):
         assert err < 2e-2, err
 
 
+@pytest.mark.parametrize("extra", [1, 33])
+def test_fm_fused_empty_trailing_blocks(extra):
+    """rows just above 32 x CUs: the per-block row count rounds up to 64, so
+    the last workgroups start at or past the last row.  They must load only
+    inside the batch (the clamp row is rows - 1, not their own start) and
+    add nothing: the loss and gradients equal the two-pass path's."""
+    torch.manual_seed(extra)
+    dev = "cuda"
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    rows, dim = 32 * cus + extra, 256
+    # the batch sits at the end of its own allocation (no slack after it)
+    x8 = (torch.randn(rows, dim, device=dev) * 2).to(torch.float8_e4m3fn).clone()
+    label = (torch.rand(rows, device=dev) > 0.5).float()
+    model = HashedFM(dim=dim, rank=16).to(dev)
+    with torch.no_grad():
+        model.w.normal_(0, 0.05)
+        model.v.normal_(0, 0.05)
+    fused = model.loss(x8, label, loss="squared")
+    assert model.gemm == "hip_mfma_bf16_fused"
+    fused.backward()
+    got = [p.grad.clone() for p in (model.w, model.v, model.bias)]
+    model.zero_grad()
+    y = model(x8)
+    ref = ((y - label) ** 2).mean()
+    ref.backward()
+    assert abs(fused.item() - ref.item()) <= 1e-4 * abs(ref.item()) + 1e-6
+    for g, p in zip(got, (model.w, model.v, model.bias)):
+        err = (g - p.grad).abs().max().item() / (p.grad.abs().max().item() + 1e-9)
+        assert err < 1e-2, err
+
+
 def test_fm_fused_step_trains():
     """A few SGD steps of the fused path lower the loss (the gradient signs
     and the mean scaling are right end to end)."""

@@ -108,6 +108,29 @@ def test_transpose_and_gather_gradient_match(csr_t):
     torch.testing.assert_close(grads["transpose"], grads["atomic"], rtol=1e-4, atol=1e-6)
 
 
+def test_transposed_dict_feeds_every_op(csr_t):
+    """A transpose's (paired) dict is a CSR like any other: spmv_t,
+    hashed_dense and transpose take it (unpaired into contiguous copies), and
+    transposing twice gives back the original CSR."""
+    import torch
+    t, csr = csr_t
+    nfeat = int(csr.max_index) + 1
+    tt = ops.transpose(t, nfeat)
+    assert ops._paired(tt)
+    xt = dense_ref({k: tt[k] for k in ("offset", "index", "value")}, csr.rows)
+    w = torch.randn(nfeat, device="cuda")
+    torch.testing.assert_close(ops.spmv_t(tt, w, csr.rows).cpu(), xt.t() @ w.cpu(),
+                               rtol=1e-4, atol=1e-4)
+    contig = {"offset": tt["offset"], "index": tt["index"].contiguous(),
+              "value": tt["value"].contiguous()}
+    torch.testing.assert_close(ops.hashed_dense(tt, 256, seed=1, fp8=False),
+                               ops.hashed_dense(contig, 256, seed=1, fp8=False), rtol=0, atol=0)
+    back = ops.transpose(tt, csr.rows)
+    np.testing.assert_array_equal(back["offset"].cpu().numpy(),
+                                  t["offset"].cpu().numpy().astype(np.int64))
+    torch.testing.assert_close(dense_ref(back, nfeat), dense_ref(t, nfeat), rtol=0, atol=0)
+
+
 def test_transpose_workspace_is_persistent_and_out_reuses(csr_t):
     """The sort's scratch is kept between builds (no multi-GB allocation per
     build); out= overwrites a previous result; both give the same CSC as a

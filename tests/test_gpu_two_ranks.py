@@ -92,3 +92,29 @@ def test_bench_share_gpu_eight_ranks(tmp_path):
         assert 0 < r["zc_pinned_peak"] <= r["zc_pin_budget"]
         assert r["last_pass_sec"] > 0 and 0 < r["last_fill_sec"] <= r["last_pass_sec"]
     assert sum(r["zc_pinned_peak"] for r in ranks) <= host_budget
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("mode", ["stream", "hbm"])
+def test_bench_two_gpus_over_rccl(tmp_path, mode):
+    """bench.py --gpus 2 on two real GPUs (no --share-gpu): the control plane
+    and the NumCol / gradient all-reduce run over RCCL (backend "nccl"), one
+    process per GPU.  Skipped where fewer than two GPUs are visible (the
+    one-GPU box); the driver's 8-GPU SCALE run takes the same branch."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs >= 2 GPUs (RCCL at world 2)")
+    env = dict(os.environ, PYTHONPATH=ROOT, DMLC_HEARTBEAT_PERIOD="1")
+    cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--rows", "200000", "--mode", mode,
+           "--data-dir", str(tmp_path / "bench")]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-5000:]
+    out = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][-1])
+    assert out["n_gpus"] == 2 and out["config"]["rows"] == 200000
+    assert "all ranks on GPU 0" not in out["config"]["parallelism"]
+    ranks = out["per_rank"]
+    assert sorted(r["rank"] for r in ranks) == [0, 1]
+    assert sum(r["rows"] for r in ranks) == 200000
+    probe = out["allreduce_busbw_GBps"]
+    assert probe["backend"] == "nccl" and probe["4MB"] > 0 and probe["256MB"] > 0

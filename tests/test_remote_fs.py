@@ -198,6 +198,49 @@ def test_http_native_receive_and_libcurl_fallback():
         srv.shutdown()
 
 
+@pytest.mark.skipif(os.environ.get("DMLC_HTTP_NATIVE", "1") == "0", reason="native path off")
+def test_http_native_path_respects_proxy_env(monkeypatch):
+    """A host libcurl would reach through http_proxy never takes the native
+    receive (it only talks to origin servers); no_proxy brings it back.  The
+    mock server is its own forward proxy, so the proxied reads still return
+    the bytes."""
+    srv = mock_remote.serve(mock_remote.PlainHandler)
+    port = srv.server_address[1]
+    try:
+        payload = _blob((2 << 20) + 5, seed=6)
+        mock_remote.PlainHandler.store["/files/p.bin"] = payload
+        url = f"http://127.0.0.1:{port}/files/p.bin"
+        monkeypatch.setenv("http_proxy", f"http://127.0.0.1:{port}")
+        monkeypatch.delenv("no_proxy", raising=False)
+        monkeypatch.delenv("NO_PROXY", raising=False)
+        s0, p0 = _dmlc.http_stats(), mock_remote.PlainHandler.proxied
+        assert _read_all(url, chunk=1 << 20) == payload
+        s1 = _dmlc.http_stats()
+        assert s1["native_gets"] == s0["native_gets"]
+        assert mock_remote.PlainHandler.proxied - p0 >= 3
+        for np_ in ("127.0.0.1", "localhost, 127.0.0.1:9", "*"):
+            monkeypatch.setenv("no_proxy", np_)
+            assert _read_all(url, chunk=1 << 20) == payload
+            s2 = _dmlc.http_stats()
+            assert s2["native_gets"] - s1["native_gets"] >= 3, np_
+            s1 = s2
+    finally:
+        srv.shutdown()
+
+
+def test_http_unreachable_host_falls_back_once():
+    """A direct connect that fails marks the authority: the request goes to
+    libcurl (which fails the same way here) and later requests skip the
+    native connect."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()  # nothing listens on this port: connect is refused at once
+    with pytest.raises(_dmlc.DMLCError):
+        _read_all(f"http://127.0.0.1:{port}/x.bin", chunk=1 << 20)
+
+
 def test_hdfs_fails_loudly_without_libhdfs():
     with pytest.raises(_dmlc.DMLCError, match="libhdfs"):
         io.Stream("hdfs://namenode:8020/x", "r")

@@ -268,6 +268,45 @@ def test_backend_dry_run(cluster, needle, tmp_path):
     assert "FOO" in p.stdout
 
 
+@pytest.mark.parametrize("nworker,gpus,per_rank", [(12, 8, False), (8, 8, False), (3, 8, True),
+                                                     (5, 0, False)])
+def test_kubernetes_one_process_per_gpu(nworker, gpus, per_rank):
+    """Worker pods never request more GPUs than they run ranks: pod-per-node
+    (G GPUs, G ranks started inside the pod with local ranks 0..G-1) or
+    pod-per-rank (1 GPU, local rank 0).  The pod command is run through bash
+    for every completion index: the task ids cover 0..N-1 once each."""
+    import subprocess
+    from dmlc_core_amd.parallel.launch import kubernetes
+    from dmlc_core_amd.parallel.launch.opts import get_opts
+    argv = ["--cluster", "kubernetes", "--num-workers", str(nworker), "--gpus-per-node", str(gpus),
+            "--num-servers", "1"]
+    if per_rank:
+        argv += ["--kube-pod-per-rank", "1"]
+    args = get_opts(argv + ["echo", "hi"])
+    ms = kubernetes.manifests(args, {}, 'echo "$DMLC_TASK_ID ${DMLC_LOCAL_RANK:-none}"')
+    worker = ms[0]
+    pods = worker["spec"]["completions"]
+    c = worker["spec"]["template"]["spec"]["containers"][0]
+    req = c["resources"]["limits"].get("amd.com/gpu", 0)
+    seen = []
+    for idx in range(pods):
+        out = subprocess.run(["bash", "-c", c["command"][2]], capture_output=True, text=True,
+                             env=dict(os.environ, JOB_COMPLETION_INDEX=str(idx)), check=True).stdout
+        ranks = [l.split() for l in out.splitlines()]
+        assert len(ranks) <= max(req, 1)  # no pod runs fewer ranks than GPUs it asked for... nor more
+        seen += ranks
+    assert sorted(int(t) for t, _ in seen) == list(range(nworker))
+    if gpus == 0:
+        assert req == 0 and pods == nworker and all(l == "none" for _, l in seen)
+    elif per_rank:
+        assert req == 1 and pods == nworker and all(l == "0" for _, l in seen)
+    else:
+        assert pods == -(-nworker // gpus) and req == min(gpus, nworker)
+        assert sorted(int(l) for t, l in seen if int(t) < gpus) == list(range(min(gpus, nworker)))
+    server = ms[2]["spec"]["template"]["spec"]["containers"][0]
+    assert "amd.com/gpu" not in server["resources"]["limits"]
+
+
 def test_ssh_dry_run(tmp_path):
     hf = tmp_path / "hosts"
     hf.write_text("10.0.0.1\n10.0.0.2:2222\n")

@@ -10,7 +10,8 @@ from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 
 import pytest
 
-from dmlc_core_amd.parallel.launch import yarn, yarn_am
+from dmlc_core_amd.parallel.launch import yarn
+import yarn_am_sim as yarn_am
 from dmlc_core_amd.parallel.launch.opts import get_opts
 
 PY = sys.executable
@@ -138,11 +139,32 @@ def test_service_spec_shapes_components():
     comps = {c["name"]: c for c in spec["components"]}
     w, s = comps["worker"], comps["server"]
     assert w["number_of_containers"] == 4 and s["number_of_containers"] == 1
-    assert w["resource"]["memory"] == "2048" and w["resource"]["additional"]["amd.com/gpu"]["value"] == 8
+    # one rank per container: one GPU each, never --gpus-per-node of them
+    assert w["resource"]["memory"] == "2048" and w["resource"]["additional"]["amd.com/gpu"]["value"] == 1
     assert "additional" not in s["resource"]
     assert w["configuration"]["env"]["DMLC_TRACKER_PORT"] == "9091"
     assert w["configuration"]["env"]["DMLC_ROLE"] == "worker" and w["configuration"]["env"]["FOO"] == "bar"
     assert w["launch_command"].endswith("python train.py")
+
+
+@pytest.mark.parametrize("instance,role", [(0, "worker"), (3, "worker"), (0, "server")])
+def test_service_containers_get_their_own_identity(instance, role):
+    """Every container derives its own DMLC_TASK_ID (workers 0..n-1, servers
+    after them, as the reference AM numbers tasks) and DMLC_NODE_HOST from
+    the service's ${COMPONENT_ID}; GPU workers bind local rank 0.  The launch
+    command is run through bash with the placeholder expanded as the YARN
+    service does."""
+    import subprocess
+    spec = yarn.service_spec(_args(), {}, "job")
+    comp = {c["name"]: c for c in spec["components"]}[role]
+    cmd = comp["launch_command"].replace("${COMPONENT_ID}", str(instance))
+    cmd = cmd[:cmd.rindex("python train.py")] + \
+        'echo "$DMLC_TASK_ID ${DMLC_LOCAL_RANK:-none} $DMLC_NODE_HOST"'
+    out = subprocess.run(["bash", "-c", cmd], capture_output=True, text=True, check=True).stdout
+    tid, local, host = out.split()
+    assert int(tid) == (instance if role == "worker" else 4 + instance)
+    assert local == ("0" if role == "worker" else "none")
+    assert host
 
 
 def test_service_job_success_and_memory_abort(rm):
@@ -225,7 +247,7 @@ def test_service_stages_files_and_archives_through_webhdfs(rm, tmp_path, monkeyp
         assert files["vocab.bin"]["type"] == "STATIC"
         assert files["env.tar.gz"] == {"type": "ARCHIVE", "src_file": base + "env.tar.gz",
                                        "dest_file": "env.tar.gz"}
-        assert comp["launch_command"] == "python ./train_job.py --epochs 3"
+        assert comp["launch_command"].endswith("; python ./train_job.py --epochs 3")
         assert comp["configuration"]["env"]["DMLC_JOB_ARCHIVES"] == "env.tar.gz"
     finally:
         srv.shutdown()
