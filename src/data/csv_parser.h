@@ -60,12 +60,34 @@ class CSVParser : public TextParserBase<IndexType, DType> {
     IndexType idx = 0;
     real_t label = 0.0f, weight = 1.0f;
     bool has_weight = false;
+    // A delimiter that no number can contain (not a digit, sign, '.', 'e' or
+    // blank) ends the field's number by itself: the number is parsed against
+    // the line end and the field ends right where it stopped when a delimiter
+    // (or the line end) follows -- no memchr per field.  Otherwise (junk
+    // after the number) the delimiter is searched from there; every byte the
+    // parse consumed precedes it, so the value equals the reference's
+    // StrToFloat over [field start, delimiter) (reference :64-104).
+    const bool direct = !isdigitchars(delim) && !isspace(delim);
     while (true) {
-      const char* fe = static_cast<const char*>(std::memchr(p, delim, le - p));
-      if (fe == nullptr) fe = le;
       const char* q = p;
-      while (q != fe && isspace(*q)) ++q;
-      const real_t v = StrToFloat(q, fe, nullptr);
+      const char* fe;
+      real_t v;
+      if (direct) {
+        while (q != le && isspace(*q)) ++q;
+        const char* e;
+        v = StrToFloat(q, le, &e);
+        if (e == le || *e == delim) {
+          fe = e;
+        } else {
+          fe = static_cast<const char*>(std::memchr(e, delim, le - e));
+          if (fe == nullptr) fe = le;
+        }
+      } else {
+        fe = static_cast<const char*>(std::memchr(p, delim, le - p));
+        if (fe == nullptr) fe = le;
+        while (q != fe && isspace(*q)) ++q;
+        v = StrToFloat(q, fe, nullptr);
+      }
       if (column == label_col) {
         label = v;
       } else if (column == weight_col) {

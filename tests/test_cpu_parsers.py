@@ -135,6 +135,23 @@ def test_csv_matches_oracle(tmp_path, label_column):
     np.testing.assert_array_equal(got["index"], np.array(idx, np.uint64))
 
 
+@pytest.mark.parametrize("delim", [",", ";", ":", "|", "e"])
+def test_csv_junk_fields_match_oracle(tmp_path, delim):
+    """Fields with bytes after the number (junk, a second number, blanks
+    before the delimiter, empty fields): the direct-delimiter fast path falls
+    back to the delimiter search and gives the reference's values."""
+    rows_txt = ["1.5abc,2,3", "  4 ,x5,6.25e1y", "7,,8.,", "-.5,+9,1e", "12 34,5 ,6"]
+    text = "\n".join(r.replace(",", delim) for r in rows_txt) + "\n"
+    p = write(str(tmp_path / "j.csv"), text)
+    # ('e' can be part of a number: the reference's delimiter search path)
+    q = p + f"?delimiter={delim}&label_column=1"
+    got = pyref.concat_blocks(list(data.iter_blocks(q, type="csv")))
+    rows = pyref.parse_csv(text, 1, delim)
+    np.testing.assert_array_equal(got["label"], np.array([r[0] for r in rows], np.float32))
+    np.testing.assert_array_equal(got["value"], np.array([v for r in rows for v in r[1]], np.float32))
+    np.testing.assert_array_equal(got["offset"], np.cumsum([0] + [len(r[1]) for r in rows]))
+
+
 # trailing delimiters, derived by hand from the reference loop
 # (csv_parser.h:83-96: parse, skip to ',', step over it, stop at the line end)
 CSV_TRAILING = "1,2,\n3,,\n,\n4,5\n6,\n"
