@@ -20,6 +20,8 @@ __global__ __launch_bounds__(256) void k_probe(uint64_t* out, int iters, uint32_
            a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
   uint32_t b = seed * 3 + threadIdx.x, c = seed ^ 0x5555u;
   uint64_t w0 = a0, w1 = a1, w2 = a2, w3 = a3;
+  if constexpr (OP == 29 || OP == 31) asm volatile("v_cmp_gt_u32 s[20:21], %0, %1" : : "v"(a0), "v"(b) : "s20", "s21");
+  if constexpr (OP == 27 || OP == 28 || OP == 30) asm volatile("v_cmp_gt_u32 vcc, %0, %1" : : "v"(a0), "v"(b) : "vcc");
   if constexpr (OP == 24) asm volatile("v_cmp_gt_u32 s[20:21], %0, %1" : : "v"(a0), "v"(b) : "s20", "s21");
   if constexpr (OP == 25) asm volatile("v_cmp_gt_u32 vcc, %0, %1" : : "v"(a0), "v"(b) : "vcc");
   __builtin_amdgcn_s_barrier();
@@ -49,9 +51,15 @@ __global__ __launch_bounds__(256) void k_probe(uint64_t* out, int iters, uint32_
     if constexpr (OP == 21) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a##I) : "v"(b), "v"(c)); \
     if constexpr (OP == 22) asm volatile("v_and_b32 %0, 0x7f7f7f7f, %0" : "+v"(a##I)); \
     if constexpr (OP == 23) asm volatile("v_and_b32_e64 %0, %0, %1" : "+v"(a##I) : "v"(b)); \
-    if constexpr (OP == 24) asm volatile("v_cndmask_b32_e64 %0, %0, %1, s[20:21]" : "+v"(a##I) : "v"(b)); \
+  if constexpr (OP == 24) asm volatile("v_cndmask_b32_e64 %0, %0, %1, s[20:21]" : "+v"(a##I) : "v"(b)); \
     if constexpr (OP == 25) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a##I) : "v"(b)); \
-    if constexpr (OP == 26) asm volatile("v_and_b32 %0, 7, %0" : "+v"(a##I));
+    if constexpr (OP == 26) asm volatile("v_and_b32 %0, 7, %0" : "+v"(a##I)); \
+    if constexpr (OP == 27) asm volatile("v_cndmask_b32_e64 %0, %0, %1, vcc" : "+v"(a##I) : "v"(b)); \
+    if constexpr (OP == 28) asm volatile("v_and_b32 %0, %0, %1\n v_and_b32 %0, %0, %1\n v_and_b32 %0, %0, %1\n v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a##I) : "v"(b)); \
+    if constexpr (OP == 29) asm volatile("v_and_b32 %0, %0, %1\n v_and_b32 %0, %0, %1\n v_and_b32 %0, %0, %1\n v_cndmask_b32_e64 %0, %0, %1, s[20:21]" : "+v"(a##I) : "v"(b)); \
+    if constexpr (OP == 30) asm volatile("v_cmp_gt_u32 vcc, %0, %1\n v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a##I) : "v"(b) : "vcc"); \
+    if constexpr (OP == 31) asm volatile("v_cmp_gt_u32 s[20:21], %0, %1\n v_cndmask_b32_e64 %0, %0, %1, s[20:21]" : "+v"(a##I) : "v"(b) : "s20", "s21"); \
+    if constexpr (OP == 32) asm volatile("v_and_b32 %0, %0, %1\n v_and_b32 %0, %0, %1\n v_and_b32 %0, %0, %1\n v_and_b32 %0, %0, %1" : "+v"(a##I) : "v"(b));
     R8(BODY)
     R8(BODY)
     if constexpr (OP == 16) {
@@ -94,7 +102,10 @@ int main(int argc, char** argv) {
       {"v_readlane_b32", k_probe<20>}, {"v_add3_u32", k_probe<21>},
       {"v_and_b32_literal", k_probe<22>}, {"v_and_b32_e64", k_probe<23>},
       {"v_cndmask_e64_sgpr", k_probe<24>}, {"v_cndmask_vcc_set", k_probe<25>},
-      {"v_and_b32_inline", k_probe<26>}};
+      {"v_and_b32_inline", k_probe<26>}, {"v_cndmask_e64_vcc", k_probe<27>},
+      {"mix3and_cndmask_vcc", k_probe<28>}, {"mix3and_cndmask_sgpr", k_probe<29>},
+      {"cmp_vcc_cndmask", k_probe<30>}, {"cmp_sgpr_cndmask", k_probe<31>},
+      {"mix4and", k_probe<32>}};
   const char* only = argc > 1 ? argv[1] : nullptr;
   const int iters = 4096;
   uint64_t* d;
