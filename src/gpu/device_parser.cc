@@ -198,6 +198,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     tiles_.Reserve(LineIndexTiles(cfg_.chunk_bytes) * sizeof(uint64_t));
     tcounts_.Reserve(TileScratchWords(TileCount(cfg_.chunk_bytes)) * sizeof(uint64_t));
     tflags_.Reserve(TileScratchWords(TileCount(cfg_.chunk_bytes)) * sizeof(uint32_t));
+    tmasks_.Reserve(TileMaskWords(TileCount(cfg_.chunk_bytes)) * sizeof(uint32_t));
     meta_.Reserve(2 * sizeof(ChunkMeta));
     hmeta_.Reserve(2 * sizeof(ChunkMeta));
     hmap_.Reserve(sizeof(ChunkMeta), /*mapped=*/true);
@@ -673,6 +674,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     const size_t tiles = TileCount(nbytes);
     tcounts_.Reserve(TileScratchWords(tiles) * sizeof(uint64_t));
     tflags_.Reserve(TileScratchWords(tiles) * sizeof(uint32_t));
+    tmasks_.Reserve(TileMaskWords(tiles) * sizeof(uint32_t));
     slots_.Reserve(std::max<size_t>(kMaxPartialBlocks, TileScratchSlots(tiles)) * sizeof(MetaPartial));
     tiles_.Reserve(LineIndexTiles(nbytes) * sizeof(uint64_t));
   }
@@ -723,13 +725,13 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
    */
   /*! \brief the tile pipeline's count + scan (LibSVM / LibFM C1 + C2, or CSV S1 + scan) */
   void LaunchCountScan(const char* text, size_t nbytes, uint64_t* counts, uint32_t* flags,
-                       ChunkMeta* dmeta, ChunkMeta* hm, hipStream_t s) {
+                       uint32_t* masks, ChunkMeta* dmeta, ChunkMeta* hm, hipStream_t s) {
     if (tcfg_.format == TextFormat::kCSV) {
       LaunchCsvTileCount(text, nbytes, tcfg_.label_column, tcfg_.weight_column, tcfg_.delimiter,
                          counts, flags, s);
       LaunchTileScanRaw(counts, flags, TileCount(nbytes), dmeta, hm, s);
     } else {
-      LaunchTileCountScan(text, nbytes, counts, flags, dmeta, hm, s);
+      LaunchTileCountScan(text, nbytes, counts, flags, masks, dmeta, hm, s);
     }
   }
 
@@ -741,6 +743,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       // are published, or about to be, in hmap_next_)
       tcounts_.swap(tcounts_next_);
       tflags_.swap(tflags_next_);
+      tmasks_.swap(tmasks_next_);
       meta_.swap(meta_next_);
       hmap_.swap(hmap_next_);
       pre_.valid = false;
@@ -750,7 +753,8 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     }
     DropPrelaunch();
     LaunchCountScan(text, nbytes, tcounts_.get<uint64_t>(), tflags_.get<uint32_t>(),
-                    meta_.get<ChunkMeta>(), hmap_.get<ChunkMeta>(), compute_->get());
+                    tmasks_.get<uint32_t>(), meta_.get<ChunkMeta>(), hmap_.get<ChunkMeta>(),
+                    compute_->get());
   }
 
   bool FastParse(const char* text, size_t nbytes, DeviceCSR<IndexType>* out, size_t row_base,
@@ -775,7 +779,8 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
         // rows without a `qid:` token have qid 0; the fill writes the others
         DMLC_HIP_CHECK(hipMemsetAsync(tgt.qid + row_base, 0, plan->nrows * sizeof(uint64_t), s));
       }
-      LaunchTileFill<IndexType>(text, nbytes, tcfg_.format, tcounts_.get<uint64_t>(), tgt,
+      LaunchTileFill<IndexType>(text, nbytes, tcfg_.format, tcounts_.get<uint64_t>(),
+                                tmasks_.get<uint32_t>(), tgt,
                                 slots_.get<MetaPartial>(), dmeta, hm, s);
       PrelaunchCount();
       ChunkMeta m = WaitMapped(hm);
@@ -888,11 +893,12 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     const size_t tiles = TileCount(nx.size);
     tcounts_next_.Reserve(TileScratchWords(tiles) * sizeof(uint64_t));
     tflags_next_.Reserve(TileScratchWords(tiles) * sizeof(uint32_t));
+    tmasks_next_.Reserve(TileMaskWords(tiles) * sizeof(uint32_t));
     // its own stream: count + scan (HBM- and VALU-light next to the fill)
     // overlap the current fill instead of queueing behind it.  The set it
     // writes was last used by the chunk before the current one, which is done.
     LaunchCountScan(nx.text, nx.size, tcounts_next_.get<uint64_t>(), tflags_next_.get<uint32_t>(),
-                    meta_next_.get<ChunkMeta>(), hmap_next_.get<ChunkMeta>(), count_stream_->get());
+                    tmasks_next_.get<uint32_t>(), meta_next_.get<ChunkMeta>(), hmap_next_.get<ChunkMeta>(), count_stream_->get());
     pre_done_->Record(count_stream_->get());
     pre_.valid = true;
     pre_.text = nx.text;
@@ -1006,7 +1012,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       tgt.nnz_limit = out->nnz_capacity();
       if (libfm && tgt.field == nullptr) tgt.nnz_limit = 0;
       const FillOnePass op{fstatus_.get<uint64_t>(), hticket_.get<unsigned long long>(), hticket0_};
-      hticket0_ += LaunchTileFill<IndexType>(text, nbytes, tcfg_.format, nullptr, tgt,
+      hticket0_ += LaunchTileFill<IndexType>(text, nbytes, tcfg_.format, nullptr, nullptr, tgt,
                                              slots_.get<MetaPartial>(), dmeta, hm, s, &op);
       ChunkMeta m = WaitMapped(hm);
       if (first_wait) {
@@ -1146,7 +1152,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
           const HashOnePass op{hstatus_.get<uint64_t>(), hticket_.get<unsigned long long>(),
                                hticket0_, htag_, out->row_cap};
           hticket0_ += LaunchTileHashed<IndexType>(
-              text, nbytes, tcfg_.format, nullptr, out->rows, 0, dim, scale, seed, fp8,
+              text, nbytes, tcfg_.format, nullptr, nullptr, out->rows, 0, dim, scale, seed, fp8,
               out->x->get(), out->label->get<float>(), slots_.get<MetaPartial>(), dmeta, hm, s, &op);
           const ChunkMeta m = WaitMapped(hm);
           AfterFirstSync();
@@ -1175,7 +1181,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
         if (!(sizes.flags & kFlagIrregular)) {
           reserve(sizes.nrows, nbytes);
           LaunchTileHashed<IndexType>(text, nbytes, tcfg_.format, tcounts_.get<uint64_t>(),
-                                      out->rows, sizes.nlines, dim, scale, seed, fp8, out->x->get(),
+                                      tmasks_.get<uint32_t>(), out->rows, sizes.nlines, dim, scale, seed, fp8, out->x->get(),
                                       out->label->get<float>(), slots_.get<MetaPartial>(), dmeta,
                                       hm, s);
           PrelaunchCount();
@@ -1243,9 +1249,9 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
   std::vector<std::unique_ptr<Event>> copied_, parsed_;
   DeviceBuffer tiles_, lines_, info_, partials_, meta_;
   /*! \brief tile parser scratch: per-tile counts (scanned in place) and flags */
-  DeviceBuffer tcounts_, tflags_;
+  DeviceBuffer tcounts_, tflags_, tmasks_;
   // the prelaunched next chunk's C1 + C2 scratch (hbm_cache ParseAll only)
-  DeviceBuffer tcounts_next_, tflags_next_, meta_next_;
+  DeviceBuffer tcounts_next_, tflags_next_, tmasks_next_, meta_next_;
   PinnedBuffer hmap_next_;
   std::unique_ptr<Stream> count_stream_;  // prelaunched counts (hbm_cache only)
   std::unique_ptr<Event> pre_done_;

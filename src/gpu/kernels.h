@@ -164,11 +164,18 @@ size_t TileScratchSlots(size_t ntiles);
  *  nnz = tokens - lines, flags (kFlagIrregular) and zeroed maxima; host_meta
  *  (mapped pinned memory, may be null) receives a copy the host reads after
  *  synchronising the stream, without a device-to-host copy.
- *  tile_counts / tile_flags need TileCount(nbytes) entries.
+ *  tile_counts / tile_flags need TileCount(nbytes) entries; tile_masks
+ *  (TileMaskWords) receives the per-16-byte start masks the fill reads.
  */
 void LaunchTileCountScan(const char* text, size_t nbytes, uint64_t* tile_counts,
-                         uint32_t* tile_flags, ChunkMeta* meta, ChunkMeta* host_meta,
-                         hipStream_t stream);
+                         uint32_t* tile_flags, uint32_t* tile_masks, ChunkMeta* meta,
+                         ChunkMeta* host_meta, hipStream_t stream);
+/*!
+ * \brief u32 words of C1's published token / line start masks for ntiles
+ *  tiles (one word per 16 text bytes: the fill and the fused hash kernel take
+ *  them instead of classifying every byte a second time)
+ */
+size_t TileMaskWords(size_t ntiles);
 /*!
  * \brief C3 + C4: parse every token of a regular chunk into out using the
  *  scanned tile prefixes; merges max index / field and flags into meta and
@@ -194,9 +201,10 @@ struct FillOnePass {
 };
 template <typename IndexType>
 size_t LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
-                      const uint64_t* tile_prefix, const FillTarget<IndexType>& out,
-                      MetaPartial* partials, ChunkMeta* meta, ChunkMeta* host_meta,
-                      hipStream_t stream, const FillOnePass* one_pass = nullptr);
+                      const uint64_t* tile_prefix, const uint32_t* tile_masks,
+                      const FillTarget<IndexType>& out, MetaPartial* partials, ChunkMeta* meta,
+                      ChunkMeta* host_meta, hipStream_t stream,
+                      const FillOnePass* one_pass = nullptr);
 
 /*!
  * \brief fused tokenize -> hash -> dense rows on the tile parser (config 5):
@@ -228,7 +236,8 @@ struct HashOnePass {
 };
 template <typename IndexType>
 size_t LaunchTileHashed(const char* text, size_t nbytes, TextFormat format,
-                        const uint64_t* tile_prefix, uint64_t row_base, uint64_t nlines, int dim,
+                        const uint64_t* tile_prefix, const uint32_t* tile_masks,
+                        uint64_t row_base, uint64_t nlines, int dim,
                         float scale, uint32_t seed, bool fp8, void* out, float* labels,
                         MetaPartial* partials, ChunkMeta* meta, ChunkMeta* host_meta,
                         hipStream_t stream, const HashOnePass* one_pass = nullptr);

@@ -163,8 +163,14 @@ __device__ __forceinline__ uint32_t prev_byte(const uint8_t* __restrict__ text, 
  */
 template <bool kFull>
 __device__ __forceinline__ bool count16(uint4 v, uint32_t pc, size_t pos, size_t n,
-                                        uint32_t* lines, uint32_t* toks, uint32_t* qtoks) {
+                                        uint32_t* lines, uint32_t* toks, uint32_t* qtoks,
+                                        uint32_t* packed = nullptr) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  // the token / line start masks in the fill's form (bit j = byte j of the 16,
+  // token starts in bits 0..15, line starts in 16..31): byte dot products
+  // gather the per-byte high bits (0x80 = 128 x the weight), two words per
+  // accumulator
+  uint32_t acc_t[2] = {0u, 0u}, acc_l[2] = {0u, 0u};
   // bytes at or past n are "separators" (no starts there); kFull: the whole
   // tile lies before n (every tile but a chunk's last), no per-word masks
   const size_t room = kFull ? 16 : (pos >= n ? 0 : (n - pos < 16 ? n - pos : 16));
@@ -194,6 +200,9 @@ __device__ __forceinline__ bool count16(uint4 v, uint32_t pc, size_t pos, size_t
     *toks += __popc(tm);
     *qtoks += __popc(tm & (x << 1));
     *lines += __popc(lm);
+    const uint32_t wgt = (i & 1) ? 0x80402010u : 0x08040201u;
+    acc_t[i >> 1] = __builtin_amdgcn_udot4(tm, wgt, acc_t[i >> 1], false);
+    acc_l[i >> 1] = __builtin_amdgcn_udot4(lm, wgt, acc_l[i >> 1], false);
     bad |= (lm & ~tm) != 0;  // a line that starts with a blank
     // (token starts outside [0-9+-.] are flagged by the fill / hash kernels:
     // such a token never passes the register-window decoder, so the check
@@ -208,6 +217,9 @@ __device__ __forceinline__ bool count16(uint4 v, uint32_t pc, size_t pos, size_t
     }
     prev_sep = (sep >> 24) & 0x80u;
     prev_eol = (eol >> 24) & 0x80u;
+  }
+  if (packed != nullptr) {
+    *packed = (acc_t[0] >> 7) | (acc_t[1] << 1) | (acc_l[0] << 9) | (acc_l[1] << 17);
   }
   return bad;
 }
@@ -287,7 +299,8 @@ constexpr int kCountLoads = static_cast<int>(kTileBytes / 1024);
 __global__ __launch_bounds__(kThreads) void k_tile_count(const uint8_t* __restrict__ text,
                                                          size_t n, size_t ntiles,
                                                          uint64_t* __restrict__ counts,
-                                                         uint32_t* __restrict__ flags) {
+                                                         uint32_t* __restrict__ flags,
+                                                         uint2* __restrict__ masks) {
   const int lane = dev::lane_id();
   const size_t tile = static_cast<size_t>(blockIdx.x) * (kThreads / dev::kWave) +
                       threadIdx.x / dev::kWave;
@@ -299,14 +312,24 @@ __global__ __launch_bounds__(kThreads) void k_tile_count(const uint8_t* __restri
   const uint32_t first = base == 0 ? static_cast<uint32_t>('\n') : text[base - 1];
   uint32_t lines = 0, toks = 0, qtoks = 0;
   bool bad = false;
+  // the fill's masks of slices 2 s and 2 s + 1 (its step s), one 8-byte store
+  // per lane per step: [tile][step][lane]
+  uint2* const mrow = masks + tile * (kTileBytes / 2048) * dev::kWave + lane;
   auto count_tile = [&](auto full) {
+    uint32_t m0 = 0;
 #pragma unroll
     for (int j = 0; j < kCountLoads; ++j) {
       const uint32_t left = dev::lane_shr1(v[j].w >> 24);
       const uint32_t wrap = j == 0 ? first : dev::lane63(v[j - 1].w >> 24);
       const uint32_t pc = lane == 0 ? wrap : left;
+      uint32_t m;
       bad |= count16<decltype(full)::value>(v[j], pc, base + j * 1024 + lane * 16, n, &lines,
-                                            &toks, &qtoks);
+                                            &toks, &qtoks, &m);
+      if (j & 1) {
+        mrow[(j >> 1) * dev::kWave] = make_uint2(m0, m);
+      } else {
+        m0 = m;
+      }
     }
   };
   if (base + kTileBytes <= n) {  // wave-uniform: every tile but a chunk's last
@@ -929,6 +952,25 @@ __device__ __forceinline__ uint4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t voff
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+
+/*! \brief the published start masks from tile `tile` on (C1's [tile][step][lane]
+ *  uint2 words), as a buffer resource: per step one 8-byte load whose lane
+ *  offset is fixed and whose step offset is scalar (no address VALU) */
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mask_rsrc(const uint32_t* masks, size_t tile,
+                                                            size_t ntiles) {
+  const size_t words = (ntiles - tile) * (kTileBytes / 16);
+  const size_t bytes = words * 4 > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : words * 4;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(masks) + tile * (kTileBytes / 16),
+                                           0, static_cast<uint32_t>(bytes), 0x00020000);
+}
+
+/*! \brief step s's two slice masks of this lane (x: slice a, y: slice b) */
+__device__ __forceinline__ uint2 load_masks(__amdgpu_buffer_rsrc_t r, uint32_t lane_off, int s) {
+  const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(r, lane_off, s * dev::kWave * 8, 0);
+  return make_uint2(v.x, v.y);
+}
+
 __device__ __forceinline__ uint4 load16_clip(const uint8_t* __restrict__ text, size_t pos, size_t n) {
   const size_t at = pos < n ? pos : 0;
   const uint4 v = *reinterpret_cast<const uint4*>(text + at);
@@ -1021,6 +1063,7 @@ struct FillPass {
   ChunkMeta* meta;              // nlines / nrows / nnz of the chunk (the last tile writes them)
   uint32_t exp;                 // pricing experiments (DMLC_FILL_EXP; 0 in production):
                                 // 1 no CSR stores, 2 no token decode (outputs are wrong)
+  const uint32_t* masks;        // counted path: C1's start masks (TileMaskWords)
 };
 
 /*! \brief the pricing experiments of a DMLC_FILL_PRICING build (scripts/
@@ -1076,7 +1119,17 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
   uint4 b = bload16(trs, loff + 1024);
   uint4 t = make_uint4(0, 0, 0, 0);
   if (!kOnePass && lane < 4) t = bload16(trs, loff + kStepBytes);
-  uint32_t carry_pc = tile0 == 0 ? static_cast<uint32_t>('\n') : text[tile0 - 1];
+  // counted path: the step's start masks come from C1 (published per 16 B),
+  // not from classifying the bytes again; one pass classifies here
+  __amdgpu_buffer_rsrc_t mrs;
+  const uint32_t moff = static_cast<uint32_t>(lane) * 8;
+  uint2 mk = make_uint2(0, 0);
+  if constexpr (!kOnePass) {
+    mrs = mask_rsrc(op.masks, tile, ntiles);
+    mk = load_masks(mrs, moff, 0);
+  }
+  uint32_t carry_pc = 0;
+  if constexpr (kOnePass) carry_pc = tile0 == 0 ? static_cast<uint32_t>('\n') : text[tile0 - 1];
   uint64_t line_base, tok_base;
   unsigned count_flags = 0;  // one pass: what C1 would have flagged for this tile
   if constexpr (kOnePass) {
@@ -1182,21 +1235,29 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
     ss[lane] = a;
     ss[64 + lane] = b;
     if (lane < 4) ss[128 + lane] = t;
-    const uint32_t left_a = dev::lane_shr1(a.w >> 24);
-    const uint32_t pc_a = lane == 0 ? carry_pc : left_a;
-    const uint32_t left_b = dev::lane_shr1(b.w >> 24);
-    // cross-lane reads run in every lane (a shuffle inside `lane == 0 ? :`
-    // would execute with only lane 0 active and read an inactive lane)
-    const uint32_t last_a = dev::lane63(a.w >> 24);
-    const uint32_t pc_b = lane == 0 ? last_a : left_b;
-    carry_pc = dev::lane63(b.w >> 24);
     uint32_t lm_a, tm_a, lm_b, tm_b;
-    if (tile0 + static_cast<size_t>(s + 1) * kStepBytes <= n) {  // wave-uniform: a full step
-      (void)lane_masks<false, true>(a, pc_a, pos_a, n, &lm_a, &tm_a);
-      (void)lane_masks<false, true>(b, pc_b, pos_a + 1024, n, &lm_b, &tm_b);
+    if constexpr (kOnePass) {
+      const uint32_t left_a = dev::lane_shr1(a.w >> 24);
+      const uint32_t pc_a = lane == 0 ? carry_pc : left_a;
+      const uint32_t left_b = dev::lane_shr1(b.w >> 24);
+      // cross-lane reads run in every lane (a shuffle inside `lane == 0 ? :`
+      // would execute with only lane 0 active and read an inactive lane)
+      const uint32_t last_a = dev::lane63(a.w >> 24);
+      const uint32_t pc_b = lane == 0 ? last_a : left_b;
+      carry_pc = dev::lane63(b.w >> 24);
+      if (tile0 + static_cast<size_t>(s + 1) * kStepBytes <= n) {  // wave-uniform: a full step
+        (void)lane_masks<false, true>(a, pc_a, pos_a, n, &lm_a, &tm_a);
+        (void)lane_masks<false, true>(b, pc_b, pos_a + 1024, n, &lm_b, &tm_b);
+      } else {
+        (void)lane_masks<false>(a, pc_a, pos_a, n, &lm_a, &tm_a);
+        (void)lane_masks<false>(b, pc_b, pos_a + 1024, n, &lm_b, &tm_b);
+      }
     } else {
-      (void)lane_masks<false>(a, pc_a, pos_a, n, &lm_a, &tm_a);
-      (void)lane_masks<false>(b, pc_b, pos_a + 1024, n, &lm_b, &tm_b);
+      // C1's masks: the same starts (its blank / control checks passed)
+      tm_a = mk.x & 0xFFFFu;
+      lm_a = mk.x >> 16;
+      tm_b = mk.y & 0xFFFFu;
+      lm_b = mk.y >> 16;
     }
     // `qid:` tokens (C1 left them out of the entry counts): taken out of the
     // list here, decoded by their lane after the scan (wave-uniform test:
@@ -1208,12 +1269,13 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
       tm_a &= ~qa;
       tm_b &= ~qb;
     }
-    // a, b, t are consumed: the next step's loads go straight into them
+    // a, b, t (and the masks) are consumed: the next step's loads go straight into them
     if (!last) {
       const uint32_t so = static_cast<uint32_t>(s + 1) * kStepBytes;
       a = bload16(trs, loff + so);
       b = bload16(trs, loff + so + 1024);
       if (lane < 4) t = bload16(trs, loff + so + kStepBytes);
+      if constexpr (!kOnePass) mk = load_masks(mrs, moff, s + 1);
     }
     // one 64-bit scan of four 16-bit counts: tokens / lines of both slices
     const uint64_t cnt = static_cast<uint64_t>(__popc(tm_a)) |
@@ -1497,6 +1559,7 @@ struct HashTarget {
   unsigned long long ticket0;   // its value at this launch
   uint64_t row_cap;             // rows of x / label
   ChunkMeta* meta;              // nlines / nrows of the chunk (the last tile writes them)
+  const uint32_t* masks;        // counted path: C1's start masks (TileMaskWords)
 };
 
 /*! \brief keep the token starts of a slice whose line ordinals are in [1, own];
@@ -1548,7 +1611,17 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
   const uint32_t loff = static_cast<uint32_t>(lane) * 16;
   uint4 a = bload16(trs, loff);
   uint4 b = bload16(trs, loff + 1024);
-  uint32_t carry_pc = tile0 == 0 ? static_cast<uint32_t>('\n') : text[tile0 - 1];
+  // counted path: C1's start masks per step (steps past the tile read the
+  // next tiles' words: the layout is contiguous over the chunk)
+  __amdgpu_buffer_rsrc_t mrs;
+  const uint32_t moff = static_cast<uint32_t>(lane) * 8;
+  uint2 mk = make_uint2(0, 0);
+  if constexpr (!kOnePass) {
+    mrs = mask_rsrc(out.masks, tile, ntiles);
+    mk = load_masks(mrs, moff, 0);
+  }
+  uint32_t carry_pc = 0;
+  if constexpr (kOnePass) carry_pc = tile0 == 0 ? static_cast<uint32_t>('\n') : text[tile0 - 1];
   uint64_t line_base;
   uint32_t own;
   if constexpr (kOnePass) {
@@ -1657,22 +1730,29 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
       st[lane] = a;
       st[64 + lane] = b;
       if (lane < 4) st[128 + lane] = t;
-      const uint32_t left_a = dev::lane_shr1(a.w >> 24);
-      const uint32_t pc_a = lane == 0 ? carry_pc : left_a;
-      const uint32_t left_b = dev::lane_shr1(b.w >> 24);
-      const uint32_t last_a = dev::lane63(a.w >> 24);
-      const uint32_t pc_b = lane == 0 ? last_a : left_b;
-      carry_pc = dev::lane63(b.w >> 24);
       uint32_t lm_a, tm_a, lm_b, tm_b;
-      // one pass: C1's checks of blank-started lines and control bytes here
-      // (token starts outside [0-9+-.] fail the decoder and are flagged there)
-      if (nxt <= n) {  // wave-uniform: a full step
-        irregular |= lane_masks<kOnePass, true, false>(a, pc_a, pos_a, n, &lm_a, &tm_a);
-        irregular |= lane_masks<kOnePass, true, false>(b, pc_b, pos_a + 1024, n, &lm_b, &tm_b);
+      if constexpr (kOnePass) {
+        const uint32_t left_a = dev::lane_shr1(a.w >> 24);
+        const uint32_t pc_a = lane == 0 ? carry_pc : left_a;
+        const uint32_t left_b = dev::lane_shr1(b.w >> 24);
+        const uint32_t last_a = dev::lane63(a.w >> 24);
+        const uint32_t pc_b = lane == 0 ? last_a : left_b;
+        // one pass: C1's checks of blank-started lines and control bytes here
+        // (token starts outside [0-9+-.] fail the decoder and are flagged there)
+        if (nxt <= n) {  // wave-uniform: a full step
+          irregular |= lane_masks<true, true, false>(a, pc_a, pos_a, n, &lm_a, &tm_a);
+          irregular |= lane_masks<true, true, false>(b, pc_b, pos_a + 1024, n, &lm_b, &tm_b);
+        } else {
+          irregular |= lane_masks<true, false, false>(a, pc_a, pos_a, n, &lm_a, &tm_a);
+          irregular |= lane_masks<true, false, false>(b, pc_b, pos_a + 1024, n, &lm_b, &tm_b);
+        }
       } else {
-        irregular |= lane_masks<kOnePass, false, false>(a, pc_a, pos_a, n, &lm_a, &tm_a);
-        irregular |= lane_masks<kOnePass, false, false>(b, pc_b, pos_a + 1024, n, &lm_b, &tm_b);
+        tm_a = mk.x & 0xFFFFu;
+        lm_a = mk.x >> 16;
+        tm_b = mk.y & 0xFFFFu;
+        lm_b = mk.y >> 16;
       }
+      carry_pc = dev::lane63(b.w >> 24);  // the step's last byte (a line end?)
       if (F == TextFormat::kLibSVM) {
         // `qid:` tokens are no features of the batch: dropped (checked as in
         // the fill, from the staged text; any other letter token sends the
@@ -1741,6 +1821,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
         a = bload16(trs, loff + so);
         b = bload16(trs, loff + so + 1024);
         if (lane < 4) t = bload16(trs, loff + so + kStepBytes);
+        if constexpr (!kOnePass) mk = load_masks(mrs, moff, s + 1);
       }
 
       list_slice<kHashListCap>(sl, tm_a, lm_a, static_cast<uint32_t>(before & 0xFFFFu),
@@ -1992,14 +2073,15 @@ void TileScan(uint64_t* tile_counts, uint32_t* tile_flags, size_t ntiles, ChunkM
 }  // namespace
 
 void LaunchTileCountScan(const char* text, size_t nbytes, uint64_t* tile_counts,
-                         uint32_t* tile_flags, ChunkMeta* meta, ChunkMeta* host_meta,
-                         hipStream_t stream) {
+                         uint32_t* tile_flags, uint32_t* tile_masks, ChunkMeta* meta,
+                         ChunkMeta* host_meta, hipStream_t stream) {
   const size_t ntiles = TileCount(nbytes);
+  CHECK(tile_masks != nullptr) << "LaunchTileCountScan: tile_masks (TileMaskWords) is required";
   if (ntiles != 0) {
     const size_t per_block = kThreads / dev::kWave;
     hipLaunchKernelGGL(k_tile_count, dim3((ntiles + per_block - 1) / per_block), dim3(kThreads), 0,
                        stream, reinterpret_cast<const uint8_t*>(text), nbytes, ntiles, tile_counts,
-                       tile_flags);
+                       tile_flags, reinterpret_cast<uint2*>(tile_masks));
   }
   TileScan(tile_counts, tile_flags, ntiles, meta, host_meta, 0, stream);
 }
@@ -2020,11 +2102,13 @@ size_t TileScratchWords(size_t ntiles) {
 
 size_t TileScratchSlots(size_t ntiles) { return ntiles + kFinishGroups; }
 
+size_t TileMaskWords(size_t ntiles) { return ntiles * (kTileBytes / 16); }
+
 template <typename IndexType>
 size_t LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
-                      const uint64_t* tile_prefix, const FillTarget<IndexType>& out,
-                      MetaPartial* partials, ChunkMeta* meta, ChunkMeta* host_meta,
-                      hipStream_t stream, const FillOnePass* one_pass) {
+                      const uint64_t* tile_prefix, const uint32_t* tile_masks,
+                      const FillTarget<IndexType>& out, MetaPartial* partials, ChunkMeta* meta,
+                      ChunkMeta* host_meta, hipStream_t stream, const FillOnePass* one_pass) {
   const size_t ntiles = TileCount(nbytes);
   const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
   const size_t groups = (ntiles + kFillWaves - 1) / kFillWaves;
@@ -2032,7 +2116,9 @@ size_t LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
     const char* v = std::getenv("DMLC_FILL_EXP");
     return v != nullptr ? static_cast<uint32_t>(std::atoi(v)) : 0u;
   }();
-  FillPass op{nullptr, nullptr, 0ull, meta, exp};
+  FillPass op{nullptr, nullptr, 0ull, meta, exp, tile_masks};
+  CHECK(one_pass != nullptr || tile_masks != nullptr || ntiles == 0)
+      << "LaunchTileFill: the counted path needs C1's tile_masks";
   if (one_pass != nullptr) {
     op.status = one_pass->status;
     op.ticket = one_pass->ticket;
@@ -2065,7 +2151,8 @@ size_t LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
 
 template <typename IndexType>
 size_t LaunchTileHashed(const char* text, size_t nbytes, TextFormat format,
-                        const uint64_t* tile_prefix, uint64_t row_base, uint64_t nlines, int dim,
+                        const uint64_t* tile_prefix, const uint32_t* tile_masks,
+                        uint64_t row_base, uint64_t nlines, int dim,
                         float scale, uint32_t seed, bool fp8, void* out, float* labels,
                         MetaPartial* partials, ChunkMeta* meta, ChunkMeta* host_meta,
                         hipStream_t stream, const HashOnePass* one_pass) {
@@ -2073,7 +2160,9 @@ size_t LaunchTileHashed(const char* text, size_t nbytes, TextFormat format,
   const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
   const size_t smem = static_cast<size_t>(kFillWaves) * dim * sizeof(float);
   HashTarget tgt{out, labels, row_base, nlines, dim, scale, seed, 0u, nullptr, nullptr, 0ull, 0ull,
-                 meta};
+                 meta, tile_masks};
+  CHECK(one_pass != nullptr || tile_masks != nullptr || ntiles == 0)
+      << "LaunchTileHashed: the counted path needs C1's tile_masks";
   const size_t groups = (ntiles + kFillWaves - 1) / kFillWaves;
   if (one_pass != nullptr) {
     tgt.tag = one_pass->tag;
@@ -2112,19 +2201,19 @@ size_t LaunchTileHashed(const char* text, size_t nbytes, TextFormat format,
 }
 
 template size_t LaunchTileHashed<uint32_t>(const char*, size_t, TextFormat, const uint64_t*,
-                                           uint64_t, uint64_t, int, float, uint32_t, bool, void*,
+                                           const uint32_t*, uint64_t, uint64_t, int, float, uint32_t, bool, void*,
                                            float*, MetaPartial*, ChunkMeta*, ChunkMeta*,
                                            hipStream_t, const HashOnePass*);
 template size_t LaunchTileHashed<uint64_t>(const char*, size_t, TextFormat, const uint64_t*,
-                                           uint64_t, uint64_t, int, float, uint32_t, bool, void*,
+                                           const uint32_t*, uint64_t, uint64_t, int, float, uint32_t, bool, void*,
                                            float*, MetaPartial*, ChunkMeta*, ChunkMeta*,
                                            hipStream_t, const HashOnePass*);
 
 template size_t LaunchTileFill<uint32_t>(const char*, size_t, TextFormat, const uint64_t*,
-                                         const FillTarget<uint32_t>&, MetaPartial*, ChunkMeta*,
+                                         const uint32_t*, const FillTarget<uint32_t>&, MetaPartial*, ChunkMeta*,
                                          ChunkMeta*, hipStream_t, const FillOnePass*);
 template size_t LaunchTileFill<uint64_t>(const char*, size_t, TextFormat, const uint64_t*,
-                                         const FillTarget<uint64_t>&, MetaPartial*, ChunkMeta*,
+                                         const uint32_t*, const FillTarget<uint64_t>&, MetaPartial*, ChunkMeta*,
                                          ChunkMeta*, hipStream_t, const FillOnePass*);
 
 }  // namespace gpu
