@@ -541,184 +541,6 @@ __device__ __forceinline__ SepIter<Ptr> sep_end(Ptr limit) {
   return SepIter<Ptr>{limit, limit, true};
 }
 
-/*! \brief 4 bytes starting at byte p of an LDS buffer (two aligned dword reads) */
-__device__ __forceinline__ uint32_t lds_u32_at(const uint8_t* lds, uint32_t p) {
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(lds + (p & ~3u));
-  return __builtin_amdgcn_alignbyte(w[1], w[0], p & 3u);  // byte shift
-}
-
-__device__ __forceinline__ uint32_t pow10_small(uint32_t k) {
-  return k >= 4 ? 10000u : (k == 3 ? 1000u : (k == 2 ? 100u : (k == 1 ? 10u : 1u)));
-}
-
-/*!
- * \brief SWAR: number of leading ASCII digits (0..4) of the 4 bytes g (first
- *  byte = lowest) and their decimal value.
- */
-__device__ __forceinline__ uint32_t lead_digits(uint32_t g, uint32_t* val) {
-  const uint32_t hi = (g & 0xF0F0F0F0u) ^ 0x30303030u;           // high nibble != 3
-  const uint32_t lo = ((g & 0x0F0F0F0Fu) + 0x06060606u) & 0x10101010u;  // low nibble > 9
-  const uint32_t bad = hi | (lo << 3);
-  const uint32_t k = bad != 0 ? (static_cast<uint32_t>(__builtin_ctz(bad)) >> 3) : 4u;
-  uint32_t x = g & 0x0F0F0F0Fu;
-  x = k == 0 ? 0u : (x << (8u * (4u - k)));  // the k digits, right-aligned, leading zeros
-  const uint32_t t = (x * 10u + (x >> 8)) & 0x00FF00FFu;
-  *val = (t & 0xFFu) * 100u + (t >> 16);
-  return k;
-}
-
-/*! \brief a decimal number `[sign] digits [. digits]` read from LDS */
-struct FastNum {
-  uint64_t ip, fp, fpow;  // integer / fraction digits and 10^(fraction digits), mod 2^64
-  uint32_t nip;           // integer digit count
-  uint32_t term;          // the byte after the number
-  uint32_t end;           // its offset
-  bool neg, dot, ok;
-};
-
-/*!
- * \brief up to 8 leading digits at p from two speculative 4-byte groups
- *  (branch-free); returns the digit count (8: more may follow), *val their
- *  value, *term the byte that ended the run (when < 8 digits).
- */
-__device__ __forceinline__ uint32_t run8(const uint8_t* lds, uint32_t p, uint32_t* val,
-                                         uint32_t* term) {
-  const uint32_t g0 = lds_u32_at(lds, p);
-  const uint32_t g1 = lds_u32_at(lds, p + 4);
-  uint32_t v0, v1;
-  const uint32_t k0 = lead_digits(g0, &v0);
-  uint32_t k1 = lead_digits(g1, &v1);
-  const bool full = k0 == 4;
-  k1 = full ? k1 : 0u;
-  v1 = full ? v1 : 0u;
-  *val = v0 * pow10_small(k1) + v1;
-  const uint32_t tg = full ? g1 : g0, tk = full ? k1 : k0;
-  *term = tk < 4 ? (tg >> (8u * tk)) & 0xFFu : static_cast<uint32_t>('0');
-  return k0 + k1;
-}
-
-/*! \brief continue a digit run past 8 digits in 64-bit (rare) */
-__device__ uint64_t digit_run_long(const uint8_t* lds, uint32_t* p, uint64_t acc, uint32_t* ndig,
-                                   uint64_t* pw, uint32_t* term, bool* ok) {
-  for (int it = 0; it < 6; ++it) {
-    const uint32_t g = lds_u32_at(lds, *p);
-    uint32_t v;
-    const uint32_t k = lead_digits(g, &v);
-    const uint32_t m = pow10_small(k);
-    acc = acc * m + v;
-    *pw *= m;
-    *ndig += k;
-    *p += k;
-    if (k < 4) {
-      *term = (g >> (8u * k)) & 0xFFu;
-      return acc;
-    }
-  }
-  *ok = false;  // > 32 digits: generic path
-  return acc;
-}
-
-__device__ __forceinline__ uint32_t pow10_u32(uint32_t k) {  // k <= 8
-  return pow10_small(k < 4 ? k : 4u) * pow10_small(k > 4 ? k - 4u : 0u);
-}
-
-__device__ __forceinline__ FastNum fast_num(const uint8_t* lds, uint32_t p) {
-  FastNum r;
-  r.ok = true;
-  const uint32_t c0 = lds[p];
-  r.neg = c0 == '-';
-  p += (c0 == '-' || c0 == '+') ? 1u : 0u;
-  uint32_t v, term;
-  uint32_t k = run8(lds, p, &v, &term);
-  r.ip = v;
-  r.nip = k;
-  p += k;
-  if (k == 8) {
-    uint64_t unused = 1;
-    r.ip = digit_run_long(lds, &p, r.ip, &r.nip, &unused, &term, &r.ok);
-  }
-  r.dot = term == '.';
-  r.fp = 0;
-  r.fpow = 1;
-  if (r.dot) {
-    ++p;
-    uint32_t nf = run8(lds, p, &v, &term);
-    r.fp = v;
-    r.fpow = pow10_u32(nf);
-    p += nf;
-    if (nf == 8) r.fp = digit_run_long(lds, &p, r.fp, &nf, &r.fpow, &term, &r.ok);
-  }
-  r.term = term;
-  r.end = p;
-  return r;
-}
-
-__device__ __forceinline__ bool is_sep(uint32_t c) {
-  return c == ' ' || c == '\t' || c == '\n' || c == '\r';
-}
-
-/*!
- * \brief the reference StrToFloat of a FastNum (strtonum.h): integer digits
- *  accumulated in float are exact below 2^24, so <= 7 of them equal the
- *  integer converted once; the fraction is uint64 digits / uint64 10^n in
- *  double, added as float.  `ok` is false when the generic parser is needed.
- */
-__device__ __forceinline__ float fast_float(const FastNum& n, bool* ok) {
-#if defined(__clang__)
-#pragma clang fp contract(off)
-#endif
-  *ok = n.ok && n.nip <= 7;
-  float v = static_cast<float>(static_cast<uint32_t>(n.ip));
-  const float frac = static_cast<float>(static_cast<double>(n.fp) / static_cast<double>(n.fpow));
-  if (n.dot) v += frac;
-  return n.neg ? -v : v;
-}
-
-/*!
- * \brief single-pass parse of a token starting at LDS offset `off` in the
- *  common shapes: label `[+-]d[.d][:[+-]d[.d]]`, LibSVM feature `d[:[+-]d[.d]]`,
- *  LibFM feature `d:d[:[+-]d[.d]]`, each ended by a separator.  Labels and
- *  features run the same number decodes (no divergence inside a wave); the
- *  second / third number is decoded speculatively and only used when the
- *  first ended in ':'.  Anything else (exponents, signs on indices, junk
- *  bytes, over-long digit runs) returns false and takes strtonum.h's generic
- *  ParsePair / ParseTriple; on the shapes it accepts the results are identical.
- */
-template <TextFormat F>
-__device__ __forceinline__ bool fast_token(const uint8_t* lds, uint32_t off, bool is_label,
-                                           int* r, uint64_t* u0, uint64_t* u1, float* f0,
-                                           float* f1) {
-  const FastNum a = fast_num(lds, off);
-  const FastNum b = fast_num(lds, a.end + 1);
-  const bool a_end = is_sep(a.term), a_col = a.term == ':';
-  const bool b_end = is_sep(b.term);
-  bool fa_ok, fb_ok;
-  const float fa = fast_float(a, &fa_ok);
-  const float fb = fast_float(b, &fb_ok);
-  if (is_label) {
-    *f0 = fa;
-    *f1 = fb;
-    *r = a_end ? 1 : 2;
-    return fa_ok && (a_end || (a_col && b_end && fb_ok));
-  }
-  const bool a_uint = a.ok && !a.neg && !a.dot && a.nip != 0;
-  *u0 = a.ip;
-  if (F == TextFormat::kLibSVM) {
-    *f0 = fb;
-    *r = a_end ? 1 : 2;
-    return a_uint && (a_end || (a_col && b_end && fb_ok));
-  }
-  // LibFM: field:index[:value]
-  const FastNum c = fast_num(lds, b.end + 1);
-  bool fc_ok;
-  const float fc = fast_float(c, &fc_ok);
-  const bool b_uint = b.ok && !b.neg && !b.dot && b.nip != 0;
-  *u1 = b.ip;
-  *f0 = fc;
-  *r = b_end ? 2 : 3;
-  return a_uint && a_col && b_uint && (b_end || (b.term == ':' && is_sep(c.term) && fc_ok));
-}
-
 /*!
  * \brief generic (strtonum.h ParsePair / ParseTriple) parse of the token at
  *  global offset gpos: tokens the register-window decoder does not cover.

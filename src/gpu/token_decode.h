@@ -119,6 +119,72 @@ __device__ __forceinline__ void pow10f(uint32_t k, float* p, float* inv) {
 }
 
 /*!
+ * \brief 12 bytes starting at byte `a` of a 16-byte-aligned LDS buffer (four
+ *  dwords read, three funnel shifts): enough for a sign, 8 digits and the
+ *  byte after them
+ */
+__device__ __forceinline__ uint3 ext12(const uint4* lds, uint32_t a) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(lds) + (a >> 2);
+  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
+  const uint32_t r = a & 3u;
+  return make_uint3(__builtin_amdgcn_alignbyte(w1, w0, r), __builtin_amdgcn_alignbyte(w2, w1, r),
+                    __builtin_amdgcn_alignbyte(w3, w2, r));
+}
+
+/*!
+ * \brief the leading decimal digits of the 8 bytes lo | hi (first byte
+ *  lowest), all 8 at once: k = their count (0..8; 8 = all eight, more may
+ *  follow), val = the value of those k digits (< 10^8), term = the byte after
+ *  them (`next` = byte 8 when k is 8).
+ *
+ *  A byte is a digit iff (byte ^ '0') < 10: after the xor the digit bytes hold
+ *  their values, and the high bit of ((t & 0x7F) + 0x76) | t marks every other
+ *  byte (no carries between bytes).  The first such byte gives k; the k digits
+ *  are right-aligned in 64 bits by a shift of 64 - 8 k (two halves, so k = 0
+ *  and k = 8 need no select); byte dot products give the four digit pairs and
+ *  three 24-bit multiply-adds join them.  About 25 VALU for up to 8 digits,
+ *  where two 4-digit groups and their join took about 45.
+ */
+struct Run8 {
+  uint32_t k, val, term;
+};
+
+__device__ __forceinline__ Run8 digit_run8(uint32_t lo, uint32_t hi, uint32_t next) {
+  const uint32_t t0 = lo ^ 0x30303030u, t1 = hi ^ 0x30303030u;
+  const uint32_t b0 = (((t0 & 0x7F7F7F7Fu) + 0x76767676u) | t0) & 0x80808080u;
+  const uint32_t b1 = (((t1 & 0x7F7F7F7Fu) + 0x76767676u) | t1) & 0x80808080u;
+  const uint64_t bad = (static_cast<uint64_t>(b1) << 32) | b0;
+  // 8 k: the first non-digit's bit is 8 k + 7 (64 when all 8 are digits)
+  const uint32_t c8 = static_cast<uint32_t>(__builtin_ctzg(bad, 64)) & ~7u;
+  const uint32_t half = 32u - (c8 >> 1);  // (64 - 8 k) / 2
+  const uint64_t t = (static_cast<uint64_t>(t1) << 32) | t0;
+  const uint64_t x = (t << half) << half;
+  const uint32_t xl = static_cast<uint32_t>(x), xh = static_cast<uint32_t>(x >> 32);
+  const uint32_t p0 = __builtin_amdgcn_udot4(xl, 0x0000010Au, 0u, false);
+  const uint32_t p1 = __builtin_amdgcn_udot4(xl, 0x010A0000u, 0u, false);
+  const uint32_t p2 = __builtin_amdgcn_udot4(xh, 0x0000010Au, 0u, false);
+  const uint32_t p3 = __builtin_amdgcn_udot4(xh, 0x010A0000u, 0u, false);
+  // (explicit 24-bit multiply-adds: every partial value is < 10^6 < 2^24)
+  // (100 is no inline constant: an SGPR operand)
+  uint32_t v;
+  asm("v_mad_u32_u24 %0, %1, %3, %2" : "=v"(v) : "v"(p0), "v"(p1), "s"(100u));
+  asm("v_mad_u32_u24 %0, %1, %3, %2" : "=v"(v) : "v"(v), "v"(p2), "s"(100u));
+  asm("v_mad_u32_u24 %0, %1, %3, %2" : "=v"(v) : "v"(v), "v"(p3), "s"(100u));
+  Run8 r;
+  r.k = c8 >> 3;
+  r.val = v;
+  const uint64_t raw = (static_cast<uint64_t>(hi) << 32) | lo;
+  r.term = c8 < 64 ? static_cast<uint32_t>(raw >> c8) & 0xFFu : next;
+  return r;
+}
+
+/*! \brief separator bytes and the zero padding: ' ' \t \n \r NUL, one 64-bit
+ *  shift of a bit set instead of five compares */
+__device__ __forceinline__ bool is_end(uint32_t c) {
+  return c <= 32u && ((0x100002601ull >> c) & 1u) != 0;
+}
+
+/*!
  * \brief one number `[+-] digits [. digits]` at LDS byte a, decoded without
  *  branches (every lane of a wave runs the same instructions; the caller
  *  selects what it needs):
@@ -135,8 +201,48 @@ struct Num {
 
 __device__ __forceinline__ Num parse_num_g(uint4 g, uint32_t a);
 
+/*!
+ * \brief parse_num on LDS: the integer digits from a 12-byte window at the
+ *  number, the fraction from a second one at the byte after the '.' (read
+ *  unconditionally: branch-free), each decoded by digit_run8.  The same
+ *  values and flags as parse_num_g on every number whose fraction fits its
+ *  16-byte window; a longer fraction (<= 7 digits) is taken here as well.
+ */
 __device__ __forceinline__ Num parse_num(const uint4* lds, uint32_t a) {
-  return parse_num_g(ext16(lds, a), a);
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+  Num o;
+  const uint3 g = ext12(lds, a);
+  const uint32_t c0 = g.x & 0xFFu;
+  const bool neg = c0 == '-';
+  const uint32_t s = (neg || c0 == '+') ? 1u : 0u;
+  const uint32_t h0 = __builtin_amdgcn_alignbyte(g.y, g.x, s);
+  const uint32_t h1 = __builtin_amdgcn_alignbyte(g.z, g.y, s);
+  const uint32_t nb = (__builtin_amdgcn_alignbyte(g.z, g.y, s + 1u) >> 24);  // byte 8 after the sign
+  const Run8 ir = digit_run8(h0, h1, nb);
+  const uint32_t k = ir.k;
+  const bool dot = ir.term == '.';
+  const uint32_t fa = a + s + k + 1u;
+  const uint3 f = ext12(lds, fa);
+  const Run8 fr = digit_run8(f.x, f.y, f.z & 0xFFu);
+  const uint32_t nf = fr.k;
+  o.ok_float = (k <= 7) & (dot ? ((nf <= 7) & ((k | nf) != 0)) : k != 0);
+  o.ok_uint = (s == 0) & !dot & (k != 0) & !((k == 8) & (ir.term - '0' < 10u));
+  o.term = dot ? fr.term : ir.term;
+  o.end = dot ? fa + nf : a + s + k;
+  o.ival = ir.val;
+  // StrToFloat: float(int digits) + float(F / 10^nf) (see file comment)
+  float p, inv;
+  pow10f(nf, &p, &inv);
+  const float ff = static_cast<float>(fr.val);
+  const float q0 = ff * inv;
+  const float rem = __builtin_fmaf(-q0, p, ff);
+  const float frac = __builtin_fmaf(rem, inv, q0);
+  float v = static_cast<float>(ir.val);
+  v = dot ? v + frac : v;
+  o.fval = neg ? -v : v;
+  return o;
 }
 
 /*! \brief parse_num on the 16 bytes g already read from LDS byte a */
@@ -205,36 +311,26 @@ __device__ __forceinline__ Num parse_num_g(uint4 g, uint32_t a) {
  */
 __device__ __forceinline__ Num parse_int(const uint4* lds, uint32_t a) {
   Num o;
-  const uint4 g = ext16(lds, a);
+  const uint3 g = ext12(lds, a);
   const uint32_t c0 = g.x & 0xFFu;
   const bool neg = c0 == '-';
   const uint32_t s = (neg || c0 == '+') ? 1u : 0u;
   const uint32_t h0 = __builtin_amdgcn_alignbyte(g.y, g.x, s);
   const uint32_t h1 = __builtin_amdgcn_alignbyte(g.z, g.y, s);
-  const uint32_t h2 = __builtin_amdgcn_alignbyte(g.w, g.z, s);
-  uint32_t v0, v1;
-  const uint32_t k0 = lead_digits(h0, &v0);
-  const uint32_t k1 = lead_digits(h1, &v1);
-  uint32_t k;
-  const uint32_t iv = join_groups(k0, v0, k1, v1, &k);
-  const uint32_t tw = k < 4 ? h0 : (k < 8 ? h1 : h2);
-  const uint32_t term = (tw >> (8u * (k & 3u))) & 0xFFu;
-  const bool dot = term == '.';
+  const uint32_t nb = (__builtin_amdgcn_alignbyte(g.z, g.y, s + 1u) >> 24);
+  const Run8 ir = digit_run8(h0, h1, nb);
+  const uint32_t k = ir.k;
+  const bool dot = ir.term == '.';
   o.ok_float = (k <= 7) & (k != 0) & !dot;
-  o.ok_uint = (s == 0) & !dot & (k != 0) & !((k == 8) & ((h2 & 0xFFu) - '0' < 10u));
-  o.term = term;
+  o.ok_uint = (s == 0) & !dot & (k != 0) & !((k == 8) & (ir.term - '0' < 10u));
+  o.term = ir.term;
   o.end = a + s + k;
-  o.ival = iv;
-  const float v = static_cast<float>(iv);
+  o.ival = ir.val;
+  const float v = static_cast<float>(ir.val);
   o.fval = neg ? -v : v;
   return o;
 }
 
-__device__ __forceinline__ bool is_end(uint32_t c) {
-  // separators, or the zero padding past the chunk end (the count pass sends
-  // chunks with other control bytes to the exact kernels)
-  return (c == ' ') | (c == '\t') | (c == '\n') | (c == '\r') | (c == 0);
-}
 
 /*! \brief fast-path result of one token */
 struct Token {
