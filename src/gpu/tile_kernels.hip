@@ -1192,10 +1192,18 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
       any_weight |= active & is_label & (t.r == 2);
       const bool feat = active & !is_label & nnz_ok & field_ok;
       const uint64_t u0 = (static_cast<uint64_t>(t.u0_hi) << 32) | t.u0;
+      // (a feature's rel = i - lc is >= 0 and < 2^13: a 32-bit byte offset
+      // from the SGPR base, no 64-bit address arithmetic per store)
+      const uint32_t boff = static_cast<uint32_t>(rel) * static_cast<uint32_t>(sizeof(IndexType));
+      const uint32_t voff = static_cast<uint32_t>(rel) * 4u;
+      auto at = [](auto* base, uint32_t off) {
+        using T = typename std::remove_pointer<decltype(base)>::type;
+        return reinterpret_cast<T*>(reinterpret_cast<char*>(base) + off);
+      };
       if constexpr (F == TextFormat::kLibSVM) {
         if (feat) {
-          idx_at[rel] = static_cast<IndexType>(u0);
-          val_at[rel] = t.r == 2 ? t.f0 : 1.0f;
+          *at(idx_at, boff) = static_cast<IndexType>(u0);
+          *at(val_at, voff) = t.r == 2 ? t.f0 : 1.0f;
         }
         any_value |= feat && t.r == 2;
         const MaxT iu = static_cast<MaxT>(static_cast<IndexType>(u0));
@@ -1203,9 +1211,9 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
       } else {
         const uint64_t u1 = (static_cast<uint64_t>(t.u1_hi) << 32) | t.u1;
         if (feat) {
-          fld_at[rel] = static_cast<IndexType>(u0);
-          idx_at[rel] = static_cast<IndexType>(u1);
-          val_at[rel] = t.r == 3 ? t.f0 : 1.0f;
+          *at(fld_at, boff) = static_cast<IndexType>(u0);
+          *at(idx_at, boff) = static_cast<IndexType>(u1);
+          *at(val_at, voff) = t.r == 3 ? t.f0 : 1.0f;
         }
         any_value |= feat && t.r == 3;
         const MaxT iu = static_cast<MaxT>(static_cast<IndexType>(u1));

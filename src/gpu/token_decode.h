@@ -165,11 +165,10 @@ __device__ __forceinline__ Run8 digit_run8(uint32_t lo, uint32_t hi, uint32_t ne
   const uint32_t p2 = __builtin_amdgcn_udot4(xh, 0x0000010Au, 0u, false);
   const uint32_t p3 = __builtin_amdgcn_udot4(xh, 0x010A0000u, 0u, false);
   // (explicit 24-bit multiply-adds: every partial value is < 10^6 < 2^24)
-  // (100 is no inline constant: an SGPR operand)
-  uint32_t v;
-  asm("v_mad_u32_u24 %0, %1, %3, %2" : "=v"(v) : "v"(p0), "v"(p1), "s"(100u));
-  asm("v_mad_u32_u24 %0, %1, %3, %2" : "=v"(v) : "v"(v), "v"(p2), "s"(100u));
-  asm("v_mad_u32_u24 %0, %1, %3, %2" : "=v"(v) : "v"(v), "v"(p3), "s"(100u));
+  // (no inline asm here: the compiler must see the dot products' consumers
+  // to place the wait states a DOT result needs before a VALU reads it)
+  // (every partial value is < 10^6 < 2^24; the compiler picks the multiply-add)
+  const uint32_t v = __umul24(__umul24(__umul24(p0, 100u) + p1, 100u) + p2, 100u) + p3;
   Run8 r;
   r.k = c8 >> 3;
   r.val = v;

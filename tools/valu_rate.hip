@@ -59,6 +59,8 @@ __global__ __launch_bounds__(256) void k_probe(uint64_t* out, int iters, uint32_
     if constexpr (OP == 29) asm volatile("v_and_b32 %0, %0, %1\n v_and_b32 %0, %0, %1\n v_and_b32 %0, %0, %1\n v_cndmask_b32_e64 %0, %0, %1, s[20:21]" : "+v"(a##I) : "v"(b)); \
     if constexpr (OP == 30) asm volatile("v_cmp_gt_u32 vcc, %0, %1\n v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a##I) : "v"(b) : "vcc"); \
     if constexpr (OP == 31) asm volatile("v_cmp_gt_u32 s[20:21], %0, %1\n v_cndmask_b32_e64 %0, %0, %1, s[20:21]" : "+v"(a##I) : "v"(b) : "s20", "s21"); \
+    if constexpr (OP == 33) asm volatile("v_mad_u64_u32 v[40:41], s[22:23], %0, %1, v[42:43]\n v_mov_b32 %0, v40" : "+v"(a##I) : "v"(b) : "v40", "v41", "v42", "v43", "s22", "s23"); \
+    if constexpr (OP == 34) asm volatile("v_mad_u32_u24 %0, %0, %1, %2" : "+v"(a##I) : "v"(b), "v"(c)); \
     if constexpr (OP == 32) asm volatile("v_and_b32 %0, %0, %1\n v_and_b32 %0, %0, %1\n v_and_b32 %0, %0, %1\n v_and_b32 %0, %0, %1" : "+v"(a##I) : "v"(b));
     R8(BODY)
     R8(BODY)
@@ -105,7 +107,7 @@ int main(int argc, char** argv) {
       {"v_and_b32_inline", k_probe<26>}, {"v_cndmask_e64_vcc", k_probe<27>},
       {"mix3and_cndmask_vcc", k_probe<28>}, {"mix3and_cndmask_sgpr", k_probe<29>},
       {"cmp_vcc_cndmask", k_probe<30>}, {"cmp_sgpr_cndmask", k_probe<31>},
-      {"mix4and", k_probe<32>}};
+      {"mix4and", k_probe<32>}, {"mad_u64_plus_mov", k_probe<33>}};
   const char* only = argc > 1 ? argv[1] : nullptr;
   const int iters = 4096;
   uint64_t* d;
