@@ -743,10 +743,15 @@ constexpr uint32_t kStageVecs = 2 * kSlotBytes / 16;       // two slots: step s 
 constexpr uint32_t kListCap = kDecodeCarry + kStepBytes / 2;  // carried + a step's tokens
 // deferred-token ring: < 64 left after a queue round + 128 from a pair round
 constexpr uint32_t kQueueCap = 256;
-// k_tile_hash: no carried entries; a step of more tokens is listed in two
-// halves.  Sized so that 5 workgroups fit a CU with a 1024-wide f32 row per
-// wave: 4 x (2112 B text + (428 + 64) x 4 B list) + 16 KiB rows + the ticket
+// k_tile_hash: the tokens after a step's last whole round (< 64) are carried
+// into the next step's rounds; their text moves with them into a 1 KiB carry
+// area in front of the staged step (the window stays contiguous), so no step
+// pays a mostly idle last round.  A step of more tokens than the list holds
+// is listed in two halves.  LDS per workgroup at dim 1024: 4 x (3136 B text +
+// 428 x 4 B list + 64 dummy slots) + 16 KiB rows: 4 workgroups per CU
 constexpr uint32_t kHashListCap = 428;
+constexpr uint32_t kHashCarry = 1024;  // carry area ahead of the staged step
+constexpr uint32_t kHashText = kHashCarry + kSlotBytes;
 
 /*!
  * \brief the 16 B at chunk offset pos, bytes at or past n zeroed (the
@@ -1415,7 +1420,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
   // one staging slot and a list without carried entries: every step decodes
   // all its tokens, so the LDS per wave (+ the dim-wide f32 row) leaves room
   // for 4 workgroups per CU up to dim 1024
-  __shared__ uint4 s_text[kFillWaves][kSlotBytes / 16];
+  __shared__ uint4 s_text[kFillWaves][kHashText / 16];
   __shared__ uint32_t s_list[kFillWaves][kHashListCap + 64];
   extern __shared__ __attribute__((aligned(16))) float s_hrow[];  // kFillWaves x dim
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / dev::kWave);
@@ -1545,6 +1550,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
     if (lane < 4) t = bload16(trs, loff + kStepBytes);
     uint32_t lcnt = 0;   // line starts seen so far (this tile's ordinals)
     uint32_t open = 0;   // ordinal of the row being accumulated (0: none yet)
+    uint32_t carry = 0;  // list entries carried from the previous step (listed, not decoded)
     uint32_t qid_prev = 0;  // LibSVM: status of the last token start (prev_token_status)
 #pragma unroll 1
     for (int s = 0;; ++s) {
@@ -1556,10 +1562,11 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
         b = clip16(b, pos_a + 1024, n);
         t = clip16(t, pos_a + kStepBytes, n);
       }
-      constexpr uint32_t sbase = 0;  // the one slot
-      st[lane] = a;
-      st[64 + lane] = b;
-      if (lane < 4) st[128 + lane] = t;
+      // the step at [kHashCarry, kHashText); carried tokens' text before it
+      constexpr uint32_t sbase = kHashCarry;
+      st[sbase / 16 + lane] = a;
+      st[sbase / 16 + 64 + lane] = b;
+      if (lane < 4) st[sbase / 16 + 128 + lane] = t;
       uint32_t lm_a, tm_a, lm_b, tm_b;
       if constexpr (kOnePass) {
         const uint32_t left_a = dev::lane_shr1(a.w >> 24);
@@ -1636,8 +1643,8 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
       // a step of more tokens than the list holds is listed and decoded in
       // its two 1 KiB halves (a half of more: the exact kernels)
       const uint32_t ntok_b = ntok - ntok_a;
-      const bool split = ntok > kHashListCap;
-      if (split && (ntok_a > kHashListCap || ntok_b > kHashListCap)) {
+      const bool split = carry + ntok > kHashListCap;
+      if (split && (carry + ntok_a > kHashListCap || ntok_b > kHashListCap)) {
         irregular = true;
         break;
       }
@@ -1654,7 +1661,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
         if constexpr (!kOnePass) mk = load_masks(mrs, moff, s + 1);
       }
 
-      list_slice<kHashListCap>(sl, tm_a, lm_a, static_cast<uint32_t>(before & 0xFFFFu),
+      list_slice<kHashListCap>(sl, tm_a, lm_a, carry + static_cast<uint32_t>(before & 0xFFFFu),
                                sbase + lane * 16, la0, lane);
       // split: the b half is listed after the a half's rounds, from two packed
       // registers (few live across the rounds)
@@ -1662,13 +1669,24 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
       const uint32_t pk_o = static_cast<uint32_t>((before >> 16) & 0xFFFFu) | (lb0 << 16);
       if (!split) {
         list_slice<kHashListCap>(sl, tm_b, lm_b,
-                                 ntok_a + static_cast<uint32_t>((before >> 16) & 0xFFFFu),
+                                 carry + ntok_a + static_cast<uint32_t>((before >> 16) & 0xFFFFu),
                                  sbase + 1024 + lane * 16, lb0, lane);
       }
       dev::wave_sync();
+      uint32_t total = 0, ndec = 0;
 #pragma unroll 1
       for (int part = 0;; ++part) {
-        const uint32_t ndec = !split ? ntok : (part == 0 ? ntok_a : ntok_b);
+        // the list: carried tokens, then this step's (or its halves'); only
+        // whole rounds run unless this is the wave's last step, or the first
+        // left-over token starts before the part of the step a carry keeps
+        // (its text would not fit the carry area: decode it all now).  The
+        // a half of a split step is decoded whole.
+        total = !split ? carry + ntok : (part == 0 ? carry + ntok_a : ntok_b);
+        uint32_t rest = (last || (split && part == 0)) ? 0u : total % dev::kWave;
+        if (rest != 0 && (dev::uniform(sl[total - rest]) & 0x1FFFu) < kHashText - kHashCarry - 64u) {
+          rest = 0;
+        }
+        ndec = total - rest;
         for (uint32_t r0 = 0; r0 < ndec; r0 += dev::kWave) {
           const uint32_t li = r0 + slot;
           const bool active = li < ndec;
@@ -1683,13 +1701,13 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
           bool ok = tok::decode<F>(st, off, is_label, &t);
           if (__any(active & !ok)) {
             if (active & !ok) {
-              const tok::ExtToken x = tok::decode_ext<F>(st, off, is_label, kSlotBytes);
+              const tok::ExtToken x = tok::decode_ext<F>(st, off, is_label, kHashText);
               if (x.ok) t = x.t;
               ok = x.ok;
             }
           }
           if (active & !ok) {
-            const size_t gpos = cur + off;
+            const size_t gpos = cur + off - sbase;  // (carried tokens: before cur)
             const GenericResult gr = generic_token<F, IndexType>(text, n, gpos, is_label);
             t = gr.t;
             bad = gr.bad;
@@ -1732,12 +1750,26 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
           }
         }
         if (!split || part == 1) break;
+        carry = 0;  // the a half's list (carried tokens included) is done
         dev::wave_sync();  // the a half's rounds are done with the list
         list_slice<kHashListCap>(sl, pk_m & 0xFFFFu, pk_m >> 16, pk_o & 0xFFFFu,
                                  sbase + 1024 + lane * 16, pk_o >> 16, lane);
         dev::wave_sync();
       }  // part
       if (last) break;
+      // carry the rest: the step's last 1 KiB of text into the carry area (the
+      // next step restages the 64 B after it), its entries to the list front
+      // with offsets moved down by the 2 KiB the text shifts
+      const uint32_t left = total - ndec;
+      dev::wave_sync();  // every lane is done with this step's rounds
+      if (left != 0) {
+        const uint4 keep = st[(kHashText - kHashCarry - 64) / 16 + lane];
+        const uint32_t moved = lane < static_cast<int>(left) ? sl[ndec + lane] : 0u;
+        dev::wave_sync();
+        st[lane] = keep;
+        if (lane < static_cast<int>(left)) sl[lane] = moved - kStepBytes;
+      }
+      carry = left;
       dev::wave_sync();  // every lane is done with this step's text and list
     }
     if (open != 0) flush(open);
