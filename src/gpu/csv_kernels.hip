@@ -33,6 +33,7 @@
  *                         a row's last field settles a missing label / weight;
  *   C4 (tile_kernels.hip) folds max index / flags and closes the offsets.
  */
+#include <dmlc/logging.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -157,14 +158,24 @@ __device__ __forceinline__ void col_scan(const CsvCfg& cfg, bool count, int lane
  *  capped at 4 GiB).  Updates the walk state (all lanes see the same values).
  */
 __device__ __forceinline__ Slice step_slice(uint4 g, uint32_t s, uint32_t nrem, const CsvCfg& cfg,
-                                            int excl_mode, Walk* w, int lane) {
-  const uint32_t p = s * kStep + 16u * lane;
-  const Classes cls = classify16(g, cfg.delim * 0x01010101u);
-  const uint32_t e = cls.eol;  // NUL: past the chunk
-  const uint32_t d = cls.delim;
-  // control bytes, and NULs inside the chunk, are text to the reference
-  const uint32_t inside = p >= nrem ? 0u : (nrem - p >= 16 ? 0xFFFFu : (1u << (nrem - p)) - 1u);
-  const bool bad = (cls.ctl & inside) != 0;
+                                            int excl_mode, Walk* w, int lane,
+                                            const uint32_t* pub = nullptr) {
+  uint32_t e, d;
+  bool bad = false;
+  if (pub != nullptr) {
+    // S1p's published masks (line ends | delimiters << 16); it checked the
+    // control bytes of the whole tile
+    e = *pub & 0xFFFFu;
+    d = *pub >> 16;
+  } else {
+    const uint32_t p = s * kStep + 16u * lane;
+    const Classes cls = classify16(g, cfg.delim * 0x01010101u);
+    e = cls.eol;  // NUL: past the chunk
+    d = cls.delim;
+    // control bytes, and NULs inside the chunk, are text to the reference
+    const uint32_t inside = p >= nrem ? 0u : (nrem - p >= 16 ? 0xFFFFu : (1u << (nrem - p)) - 1u);
+    bad = (cls.ctl & inside) != 0;
+  }
   const uint32_t last_e = (e >> 15) & 1u, last_d = (d >> 15) & 1u;
   const uint32_t up_e = lane_shr1(last_e);
   const uint32_t up_d = lane_shr1(last_d);
@@ -323,7 +334,8 @@ __global__ __launch_bounds__(kThreads) void k_csv_tile_count_pos(const uint8_t* 
                                                                  size_t n, size_t ntiles,
                                                                  CsvCfg cfg,
                                                                  uint64_t* __restrict__ counts,
-                                                                 uint32_t* __restrict__ flags) {
+                                                                 uint32_t* __restrict__ flags,
+                                                                 uint32_t* __restrict__ masks) {
   constexpr int kLoads = static_cast<int>(kTileBytes / 1024);
   const int lane = lane_id();
   const size_t tile = static_cast<size_t>(blockIdx.x) * kWaves + threadIdx.x / kWave;
@@ -339,19 +351,32 @@ __global__ __launch_bounds__(kThreads) void k_csv_tile_count_pos(const uint8_t* 
     pd = c == cfg.delim ? 1u : 0u;
   }
   const uint32_t delim4 = cfg.delim * 0x01010101u;
-  uint32_t rows = 0, fields = 0;
+  uint32_t rows = 0, fields = 0, ctl_any = 0;
+  const bool full = tile0 + kTileBytes <= n;  // (else the bytes past n are no text)
 #pragma unroll
   for (int j = 0; j < kLoads; ++j) {
     const uint32_t w4[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
-    uint32_t he[4], hd[4];
+    uint32_t he[4], hd[4], hc[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       // line ends, and the zeros past the chunk (no field starts there)
-      he[k] = hb_eq(w4[k], 0x0A0A0A0Au) | hb_eq(w4[k], 0x0D0D0D0Du) | hb_eq(w4[k], 0u);
+      const uint32_t nl = hb_eq(w4[k], 0x0A0A0A0Au), cr = hb_eq(w4[k], 0x0D0D0D0Du);
+      he[k] = nl | cr | hb_eq(w4[k], 0u);
       hd[k] = hb_eq(w4[k], delim4);
+      // control bytes other than \t \n \r (NUL included): text to the
+      // reference, so the chunk goes to the exact kernels (the fill's check,
+      // made here once for the whole tile)
+      hc[k] = hb_lt20(w4[k]) & ~(hb_eq(w4[k], 0x09090909u) | nl | cr);
     }
     const uint32_t e = mask16(he[0], he[1], he[2], he[3]);
     const uint32_t d = mask16(hd[0], hd[1], hd[2], hd[3]);
+    uint32_t c = hc[0] | hc[1] | hc[2] | hc[3];
+    if (!full) {  // wave-uniform: only the chunk's last tile
+      const size_t p = tile0 + j * 1024 + 16u * lane;
+      c = p >= n ? 0u : (n - p >= 16 ? c : mask16(hc[0], hc[1], hc[2], hc[3]) & ((1u << (n - p)) - 1u));
+    }
+    ctl_any |= c;
+    masks[(tile * kLoads + j) * kWave + lane] = e | (d << 16);
     const uint32_t last_e = (e >> 15) & 1u, last_d = (d >> 15) & 1u;
     // the byte before each lane's 16: lane - 1's last, lane 0 the previous load's lane 63
     const uint32_t up_e = lane_shr1(last_e), up_d = lane_shr1(last_d);
@@ -364,11 +389,12 @@ __global__ __launch_bounds__(kThreads) void k_csv_tile_count_pos(const uint8_t* 
     fields += static_cast<uint32_t>(__popc(fm));
   }
   const uint64_t c = wave_sum_2x32((static_cast<uint64_t>(rows) << 32) | fields);
+  const bool any_ctl = __any(ctl_any != 0);
   if (lane == 0) {
     const uint32_t r = static_cast<uint32_t>(c >> 32);
     counts[tile] = (c & 0xFFFFFFFF00000000ull) |
                    (static_cast<uint32_t>(c) - r * static_cast<uint32_t>(cfg.zero_excl));
-    flags[tile] = 0u;
+    flags[tile] = any_ctl ? kFlagIrregular : 0u;
   }
 }
 
@@ -396,6 +422,7 @@ __global__ __launch_bounds__(kThreads)
 __attribute__((amdgpu_waves_per_eu(6))) void k_csv_tile_fill(const uint8_t* __restrict__ text,
                                                             size_t n, size_t ntiles, CsvCfg cfg,
                                                             const uint64_t* __restrict__ prefix,
+                                                            const uint32_t* __restrict__ masks,
                                                             FillTarget<IndexType> out,
                                                             MetaPartial* __restrict__ partials,
                                                             uint32_t exp) {
@@ -446,6 +473,21 @@ __attribute__((amdgpu_waves_per_eu(6))) void k_csv_tile_fill(const uint8_t* __re
   }
   const size_t at1 = tile0 + kStep + 16u * lane;
   uint4 pv = *reinterpret_cast<const uint4*>(text + (at1 + 16 <= n ? at1 : 0));
+  // S1p published the line-end / delimiter masks of every 16 bytes: the walk
+  // takes them instead of classifying the bytes again (buffer loads: steps
+  // past the chunk's last tile read zeros)
+  const bool pub = cfg.pos != 0;
+  __amdgpu_buffer_rsrc_t mrs;
+  uint32_t mk = 0;
+  if (pub) {
+    const size_t words = (ntiles - tile) * (kTileBytes / 16);
+    mrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(masks) + tile * (kTileBytes / 16), 0,
+                                            static_cast<uint32_t>(words * 4 > 0xFFFFFFF0ull
+                                                                      ? 0xFFFFFFF0ull
+                                                                      : words * 4),
+                                            0x00020000);
+    mk = __builtin_amdgcn_raw_buffer_load_b32(mrs, static_cast<uint32_t>(lane) * 4, 0, 0);
+  }
   for (uint32_t s = 0; s < kMaxSteps; ++s) {
     const uint32_t slot = (s & 1u) * (kStep / 16);
     // stage step s + 1 in the other slot (its head mirrored when that is slot 0)
@@ -462,7 +504,13 @@ __attribute__((amdgpu_waves_per_eu(6))) void k_csv_tile_fill(const uint8_t* __re
     }
     wave_sync();
     // the fill lists every field with its column: always the column scan
-    const Slice sl = step_slice(ring[slot + lane], s, nrem, cfg, kExclCols, &w, lane);
+    const uint32_t mk_s = mk;
+    if (pub && s + 1 < kMaxSteps) {
+      mk = __builtin_amdgcn_raw_buffer_load_b32(mrs, static_cast<uint32_t>(lane) * 4,
+                                                (s + 1) * kWave * 4, 0);
+    }
+    const Slice sl = step_slice(ring[slot + lane], s, nrem, cfg, kExclCols, &w, lane,
+                                pub ? &mk_s : nullptr);
     // list the lane's fields: x = ring byte | row in tile << 16, y = column | entry in tile << 16
     {
       uint32_t col = sl.col0;
@@ -501,33 +549,25 @@ __attribute__((amdgpu_waves_per_eu(6))) void k_csv_tile_fill(const uint8_t* __re
         const uint32_t col = en.y & 0xFFFFu;
         const uint32_t ent = en.y >> 16;
         const uint8_t* rb = reinterpret_cast<const uint8_t*>(ring);
-        // one LDS read per field: the 16 bytes from the field start serve the
-        // number, its first byte and (usually) the byte after its delimiter
-        const uint4 g16 = tok::ext16(ring, off);
-        const uint32_t c0 = g16.x & 0xFFu;
+        // line end or the zeros past the chunk: one 64-bit shift of a bit set
+        auto eol_c = [](uint32_t c) { return c <= 13u && ((0x2401u >> c) & 1u) != 0; };
         // a field ended by a delimiter is still the row's last one when the
-        // line ends right after that delimiter (no empty trailing field)
-        const uint64_t glo = (static_cast<uint64_t>(g16.y) << 32) | g16.x;
-        const uint64_t ghi = (static_cast<uint64_t>(g16.w) << 32) | g16.z;
-        auto eol_at = [=](uint32_t o) {
-          const uint32_t i = o - off;  // a 64-bit shift, not an indexed array (scratch)
-          const uint64_t h = i < 8u ? glo : ghi;
-          const uint32_t c = i < 16u ? static_cast<uint32_t>((h >> (8u * (i & 7u))) & 0xFFu) : rb[o];
-          return c == '\n' || c == '\r' || c == 0;
-        };
+        // line ends right after that delimiter (no empty trailing field):
+        // single LDS byte reads (the ring mirrors slot 0's head past slot 1)
+        const uint32_t c0 = rb[off];
         float v;
         bool last;
         if (exp & 1u) {  // pricing: no number decode
           v = static_cast<float>(c0);
-          last = eol_at(off + 8);
-        } else if (c0 == delim || c0 == '\n' || c0 == '\r' || c0 == 0) {
+          last = eol_c(rb[off + 8]);
+        } else if (c0 == delim || eol_c(c0)) {
           v = 0.0f;  // empty field
-          last = c0 != delim || eol_at(off + 1);
+          last = c0 != delim || eol_c(rb[off + 1]);
         } else {
-          const tok::Num x = tok::parse_num_g(g16, off);
-          const bool t_eol = x.term == '\n' || x.term == '\r' || x.term == 0;
-          // (the window is dead before the generic call below)
-          const bool last_fast = t_eol || eol_at(x.end + 1);
+          // the 8-digit run decoder of the LibSVM fill (token_decode.h)
+          const tok::Num x = tok::parse_num(ring, off);
+          const bool t_eol = eol_c(x.term);
+          const bool last_fast = t_eol || eol_c(rb[x.end + 1]);
           if (x.ok_float && (x.term == delim || t_eol)) {
             v = x.fval;
             last = last_fast;
@@ -622,20 +662,27 @@ CsvCfg MakeCfg(int label_column, int weight_column, char delimiter) {
 
 void LaunchCsvTileCount(const char* text, size_t nbytes, int label_column, int weight_column,
                         char delimiter, uint64_t* tile_counts, uint32_t* tile_flags,
-                        hipStream_t stream) {
+                        uint32_t* tile_masks, hipStream_t stream) {
   const size_t ntiles = TileCount(nbytes);
   if (ntiles == 0) return;
   const CsvCfg cfg = MakeCfg(label_column, weight_column, delimiter);
-  hipLaunchKernelGGL(cfg.pos ? k_csv_tile_count_pos : k_csv_tile_count,
-                     dim3((ntiles + kWaves - 1) / kWaves), dim3(kThreads), 0, stream,
-                     reinterpret_cast<const uint8_t*>(text), nbytes, ntiles, cfg, tile_counts,
-                     tile_flags);
+  const dim3 grid((ntiles + kWaves - 1) / kWaves);
+  const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
+  if (cfg.pos) {
+    CHECK(tile_masks != nullptr) << "LaunchCsvTileCount: positional counts publish tile_masks";
+    hipLaunchKernelGGL(k_csv_tile_count_pos, grid, dim3(kThreads), 0, stream, t, nbytes, ntiles, cfg,
+                       tile_counts, tile_flags, tile_masks);
+  } else {
+    hipLaunchKernelGGL(k_csv_tile_count, grid, dim3(kThreads), 0, stream, t, nbytes, ntiles, cfg,
+                       tile_counts, tile_flags);
+  }
 }
 
 template <typename IndexType>
 void LaunchCsvTileFill(const char* text, size_t nbytes, int label_column, int weight_column,
-                       char delimiter, const uint64_t* tile_prefix, const FillTarget<IndexType>& out,
-                       MetaPartial* partials, hipStream_t stream) {
+                       char delimiter, const uint64_t* tile_prefix, const uint32_t* tile_masks,
+                       const FillTarget<IndexType>& out, MetaPartial* partials,
+                       hipStream_t stream) {
   const size_t ntiles = TileCount(nbytes);
   if (ntiles == 0) return;
   static const uint32_t exp = [] {
@@ -644,14 +691,16 @@ void LaunchCsvTileFill(const char* text, size_t nbytes, int label_column, int we
   }();
   hipLaunchKernelGGL((k_csv_tile_fill<IndexType>), dim3((ntiles + kWaves - 1) / kWaves),
                      dim3(kThreads), 0, stream, reinterpret_cast<const uint8_t*>(text), nbytes,
-                     ntiles, MakeCfg(label_column, weight_column, delimiter), tile_prefix, out,
-                     partials, exp);
+                     ntiles, MakeCfg(label_column, weight_column, delimiter), tile_prefix,
+                     tile_masks, out, partials, exp);
 }
 
 template void LaunchCsvTileFill<uint32_t>(const char*, size_t, int, int, char, const uint64_t*,
-                                          const FillTarget<uint32_t>&, MetaPartial*, hipStream_t);
+                                          const uint32_t*, const FillTarget<uint32_t>&,
+                                          MetaPartial*, hipStream_t);
 template void LaunchCsvTileFill<uint64_t>(const char*, size_t, int, int, char, const uint64_t*,
-                                          const FillTarget<uint64_t>&, MetaPartial*, hipStream_t);
+                                          const uint32_t*, const FillTarget<uint64_t>&,
+                                          MetaPartial*, hipStream_t);
 
 }  // namespace gpu
 }  // namespace dmlc

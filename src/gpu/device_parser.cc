@@ -728,7 +728,7 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
                        uint32_t* masks, ChunkMeta* dmeta, ChunkMeta* hm, hipStream_t s) {
     if (tcfg_.format == TextFormat::kCSV) {
       LaunchCsvTileCount(text, nbytes, tcfg_.label_column, tcfg_.weight_column, tcfg_.delimiter,
-                         counts, flags, s);
+                         counts, flags, masks, s);
       LaunchTileScanRaw(counts, flags, TileCount(nbytes), dmeta, hm, s);
     } else {
       LaunchTileCountScan(text, nbytes, counts, flags, masks, dmeta, hm, s);
@@ -822,7 +822,8 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     const bool need_weight = tcfg_.weight_column >= 0;
     FillTarget<IndexType> tgt = PrepareOutput(out, row_base, nnz_base, *plan, need_weight, nbytes);
     LaunchCsvTileFill<IndexType>(text, nbytes, tcfg_.label_column, tcfg_.weight_column,
-                                 tcfg_.delimiter, tcounts_.get<uint64_t>(), tgt,
+                                 tcfg_.delimiter, tcounts_.get<uint64_t>(),
+                                 tmasks_.get<uint32_t>(), tgt,
                                  slots_.get<MetaPartial>(), s);
     LaunchTileFinish(slots_.get<MetaPartial>(), ntiles, dmeta, hm, tgt.offset, row_base, nnz_base,
                      s);

@@ -266,11 +266,13 @@ void LaunchTileFinish(MetaPartial* partials, size_t nslots, ChunkMeta* meta, Chu
  *  With label / weight columns of at most 0 the counts are positional (S1p:
  *  row starts and entries whose first byte is in the tile, no flags) and the
  *  fill flags irregular chunks; LaunchCsvTileFill takes the same columns, so
- *  both pick the same mode.
+ *  both pick the same mode.  The positional count also publishes every 16
+ *  bytes' line-end / delimiter masks into tile_masks (TileMaskWords) and
+ *  flags control bytes; the fill then reads the masks instead of classifying.
  */
 void LaunchCsvTileCount(const char* text, size_t nbytes, int label_column, int weight_column,
                         char delimiter, uint64_t* tile_counts, uint32_t* tile_flags,
-                        hipStream_t stream);
+                        uint32_t* tile_masks, hipStream_t stream);
 /*!
  * \brief S2: every row of a regular chunk into out (index / value / label /
  *  weight / offset) from the scanned S1 prefixes; one MetaPartial per tile
@@ -278,8 +280,9 @@ void LaunchCsvTileCount(const char* text, size_t nbytes, int label_column, int w
  */
 template <typename IndexType>
 void LaunchCsvTileFill(const char* text, size_t nbytes, int label_column, int weight_column,
-                       char delimiter, const uint64_t* tile_prefix, const FillTarget<IndexType>& out,
-                       MetaPartial* partials, hipStream_t stream);
+                       char delimiter, const uint64_t* tile_prefix, const uint32_t* tile_masks,
+                       const FillTarget<IndexType>& out, MetaPartial* partials,
+                       hipStream_t stream);
 
 // ----------------------------- RecordIO (K7) -----------------------------
 /*! \brief error bits reported by the RecordIO kernels */
