@@ -156,8 +156,9 @@ def transpose(csr: Dict, num_features: int, out: Optional[Dict] = None) -> Dict:
     written once, instead of one memory-side f32 atomic per nonzero, which
     runs ~17x below the contiguous atomic rate when 64 lanes hit 64 different
     rows (MI355X_MICROARCH.md, Global float atomics).  Feature ids must be
-    < num_features <= ``_dmlc.csr_transpose_max_features()`` (2^22); an id
-    outside raises.
+    < num_features <= ``_dmlc.csr_transpose_max_features()`` (2^28: up to
+    2^22 columns a two-level sort, above it three levels); an id outside
+    raises.
 
     The sort's scratch (~10 bytes per entry) is a persistent per-device,
     per-stream workspace (:func:`release_workspace` frees it).  ``out``: a
@@ -258,7 +259,7 @@ class SpMVFunction(torch.autograd.Function):
             ctx.holder["_backward_calls"] = uses
             ctx.holder["_calls_key"] = key
             # auto: only feature spaces the counting-sort transpose takes
-            # (<= 2^22 columns); wider models keep the atomic scatter, which
+            # (<= 2^28 columns); wider models keep the atomic scatter, which
             # has no column limit.  "transpose" asked for it: transpose() raises
             fits = ctx.num_features <= _dmlc.csr_transpose_max_features()
             if ctx.grad == "transpose" or (fits and (uses >= 2 or _whole(ctx.csr))):
@@ -280,8 +281,9 @@ def csr_spmv(csr: Dict, w: torch.Tensor, bias: torch.Tensor, grad: str = "auto")
     10 M x 1 M batch) or as an
     f32-atomic scatter: grad="auto" (the default) builds the transpose on the
     first backward of a whole CSR and once a row-slice dict is seen a second
-    time (only up to ``_dmlc.csr_transpose_max_features()`` columns; wider
-    models stay on the atomic form), "transpose" at once, "atomic" never."""
+    time (only up to ``_dmlc.csr_transpose_max_features()`` = 2^28 columns;
+    wider models stay on the atomic form), "transpose" at once, "atomic"
+    never."""
     if grad not in ("auto", "transpose", "atomic"):
         raise ValueError(f"grad must be 'auto', 'transpose' or 'atomic', got {grad!r}")
     return SpMVFunction.apply(w, bias, (csr["offset"], csr["index"], csr.get("value")), csr, grad)

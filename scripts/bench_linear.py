@@ -21,7 +21,12 @@ def main():
     ap.add_argument("--rows", type=int, default=10_000_000)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--data", default="/tmp/dmlc_linear_bench")
+    ap.add_argument("--num-features", type=int, default=0,
+                    help="feature space of the synthetic data (0: the generator's default, ~1 M)")
+    ap.add_argument("--skip-models", action="store_true", help="kernels and transpose only")
     args = ap.parse_args()
+    if args.num_features:
+        args.data = f"{args.data}_{args.num_features}"
     import torch
 
     from dmlc_core_amd import data, ops
@@ -33,12 +38,13 @@ def main():
     for i in range(nfiles):
         f = os.path.join(args.data, f"part-{i:03d}.libsvm")
         if not os.path.exists(f):
+            kw = {"num_features": args.num_features} if args.num_features else {}
             data.write_synthetic(f + ".tmp", i * per, min(args.rows, (i + 1) * per), seed=0,
-                                 nthread=16)
+                                 nthread=16, **kw)
             os.replace(f + ".tmp", f)
     csr = data.GPUParser(args.data).parse_all()
     t = data.csr_to_torch(csr)
-    nrows, nnz, nfeat = csr.rows, csr.nnz, csr.max_index + 1
+    nrows, nnz, nfeat = csr.rows, csr.nnz, max(csr.max_index + 1, args.num_features)
     w = torch.randn(nfeat, device="cuda") * 0.01
     d = torch.randn(nrows, device="cuda")
 
@@ -87,7 +93,7 @@ def main():
     tt_bytes = nnz * 8 + (nfeat + 1) * 8
     res["spmv_t_gather"] = {"ms": round(ms, 3), "csc_GBps": round(tt_bytes / ms / 1e6, 1)}
     del tt
-    for mode in ("atomic", "transpose"):
+    for mode in () if args.skip_models else ("atomic", "transpose"):
         model = SparseLogReg(nfeat, grad=mode).cuda()
 
         def step():

@@ -10,7 +10,8 @@
  *
  *  Column c = (bucket c >> kB, low key c & (L - 1)), L = 2^kB columns per
  *  bucket (kB = 10 .. 12, LowBits: the narrowest that keeps at most
- *  kMaxBuckets buckets, so feature ids < 2^22):
+ *  kMaxBuckets buckets, so feature ids < 2^22; wider feature spaces, up to
+ *  2^28, take the three-level sort of RunSort3 below):
  *   T1 k_bucket_hist  one workgroup per block of BlockSubs() sub-tiles (in CSR
  *      order): LDS histogram of buckets -> G[bucket][block].
  *   T2 exclusive scan of G (bucket-major): where each (bucket, block) run
@@ -151,13 +152,13 @@ __global__ void k_chunk_rows(const uint64_t* __restrict__ offset, size_t nrows, 
   if (c * kChunk < nnz) chunk_row[c] = row_of(offset, nrows, base, c * kChunk);
 }
 
-template <typename IndexType, int kB>
+template <typename IndexType, int kB, typename KeyT = uint16_t>
 __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
     const uint64_t* __restrict__ offset, size_t nrows, uint64_t base,
     const IndexType* __restrict__ index, const float* __restrict__ value, uint64_t nnz,
     uint64_t num_features, uint32_t nbuckets, int bucket_bits, const uint64_t* __restrict__ G,
     size_t nblocks, uint64_t block_elems, const uint32_t* __restrict__ chunk_row,
-    uint16_t* __restrict__ t_key, uint32_t* __restrict__ t_row, uint2* __restrict__ t_rv) {
+    KeyT* __restrict__ t_key, uint32_t* __restrict__ t_row, uint2* __restrict__ t_rv) {
   // the sub-tile, sorted by (bucket, position) in LDS before it leaves
   __shared__ uint32_t s_col[kSubElems];
   __shared__ uint32_t s_row[kSubElems];
@@ -327,7 +328,7 @@ __global__ __launch_bounds__(kThreads) void k_bucket_scatter(
       const uint32_t c = s_col[j];
       const uint32_t b = c >> kB;
       const uint64_t p = static_cast<uint64_t>(gcur[b]) + (j - lstart[b]);
-      t_key[p] = static_cast<uint16_t>(c & ((1u << kB) - 1u));
+      t_key[p] = static_cast<KeyT>(c & ((1u << kB) - 1u));
       // (row, value) as one 8-byte pair: two store streams per sub-tile
       // instead of three, one load per entry in T4c
       if (value != nullptr) {
@@ -559,6 +560,205 @@ __global__ __launch_bounds__(dev::kWave) void k_lowkey_scatter(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Three levels (feature spaces above 2^22, up to 2^28).  T1-T3 split the
+// entries into <= 1024 buckets of 2^S columns (S = 16 .. 18, the low S bits
+// kept as a u32 key); a bucket's 2^S columns are too many for one LDS cursor
+// table, so two more stable counting-sort passes of T4's shape follow:
+//   L2 per (bucket, segment): digit = key >> 8 (2^(S-8) values) -> the
+//      entries in (bucket, mid) "super-bucket" order, the low 8 bits kept as
+//      a u8 key; the super-bucket starts come from L2's scan;
+//   L3 per super-bucket (one segment: ~400 entries each at 2^26 x 400 M):
+//      digit = the low 8 bits -> the final CSC position, the column pointer.
+// Every pass scatters into at most 1024 (L2) / 256 (L3) open runs per wave
+// (T4c's 1024 - 4096 in the two-level sort).
+
+/*! \brief [begin, end) of segment s of kSeg segments of bucket b */
+template <int kSeg>
+__device__ __forceinline__ void seg_range(const uint64_t* __restrict__ bstart, uint32_t b, int s,
+                                          uint64_t* begin, uint64_t* end) {
+  const uint64_t b0 = bstart[b], b1 = bstart[b + 1];
+  const uint64_t n = b1 - b0;
+  *begin = b0 + n * static_cast<uint64_t>(s) / kSeg;
+  *end = b0 + n * static_cast<uint64_t>(s + 1) / kSeg;
+}
+
+/*! \brief L2 / L3 histogram: per (bucket, segment), the digit (key >> kShift)
+ *  & (2^kB - 1) of its entries -> H[bucket][segment][2^kB] */
+template <typename KeyIn, int kShift, int kB, int kSeg>
+__global__ __launch_bounds__(kThreads) void k_digit_hist(const KeyIn* __restrict__ key,
+                                                         const uint64_t* __restrict__ bstart,
+                                                         uint32_t* __restrict__ H) {
+  constexpr uint32_t kLow = 1u << kB;
+  __shared__ uint32_t hist[kLow];
+  const uint32_t b = blockIdx.x / kSeg;
+  const int s = static_cast<int>(blockIdx.x % kSeg);
+  for (uint32_t c = threadIdx.x; c < kLow; c += kThreads) hist[c] = 0;
+  __syncthreads();
+  uint64_t e0, e1;
+  seg_range<kSeg>(bstart, b, s, &e0, &e1);
+  for (uint64_t e = e0 + threadIdx.x; e < e1; e += kThreads) {
+    atomicAdd(&hist[(static_cast<uint32_t>(key[e]) >> kShift) & (kLow - 1u)], 1u);
+  }
+  __syncthreads();
+  uint32_t* out = H + static_cast<size_t>(blockIdx.x) * kLow;
+  for (uint32_t c = threadIdx.x; c < kLow; c += kThreads) out[c] = hist[c];
+}
+
+/*! \brief L2 / L3 scan, per bucket: digit totals over the segments -> the
+ *  exclusive starts `starts[b * 2^kB + digit]` (absolute positions; entries
+ *  past nstarts are not written) and absolute per-segment cursors in H */
+template <int kB, int kSeg>
+__global__ __launch_bounds__(kThreads) void k_digit_scan(uint32_t* __restrict__ H,
+                                                         const uint64_t* __restrict__ bstart,
+                                                         uint64_t nstarts,
+                                                         uint64_t* __restrict__ starts) {
+  constexpr uint32_t kLow = 1u << kB;
+  constexpr uint32_t kPer = (kLow + kThreads - 1) / kThreads;
+  __shared__ uint32_t s_tot[kLow];
+  __shared__ uint64_t swave[kWaves];
+  const uint32_t b = blockIdx.x;
+  uint32_t* Hb = H + static_cast<size_t>(b) * kSeg * kLow;
+  for (uint32_t c = threadIdx.x; c < kLow; c += kThreads) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int q = 0; q < kSeg; ++q) {
+      const uint32_t h = Hb[static_cast<size_t>(q) * kLow + c];
+      Hb[static_cast<size_t>(q) * kLow + c] = acc;
+      acc += h;
+    }
+    s_tot[c] = acc;
+  }
+  __syncthreads();
+  const uint32_t c0 = threadIdx.x * kPer;
+  uint32_t tot[kPer];
+  uint64_t sum = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) {
+    tot[i] = c0 + i < kLow ? s_tot[c0 + i] : 0u;
+    sum += tot[i];
+  }
+  uint64_t wtot;
+  const uint64_t wx = dev::wave_excl_scan(sum, &wtot);
+  const int w = threadIdx.x / dev::kWave;
+  if (dev::lane_id() == 0) swave[w] = wtot;
+  __syncthreads();
+  uint64_t x = wx;
+  for (int q = 0; q < w; ++q) x += swave[q];
+  const uint64_t base = bstart[b];
+  __syncthreads();  // every thread has read s_tot
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) {
+    const uint32_t c = c0 + i;
+    if (c < kLow) {
+      const uint64_t g = static_cast<uint64_t>(b) * kLow + c;
+      if (g < nstarts) starts[g] = base + x;
+      s_tot[c] = static_cast<uint32_t>(x);
+      x += tot[i];
+    }
+  }
+  __syncthreads();
+  for (uint32_t c = threadIdx.x; c < kLow; c += kThreads) {
+    const uint32_t start = s_tot[c];
+#pragma unroll
+    for (int q = 0; q < kSeg; ++q) Hb[static_cast<size_t>(q) * kLow + c] += start;
+  }
+}
+
+/*!
+ * \brief L2 / L3 stable scatter: one wave per (bucket, segment), digit ranks
+ *  by ballots as in T4c; the (row, value) pair (or the row) moves to
+ *  bucket base + cursor, and with key_out the key's low 8 bits go along (L2).
+ *  Output pairs when kPair (row / value arrays of the final CSC, or L2's
+ *  intermediate pair array); rows alone otherwise.
+ */
+template <typename KeyIn, int kShift, int kB, int kSeg, bool kPair>
+__global__ __launch_bounds__(dev::kWave) void k_digit_scatter(
+    const KeyIn* __restrict__ key, const uint32_t* __restrict__ t_row,
+    const uint2* __restrict__ t_rv, const uint64_t* __restrict__ bstart,
+    const uint32_t* __restrict__ H, uint8_t* __restrict__ key_out, uint32_t* __restrict__ row_out,
+    float* __restrict__ val_out, bool with_values) {
+  constexpr uint32_t kLow = 1u << kB;
+  constexpr int kDepth = 8;
+  __shared__ uint32_t cur[kLow];
+  const uint32_t b = blockIdx.x / kSeg;
+  const int s = static_cast<int>(blockIdx.x % kSeg);
+  const int lane = dev::lane_id();
+  const uint32_t* Hs = H + static_cast<size_t>(blockIdx.x) * kLow;
+  for (uint32_t c = lane; c < kLow; c += dev::kWave) cur[c] = Hs[c];
+  dev::wave_sync();
+  uint64_t e0, e1;
+  seg_range<kSeg>(bstart, b, s, &e0, &e1);
+  const uint64_t base = bstart[b];
+  const uint64_t below = lanes_below();
+  struct Batch {
+    uint32_t k[kDepth], r[kDepth], v[kDepth];
+  };
+  auto load = [&](uint64_t at, Batch* x) {
+#pragma unroll
+    for (int j = 0; j < kDepth; ++j) {
+      const uint64_t e = at + static_cast<uint64_t>(j) * dev::kWave + lane;
+      const bool ok = e < e1;
+      x->k[j] = ok ? static_cast<uint32_t>(key[e]) : 0u;
+      if (with_values) {
+        const uint2 rv = ok ? t_rv[e] : make_uint2(0u, 0u);
+        x->r[j] = rv.x;
+        x->v[j] = rv.y;
+      } else {
+        x->r[j] = ok ? t_row[e] : 0u;
+        x->v[j] = 0u;
+      }
+    }
+  };
+  auto process = [&](uint64_t at, const Batch& x) {
+    uint32_t rk[kDepth];
+#pragma unroll
+    for (int j = 0; j < kDepth; ++j) {
+      const bool valid = at + static_cast<uint64_t>(j) * dev::kWave + lane < e1;
+      const uint64_t m = match_lanes((x.k[j] >> kShift) & (kLow - 1u), kB, valid);
+      rk[j] = static_cast<uint32_t>(__popcll(m & below)) |
+              (static_cast<uint32_t>(__popcll(m)) << 8);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int j = 0; j < kDepth; ++j) {
+      const uint64_t g = at + static_cast<uint64_t>(j) * dev::kWave;
+      if (g >= e1) break;  // wave-uniform
+      const bool valid = g + lane < e1;
+      const uint32_t d = (x.k[j] >> kShift) & (kLow - 1u);
+      const uint32_t rank = rk[j] & 0xFFu, n = rk[j] >> 8;
+      const uint32_t before = valid ? cur[d] : 0u;
+      dev::wave_sync();
+      if (valid) {
+        const uint64_t pos = base + before + rank;  // (cursors: from the bucket base)
+        if (key_out != nullptr) key_out[pos] = static_cast<uint8_t>(x.k[j] & 0xFFu);
+        if constexpr (kPair) {
+          reinterpret_cast<uint2*>(row_out)[pos] = make_uint2(x.r[j], x.v[j]);
+        } else {
+          row_out[pos] = x.r[j];
+          if (val_out != nullptr) val_out[pos] = __uint_as_float(x.v[j]);
+        }
+        if (rank + 1 == n) cur[d] = before + n;
+      }
+      dev::wave_sync();
+    }
+  };
+  constexpr uint64_t kBatch = static_cast<uint64_t>(kDepth) * dev::kWave;
+  Batch A, B;
+  load(e0, &A);
+  for (uint64_t at = e0; at < e1; at += 2 * kBatch) {
+    load(at + kBatch, &B);
+    process(at, A);
+    if (at + kBatch >= e1) break;
+    load(at + 2 * kBatch, &A);
+    process(at + kBatch, B);
+  }
+}
+
+__global__ void k_starts_close(uint64_t* __restrict__ starts, uint64_t n, uint64_t nnz) {
+  starts[n] = nnz;
+}
+
 __global__ void k_transpose_close(const uint64_t* __restrict__ bstart, uint32_t nbuckets,
                                   uint64_t num_features, uint64_t* __restrict__ col_ptr) {
   col_ptr[num_features] = bstart[nbuckets];
@@ -574,7 +774,15 @@ struct TransposePlan {
   size_t nblocks;
   size_t g_words, partials_words, h_words, nchunks;
   size_t key_off, row_off, val_off, g_off, partials_off, h_off, chunk_off, total;
+  // three levels (low_bits = S > kMaxLowBits): L2 digits 2^(S - 8), super-buckets
+  bool three;
+  uint64_t nsuper;
+  size_t key2_off, rv2_off, super_off;
 };
+
+constexpr int kL2Seg = 16;  // L2 segments per bucket
+constexpr int kL3Bits = 8;  // L3 digit: the low 8 bits
+constexpr int kMaxBits3 = 18;  // S <= 18: 2^28 features
 
 /*!
  * \brief columns per bucket for a feature space: the narrowest of 2^10 ..
@@ -608,7 +816,16 @@ int BlockSubs() {
 
 TransposePlan Plan(uint64_t nnz, uint64_t num_features) {
   TransposePlan p;
+  p.three = num_features > (static_cast<uint64_t>(kMaxBuckets) << kMaxLowBits);
   p.low_bits = LowBits(num_features);
+  if (p.three) {
+    // S = 16 .. 18: the narrowest bucket width that keeps <= kMaxBuckets buckets
+    p.low_bits = 16;
+    while (p.low_bits < kMaxBits3 &&
+           num_features > (static_cast<uint64_t>(kMaxBuckets) << p.low_bits)) {
+      ++p.low_bits;
+    }
+  }
   const uint64_t low = uint64_t(1) << p.low_bits;
   p.nbuckets = static_cast<uint32_t>((num_features + low - 1) / low);
   if (p.nbuckets == 0) p.nbuckets = 1;
@@ -620,10 +837,18 @@ TransposePlan Plan(uint64_t nnz, uint64_t num_features) {
   p.g_words = static_cast<size_t>(p.nbuckets) * p.nblocks + 1;  // + the bucket-end sentinel
   p.partials_words = ScanPartials(p.g_words) + 2;
   p.h_words = static_cast<size_t>(p.nbuckets) * kSegments * low;
+  p.nsuper = 0;
+  if (p.three) {
+    const uint64_t mid = uint64_t(1) << (p.low_bits - kL3Bits);
+    p.nsuper = static_cast<uint64_t>(p.nbuckets) * mid;
+    const size_t h2 = static_cast<size_t>(p.nbuckets) * kL2Seg * mid;
+    const size_t h3 = static_cast<size_t>(p.nsuper) << kL3Bits;
+    p.h_words = h2 > h3 ? h2 : h3;
+  }
   p.nchunks = (nnz + kChunk - 1) / kChunk;
   size_t off = 0;
   p.key_off = off;
-  off += AlignUp(nnz * sizeof(uint16_t));
+  off += AlignUp(nnz * (p.three ? sizeof(uint32_t) : sizeof(uint16_t)));
   p.row_off = off;
   off += AlignUp(nnz * sizeof(uint32_t));
   p.val_off = off;
@@ -636,6 +861,15 @@ TransposePlan Plan(uint64_t nnz, uint64_t num_features) {
   off += AlignUp(p.h_words * sizeof(uint32_t));
   p.chunk_off = off;
   off += AlignUp((p.nchunks + 1) * sizeof(uint32_t));
+  p.key2_off = p.rv2_off = p.super_off = 0;
+  if (p.three) {
+    p.key2_off = off;
+    off += AlignUp(nnz * sizeof(uint8_t));
+    p.rv2_off = off;
+    off += AlignUp(nnz * sizeof(uint2));
+    p.super_off = off;
+    off += AlignUp((p.nsuper + 1) * sizeof(uint64_t));
+  }
   p.total = off;
   return p;
 }
@@ -703,6 +937,79 @@ void RunSort(const TransposePlan& p, const uint64_t* offset, size_t nrows, uint6
   hipLaunchKernelGGL(k_transpose_close, dim3(1), dim3(1), 0, stream, bstart, p.nbuckets,
                      num_features, col_ptr);
 }
+/*! \brief the three-level sort (feature spaces above 2^22): T1-T3 into
+ *  buckets of 2^S columns with u32 keys, L2 into super-buckets of 256
+ *  columns, L3 into the CSC */
+template <typename IndexType, int kS>
+void RunSort3(const TransposePlan& p, const uint64_t* offset, size_t nrows, uint64_t base,
+              uint64_t nnz, const IndexType* index, const float* value, uint64_t num_features,
+              uint64_t* col_ptr, uint32_t* row_out, float* val_out, void* scratch,
+              uint32_t* error, hipStream_t stream) {
+  constexpr int kMid = kS - kL3Bits;  // L2 digit bits
+  char* sc = static_cast<char*>(scratch);
+  uint32_t* t_key = reinterpret_cast<uint32_t*>(sc + p.key_off);
+  uint32_t* t_row = reinterpret_cast<uint32_t*>(sc + p.row_off);
+  uint2* t_rv = reinterpret_cast<uint2*>(sc + p.row_off);
+  uint64_t* G = reinterpret_cast<uint64_t*>(sc + p.g_off);
+  uint64_t* partials = reinterpret_cast<uint64_t*>(sc + p.partials_off);
+  uint32_t* H = reinterpret_cast<uint32_t*>(sc + p.h_off);
+  uint32_t* chunk_row = reinterpret_cast<uint32_t*>(sc + p.chunk_off);
+  uint8_t* t_key2 = reinterpret_cast<uint8_t*>(sc + p.key2_off);
+  uint2* t_rv2 = reinterpret_cast<uint2*>(sc + p.rv2_off);
+  uint32_t* t_row2 = reinterpret_cast<uint32_t*>(sc + p.rv2_off);
+  uint64_t* sstart = reinterpret_cast<uint64_t*>(sc + p.super_off);
+  uint64_t* bstart = reinterpret_cast<uint64_t*>(sc + p.total);
+  const IndexType* idx = index + base;
+  const float* val = value != nullptr ? value + base : nullptr;
+  const bool with_values = value != nullptr;
+  // L1 = T1 + T2 + T3 at 2^kS columns per bucket (u32 keys)
+  DMLC_HIP_CHECK(hipMemsetAsync(G, 0, p.g_words * sizeof(uint64_t), stream));
+  if (nnz != 0) {
+    hipLaunchKernelGGL((k_bucket_hist<IndexType, kS>), dim3(p.nblocks), dim3(kThreads), 0, stream,
+                       idx, nnz, num_features, p.nbuckets, G, p.nblocks, p.block_elems, error);
+  }
+  LaunchScanU64(G, p.g_words, partials, partials + p.partials_words - 1, stream);
+  hipLaunchKernelGGL(k_bucket_starts, dim3((p.nbuckets + kThreads) / kThreads), dim3(kThreads), 0,
+                     stream, G, p.nblocks, p.nbuckets, nnz, bstart);
+  if (nnz != 0) {
+    hipLaunchKernelGGL(k_chunk_rows, dim3((p.nchunks + kThreads - 1) / kThreads), dim3(kThreads),
+                       0, stream, offset, nrows, base, nnz, chunk_row);
+    hipLaunchKernelGGL((k_bucket_scatter<IndexType, kS, uint32_t>), dim3(p.nblocks),
+                       dim3(kThreads), 0, stream, offset, nrows, base, idx, val, nnz,
+                       num_features, p.nbuckets, p.bucket_bits, G, p.nblocks, p.block_elems,
+                       chunk_row, t_key, t_row, t_rv);
+  }
+  // L2: per (bucket, segment), digit = key >> 8 -> super-bucket order
+  const unsigned n2 = p.nbuckets * kL2Seg;
+  hipLaunchKernelGGL((k_digit_hist<uint32_t, kL3Bits, kMid, kL2Seg>), dim3(n2), dim3(kThreads), 0,
+                     stream, t_key, bstart, H);
+  hipLaunchKernelGGL((k_digit_scan<kMid, kL2Seg>), dim3(p.nbuckets), dim3(kThreads), 0, stream, H,
+                     bstart, p.nsuper, sstart);
+  hipLaunchKernelGGL(k_starts_close, dim3(1), dim3(1), 0, stream, sstart, p.nsuper, nnz);
+  // (L2 always writes (row, value) pairs -- (row, 0) without values -- which L3 reads)
+  hipLaunchKernelGGL((k_digit_scatter<uint32_t, kL3Bits, kMid, kL2Seg, true>), dim3(n2),
+                     dim3(dev::kWave), 0, stream, t_key, t_row, t_rv, bstart, H, t_key2,
+                     with_values ? reinterpret_cast<uint32_t*>(t_rv2) : t_row2, nullptr,
+                     with_values);
+  // L3: per super-bucket (one segment), digit = the low 8 bits -> the CSC
+  const unsigned n3 = static_cast<unsigned>(p.nsuper);
+  hipLaunchKernelGGL((k_digit_hist<uint8_t, 0, kL3Bits, 1>), dim3(n3), dim3(kThreads), 0, stream,
+                     t_key2, sstart, H);
+  hipLaunchKernelGGL((k_digit_scan<kL3Bits, 1>), dim3(n3), dim3(kThreads), 0, stream, H, sstart,
+                     num_features, col_ptr);
+  const bool paired = val_out != nullptr && val_out == reinterpret_cast<float*>(row_out) + 1;
+  if (paired) {
+    CHECK_EQ(reinterpret_cast<uintptr_t>(row_out) & 7u, 0u) << "transpose: pair output not 8-byte aligned";
+    hipLaunchKernelGGL((k_digit_scatter<uint8_t, 0, kL3Bits, 1, true>), dim3(n3), dim3(dev::kWave),
+                       0, stream, t_key2, t_row2, t_rv2, sstart, H, nullptr, row_out, val_out, true);
+  } else {
+    hipLaunchKernelGGL((k_digit_scatter<uint8_t, 0, kL3Bits, 1, false>), dim3(n3),
+                       dim3(dev::kWave), 0, stream, t_key2, t_row2, t_rv2, sstart, H, nullptr,
+                       row_out, val_out, true);
+  }
+  hipLaunchKernelGGL(k_transpose_close, dim3(1), dim3(1), 0, stream, bstart, p.nbuckets,
+                     num_features, col_ptr);
+}
 }  // namespace
 
 size_t CSRTransposeScratchBytes(uint64_t nnz, uint64_t num_features) {
@@ -710,7 +1017,7 @@ size_t CSRTransposeScratchBytes(uint64_t nnz, uint64_t num_features) {
   return Plan(nnz, num_features).total + AlignUp((kMaxBuckets + 1) * sizeof(uint64_t));
 }
 
-uint64_t CSRTransposeMaxFeatures() { return static_cast<uint64_t>(kMaxBuckets) << kMaxLowBits; }
+uint64_t CSRTransposeMaxFeatures() { return static_cast<uint64_t>(kMaxBuckets) << kMaxBits3; }
 
 template <typename IndexType>
 void LaunchCSRTranspose(const uint64_t* offset, size_t nrows, uint64_t base, uint64_t nnz,
@@ -722,6 +1029,23 @@ void LaunchCSRTranspose(const uint64_t* offset, size_t nrows, uint64_t base, uin
   CHECK_LT(nnz, uint64_t(1) << 32) << "transpose: at most 2^32 - 1 entries";
   CHECK_LT(nrows, size_t(1) << 32) << "transpose: at most 2^32 - 1 rows";
   const TransposePlan p = Plan(nnz, num_features);
+  if (p.three) {
+    switch (p.low_bits) {
+      case 16:
+        RunSort3<IndexType, 16>(p, offset, nrows, base, nnz, index, value, num_features, col_ptr,
+                                row_out, val_out, scratch, error, stream);
+        break;
+      case 17:
+        RunSort3<IndexType, 17>(p, offset, nrows, base, nnz, index, value, num_features, col_ptr,
+                                row_out, val_out, scratch, error, stream);
+        break;
+      default:
+        RunSort3<IndexType, 18>(p, offset, nrows, base, nnz, index, value, num_features, col_ptr,
+                                row_out, val_out, scratch, error, stream);
+        break;
+    }
+    return;
+  }
   switch (p.low_bits) {
     case 10:
       RunSort<IndexType, 10>(p, offset, nrows, base, nnz, index, value, num_features, col_ptr,

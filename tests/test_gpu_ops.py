@@ -238,12 +238,17 @@ def _ref_transpose(t, nfeat):
 
 
 @pytest.mark.parametrize("nfeat,rows,index64", [(5000, 3000, False), (1 << 22, 20000, False),
-                                                  (70000, 5000, True), (1, 50, False)])
+                                                  (70000, 5000, True), (1, 50, False),
+                                                  ((1 << 22) + 1, 20000, False),
+                                                  (1 << 24, 20000, False), (1 << 26, 20000, False),
+                                                  (1 << 26, 5000, True)])
 def test_transpose_kernel_is_a_stable_csc(tmp_path, nfeat, rows, index64):
     """the HIP counting-sort transpose equals numpy's stable argsort CSC
     exactly (row ids ascending within every column, values moved with them),
-    across bucket counts (1 .. 1024 buckets of 4096 columns), 64-bit indices,
-    and a single column"""
+    across bucket counts (1 .. 1024 buckets of 1024 - 4096 columns), the
+    three-level sort of wider feature spaces (2^22 + 1 .. 2^26 columns:
+    buckets of 2^16 .. 2^18 columns, 256-column super-buckets), 64-bit
+    indices, and a single column"""
     p = str(tmp_path / "t.libsvm")
     data.write_synthetic(p, 0, rows, seed=5, num_features=nfeat, min_nnz=1, max_nnz=40)
     t = data.csr_to_torch(data.GPUParser(p, index64=index64).parse_all(data.DeviceCSR(index64)))
@@ -310,8 +315,39 @@ def test_transpose_rejects_out_of_range_ids(csr_t):
     t, csr = csr_t
     with pytest.raises(ValueError, match="num_features"):
         ops.transpose(t, int(csr.max_index))  # the largest id is out of range
+    from dmlc_core_amd import _dmlc
+    assert _dmlc.csr_transpose_max_features() == 1 << 28
     with pytest.raises(ValueError):
-        ops.transpose(t, (1 << 22) + 1)
+        ops.transpose(t, _dmlc.csr_transpose_max_features() + 1)
+
+
+def test_wide_model_auto_grad_uses_the_three_level_transpose(tmp_path):
+    """SparseLogReg(2^24) under grad='auto' builds the (three-level) transpose
+    on the first backward of a whole CSR; the gradient equals the atomic
+    form.  A CSR without values transposes to the same rows."""
+    import torch
+    from dmlc_core_amd.models import SparseLogReg
+    nfeat = 1 << 24
+    p = str(tmp_path / "w.libsvm")
+    data.write_synthetic(p, 0, 8000, seed=9, num_features=nfeat, min_nnz=1, max_nnz=30)
+    t = data.csr_to_torch(data.GPUParser(p).parse_all())
+    m = SparseLogReg(nfeat).cuda()
+    with torch.no_grad():
+        m.weight.normal_(0, 0.1)
+    m.loss(t).backward()
+    assert "transpose" in t
+    a = SparseLogReg(nfeat, grad="atomic").cuda()
+    with torch.no_grad():
+        a.weight.copy_(m.weight)
+        a.bias.copy_(m.bias)
+    a.loss({k: v for k, v in t.items() if k in ("offset", "index", "value", "label")}).backward()
+    torch.testing.assert_close(m.weight.grad, a.weight.grad, rtol=1e-4, atol=1e-6)
+    novals = {"offset": t["offset"], "index": t["index"]}
+    tt = ops.transpose(novals, nfeat)
+    assert tt["value"] is None
+    ptr, r, _ = _ref_transpose(t, nfeat)
+    np.testing.assert_array_equal(tt["offset"].cpu().numpy(), ptr)
+    np.testing.assert_array_equal(tt["index"].cpu().numpy(), r)
 
 
 def test_auto_grad_builds_the_transpose_on_a_whole_csr(csr_t):
@@ -334,7 +370,7 @@ def test_auto_grad_builds_the_transpose_on_a_whole_csr(csr_t):
 
 def test_auto_grad_above_the_transpose_limit_stays_atomic(csr_t):
     """grad='auto' on a model wider than the counting-sort transpose takes
-    (2^22 + 1 columns): backward keeps the atomic scatter instead of raising,
+    (2^28 + 1 columns): backward keeps the atomic scatter instead of raising,
     twice (the second-backward rule must not build it either), and the
     gradient equals grad='atomic'"""
     import torch
