@@ -6,10 +6,16 @@
 
 #include <dmlc/common.h>
 #include <dmlc/logging.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <regex>
+
+#include "./local_filesys.h"
 
 namespace dmlc {
 namespace io {
@@ -35,7 +41,73 @@ void InputSplitBase::Init(FileSystem* fs, const char* uri, size_t align_bytes,
   align_bytes_ = align_bytes;
 }
 
-InputSplitBase::~InputSplitBase() { delete fs_; }
+InputSplitBase::~InputSplitBase() {
+  Unmap();
+  delete fs_;
+}
+
+void InputSplitBase::Unmap() {
+  for (const auto& m : maps_) ::munmap(m.first, m.second);
+  maps_.clear();
+  map_base_ = nullptr;
+  map_len_ = 0;
+  map_file_ = static_cast<size_t>(-1);
+}
+
+int InputSplitBase::LoadMapped(Chunk* chunk, size_t buffer_words) {
+  if (mmap_mode_ < 0) {
+    // local files only (not stdin), unless DMLC_SPLIT_MMAP=0
+    const char* e = std::getenv("DMLC_SPLIT_MMAP");
+    bool ok = (e == nullptr || std::atoi(e) != 0) && MappableChunks() &&
+              dynamic_cast<LocalFileSystem*>(filesys_) != nullptr;
+    for (const FileInfo& f : files_) ok = ok && f.path.name != "stdin" && f.path.name != "-";
+    mmap_mode_ = ok ? 1 : 0;
+  }
+  if (mmap_mode_ == 0) return -1;
+  if (offset_curr_ >= offset_end_) return 0;
+  const size_t fp = static_cast<size_t>(
+      std::upper_bound(file_offset_.begin(), file_offset_.end(), offset_curr_) -
+      file_offset_.begin() - 1);
+  if (fp != map_file_) {
+    const int fd = ::open(files_[fp].path.name.c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) {
+      mmap_mode_ = 0;
+      return -1;
+    }
+    const size_t len = files_[fp].size;
+    void* m = ::mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE, fd, 0);
+    ::close(fd);
+    if (m == MAP_FAILED) {
+      mmap_mode_ = 0;
+      return -1;
+    }
+    ::madvise(m, len, MADV_SEQUENTIAL);
+    maps_.emplace_back(static_cast<char*>(m), len);
+    map_base_ = static_cast<char*>(m);
+    map_len_ = len;
+    map_file_ = fp;
+  }
+  const size_t o = offset_curr_ - file_offset_[fp];
+  const size_t limit = std::min(offset_end_, file_offset_[fp + 1]) - file_offset_[fp];
+  char* const b = map_base_ + o;
+  size_t want = buffer_words * sizeof(uint32_t);
+  for (;;) {
+    if (limit - o <= want) {  // the rest of this file's part of the partition
+      chunk->begin = b;
+      chunk->end = map_base_ + limit;
+      break;
+    }
+    const char* e = FindLastRecordBegin(b, b + want);
+    if (e != b) {
+      chunk->begin = b;
+      chunk->end = const_cast<char*>(e);
+      break;
+    }
+    want *= 2;  // one record longer than the view: widen it
+  }
+  offset_curr_ += static_cast<size_t>(chunk->end - chunk->begin);
+  return 1;
+}
 
 void InputSplitBase::ResetPartition(unsigned rank, unsigned nsplit) {
   CHECK(nsplit != 0 && rank < nsplit) << "invalid partition " << rank << "/" << nsplit;
@@ -48,6 +120,7 @@ void InputSplitBase::ResetPartition(unsigned rank, unsigned nsplit) {
   delete fs_;
   fs_ = nullptr;
   overflow_.clear();
+  Unmap();
   if (offset_begin_ == offset_end_) return;
   auto file_of = [this](size_t off) {
     return static_cast<size_t>(std::upper_bound(file_offset_.begin(), file_offset_.end(), off) -
@@ -74,6 +147,7 @@ void InputSplitBase::ResetPartition(unsigned rank, unsigned nsplit) {
 }
 
 void InputSplitBase::BeforeFirst() {
+  Unmap();  // (a copy-on-write mapping may hold compacted records)
   overflow_.clear();
   tmp_chunk_.begin = tmp_chunk_.end = nullptr;
   last_byte_ = -1;
@@ -225,6 +299,8 @@ bool InputSplitBase::ReadChunk(void* buf, size_t* size) {
 }
 
 bool InputSplitBase::Chunk::Load(InputSplitBase* split, size_t buffer_size) {
+  const int mapped = split->LoadMapped(this, buffer_size);
+  if (mapped >= 0) return mapped == 1;
   if (data.size() < buffer_size + 1) data.resize(buffer_size + 1);
   while (true) {
     size_t size = (data.size() - 1) * sizeof(uint32_t);

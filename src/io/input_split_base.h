@@ -31,6 +31,7 @@
 
 #include <cstdint>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "./filesys.h"
@@ -96,6 +97,10 @@ class InputSplitBase : public InputSplit {
   }
   /*! \brief text splits get '\n' inserted between files */
   virtual bool IsTextParser() const { return false; }
+  /*! \brief chunks may be views of a file mapping (LoadMapped): only when
+   *  record extraction writes nothing past a record (RecordIO; the line
+   *  splitter's NextRecord terminates a line in the byte after it) */
+  virtual bool MappableChunks() const { return false; }
   /*!
    * \brief start of the last (possibly incomplete) record in [begin, end);
    *  returns begin when no record head is found after begin
@@ -104,6 +109,17 @@ class InputSplitBase : public InputSplit {
 
   /*! \brief raw partition bytes (crosses files); 0 at end of partition */
   size_t Read(void* ptr, size_t size);
+  /*!
+   * \brief local files: point `chunk` at the next whole records inside a
+   *  private mapping of the current file -- no copy out of the page cache
+   *  (the reference freads every chunk into a buffer).  Chunks never span
+   *  files (so no newline needs inserting between files); a record longer
+   *  than the buffer widens the view.  The mapping is copy-on-write, so the
+   *  in-place compaction of multi-part RecordIO records works, and it is
+   *  dropped (a fresh one maps the file again) on BeforeFirst / ResetPartition.
+   * \return 1 loaded, 0 end of partition, -1 not a mappable file (use Read)
+   */
+  int LoadMapped(Chunk* chunk, size_t buffer_words);
   /*!
    * \brief fill buf with whole records (< *size bytes); carries the tail
    * \return false at end; *size == 0 with true means "buffer too small"
@@ -145,6 +161,17 @@ class InputSplitBase : public InputSplit {
   int last_byte_{-1};
   /*! \brief a '\n' must be emitted before reading the current file */
   bool pending_newline_{false};
+  /*! \brief LoadMapped state: whether this split's files may be mapped
+   *  (-1 undecided), the current file's mapping */
+  int mmap_mode_{-1};
+  char* map_base_{nullptr};
+  size_t map_len_{0};
+  size_t map_file_{static_cast<size_t>(-1)};
+  /*! \brief every mapping of this pass: a prefetching consumer
+   *  (ThreadedInputSplit) may still hold chunks of earlier files, so they
+   *  are dropped only at BeforeFirst / ResetPartition */
+  std::vector<std::pair<char*, size_t>> maps_;
+  void Unmap();
 
  private:
   std::vector<URI> ConvertToURIs(const std::string& uri);

@@ -31,6 +31,8 @@ class RecordIOSplitterBase : public InputSplitBase {
  public:
   bool ExtractNextRecord(Blob* out_rec, Chunk* chunk) override;
   const char* FindLastRecordBegin(const char* begin, const char* end) override;
+  /*! \brief local files: chunks are views of the file mapping (no copy) */
+  bool MappableChunks() const override { return true; }
 
  protected:
   size_t SeekRecordBegin(Stream* fi) override;

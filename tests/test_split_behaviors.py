@@ -9,6 +9,8 @@ are pinned against std::mt19937 oracles in tests/cpp/unittest_split_behaviors.cc
 * ``uri#cache``: the cache file is written during the first pass and replayed.
 """
 import os
+
+import numpy as np
 import subprocess
 import sys
 
@@ -122,3 +124,47 @@ def test_shuffle_parts_order_matches_input_split_shuffle(tmp_path):
             for sub in order:
                 want += [r.rstrip(b"\0\r\n") for r in io.iter_records(uri, part * k + sub, nparts * k)]
             assert got == want, (part, epoch, order)
+
+
+def test_recordio_mapped_chunks_multi_file_multi_part_two_epochs(tmp_path, monkeypatch):
+    """RecordIO splits over local files read chunks as views of a file
+    mapping (no copy out of the page cache).  Records that contain the magic
+    word (multi-part, compacted in place on extraction), several files, and a
+    second epoch (the copy-on-write mapping is dropped at BeforeFirst) give
+    the records written -- the same as the buffered path (DMLC_SPLIT_MMAP=0)."""
+    import struct
+    from dmlc_core_amd import io
+    magic = struct.pack("<I", 0xCED7230A)
+    rng = np.random.default_rng(3)
+    recs = []
+    for f in range(3):
+        w = io.RecordIOWriter(str(tmp_path / f"r{f}.rec"))
+        for i in range(700):
+            n = int(rng.integers(0, 3000))
+            body = bytearray(rng.integers(0, 256, size=n, dtype=np.uint8).tobytes())
+            if i % 7 == 0 and n >= 8:
+                body[(n // 2) & ~3:((n // 2) & ~3) + 4] = magic  # a multi-part record
+            w.write(bytes(body))
+            recs.append(bytes(body))
+        w.close()
+    uri = str(tmp_path / r"r\d\.rec")
+    got = []
+    for part in range(3):
+        s = io.InputSplit(uri, part, 3, "recordio")
+        for epoch in range(2):
+            out = []
+            while True:
+                r = s.next_record()
+                if r is None:
+                    break
+                out.append(bytes(r))
+            if epoch == 0:
+                got += out
+                first = out
+            else:
+                assert out == first
+            s.before_first()
+    assert got == recs
+    monkeypatch.setenv("DMLC_SPLIT_MMAP", "0")
+    buffered = [bytes(r) for p in range(3) for r in io.iter_records(uri, p, 3, "recordio")]
+    assert buffered == recs
