@@ -10,9 +10,10 @@ are pinned against std::mt19937 oracles in tests/cpp/unittest_split_behaviors.cc
 """
 import os
 
-import numpy as np
 import subprocess
 import sys
+
+import numpy as np
 
 from dmlc_core_amd import io
 
