@@ -568,8 +568,10 @@ __global__ __launch_bounds__(dev::kWave) void k_lowkey_scatter(
 //   L2 per (bucket, segment): digit = key >> 8 (2^(S-8) values) -> the
 //      entries in (bucket, mid) "super-bucket" order, the low 8 bits kept as
 //      a u8 key; the super-bucket starts come from L2's scan;
-//   L3 per super-bucket (one segment: ~400 entries each at 2^26 x 400 M):
-//      digit = the low 8 bits -> the final CSC position, the column pointer.
+//   L3 per super-bucket (~1500 entries each at 2^26 x 400 M), one wave:
+//      digit = the low 8 bits -> the final CSC position, the column pointer
+//      (k_local_sort256: counts, scan and placement without a global
+//      histogram).
 // Every pass scatters into at most 1024 (L2) / 256 (L3) open runs per wave
 // (T4c's 1024 - 4096 in the two-level sort).
 
@@ -597,9 +599,26 @@ __global__ __launch_bounds__(kThreads) void k_digit_hist(const KeyIn* __restrict
   __syncthreads();
   uint64_t e0, e1;
   seg_range<kSeg>(bstart, b, s, &e0, &e1);
-  for (uint64_t e = e0 + threadIdx.x; e < e1; e += kThreads) {
-    atomicAdd(&hist[(static_cast<uint32_t>(key[e]) >> kShift) & (kLow - 1u)], 1u);
+  auto add = [&](uint32_t k) { atomicAdd(&hist[(k >> kShift) & (kLow - 1u)], 1u); };
+  if constexpr (sizeof(KeyIn) == 4) {
+    // four keys per 16-byte load over the aligned middle of the segment
+    const uint64_t a0 = (e0 + 3) & ~3ull, a1 = e1 & ~3ull;
+    if (a0 < a1) {
+      for (uint64_t e = e0 + threadIdx.x; e < a0; e += kThreads) add(key[e]);
+      for (uint64_t e = a1 + threadIdx.x; e < e1; e += kThreads) add(key[e]);
+      const uint4* k4 = reinterpret_cast<const uint4*>(key + a0);
+      const uint64_t n4 = (a1 - a0) / 4;
+      for (uint64_t i = threadIdx.x; i < n4; i += kThreads) {
+        const uint4 q = k4[i];
+        add(q.x);
+        add(q.y);
+        add(q.z);
+        add(q.w);
+      }
+      e0 = e1;  // done
+    }
   }
+  for (uint64_t e = e0 + threadIdx.x; e < e1; e += kThreads) add(static_cast<uint32_t>(key[e]));
   __syncthreads();
   uint32_t* out = H + static_cast<size_t>(blockIdx.x) * kLow;
   for (uint32_t c = threadIdx.x; c < kLow; c += kThreads) out[c] = hist[c];
@@ -755,6 +774,91 @@ __global__ __launch_bounds__(dev::kWave) void k_digit_scatter(
   }
 }
 
+/*!
+ * \brief L3 in one pass over a super-bucket: one wave per super-bucket (4
+ *  per workgroup) counts its low bytes in LDS, scans the 256 counts (the
+ *  column pointer of its 256 columns), then places its entries in order with
+ *  ballot ranks -- no histogram round trip through global memory, no
+ *  per-super-bucket workgroup of its own for the count and the scan.
+ */
+__global__ __launch_bounds__(kThreads) void k_local_sort256(
+    const uint8_t* __restrict__ key, const uint2* __restrict__ rv,
+    const uint64_t* __restrict__ sstart, uint64_t nsuper, uint64_t num_features,
+    uint64_t* __restrict__ col_ptr, uint32_t* __restrict__ row_out, float* __restrict__ val_out,
+    bool paired) {
+  __shared__ uint32_t s_cnt[kWaves][256];
+  const int w = threadIdx.x / dev::kWave;
+  const int lane = dev::lane_id();
+  const uint64_t sb = static_cast<uint64_t>(blockIdx.x) * kWaves + w;
+  if (sb >= nsuper) return;  // whole waves leave; nothing below synchronises waves
+  uint32_t* cnt = s_cnt[w];
+  const uint64_t b0 = sstart[sb], b1 = sstart[sb + 1];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) cnt[lane * 4 + i] = 0u;
+  dev::wave_sync();
+  // pass 1: counts (4 keys per 4-byte load over the aligned middle)
+  const uint64_t a0 = (b0 + 3) & ~3ull, a1 = b1 & ~3ull;
+  if (a0 < a1) {
+    for (uint64_t e = b0 + lane; e < a0; e += dev::kWave) atomicAdd(&cnt[key[e]], 1u);
+    for (uint64_t e = a1 + lane; e < b1; e += dev::kWave) atomicAdd(&cnt[key[e]], 1u);
+    const uint32_t* k4 = reinterpret_cast<const uint32_t*>(key + a0);
+    const uint64_t n4 = (a1 - a0) / 4;
+    for (uint64_t i = lane; i < n4; i += dev::kWave) {
+      const uint32_t q = k4[i];
+      atomicAdd(&cnt[q & 0xFFu], 1u);
+      atomicAdd(&cnt[(q >> 8) & 0xFFu], 1u);
+      atomicAdd(&cnt[(q >> 16) & 0xFFu], 1u);
+      atomicAdd(&cnt[q >> 24], 1u);
+    }
+  } else {
+    for (uint64_t e = b0 + lane; e < b1; e += dev::kWave) atomicAdd(&cnt[key[e]], 1u);
+  }
+  dev::wave_sync();
+  // scan: lane l owns columns 4 l .. 4 l + 3
+  uint32_t c4[4];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    c4[i] = cnt[lane * 4 + i];
+    sum += c4[i];
+  }
+  uint32_t tot;
+  uint32_t x = dev::wave_excl_scan(sum, &tot);
+  dev::wave_sync();  // every lane has read its counts
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint64_t c = (sb << 8) + static_cast<uint64_t>(lane * 4 + i);
+    if (c < num_features) col_ptr[c] = b0 + x;
+    cnt[lane * 4 + i] = x;
+    x += c4[i];
+  }
+  dev::wave_sync();
+  // pass 2: entries in order, 64 at a time, ranks among equal keys by ballots
+  const uint64_t below = lanes_below();
+  for (uint64_t g = b0; g < b1; g += dev::kWave) {
+    const uint64_t e = g + lane;
+    const bool valid = e < b1;
+    const uint32_t k = valid ? key[e] : 0u;
+    const uint2 p = valid ? rv[e] : make_uint2(0u, 0u);
+    const uint64_t m = match_lanes(k, 8, valid);
+    const uint32_t rank = static_cast<uint32_t>(__popcll(m & below));
+    const uint32_t n = static_cast<uint32_t>(__popcll(m));
+    const uint32_t before = valid ? cnt[k] : 0u;
+    dev::wave_sync();
+    if (valid) {
+      const uint64_t pos = b0 + before + rank;
+      if (paired) {
+        reinterpret_cast<uint2*>(row_out)[pos] = p;
+      } else {
+        row_out[pos] = p.x;
+        if (val_out != nullptr) val_out[pos] = __uint_as_float(p.y);
+      }
+      if (rank + 1 == n) cnt[k] = before + n;
+    }
+    dev::wave_sync();
+  }
+}
+
 __global__ void k_starts_close(uint64_t* __restrict__ starts, uint64_t n, uint64_t nnz) {
   starts[n] = nnz;
 }
@@ -841,9 +945,7 @@ TransposePlan Plan(uint64_t nnz, uint64_t num_features) {
   if (p.three) {
     const uint64_t mid = uint64_t(1) << (p.low_bits - kL3Bits);
     p.nsuper = static_cast<uint64_t>(p.nbuckets) * mid;
-    const size_t h2 = static_cast<size_t>(p.nbuckets) * kL2Seg * mid;
-    const size_t h3 = static_cast<size_t>(p.nsuper) << kL3Bits;
-    p.h_words = h2 > h3 ? h2 : h3;
+    p.h_words = static_cast<size_t>(p.nbuckets) * kL2Seg * mid;  // (L3 keeps its counts in LDS)
   }
   p.nchunks = (nnz + kChunk - 1) / kChunk;
   size_t off = 0;
@@ -991,22 +1093,16 @@ void RunSort3(const TransposePlan& p, const uint64_t* offset, size_t nrows, uint
                      dim3(dev::kWave), 0, stream, t_key, t_row, t_rv, bstart, H, t_key2,
                      with_values ? reinterpret_cast<uint32_t*>(t_rv2) : t_row2, nullptr,
                      with_values);
-  // L3: per super-bucket (one segment), digit = the low 8 bits -> the CSC
-  const unsigned n3 = static_cast<unsigned>(p.nsuper);
-  hipLaunchKernelGGL((k_digit_hist<uint8_t, 0, kL3Bits, 1>), dim3(n3), dim3(kThreads), 0, stream,
-                     t_key2, sstart, H);
-  hipLaunchKernelGGL((k_digit_scan<kL3Bits, 1>), dim3(n3), dim3(kThreads), 0, stream, H, sstart,
-                     num_features, col_ptr);
+  // L3: one wave per super-bucket sorts it by the low 8 bits into the CSC
+  // (counts, column pointer and placement in one kernel)
   const bool paired = val_out != nullptr && val_out == reinterpret_cast<float*>(row_out) + 1;
   if (paired) {
     CHECK_EQ(reinterpret_cast<uintptr_t>(row_out) & 7u, 0u) << "transpose: pair output not 8-byte aligned";
-    hipLaunchKernelGGL((k_digit_scatter<uint8_t, 0, kL3Bits, 1, true>), dim3(n3), dim3(dev::kWave),
-                       0, stream, t_key2, t_row2, t_rv2, sstart, H, nullptr, row_out, val_out, true);
-  } else {
-    hipLaunchKernelGGL((k_digit_scatter<uint8_t, 0, kL3Bits, 1, false>), dim3(n3),
-                       dim3(dev::kWave), 0, stream, t_key2, t_row2, t_rv2, sstart, H, nullptr,
-                       row_out, val_out, true);
   }
+  (void)t_row2;
+  hipLaunchKernelGGL(k_local_sort256, dim3(static_cast<unsigned>((p.nsuper + kWaves - 1) / kWaves)),
+                     dim3(kThreads), 0, stream, t_key2, t_rv2, sstart, p.nsuper, num_features,
+                     col_ptr, row_out, val_out, paired);
   hipLaunchKernelGGL(k_transpose_close, dim3(1), dim3(1), 0, stream, bstart, p.nbuckets,
                      num_features, col_ptr);
 }
