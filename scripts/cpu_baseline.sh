@@ -9,7 +9,8 @@
 # RecordIO 512 B) plus the headline's 10 M-row LibSVM shard, at 1 / 8 / 16
 # OpenMP threads (16 = this box's CPU share).  JSON lines -> $OUT/cpu.jsonl.
 set -euo pipefail
-OUT=${OUT:-gpurun_out/r05_cpu}
+OUT=${OUT:-gpurun_out/r06_cpu}
+REPS=${REPS:-2}
 DATA=${DATA:-/tmp/dmlc_cpu_baseline}
 THREADS=${THREADS:-"1 8 16"}
 mkdir -p "$OUT" "$DATA"
@@ -37,6 +38,9 @@ run() {  # tag threads cmd...
   line=$(OMP_NUM_THREADS=$t timeout -k 10 300 "$@" | tail -1)
   echo "{\"impl\": \"$tag\", \"omp_threads\": $t, \"result\": $line}" | tee -a "$J"
 }
+# ref and repo alternate, REPS rounds (best of all of them is reported by
+# scripts/cpu_table.py): a page-cache or clock swing hits both alike
+for rep in $(seq "$REPS"); do
 for t in $THREADS; do
   for impl in ref repo; do
     if [ $impl = ref ]; then P=$R/ref_bench_cpu; S=$R/ref_bench_split_cpu; else P=$B/dmlc_bench_cpu; S=$B/dmlc_bench_split_cpu; fi
@@ -48,4 +52,6 @@ for t in $THREADS; do
     run $impl "$t" $P "$DATA/ls10m-0.libsvm" libsvm 0 1 2
   done
 done
+done
+python3 scripts/cpu_table.py "$J" > "$OUT/table.md" && cat "$OUT/table.md"
 echo "cpu baseline done: $J"
