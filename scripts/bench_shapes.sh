@@ -14,7 +14,7 @@ for shape in uniform skewed mixed; do
   # shape parses about the same bytes (fixed per-epoch costs weigh the same)
   n=$rows
   [ "$shape" != uniform ] && n=$((rows * 4))
-  for mode in stream hbm; do
+  for mode in ${MODES:-stream hbm}; do
     timeout -k 10 400 python bench.py --format $fmt --shape $shape --mode $mode --rows $n \
       --steps 5 --warmup 2 > "$out/${fmt}_${shape}_${mode}.json" 2> "$out/${fmt}_${shape}_${mode}.err" \
       || { tail -20 "$out/${fmt}_${shape}_${mode}.err"; exit 1; }
