@@ -110,9 +110,10 @@ class InputSplitBase : public InputSplit {
   /*! \brief raw partition bytes (crosses files); 0 at end of partition */
   size_t Read(void* ptr, size_t size);
   /*!
-   * \brief local files: point `chunk` at the next whole records inside a
-   *  private mapping of the current file -- no copy out of the page cache
-   *  (the reference freads every chunk into a buffer).  Chunks never span
+   * \brief with DMLC_SPLIT_MMAP=1, local files: point `chunk` at the next
+   *  whole records inside a private mapping of the current file -- no copy
+   *  out of the page cache (the default, like the reference, reads every
+   *  chunk into a buffer: faster on the MI355X hosts).  Chunks never span
    *  files (so no newline needs inserting between files); a record longer
    *  than the buffer widens the view.  The mapping is copy-on-write, so the
    *  in-place compaction of multi-part RecordIO records works, and it is

@@ -128,11 +128,11 @@ def test_shuffle_parts_order_matches_input_split_shuffle(tmp_path):
 
 
 def test_recordio_mapped_chunks_multi_file_multi_part_two_epochs(tmp_path, monkeypatch):
-    """RecordIO splits over local files read chunks as views of a file
-    mapping (no copy out of the page cache).  Records that contain the magic
+    """With DMLC_SPLIT_MMAP=1, RecordIO splits over local files read chunks
+    as views of a file mapping (no copy out of the page cache).  Records that contain the magic
     word (multi-part, compacted in place on extraction), several files, and a
     second epoch (the copy-on-write mapping is dropped at BeforeFirst) give
-    the records written -- the same as the buffered path (DMLC_SPLIT_MMAP=0)."""
+    the records written -- the same as the buffered (default) path."""
     import struct
     from dmlc_core_amd import io
     magic = struct.pack("<I", 0xCED7230A)
@@ -149,6 +149,7 @@ def test_recordio_mapped_chunks_multi_file_multi_part_two_epochs(tmp_path, monke
             recs.append(bytes(body))
         w.close()
     uri = str(tmp_path / r"r\d\.rec")
+    monkeypatch.setenv("DMLC_SPLIT_MMAP", "1")
     got = []
     for part in range(3):
         s = io.InputSplit(uri, part, 3, "recordio")
