@@ -45,6 +45,7 @@ using namespace dev;  // NOLINT(build/namespaces)
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef int v2i __attribute__((ext_vector_type(2)));
 
 constexpr int kFwdThreads = 256;
 constexpr int kBwdThreads = 512;  // 8 waves x 128 features = 1024 features per workgroup
@@ -472,9 +473,11 @@ __global__ __launch_bounds__(256) void k_fm_prep(const float* __restrict__ w,
  * [128 w, 128 w + 128) for both halves of the step.  Per 32-row tile, with
  * the tile's X fragment (F1's and F2's lane layout are the same: lane (col, h)
  * holds 64 bytes of row col) loaded once:
- *   P1  G^T X of the tile two back (F2, its X fragment kept in LDS, G^T
- *       from s_gt / s_g), then this tile's x.[w | V] block products (F1,
- *       [w | V] in LDS) and x^2.q; the 32 x 18 partial sums go to s_part.
+ *   P1  G^T X of the tile two back (its X image kept in LDS and read back
+ *       transposed by ds_read_b64_tr_b8, rows along K, so F2's identity
+ *       MFMA and its f32 -> bf16 repacking are gone; G^T from s_gt / s_g),
+ *       then this tile's x.[w | V] block products (F1, [w | V] in LDS) and
+ *       x^2.q; the 32 x 18 partial sums go to s_part.
  *                                                          barrier
  *   P2  16 threads per row sum the W partials of its 18 columns, form y, the
  *       loss and g, and write G^T = [g, g sx xV] (bf16) and g.
@@ -507,14 +510,16 @@ __global__ __launch_bounds__(64 * W) void k_fm_fused(
   constexpr int kLdw = D + 8;
   constexpr int P = W + 1;  // odd stride of the partials: conflict-free column writes
   constexpr int kThreads = 64 * W;
-  __shared__ __attribute__((aligned(16))) __bf16 s_wt[kFmCols * kLdw];  // F1's [17][D + 8]
+  // F1's [17][D + 8] plus one zero row, the B row of lanes 17..31
+  __shared__ __attribute__((aligned(16))) __bf16 s_wt[(kFmCols + 1) * kLdw];
   __shared__ __attribute__((aligned(16))) float s_q[D];
   // double-buffered by tile parity: one barrier per tile (see the loop)
   __shared__ float s_part[2][32 * 18 * P];                             // [row][column][wave]
   __shared__ __attribute__((aligned(16))) __bf16 s_gt[2][32 * 40];     // G^T [column][row]
   __shared__ __attribute__((aligned(16))) float s_g[2][32];
-  // each wave's X fragment of a tile, kept two tiles for its backward
-  // (lane-interleaved: conflict-free 16-byte accesses)
+  // each wave's X fragment of a tile, kept two tiles for its backward:
+  // 16-byte chunk (wave, i, lane) at (wave * 4 + i) * 64 + (lane ^ 8 (i & 1))
+  // (the swizzle keeps the backward's transposed reads conflict-free)
   __shared__ uint4 s_x[2][W * 4 * 64];
   __shared__ float s_red[2 * W];
   const int tid = threadIdx.x;
@@ -526,22 +531,32 @@ __global__ __launch_bounds__(64 * W) void k_fm_fused(
     *reinterpret_cast<uint4*>(s_wt + c * kLdw + 8 * k8) =
         reinterpret_cast<const uint4*>(wt + static_cast<size_t>(c) * D)[k8];
   }
+  for (int i = tid; i < kLdw / 8; i += kThreads) {
+    reinterpret_cast<uint4*>(s_wt + kFmCols * kLdw)[i] = make_uint4(0, 0, 0, 0);
+  }
   for (int i = tid; i < D / 4; i += kThreads) {
     reinterpret_cast<float4*>(s_q)[i] = reinterpret_cast<const float4*>(q)[i];
   }
   for (int i = tid; i < 2 * 32 * 40; i += kThreads) (&s_gt[0][0])[i] = static_cast<__bf16>(0.0f);
+  // zero X and G images: the backward runs from the first tile on (tiles -2
+  // and -1 add 0 x 0), so no branch splits the accumulators' live ranges
+  for (int i = tid; i < 2 * W * 4 * 64; i += kThreads) (&s_x[0][0])[i] = make_uint4(0, 0, 0, 0);
   if (tid < 64) (&s_g[0][0])[tid] = 0.0f;
   const int kbase = 128 * wave + 64 * h;
-  // F2's identity B fragments
-  bf16x8 eye[2];
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const bool one = h == (col >> 4) && s == ((col >> 3) & 1) && j == (col & 7);
-      eye[s][j] = static_cast<__bf16>(one ? 1.0f : 0.0f);
-    }
-  }
+  // this lane's B row of [w | V] (lanes 17..31: the zero row)
+  const __bf16* const wrow = s_wt + (col < kFmCols ? col : kFmCols) * kLdw + kbase;
+  // F2's transposed X reads (ds_read_b64_tr_b8): in each 16-lane group gr,
+  // lane 2 qq + pp supplies row 8 (gr >> 1) + qq (+ 16 s) and bytes 8 pp ..
+  // 8 pp + 7 of the group's 16 features 16 (gr & 1) (+ 32 b); lane i of the
+  // group receives feature i of those 8 rows, row qq in byte qq
+  // (tools/tr8_probe.hip checks this map).  The chunk of (row, 16 features)
+  // follows s_x's swizzle; (bf, b, s) add compile-time offsets
+  const int gr = lane >> 4, qq = (lane & 15) >> 1, pp = lane & 1;
+  const uint32_t xt_base =
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>(&s_x[0][0])) +
+      16u * static_cast<uint32_t>((wave * 4 + (gr & 1)) * 64 +
+                                  ((8 * (gr >> 1) + qq) ^ (8 * (gr & 1)))) +
+      8u * static_cast<uint32_t>(pp);
   const float b0 = *bias;
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
   const int64_t r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
@@ -550,16 +565,14 @@ __global__ __launch_bounds__(64 * W) void k_fm_fused(
   // 32, so trailing blocks can be empty); such a block loads row rows - 1,
   // zeroes it and writes zero partials
   const int64_t rlast = r1 > r0 ? r1 - 1 : rows - 1;
+  // rows past the block's end load the clamp row (finite codes): their g is
+  // zero, so they add nothing to the backward, and P2 stores nothing for them
   auto load_x = [&](int64_t t, uint4 (&v)[4]) {
     const int64_t r = t + col;
-    const bool ok = r < r1;
     const int64_t rc = r < rlast ? r : rlast;
     const uint4* p = reinterpret_cast<const uint4*>(x + rc * D + kbase);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint4 u = p[i];
-      v[i] = ok ? u : make_uint4(0, 0, 0, 0);
-    }
+    for (int i = 0; i < 4; ++i) v[i] = p[i];
   };
   // labels / weights of a tile: lane l holds row (l & 31), loaded a tile ahead
   auto load_lw = [&](int64_t t, float* lab, float* wgt) {
@@ -571,52 +584,43 @@ __global__ __launch_bounds__(64 * W) void k_fm_fused(
     *wgt = w;
   };
   f32x16 acc[4] = {};
-  float tacc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  f32x2 tacc[4] = {};
   float lsum = 0.0f, gsum = 0.0f;
-  // F2 on the tile of parity bf: its X fragment from s_x, G^T from s_gt / s_g
+  // F2 on the tile of parity bf: B = X with rows along K straight from the
+  // LDS image by transposed reads (element j: row 16 s + 8 h + j of feature
+  // 128 wave + 32 b + col), A = G^T from s_gt in the same natural row order;
+  // t = (x^2)^T g accumulates from the same bytes
   auto backward = [&](int bf) {
-    uint4 xw[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) xw[i] = s_x[bf][(wave * 4 + i) * 64 + lane];
     bf16x8 ga[2];
-    const uint2* gt_row = reinterpret_cast<const uint2*>(s_gt[bf] + col * 40);
+    f32x2 g2[2][4];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const uint2 lo = gt_row[4 * s + h], hi = gt_row[4 * s + 2 + h];
-      ga[s] = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      ga[s] = *reinterpret_cast<const bf16x8*>(s_gt[bf] + col * 40 + 16 * s + 8 * h);
+      const float4 ga4 = *reinterpret_cast<const float4*>(s_g[bf] + 16 * s + 8 * h);
+      const float4 gb4 = *reinterpret_cast<const float4*>(s_g[bf] + 16 * s + 8 * h + 4);
+      g2[s][0] = f32x2{ga4.x, ga4.y};
+      g2[s][1] = f32x2{ga4.z, ga4.w};
+      g2[s][2] = f32x2{gb4.x, gb4.y};
+      g2[s][3] = f32x2{gb4.z, gb4.w};
     }
-    float gr[16];
-#pragma unroll
-    for (int r4 = 0; r4 < 4; ++r4) {
-      const float4 g4 = *reinterpret_cast<const float4*>(s_g[bf] + 8 * r4 + 4 * h);
-      gr[4 * r4 + 0] = g4.x;
-      gr[4 * r4 + 1] = g4.y;
-      gr[4 * r4 + 2] = g4.z;
-      gr[4 * r4 + 3] = g4.w;
-    }
+    typedef __attribute__((address_space(3))) v2i lds_v2i;
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
-      f32x16 tt = {};
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        tt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-            fp8x8_bf16(word(xw, 2 * (2 * b + s)), word(xw, 2 * (2 * b + s) + 1)), eye[s], tt, 0, 0,
-            0);
+        const uint32_t a = xt_base + static_cast<uint32_t>(bf) * (W * 4 * 64 * 16) +
+                           2048u * (b & 1) + 512u * (b >> 1) + 256u * s;
+        const v2i raw = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(static_cast<uintptr_t>(a)));
+        const uint32_t lo = static_cast<uint32_t>(raw.x), hi = static_cast<uint32_t>(raw.y);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[s], fp8x8_bf16(lo, hi), acc[b], 0, 0, 0);
+        float f[8];
+        fp8x8(lo, hi, f);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const f32x2 x2 = f32x2{f[2 * k], f[2 * k + 1]};
+          tacc[b] = __builtin_elementwise_fma(x2 * x2, g2[s][k], tacc[b]);
+        }
       }
-      float ta = 0.0f;
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) ta += tt[reg] * tt[reg] * gr[reg];
-      tacc[b] += ta;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8 tb;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) tb[j] = static_cast<__bf16>(tt[8 * s + j]);
-        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[s], tb, acc[b], 0, 0, 0);
-      }
-      // one feature block's transpose live at a time (else the scheduler
-      // interleaves all four and the kernel spills its accumulators)
-      __builtin_amdgcn_sched_barrier(0);
     }
   };
   float lab_n = 0.0f, wgt_n = 1.0f;
@@ -630,20 +634,16 @@ __global__ __launch_bounds__(64 * W) void k_fm_fused(
   // s_part[bf] is next written by forward(j + 2), after barrier j + 1, which
   // every thread reaches only after its P2(j): one barrier per tile, and a
   // wave done with P2 runs on into the next tile's products
-  uint4 xn[4];
-  load_x(r0, xn);
-  int j = 0;
-  for (int64_t t0 = r0; t0 < r1; t0 += 32, ++j) {
+  // one tile: X(t0) in xc, X(t0 + 32) loaded into xn.  The loop runs two
+  // tiles per trip with the register sets swapped (no copy of the prefetch);
+  // a block of an odd number of tiles ends on one of rows past r1 (g = 0)
+  auto step = [&](int64_t t0, int j, const uint4 (&xc)[4], uint4 (&xn)[4]) {
     const int bf = j & 1;
     const float lab_t = lab_n, wgt_t = wgt_n;
     load_lw(t0 + 32, &lab_n, &wgt_n);
-    if (j >= 2) backward(bf);
-    uint4 xc[4];
+    backward(bf);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      xc[i] = xn[i];
-      s_x[bf][(wave * 4 + i) * 64 + lane] = xc[i];
-    }
+    for (int i = 0; i < 4; ++i) s_x[bf][(wave * 4 + i) * 64 + (lane ^ (8 * (i & 1)))] = xc[i];
     load_x(t0 + 32, xn);
     __builtin_amdgcn_sched_barrier(0);
     f32x16 fa = {};
@@ -659,9 +659,7 @@ __global__ __launch_bounds__(64 * W) void k_fm_fused(
       const f32x2 qq[4] = {{q0.x, q0.y}, {q0.z, q0.w}, {q1.x, q1.y}, {q1.z, q1.w}};
 #pragma unroll
       for (int k = 0; k < 4; ++k) x2q2 = __builtin_elementwise_fma(sq[k] * sq[k], qq[k], x2q2);
-      const bf16x8 b = col < kFmCols
-                           ? *reinterpret_cast<const bf16x8*>(s_wt + col * kLdw + kbase + 8 * i)
-                           : bf16x8{};
+      const bf16x8 b = *reinterpret_cast<const bf16x8*>(wrow + 8 * i);
       fa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fp8x8_bf16(lo, hi), b, fa, 0, 0, 0);
     }
     float x2q = x2q2[0] + x2q2[1];
@@ -710,9 +708,13 @@ __global__ __launch_bounds__(64 * W) void k_fm_fused(
         l = d * d;
         g = 2.0f * d;
       } else {
+        // e in (0, 1]: log(1 + e) and 1 / (1 + e) by the hardware
+        // log / reciprocal (1 ulp; no libm range reduction needed)
         const float e = __expf(-fabsf(yv));
-        l = fmaxf(yv, 0.0f) - yv * lab + log1pf(e);
-        const float sig = yv >= 0.0f ? 1.0f / (1.0f + e) : e / (1.0f + e);
+        const float ope = 1.0f + e;
+        l = fmaxf(yv, 0.0f) - yv * lab + __logf(ope);
+        const float rc = __builtin_amdgcn_rcpf(ope);
+        const float sig = yv >= 0.0f ? rc : e * rc;
         g = sig - lab;
       }
       g = valid ? g * wg * inv_n : 0.0f;
@@ -727,23 +729,31 @@ __global__ __launch_bounds__(64 * W) void k_fm_fused(
         }
       }
     }
+  };
+  uint4 xa[4], xb[4];
+  load_x(r0, xa);
+  int j = 0;
+  for (int64_t t0 = r0; t0 < r1; t0 += 64, j += 2) {
+    step(t0, j, xa, xb);
+    step(t0 + 32, j + 1, xb, xa);
   }
   // the last two tiles' backward, after every thread's last P2
   __syncthreads();
-  if (j >= 2) backward(j & 1);
-  if (j >= 1) backward((j - 1) & 1);
+  backward(0);
+  backward(1);
   // ---- partials
   float* out = part + static_cast<size_t>(blockIdx.x) * (kFmCols + 1) * D;
   const int fbase = 128 * wave;
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
-    const int feat = fbase + 64 * (col >> 4) + 16 * b + 8 * ((col >> 3) & 1) + (col & 7);
+    const int feat = fbase + 32 * b + col;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
       const int c = (reg & 3) + 8 * (reg >> 2) + 4 * h;
       if (c < kFmCols) out[static_cast<size_t>(c) * D + feat] = acc[b][reg];
     }
-    const float tt = tacc[b] + __shfl_xor(tacc[b], 32, kWave);
+    const float t1 = tacc[b][0] + tacc[b][1];
+    const float tt = t1 + __shfl_xor(t1, 32, kWave);
     if (h == 0) out[static_cast<size_t>(kFmCols) * D + feat] = tt;
   }
 #pragma unroll
