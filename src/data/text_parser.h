@@ -102,7 +102,14 @@ class TextParserBase : public ParserImpl<IndexType, DType> {
 #pragma omp parallel for num_threads(nthread) schedule(static, 1)
     for (int t = 0; t < nthread; ++t) {
       try {
-        ParseBlock(cut[t], cut[t + 1], &(*data)[t]);
+        // parse into a container on this thread's stack (the vectors move in
+        // and out: O(1)): the threads' containers sit side by side in `data`,
+        // and every push_back updates a vector's end pointer -- adjacent
+        // containers share cache lines at their edges
+        typename Container::value_type local;
+        std::swap(local, (*data)[t]);
+        ParseBlock(cut[t], cut[t + 1], &local);
+        std::swap(local, (*data)[t]);
       } catch (...) {
         std::lock_guard<std::mutex> lock(err_mu);
         if (err == nullptr) err = std::current_exception();
