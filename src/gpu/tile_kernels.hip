@@ -676,19 +676,14 @@ struct PrevTok {
 };
 __device__ __forceinline__ PrevTok prev_token_status(uint32_t tm_a, uint32_t lm_a, uint32_t tm_b,
                                                      uint32_t lm_b, uint32_t carried, int lane) {
-  auto scan = [lane](uint32_t v) {  // inclusive max over lanes <= lane
-#pragma unroll
-    for (int d = 1; d < dev::kWave; d <<= 1) {
-      const uint32_t u = __shfl_up(v, d, dev::kWave);
-      if (lane >= d) v = u > v ? u : v;
-    }
-    return v;
+  // inclusive max over lanes <= lane: the DPP ladder (no LDS round trips)
+  auto scan = [](uint32_t v) {
+    return dev::wave_incl_scan_op(v, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
   };
   const uint32_t ia = scan(tm_a != 0 ? ((lane + 1u) << 2) | slice_last(tm_a, lm_a) : 0u);
   const uint32_t ib = scan(tm_b != 0 ? ((lane + 1u) << 2) | slice_last(tm_b, lm_b) : 0u);
-  uint32_t xa = __shfl_up(ia, 1, dev::kWave), xb = __shfl_up(ib, 1, dev::kWave);
-  if (lane == 0) xa = xb = 0;
-  const uint32_t ta = __shfl(ia, dev::kWave - 1, dev::kWave);
+  const uint32_t xa = dev::lane_shr1(ia), xb = dev::lane_shr1(ib);  // lane 0: 0
+  const uint32_t ta = dev::lane63(ia);
   PrevTok r;
   r.a = xa != 0 ? (xa & 3u) : carried;
   r.b = xb != 0 ? (xb & 3u) : (ta != 0 ? (ta & 3u) : carried);

@@ -475,68 +475,80 @@ __device__ __forceinline__ ExtNum parse_num_ext(const uint4* lds, uint32_t a, ui
 #pragma clang fp contract(off)
 #endif
   ExtNum o;
-  const uint4 g0 = ext16(lds, a), g1 = ext16(lds, a + 16);
-  const uint32_t c0 = g0.x & 0xFFu;
+  // every digit run is read from a 12-byte LDS window at its own start and
+  // decoded 8 digits at a time (digit_run8): no lane-varying selects over a
+  // register window (the round-5 form spent ~60 % of its VALU on those)
+  const uint3 g = ext12(lds, a);
+  const uint32_t c0 = g.x & 0xFFu;
   const bool neg = c0 == '-';
   const uint32_t s = (neg || c0 == '+') ? 1u : 0u;
-  // integer digits (<= 7 for an exact float; 8 or more: generic)
-  uint32_t v0, v1;
-  const uint32_t k0 = lead_digits(win_word(g0, g1, s), &v0);
-  const uint32_t k1 = lead_digits(win_word(g0, g1, s + 4), &v1);
-  uint32_t k;
-  const uint32_t iv = join_groups(k0, v0, k1, v1, &k);
-  uint32_t pos = s + k;
-  const bool dot = win_byte(g0, g1, pos) == '.';
-  // fraction digits, four 4-byte groups (<= 16 digits)
-  uint64_t fv = 0, pw = 1;
-  uint32_t nf = 0;
-  if (dot) {
-    const uint32_t fs = pos + 1;
-    bool more = true;
-#pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) {
-      uint32_t v;
-      const uint32_t kk = lead_digits(win_word(g0, g1, fs + 4 * j), &v);
-      if (more) {
-        const uint64_t m = pow10_u(kk);
-        fv = fv * m + v;
-        pw *= m;
-        nf += kk;
-        more = kk == 4;
-      }
-    }
-    pos = fs + nf;
-  }
-  // exponent: (e|E) [+-] digits (<= 4)
-  const uint32_t ce = win_byte(g0, g1, pos);
-  const bool has_e = ce == 'e' || ce == 'E';
-  bool eneg = false;
-  uint32_t ex = 0, ne = 0;
-  if (has_e) {
-    const uint32_t cs = win_byte(g0, g1, pos + 1);
-    eneg = cs == '-';
-    const uint32_t es = pos + 1 + ((cs == '-' || cs == '+') ? 1u : 0u);
-    uint32_t v;
-    ne = lead_digits(win_word(g0, g1, es < 28 ? es : 28u), &v);
-    ex = v;
-    pos = es + ne;
-  }
-  o.term = win_byte(g0, g1, pos < 31 ? pos : 31u);
-  o.end = a + pos;
-  o.ok = k <= 7 && (k | nf) != 0 && nf < 16 && ne < 4 && pos < 28 && a + pos < limit;
+  const uint32_t h0 = __builtin_amdgcn_alignbyte(g.y, g.x, s);
+  const uint32_t h1 = __builtin_amdgcn_alignbyte(g.z, g.y, s);
+  const uint32_t nb = __builtin_amdgcn_alignbyte(g.z, g.y, s + 1u) >> 24;
+  const Run8 ir = digit_run8(h0, h1, nb);  // integer digits (<= 7 for an exact float)
+  const uint32_t k = ir.k;
+  const bool dot = ir.term == '.';
+  // fraction digits: two runs of up to 8 (<= 16 digits)
+  const uint32_t fa = a + s + k + 1u;
+  const uint3 f1 = ext12(lds, fa);
+  const Run8 r1 = digit_run8(f1.x, f1.y, f1.z & 0xFFu);
+  const uint3 f2 = ext12(lds, fa + 8u);
+  const Run8 r2 = digit_run8(f2.x, f2.y, f2.z & 0xFFu);
+  const bool two = r1.k == 8u;
+  const uint32_t nf = dot ? (two ? 8u + r2.k : r1.k) : 0u;
+  const uint32_t after = dot ? fa + nf : a + s + k;  // LDS byte after the mantissa
+  const uint32_t cterm = dot ? (two ? r2.term : r1.term) : ir.term;
+  // exponent: (e|E) [+-] digits (<= 3)
+  const bool has_e = cterm == 'e' || cterm == 'E';
+  const uint3 e = ext12(lds, after + 1u);
+  const uint32_t cs = e.x & 0xFFu;
+  const bool eneg = cs == '-';
+  const uint32_t es = (cs == '-' || cs == '+') ? 1u : 0u;
+  const Run8 er = digit_run8(__builtin_amdgcn_alignbyte(e.y, e.x, es),
+                             __builtin_amdgcn_alignbyte(e.z, e.y, es), 0u);
+  const uint32_t ne = has_e ? er.k : 0u;
+  const uint32_t ex = er.val;
+  const uint32_t end = has_e ? after + 1u + es + ne : after;
+  const uint32_t pos = end - a;
+  o.term = has_e ? er.term : cterm;
+  o.end = end;
+  o.ok = k <= 7 && (k | nf) != 0 && nf < 16 && ne < 4 && pos < 28 && end < limit;
   // the reference arithmetic (strtonum.h StrToFloatT)
-  float value = static_cast<float>(iv);
-  if (dot) value += static_cast<float>(static_cast<double>(fv) / static_cast<double>(pw));
-  if (has_e) {
-    float scale = 1.0f;
-    uint32_t e = ex > 38 ? 38u : ex;
-    while (e >= 8) {
-      scale = static_cast<float>(static_cast<double>(scale) * 1e8);
-      e -= 8;
+  float value = static_cast<float>(ir.val);
+  if (dot) {
+    // F / 10^nf: the float form of parse_num for nf <= 7 (equal to the
+    // rounded double quotient there, see the file comment), the double
+    // quotient of the reference for longer fractions
+    float p, inv;
+    pow10f(nf < 8u ? nf : 7u, &p, &inv);
+    const float ff = static_cast<float>(r1.val);
+    const float q0 = ff * inv;
+    const float rem = __builtin_fmaf(-q0, p, ff);
+    float frac = __builtin_fmaf(rem, inv, q0);
+    if (nf >= 8u) {
+      const uint64_t fv = static_cast<uint64_t>(r1.val) * pow10_u(r2.k) + r2.val;
+      const double pw = 1e8 * static_cast<double>(pow10_u(r2.k));  // 10^nf, exact
+      frac = static_cast<float>(static_cast<double>(fv) / pw);
     }
-    while (e > 0) {
-      scale = static_cast<float>(static_cast<double>(scale) * 10.0);
-      e -= 1;
+    value += frac;
+  }
+  if (has_e) {
+    float scale;
+    if (ex <= 10u) {
+      // 10^ex is exact in float up to 10^10: the reference loop's products
+      // are all exact there
+      scale = ex <= 7u ? static_cast<float>(pow10_u(ex)) : (ex == 8u ? 1e8f : (ex == 9u ? 1e9f : 1e10f));
+    } else {
+      scale = 1.0f;
+      uint32_t m = ex > 38 ? 38u : ex;
+      while (m >= 8) {
+        scale = static_cast<float>(static_cast<double>(scale) * 1e8);
+        m -= 8;
+      }
+      while (m > 0) {
+        scale = static_cast<float>(static_cast<double>(scale) * 10.0);
+        m -= 1;
+      }
     }
     value = eneg ? (value / scale) : (value * scale);
   }
