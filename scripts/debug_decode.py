@@ -25,4 +25,5 @@ print("mismatches", len(bad))
 text = open(p, "rb").read()
 toks = [t for line in text.split(b"\n") for t in line.split(b" ")[1:] if t]
 for k in bad[:20]:
-    print(k, "cpu", idx[k], val[k], "gpu", g["index"][k], g["value"][k], "text", toks[k] if k < len(toks) else None)
+    print(k, "cpu", idx[k], val[k], "gpu", g["index"][k], g["value"][k],
+          "text", toks[k] if k < len(toks) else None)

@@ -899,7 +899,8 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     // overlap the current fill instead of queueing behind it.  The set it
     // writes was last used by the chunk before the current one, which is done.
     LaunchCountScan(nx.text, nx.size, tcounts_next_.get<uint64_t>(), tflags_next_.get<uint32_t>(),
-                    tmasks_next_.get<uint32_t>(), meta_next_.get<ChunkMeta>(), hmap_next_.get<ChunkMeta>(), count_stream_->get());
+                    tmasks_next_.get<uint32_t>(), meta_next_.get<ChunkMeta>(),
+                    hmap_next_.get<ChunkMeta>(), count_stream_->get());
     pre_done_->Record(count_stream_->get());
     pre_.valid = true;
     pre_.text = nx.text;
@@ -1182,7 +1183,8 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
         if (!(sizes.flags & kFlagIrregular)) {
           reserve(sizes.nrows, nbytes);
           LaunchTileHashed<IndexType>(text, nbytes, tcfg_.format, tcounts_.get<uint64_t>(),
-                                      tmasks_.get<uint32_t>(), out->rows, sizes.nlines, dim, scale, seed, fp8, out->x->get(),
+                                      tmasks_.get<uint32_t>(), out->rows, sizes.nlines, dim, scale,
+                                      seed, fp8, out->x->get(),
                                       out->label->get<float>(), slots_.get<MetaPartial>(), dmeta,
                                       hm, s);
           PrelaunchCount();

@@ -2058,20 +2058,20 @@ size_t LaunchTileHashed(const char* text, size_t nbytes, TextFormat format,
 }
 
 template size_t LaunchTileHashed<uint32_t>(const char*, size_t, TextFormat, const uint64_t*,
-                                           const uint32_t*, uint64_t, uint64_t, int, float, uint32_t, bool, void*,
-                                           float*, MetaPartial*, ChunkMeta*, ChunkMeta*,
+                                           const uint32_t*, uint64_t, uint64_t, int, float, uint32_t,
+                                           bool, void*, float*, MetaPartial*, ChunkMeta*, ChunkMeta*,
                                            hipStream_t, const HashOnePass*);
 template size_t LaunchTileHashed<uint64_t>(const char*, size_t, TextFormat, const uint64_t*,
-                                           const uint32_t*, uint64_t, uint64_t, int, float, uint32_t, bool, void*,
-                                           float*, MetaPartial*, ChunkMeta*, ChunkMeta*,
+                                           const uint32_t*, uint64_t, uint64_t, int, float, uint32_t,
+                                           bool, void*, float*, MetaPartial*, ChunkMeta*, ChunkMeta*,
                                            hipStream_t, const HashOnePass*);
 
 template size_t LaunchTileFill<uint32_t>(const char*, size_t, TextFormat, const uint64_t*,
-                                         const uint32_t*, const FillTarget<uint32_t>&, MetaPartial*, ChunkMeta*,
-                                         ChunkMeta*, hipStream_t, const FillOnePass*);
+                                         const uint32_t*, const FillTarget<uint32_t>&, MetaPartial*,
+                                         ChunkMeta*, ChunkMeta*, hipStream_t, const FillOnePass*);
 template size_t LaunchTileFill<uint64_t>(const char*, size_t, TextFormat, const uint64_t*,
-                                         const uint32_t*, const FillTarget<uint64_t>&, MetaPartial*, ChunkMeta*,
-                                         ChunkMeta*, hipStream_t, const FillOnePass*);
+                                         const uint32_t*, const FillTarget<uint64_t>&, MetaPartial*,
+                                         ChunkMeta*, ChunkMeta*, hipStream_t, const FillOnePass*);
 
 }  // namespace gpu
 }  // namespace dmlc

@@ -20,8 +20,10 @@ __global__ __launch_bounds__(256) void k_probe(uint64_t* out, int iters, uint32_
            a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
   uint32_t b = seed * 3 + threadIdx.x, c = seed ^ 0x5555u;
   uint64_t w0 = a0, w1 = a1, w2 = a2, w3 = a3;
-  if constexpr (OP == 29 || OP == 31) asm volatile("v_cmp_gt_u32 s[20:21], %0, %1" : : "v"(a0), "v"(b) : "s20", "s21");
-  if constexpr (OP == 27 || OP == 28 || OP == 30) asm volatile("v_cmp_gt_u32 vcc, %0, %1" : : "v"(a0), "v"(b) : "vcc");
+  if constexpr (OP == 29 || OP == 31)
+    asm volatile("v_cmp_gt_u32 s[20:21], %0, %1" : : "v"(a0), "v"(b) : "s20", "s21");
+  if constexpr (OP == 27 || OP == 28 || OP == 30)
+    asm volatile("v_cmp_gt_u32 vcc, %0, %1" : : "v"(a0), "v"(b) : "vcc");
   if constexpr (OP == 24) asm volatile("v_cmp_gt_u32 s[20:21], %0, %1" : : "v"(a0), "v"(b) : "s20", "s21");
   if constexpr (OP == 25) asm volatile("v_cmp_gt_u32 vcc, %0, %1" : : "v"(a0), "v"(b) : "vcc");
   __builtin_amdgcn_s_barrier();
@@ -30,7 +32,8 @@ __global__ __launch_bounds__(256) void k_probe(uint64_t* out, int iters, uint32_
 #define BODY(I) \
     if constexpr (OP == 0) asm volatile("v_and_b32 %0, %0, %1" : "+v"(a##I) : "v"(b)); \
     if constexpr (OP == 1) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a##I) : "v"(b)); \
-    if constexpr (OP == 2) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a##I) : "v"(b), "v"(c)); \
+    if constexpr (OP == 2) \
+      asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a##I) : "v"(b), "v"(c)); \
     if constexpr (OP == 3) asm volatile("v_alignbyte_b32 %0, %0, %1, %2" : "+v"(a##I) : "v"(b), "v"(c)); \
     if constexpr (OP == 4) asm volatile("v_bcnt_u32_b32 %0, %0, %1" : "+v"(a##I) : "v"(b)); \
     if constexpr (OP == 5) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a##I) : "v"(b)); \
@@ -46,7 +49,8 @@ __global__ __launch_bounds__(256) void k_probe(uint64_t* out, int iters, uint32_
     if constexpr (OP == 15) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a##I) : "v"(b)); \
     if constexpr (OP == 17) asm volatile("v_mad_u32_u24 %0, %0, %1, %2" : "+v"(a##I) : "v"(b), "v"(c)); \
     if constexpr (OP == 18) asm volatile("v_cmp_eq_u32 vcc, %0, %1" : : "v"(a##I), "v"(b) : "vcc"); \
-    if constexpr (OP == 19) asm volatile("v_mov_b32_dpp %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(a##I)); \
+    if constexpr (OP == 19) \
+      asm volatile("v_mov_b32_dpp %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(a##I)); \
     if constexpr (OP == 20) asm volatile("v_readlane_b32 s0, %0, 1" : : "v"(a##I) : "s0"); \
     if constexpr (OP == 21) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a##I) : "v"(b), "v"(c)); \
     if constexpr (OP == 22) asm volatile("v_and_b32 %0, 0x7f7f7f7f, %0" : "+v"(a##I)); \
@@ -55,13 +59,31 @@ __global__ __launch_bounds__(256) void k_probe(uint64_t* out, int iters, uint32_
     if constexpr (OP == 25) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a##I) : "v"(b)); \
     if constexpr (OP == 26) asm volatile("v_and_b32 %0, 7, %0" : "+v"(a##I)); \
     if constexpr (OP == 27) asm volatile("v_cndmask_b32_e64 %0, %0, %1, vcc" : "+v"(a##I) : "v"(b)); \
-    if constexpr (OP == 28) asm volatile("v_and_b32 %0, %0, %1\n v_and_b32 %0, %0, %1\n v_and_b32 %0, %0, %1\n v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a##I) : "v"(b)); \
-    if constexpr (OP == 29) asm volatile("v_and_b32 %0, %0, %1\n v_and_b32 %0, %0, %1\n v_and_b32 %0, %0, %1\n v_cndmask_b32_e64 %0, %0, %1, s[20:21]" : "+v"(a##I) : "v"(b)); \
-    if constexpr (OP == 30) asm volatile("v_cmp_gt_u32 vcc, %0, %1\n v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a##I) : "v"(b) : "vcc"); \
-    if constexpr (OP == 31) asm volatile("v_cmp_gt_u32 s[20:21], %0, %1\n v_cndmask_b32_e64 %0, %0, %1, s[20:21]" : "+v"(a##I) : "v"(b) : "s20", "s21"); \
-    if constexpr (OP == 33) asm volatile("v_mad_u64_u32 v[40:41], s[22:23], %0, %1, v[42:43]\n v_mov_b32 %0, v40" : "+v"(a##I) : "v"(b) : "v40", "v41", "v42", "v43", "s22", "s23"); \
+    if constexpr (OP == 28) \
+      asm volatile("v_and_b32 %0, %0, %1\n" \
+                   " v_and_b32 %0, %0, %1\n" \
+                   " v_and_b32 %0, %0, %1\n" \
+                   " v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a##I) : "v"(b)); \
+    if constexpr (OP == 29) \
+      asm volatile("v_and_b32 %0, %0, %1\n" \
+                   " v_and_b32 %0, %0, %1\n" \
+                   " v_and_b32 %0, %0, %1\n" \
+                   " v_cndmask_b32_e64 %0, %0, %1, s[20:21]" : "+v"(a##I) : "v"(b)); \
+    if constexpr (OP == 30) \
+      asm volatile("v_cmp_gt_u32 vcc, %0, %1\n" \
+                   " v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a##I) : "v"(b) : "vcc"); \
+    if constexpr (OP == 31) \
+      asm volatile("v_cmp_gt_u32 s[20:21], %0, %1\n" \
+                   " v_cndmask_b32_e64 %0, %0, %1, s[20:21]" : "+v"(a##I) : "v"(b) : "s20", "s21"); \
+    if constexpr (OP == 33) \
+      asm volatile("v_mad_u64_u32 v[40:41], s[22:23], %0, %1, v[42:43]\n" \
+                   " v_mov_b32 %0, v40" : "+v"(a##I) : "v"(b) : "v40", "v41", "v42", "v43", "s22", "s23"); \
     if constexpr (OP == 34) asm volatile("v_mad_u32_u24 %0, %0, %1, %2" : "+v"(a##I) : "v"(b), "v"(c)); \
-    if constexpr (OP == 32) asm volatile("v_and_b32 %0, %0, %1\n v_and_b32 %0, %0, %1\n v_and_b32 %0, %0, %1\n v_and_b32 %0, %0, %1" : "+v"(a##I) : "v"(b));
+    if constexpr (OP == 32) \
+      asm volatile("v_and_b32 %0, %0, %1\n" \
+                   " v_and_b32 %0, %0, %1\n" \
+                   " v_and_b32 %0, %0, %1\n" \
+                   " v_and_b32 %0, %0, %1" : "+v"(a##I) : "v"(b));
     R8(BODY)
     R8(BODY)
     if constexpr (OP == 16) {
@@ -117,7 +139,10 @@ int main(int argc, char** argv) {
   printf("{\"cus\": %d, \"iters\": %d, \"instr_per_iter\": 16, \"results\": [\n", cus, iters);
   bool first = true;
   for (const Probe& p : probes) {
-    if (only != nullptr && std::string(only).find(std::string(",") + p.name + ",") == std::string::npos) continue;
+    if (only != nullptr &&
+        std::string(only).find(std::string(",") + p.name + ",") == std::string::npos) {
+      continue;
+    }
     for (int wps : {2, 4, 8}) {  // waves per SIMD: blocks of 4 waves, wps blocks per CU
       const int blocks = cus * wps;
       hipLaunchKernelGGL(p.fn, dim3(blocks), dim3(256), 0, 0, d, 16, 1u);  // warm
