@@ -124,7 +124,7 @@ $(BUILD)/dmlc_gpu_api_check: tools/dmlc_gpu_api_check.cc $(LIB) $(HEADERS)
 # loopback S3 / HTTP object server (sendfile) for the remote-reader benchmarks
 $(BUILD)/dmlc_objserver: tools/dmlc_objserver.cc
 	@mkdir -p $(BUILD)
-	$(CXX) -std=c++17 -O2 -Wall -pthread $< -o $@
+	$(CXX) -std=c++17 -O2 -Wall -pthread $< -o $@ -lssl -lcrypto
 
 $(BUILD)/dmlc_bench_split_cpu: tools/dmlc_bench_split_cpu.cc $(LIB) $(HEADERS)
 	@mkdir -p $(BUILD)

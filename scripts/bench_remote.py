@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--data", default="/tmp/dmlc_remote_bench")
     ap.add_argument("--reader-threads", default="8,16,32,64",
                     help="read_threads values for the reader-alone runs (tools/dmlc_bench_read)")
+    ap.add_argument("--tls", action="store_true",
+                    help="serve https (the objserver's --tls) and read s3:// / https:// over it")
     args = ap.parse_args()
 
     import torch
@@ -48,11 +50,24 @@ def main():
                                  nthread=16)
             os.replace(f + ".tmp", f)
     nbytes = sum(os.path.getsize(os.path.join(bucket, x)) for x in os.listdir(bucket))
-    srv = subprocess.Popen([os.path.join(ROOT, "build", "dmlc_objserver"), "--root", args.data],
-                           stdout=subprocess.PIPE, text=True)
+    cmd = [os.path.join(ROOT, "build", "dmlc_objserver"), "--root", args.data]
+    scheme = "http"
+    if args.tls:
+        # https with a self-signed certificate that both the native receive
+        # (OpenSSL) and libcurl trust (SSL_CERT_FILE / CURL_CA_BUNDLE): peer
+        # and host verified as against a real endpoint
+        crt, key = os.path.join(args.data, "tls.crt"), os.path.join(args.data, "tls.key")
+        if not os.path.exists(crt):
+            subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", key,
+                            "-out", crt, "-days", "7", "-subj", "/CN=127.0.0.1",
+                            "-addext", "subjectAltName=IP:127.0.0.1"], check=True, capture_output=True)
+        cmd += ["--tls", crt, key]
+        os.environ.update({"SSL_CERT_FILE": crt, "CURL_CA_BUNDLE": crt})
+        scheme = "https"
+    srv = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True)
     try:
         port = int(srv.stdout.readline().split()[1])
-        os.environ.update({"S3_ENDPOINT": f"http://127.0.0.1:{port}", "S3_ACCESS_KEY_ID": "bench",
+        os.environ.update({"S3_ENDPOINT": f"{scheme}://127.0.0.1:{port}", "S3_ACCESS_KEY_ID": "bench",
                            "S3_SECRET_ACCESS_KEY": "bench", "S3_REGION": "us-east-1"})
         # the host stage alone (ShardReader.Fill into a 64 MiB buffer, no GPU):
         # what the ring's reader can deliver, natively received and via libcurl
@@ -69,9 +84,12 @@ def main():
                 print(json.dumps(rec), file=sys.stderr, flush=True)
         runs = [("local", bucket + "/", 8)]
         runs += [("s3", "s3://bench/train/", int(t)) for t in args.threads.split(",") if t]
-        runs.append(("http_one_file", f"http://127.0.0.1:{port}/bench/train/part-000.libsvm", 16))
+        runs.append(("http_one_file", f"{scheme}://127.0.0.1:{port}/bench/train/part-000.libsvm", 16))
         out = {"rows": args.rows, "files": args.files, "bytes": nbytes, "epochs": args.epochs,
-               "server": "tools/dmlc_objserver (loopback, sendfile)", "reader_alone": out_reader,
+               "scheme": scheme,
+               "server": "tools/dmlc_objserver (loopback, " + ("TLS, pread + SSL_write)" if args.tls
+                                                               else "sendfile)"),
+               "reader_alone": out_reader,
                "runs": []}
         for name, uri, threads in runs:
             gp = data.GPUParser(uri, format="libsvm", read_threads=threads)

@@ -4,6 +4,7 @@
  */
 #include "./http.h"
 
+#include <arpa/inet.h>
 #include <dlfcn.h>
 #include <dmlc/fault.h>
 #include <dmlc/logging.h>
@@ -12,6 +13,8 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <openssl/ssl.h>
+#include <openssl/x509v3.h>
 #include <poll.h>
 #include <sys/socket.h>
 #include <sys/time.h>
@@ -19,6 +22,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <climits>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -35,7 +39,7 @@ namespace {
 constexpr int kOptWriteData = 10001, kOptUrl = 10002, kOptTimeout = 13,
               kOptReadData = 10009, kOptPostFields = 10015, kOptHttpHeader = 10023,
               kOptHeaderData = 10029, kOptCustomRequest = 10036, kOptNoBody = 44,
-              kOptUpload = 46, kOptFollow = 52, kOptSslVerifyPeer = 64,
+              kOptUpload = 46, kOptFollow = 52, kOptSslVerifyPeer = 64, kOptCaInfo = 10065,
               kOptConnectTimeout = 78, kOptSslVerifyHost = 81, kOptNoSignal = 99,
               kOptWriteFunction = 20011, kOptReadFunction = 20012,
               kOptHeaderFunction = 20079, kOptInFileSizeLarge = 30115,
@@ -85,6 +89,18 @@ struct CurlApi {
   }
   bool ok() const { return handle != nullptr && error.empty(); }
 };
+
+/*! \brief CURL_CA_BUNDLE, else SSL_CERT_FILE; nullptr: the built-in store */
+const char* CaBundle() {
+  static const std::string ca = [] {
+    for (const char* e : {"CURL_CA_BUNDLE", "SSL_CERT_FILE"}) {
+      const char* v = std::getenv(e);
+      if (v != nullptr && *v != '\0') return std::string(v);
+    }
+    return std::string();
+  }();
+  return ca.empty() ? nullptr : ca.c_str();
+}
 
 CurlApi& Curl() {
   static CurlApi* api = new CurlApi();
@@ -150,24 +166,94 @@ size_t OnHeader(char* data, size_t size, size_t nmemb, void* user) {
 }
 
 // ------------------------------------------------------------------------
-// Plain-http GETs received straight into the caller's memory.  libcurl reads
-// the socket into its own 16 KiB buffer and hands it to OnWrite, which copies
-// it into req.out (the pinned ring slot): two copies of every byte, ~30 GB/s
-// of loopback per host in round 3 (profiles/r03_remote).  Here the body is
-// recv()ed with MSG_WAITALL directly into req.out -- the kernel's socket copy
-// is the only one.  Keep-alive connections are per thread (one per pool
-// worker).  Anything unusual (https, a non-2xx status, chunked or
-// length-less bodies, a transport error) closes the connection and the
-// request goes to libcurl instead.  Hosts libcurl would reach through a proxy
-// (http_proxy / all_proxy minus no_proxy) never take the native path, the
-// connect waits at most libcurl's 30 s, and an authority whose direct connect
-// failed is remembered, so later requests go straight to libcurl.
+// GETs received straight into the caller's memory.  libcurl reads the socket
+// into its own 16 KiB buffer and hands it to OnWrite, which copies it into
+// req.out (the pinned ring slot): two copies of every byte, ~30 GB/s of
+// loopback per host in round 3 (profiles/r03_remote).  Here a plain-http body
+// is recv()ed with MSG_WAITALL directly into req.out -- the kernel's socket
+// copy is the only one -- and an https body is SSL_read() into req.out
+// (OpenSSL 3 by dlopen: it decrypts each record and copies it out once, where
+// libcurl's OnWrite adds a second copy).  Keep-alive connections are per
+// thread (one per pool worker).  Anything unusual (a non-2xx status, chunked
+// or length-less bodies, a transport or handshake error) closes the
+// connection and the request goes to libcurl instead.  Hosts libcurl would
+// reach through a proxy (http_proxy / https_proxy / all_proxy minus no_proxy)
+// never take the native path, the connect waits at most libcurl's 30 s, and
+// an authority whose direct connect failed is remembered, so later requests
+// go straight to libcurl.
+
+/*! \brief the OpenSSL 3 calls of the native https path (libssl.so.3, dlopen) */
+struct TlsApi {
+  void* handle{nullptr};
+  const SSL_METHOD* (*client_method)(){nullptr};
+  SSL_CTX* (*ctx_new)(const SSL_METHOD*){nullptr};
+  int (*ctx_default_paths)(SSL_CTX*){nullptr};
+  void (*ctx_set_verify)(SSL_CTX*, int, SSL_verify_cb){nullptr};
+  SSL* (*ssl_new)(SSL_CTX*){nullptr};
+  void (*ssl_free)(SSL*){nullptr};
+  int (*set_fd)(SSL*, int){nullptr};
+  long (*ctrl)(SSL*, int, long, void*){nullptr};  // NOLINT(runtime/int): the OpenSSL ABI
+  int (*set1_host)(SSL*, const char*){nullptr};
+  X509_VERIFY_PARAM* (*get0_param)(SSL*){nullptr};
+  int (*param_ip)(X509_VERIFY_PARAM*, const char*){nullptr};
+  int (*connect)(SSL*){nullptr};
+  int (*read)(SSL*, void*, int){nullptr};
+  int (*write)(SSL*, const void*, int){nullptr};
+  SSL_CTX* verify_ctx{nullptr};    // peer and host verified (libcurl's default)
+  SSL_CTX* noverify_ctx{nullptr};  // verify_ssl = false (S3_VERIFY_SSL=0 ...)
+
+  TlsApi() {
+    handle = dlopen("libssl.so.3", RTLD_NOW | RTLD_LOCAL);
+    if (handle == nullptr) return;
+    bool ok = true;
+#define DMLC_TLS_SYM(f, name) \
+  f = reinterpret_cast<decltype(f)>(dlsym(handle, name)); \
+  ok = ok && f != nullptr;
+    DMLC_TLS_SYM(client_method, "TLS_client_method")
+    DMLC_TLS_SYM(ctx_new, "SSL_CTX_new")
+    DMLC_TLS_SYM(ctx_default_paths, "SSL_CTX_set_default_verify_paths")
+    DMLC_TLS_SYM(ctx_set_verify, "SSL_CTX_set_verify")
+    DMLC_TLS_SYM(ssl_new, "SSL_new")
+    DMLC_TLS_SYM(ssl_free, "SSL_free")
+    DMLC_TLS_SYM(set_fd, "SSL_set_fd")
+    DMLC_TLS_SYM(ctrl, "SSL_ctrl")
+    DMLC_TLS_SYM(set1_host, "SSL_set1_host")
+    DMLC_TLS_SYM(get0_param, "SSL_get0_param")
+    DMLC_TLS_SYM(param_ip, "X509_VERIFY_PARAM_set1_ip_asc")  // libcrypto, a dependency
+    DMLC_TLS_SYM(connect, "SSL_connect")
+    DMLC_TLS_SYM(read, "SSL_read")
+    DMLC_TLS_SYM(write, "SSL_write")
+#undef DMLC_TLS_SYM
+    if (!ok) return;
+    verify_ctx = ctx_new(client_method());
+    noverify_ctx = ctx_new(client_method());
+    if (verify_ctx == nullptr || noverify_ctx == nullptr) return;
+    ctx_default_paths(verify_ctx);  // the system store; SSL_CERT_FILE / SSL_CERT_DIR honoured
+    if (const char* ca = std::getenv("CURL_CA_BUNDLE")) {
+      auto load = reinterpret_cast<int (*)(SSL_CTX*, const char*, const char*)>(
+          dlsym(handle, "SSL_CTX_load_verify_locations"));
+      if (load != nullptr && *ca != '\0') load(verify_ctx, ca, nullptr);
+    }
+    ctx_set_verify(verify_ctx, SSL_VERIFY_PEER, nullptr);
+    ctx_set_verify(noverify_ctx, SSL_VERIFY_NONE, nullptr);
+  }
+  bool ok() const { return verify_ctx != nullptr && noverify_ctx != nullptr; }
+};
+
+TlsApi& Tls() {
+  static TlsApi* api = new TlsApi();
+  return *api;
+}
 
 struct NativeConn {
-  std::string authority;  // host[:port] the socket is connected to
+  std::string authority;  // scheme://host[:port] the socket is connected to
+  bool verify{true};      // the TLS verification the connection was made with
   int fd{-1};
+  SSL* ssl{nullptr};      // https: the TLS session over fd
   ~NativeConn() { Close(); }
   void Close() {
+    if (ssl != nullptr) Tls().ssl_free(ssl);
+    ssl = nullptr;
     if (fd >= 0) ::close(fd);
     fd = -1;
   }
@@ -206,10 +292,13 @@ std::string LowerEnv(const char* a, const char* b) {
  *  leading dot).  The native path then stays off: it only speaks to origin
  *  servers directly.
  */
-bool ProxyApplies(const std::string& host) {
-  const char* hp = std::getenv("http_proxy");  // curl reads only lowercase http_proxy
-  const std::string proxy = hp != nullptr && *hp != '\0' ? std::string(hp)
-                                                           : LowerEnv("all_proxy", "ALL_PROXY");
+bool ProxyApplies(const std::string& host, bool https = false) {
+  // curl reads only lowercase http_proxy; https_proxy in either case
+  const std::string hp = https ? LowerEnv("https_proxy", "HTTPS_PROXY") : [] {
+    const char* v = std::getenv("http_proxy");
+    return std::string(v == nullptr ? "" : v);
+  }();
+  const std::string proxy = !hp.empty() ? hp : LowerEnv("all_proxy", "ALL_PROXY");
   if (proxy.empty()) return false;
   std::string h = host;
   std::transform(h.begin(), h.end(), h.begin(), ::tolower);
@@ -324,18 +413,75 @@ bool RecvAll(int fd, char* p, size_t n) {
   return true;
 }
 
+/*! \brief write all of p (TLS or plain) */
+bool ConnSend(NativeConn& c, const char* p, size_t n) {
+  if (c.ssl == nullptr) return SendAll(c.fd, p, n);
+  while (n > 0) {
+    const int k = Tls().write(c.ssl, p, static_cast<int>(std::min<size_t>(n, INT_MAX)));
+    if (k <= 0) return false;
+    p += k;
+    n -= static_cast<size_t>(k);
+  }
+  return true;
+}
+
+/*! \brief what is there, up to n bytes (<= 0: closed or failed) */
+ssize_t ConnRecvSome(NativeConn& c, char* p, size_t n) {
+  if (c.ssl != nullptr) return Tls().read(c.ssl, p, static_cast<int>(std::min<size_t>(n, INT_MAX)));
+  for (;;) {
+    const ssize_t k = ::recv(c.fd, p, n, 0);
+    if (k < 0 && errno == EINTR) continue;
+    return k;
+  }
+}
+
+/*! \brief exactly n bytes: one MSG_WAITALL recv on plain sockets, record by
+ *  record (SSL_read into p, no staging buffer of ours) on TLS */
+bool ConnRecvAll(NativeConn& c, char* p, size_t n) {
+  if (c.ssl == nullptr) return RecvAll(c.fd, p, n);
+  while (n > 0) {
+    const ssize_t k = ConnRecvSome(c, p, n);
+    if (k <= 0) return false;
+    p += k;
+    n -= static_cast<size_t>(k);
+  }
+  return true;
+}
+
+/*! \brief TLS over c.fd: SNI, the peer checked against host (name or IP
+ *  literal) when verify is on */
+bool StartTls(NativeConn& c, const std::string& host, bool verify) {
+  TlsApi& t = Tls();
+  c.ssl = t.ssl_new(verify ? t.verify_ctx : t.noverify_ctx);
+  if (c.ssl == nullptr || t.set_fd(c.ssl, c.fd) != 1) return false;
+  in6_addr a6;
+  in_addr a4;
+  const bool ip = inet_pton(AF_INET, host.c_str(), &a4) == 1 ||
+                  inet_pton(AF_INET6, host.c_str(), &a6) == 1;
+  if (!ip) {
+    t.ctrl(c.ssl, SSL_CTRL_SET_TLSEXT_HOSTNAME, TLSEXT_NAMETYPE_host_name,
+           const_cast<char*>(host.c_str()));
+  }
+  if (verify) {
+    const int r = ip ? t.param_ip(t.get0_param(c.ssl), host.c_str()) : t.set1_host(c.ssl, host.c_str());
+    if (r != 1) return false;
+  }
+  return t.connect(c.ssl) == 1;
+}
+
 /*!
  * \brief one GET on the thread's keep-alive connection into req.out.
  * \return true if `resp` holds the outcome; false = use libcurl (the
  *  connection is closed, nothing of `resp` is kept)
  */
 bool NativeGet(const HttpRequest& req, HttpResponse* resp) {
-  static const std::string kScheme = "http://";
-  if (req.url.compare(0, kScheme.size(), kScheme) != 0) return false;
-  const size_t slash = req.url.find('/', kScheme.size());
+  const bool https = req.url.compare(0, 8, "https://") == 0;
+  if (!https && req.url.compare(0, 7, "http://") != 0) return false;
+  if (https && !Tls().ok()) return false;  // no libssl.so.3: libcurl
+  const size_t skip = https ? 8 : 7;
+  const size_t slash = req.url.find('/', skip);
   const std::string authority =
-      req.url.substr(kScheme.size(), slash == std::string::npos ? std::string::npos
-                                                                  : slash - kScheme.size());
+      req.url.substr(skip, slash == std::string::npos ? std::string::npos : slash - skip);
   const std::string target = slash == std::string::npos ? "/" : req.url.substr(slash);
   if (authority.empty() || authority.find('@') != std::string::npos ||
       authority.front() == '[') {
@@ -343,16 +489,18 @@ bool NativeGet(const HttpRequest& req, HttpResponse* resp) {
   }
   const size_t colon = authority.rfind(':');
   const std::string host = authority.substr(0, colon);
-  const std::string port = colon == std::string::npos ? "80" : authority.substr(colon + 1);
+  const std::string port =
+      colon == std::string::npos ? (https ? "443" : "80") : authority.substr(colon + 1);
+  const std::string key = req.url.substr(0, skip) + authority;  // connections per scheme
   // a proxied host, or one whose direct connect already failed: libcurl
-  if (ProxyApplies(host) || KnownUnreachable(authority)) return false;
+  if (ProxyApplies(host, https) || KnownUnreachable(key)) return false;
 
   std::string head = "GET " + target + " HTTP/1.1\r\nHost: " + authority + "\r\n";
   for (const auto& h : req.headers) head += h + "\r\n";
   head += "\r\n";
 
   NativeConn& c = ThreadConn();
-  if (c.fd >= 0 && c.authority != authority) c.Close();
+  if (c.fd >= 0 && (c.authority != key || c.verify != req.verify_ssl)) c.Close();
   char hdr[16384];
   size_t have = 0, hend = std::string::npos;
   for (int attempt = 0; attempt < 2; ++attempt) {
@@ -360,16 +508,20 @@ bool NativeGet(const HttpRequest& req, HttpResponse* resp) {
     if (!reused) {
       c.fd = ConnectTo(host, port, req.timeout_sec);
       if (c.fd < 0) {
-        MarkUnreachable(authority);
+        MarkUnreachable(key);
         return false;
       }
-      c.authority = authority;
+      c.authority = key;
+      c.verify = req.verify_ssl;
+      if (https && !StartTls(c, host, req.verify_ssl)) {
+        c.Close();  // handshake or verification failed: libcurl reports it
+        return false;
+      }
     }
     have = 0;
-    bool ok = SendAll(c.fd, head.data(), head.size());
+    bool ok = ConnSend(c, head.data(), head.size());
     while (ok && hend == std::string::npos) {
-      const ssize_t k = ::recv(c.fd, hdr + have, sizeof(hdr) - have, 0);
-      if (k < 0 && errno == EINTR) continue;
+      const ssize_t k = ConnRecvSome(c, hdr + have, sizeof(hdr) - have);
       if (k <= 0) {
         ok = false;
         break;
@@ -425,7 +577,7 @@ bool NativeGet(const HttpRequest& req, HttpResponse* resp) {
   const size_t early_in = std::min(early, into);
   std::memcpy(req.out, hdr + hend, early_in);
   if (early > early_in) r.body.append(hdr + hend + early_in, early - early_in);
-  bool ok = RecvAll(c.fd, req.out + early_in, into - early_in);
+  bool ok = ConnRecvAll(c, req.out + early_in, into - early_in);
   bool drop = close_after;
   if (ok && len > std::max(early, into)) {
     // overflow beyond out_cap (e.g. a server that ignored Range): keep a
@@ -434,7 +586,7 @@ bool NativeGet(const HttpRequest& req, HttpResponse* resp) {
     if (rest <= (64u << 10)) {
       const size_t at = r.body.size();
       r.body.resize(at + rest);
-      ok = RecvAll(c.fd, &r.body[at], rest);
+      ok = ConnRecvAll(c, &r.body[at], rest);
     } else {
       drop = true;
     }
@@ -483,6 +635,9 @@ HttpResponse Http::Perform(const HttpRequest& req) {
   c.easy_setopt(h, kOptConnectTimeout, 30L);
   c.easy_setopt(h, kOptTimeout, req.timeout_sec);
   c.easy_setopt(h, kOptSslVerifyPeer, req.verify_ssl ? 1L : 0L);
+  // one trust store for both https paths: a CA bundle named by CURL_CA_BUNDLE
+  // or SSL_CERT_FILE (the native path's OpenSSL reads SSL_CERT_FILE itself)
+  if (const char* ca = CaBundle()) c.easy_setopt(h, kOptCaInfo, ca);
   c.easy_setopt(h, kOptSslVerifyHost, req.verify_ssl ? 2L : 0L);
   if (req.method == "HEAD") {
     c.easy_setopt(h, kOptNoBody, 1L);

@@ -371,3 +371,76 @@ print("ok")
                        timeout=120)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
     assert (root / "out" / "blob.bin").read_bytes() == bytes(range(256)) * 40 + b"tail"
+
+
+_HTTPS_CLIENT = r'''
+import json, os, sys
+sys.path.insert(0, os.environ["TESTS_DIR"])
+import numpy as np
+import mock_remote
+from dmlc_core_amd import _dmlc, io
+
+crt, key = sys.argv[1], sys.argv[2]
+
+def read_all(uri, chunk=1 << 20):
+    s = io.Stream(uri, "r")
+    out = bytearray()
+    while True:
+        b = s.read(chunk)
+        if not b:
+            return bytes(out)
+        out += b
+
+res = {}
+payload = np.random.default_rng(11).integers(0, 256, (3 << 20) + 333, dtype=np.uint8).tobytes()
+srv = mock_remote.serve_tls(mock_remote.PlainHandler, crt, key)
+mock_remote.PlainHandler.store["/files/t.bin"] = payload
+s0 = _dmlc.http_stats()
+res["https_equal"] = read_all(f"https://127.0.0.1:{srv.server_address[1]}/files/t.bin") == payload
+s1 = _dmlc.http_stats()
+res["https_native"] = s1["native_gets"] - s0["native_gets"]
+res["https_fallbacks"] = s1["native_fallbacks"] - s0["native_fallbacks"]
+s3 = mock_remote.serve_tls(mock_remote.S3Handler, crt, key)
+os.environ.update({"S3_ENDPOINT": f"https://127.0.0.1:{s3.server_address[1]}",
+                   "S3_ACCESS_KEY_ID": "AKIDTEST", "S3_SECRET_ACCESS_KEY": "secret",
+                   "S3_REGION": "us-east-1", "S3_VERIFY_SSL": "0"})
+w = io.Stream("s3://tls/obj.bin", "w")
+w.write(payload)
+w.close()
+s2 = _dmlc.http_stats()
+res["s3_equal"] = read_all("s3://tls/obj.bin") == payload
+s3s = _dmlc.http_stats()
+res["s3_native"] = s3s["native_gets"] - s2["native_gets"]
+res["s3_fallbacks"] = s3s["native_fallbacks"] - s2["native_fallbacks"]
+print(json.dumps(res))
+'''
+
+
+@pytest.mark.skipif(os.environ.get("DMLC_HTTP_NATIVE", "1") == "0", reason="native path off")
+def test_https_native_receive_into_caller_memory(tmp_path):
+    """https GETs take the native receive too (OpenSSL 3 by dlopen, SSL_read
+    into the destination): with verification against the trust store that
+    CURL_CA_BUNDLE / SSL_CERT_FILE name (the test's self-signed certificate,
+    for libcurl's HEAD and the native GETs alike) and with
+    S3_VERIFY_SSL=0; the bytes equal what was served or written.  A fresh
+    process: the trust store is read once per process."""
+    import shutil
+    import subprocess
+    import sys
+    if shutil.which("openssl") is None:
+        pytest.skip("no openssl CLI to make a test certificate")
+    crt, key = str(tmp_path / "c.pem"), str(tmp_path / "k.pem")
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", key,
+                    "-out", crt, "-days", "2", "-subj", "/CN=127.0.0.1",
+                    "-addext", "subjectAltName=IP:127.0.0.1"], check=True, capture_output=True)
+    env = dict(os.environ, SSL_CERT_FILE=crt, CURL_CA_BUNDLE=crt, TESTS_DIR=os.path.dirname(__file__))
+    for k in ("http_proxy", "https_proxy", "HTTPS_PROXY", "all_proxy", "ALL_PROXY"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, "-c", _HTTPS_CLIENT, crt, key], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    import json
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["https_equal"] and r["s3_equal"], r
+    assert r["https_native"] >= 3 and r["https_fallbacks"] == 0, r
+    assert r["s3_native"] >= 3 and r["s3_fallbacks"] == 0, r

@@ -4,7 +4,10 @@
  *  (BASELINE config 4): S3 path-style and plain HTTP over one directory,
  *  object bodies sent with sendfile(2) from the page cache.
  *
- *   dmlc_objserver --root DIR [--port P] [--host 127.0.0.1]
+ *   dmlc_objserver --root DIR [--port P] [--host 127.0.0.1] [--tls CERT KEY]
+ *
+ * --tls serves https (OpenSSL; bodies read with pread and written with
+ * SSL_write -- no sendfile through TLS without kernel TLS).
  *
  * Prints "PORT <n>" on stdout once listening (port 0 picks a free one), then
  * serves until killed.  Requests (HTTP/1.1, keep-alive, thread per
@@ -22,6 +25,7 @@
 #include <fcntl.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <openssl/ssl.h>
 #include <sys/sendfile.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
@@ -44,6 +48,13 @@ namespace {
 namespace fs = std::filesystem;
 
 std::string g_root;
+SSL_CTX* g_tls = nullptr;  // --tls: https
+
+/*! \brief one client connection: a socket, and its TLS session under --tls */
+struct Conn {
+  int fd;
+  SSL* ssl;
+};
 
 std::string UrlDecode(const std::string& s) {
   std::string o;
@@ -74,9 +85,10 @@ std::string XmlEscape(const std::string& s) {
   return o;
 }
 
-bool SendAll(int fd, const char* p, size_t n) {
+bool SendAll(const Conn& c, const char* p, size_t n) {
   while (n != 0) {
-    const ssize_t k = ::send(fd, p, n, MSG_NOSIGNAL);
+    const int chunk = static_cast<int>(std::min<size_t>(n, 1u << 30));
+    const ssize_t k = c.ssl != nullptr ? ::SSL_write(c.ssl, p, chunk) : ::send(c.fd, p, n, MSG_NOSIGNAL);
     if (k <= 0) return false;
     p += k;
     n -= static_cast<size_t>(k);
@@ -84,7 +96,11 @@ bool SendAll(int fd, const char* p, size_t n) {
   return true;
 }
 
-bool Reply(int fd, int code, const char* reason, const std::string& body,
+ssize_t RecvSome(const Conn& c, char* p, size_t n) {
+  return c.ssl != nullptr ? ::SSL_read(c.ssl, p, static_cast<int>(n)) : ::recv(c.fd, p, n, 0);
+}
+
+bool Reply(const Conn& fd, int code, const char* reason, const std::string& body,
            const std::vector<std::string>& headers, bool head_only) {
   std::string h = "HTTP/1.1 " + std::to_string(code) + " " + reason + "\r\n";
   for (const auto& x : headers) h += x + "\r\n";
@@ -146,7 +162,7 @@ std::string ListXml(const std::string& bucket, std::map<std::string, std::string
 }
 
 /*! \brief one request; false ends the connection */
-bool Serve(int fd, const std::string& method, const std::string& target,
+bool Serve(const Conn& fd, const std::string& method, const std::string& target,
            const std::map<std::string, std::string>& hdr) {
   const bool head = method == "HEAD";
   if (method != "GET" && !head) return Reply(fd, 501, "Not Implemented", "", {}, false);
@@ -215,11 +231,21 @@ bool Serve(int fd, const std::string& method, const std::string& target,
   }
   h += "Accept-Ranges: bytes\r\nContent-Length: " + std::to_string(len) + "\r\n\r\n";
   bool ok = SendAll(fd, h.data(), h.size());
-  if (ok && !head) {
+  if (ok && !head && fd.ssl != nullptr) {
+    // TLS: read and encrypt 1 MiB at a time
+    thread_local std::vector<char> buf(1u << 20);
+    uint64_t off = b, left = len;
+    while (ok && left != 0) {
+      const ssize_t k = ::pread(f, buf.data(), std::min<uint64_t>(left, buf.size()), static_cast<off_t>(off));
+      ok = k > 0 && SendAll(fd, buf.data(), static_cast<size_t>(k));
+      off += static_cast<uint64_t>(k > 0 ? k : 0);
+      left -= static_cast<uint64_t>(k > 0 ? k : 0);
+    }
+  } else if (ok && !head) {
     off_t off = static_cast<off_t>(b);
     uint64_t left = len;
     while (left != 0) {
-      const ssize_t k = ::sendfile(fd, f, &off, std::min<uint64_t>(left, 1u << 30));
+      const ssize_t k = ::sendfile(fd.fd, f, &off, std::min<uint64_t>(left, 1u << 30));
       if (k <= 0) {
         ok = false;
         break;
@@ -231,22 +257,35 @@ bool Serve(int fd, const std::string& method, const std::string& target,
   return ok;
 }
 
-void Connection(int fd) {
+void Connection(int sock) {
   const int one = 1;
-  ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  ::setsockopt(sock, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  Conn fd{sock, nullptr};
+  if (g_tls != nullptr) {
+    fd.ssl = ::SSL_new(g_tls);
+    if (fd.ssl == nullptr || ::SSL_set_fd(fd.ssl, sock) != 1 || ::SSL_accept(fd.ssl) != 1) {
+      if (fd.ssl != nullptr) ::SSL_free(fd.ssl);
+      ::close(sock);
+      return;
+    }
+  }
+  auto finish = [&] {
+    if (fd.ssl != nullptr) ::SSL_free(fd.ssl);
+    ::close(sock);
+  };
   std::string buf;
   char tmp[16384];
   for (;;) {
     size_t end;
     while ((end = buf.find("\r\n\r\n")) == std::string::npos) {
-      const ssize_t k = ::recv(fd, tmp, sizeof(tmp), 0);
+      const ssize_t k = RecvSome(fd, tmp, sizeof(tmp));
       if (k <= 0) {
-        ::close(fd);
+        finish();
         return;
       }
       buf.append(tmp, static_cast<size_t>(k));
       if (buf.size() > (1u << 20)) {
-        ::close(fd);
+        finish();
         return;
       }
     }
@@ -275,9 +314,9 @@ void Connection(int fd) {
     if (hdr.count("content-length")) {
       size_t n = std::strtoul(hdr["content-length"].c_str(), nullptr, 10);
       while (buf.size() < n) {
-        const ssize_t k = ::recv(fd, tmp, sizeof(tmp), 0);
+        const ssize_t k = RecvSome(fd, tmp, sizeof(tmp));
         if (k <= 0) {
-          ::close(fd);
+          finish();
           return;
         }
         buf.append(tmp, static_cast<size_t>(k));
@@ -287,7 +326,7 @@ void Connection(int fd) {
     if (!Serve(fd, line.substr(0, s1), line.substr(s1 + 1, s2 - s1 - 1), hdr)) break;
     if (hdr.count("connection") && hdr["connection"] == "close") break;
   }
-  ::close(fd);
+  finish();
 }
 
 }  // namespace
@@ -303,8 +342,16 @@ int main(int argc, char** argv) {
       port = std::atoi(argv[++i]);
     } else if (a == "--host" && i + 1 < argc) {
       host = argv[++i];
+    } else if (a == "--tls" && i + 2 < argc) {
+      g_tls = ::SSL_CTX_new(::TLS_server_method());
+      if (g_tls == nullptr || ::SSL_CTX_use_certificate_chain_file(g_tls, argv[i + 1]) != 1 ||
+          ::SSL_CTX_use_PrivateKey_file(g_tls, argv[i + 2], SSL_FILETYPE_PEM) != 1) {
+        std::fprintf(stderr, "--tls: cannot load %s / %s\n", argv[i + 1], argv[i + 2]);
+        return 2;
+      }
+      i += 2;
     } else {
-      std::fprintf(stderr, "usage: %s --root DIR [--port P] [--host ADDR]\n", argv[0]);
+      std::fprintf(stderr, "usage: %s --root DIR [--port P] [--host ADDR] [--tls CERT KEY]\n", argv[0]);
       return 2;
     }
   }
