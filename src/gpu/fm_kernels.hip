@@ -18,10 +18,10 @@
  * F2 k_fm_bwd: with g = dL/dy and G_r = [g_r, g_r xV_r] (17 columns),
  *   Z = G^T X (summed over rows) and t = (x^2)^T g give every gradient:
  *   dw = s Z_0, dV_nf = s Z_{1+f,n} - V_nf s^2 t_n.  Rows are the reduction
- *   index, so X must arrive with rows along K: an identity MFMA turns each
- *   32 x 32 X tile into an accumulator with features on lanes and rows in
- *   registers, which is exactly the B operand of the next MFMA (G^T from LDS
- *   in the matching permuted row order).  Eight waves share one G tile
+ *   index, so X must arrive with rows along K: each wave writes its 32-row X
+ *   tile to LDS and reads it back transposed (ds_read_b64_tr_b8: 8 rows of
+ *   one feature per lane), the B operand of the MFMA with G^T from LDS in
+ *   the same row order.  Eight waves share one G tile
  *   (double-buffered in LDS: one barrier per 32-row tile); each
  *   keeps 128 features of Z in 64 accumulator registers and writes one
  *   partial per workgroup.
@@ -241,6 +241,9 @@ __global__ __launch_bounds__(kBwdThreads) void k_fm_bwd(const uint8_t* __restric
   // tile's G is written while this one is consumed, one barrier per tile
   __shared__ __attribute__((aligned(16))) __bf16 s_gt[2][32][32 + 8];
   __shared__ __attribute__((aligned(16))) float s_g[2][32];
+  // each wave's X tile, read back transposed (as in F5: chunk (i, lane) at
+  // i * 64 + (lane ^ 8 (i & 1)))
+  __shared__ uint4 s_xb[kBwdThreads / kWave][4 * 64];
   const int lane = lane_id();
   const int h = lane >> 5, n = lane & 31;
   const int wave = threadIdx.x / kWave;
@@ -251,18 +254,14 @@ __global__ __launch_bounds__(kBwdThreads) void k_fm_bwd(const uint8_t* __restric
   }
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
   const int64_t r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
-  // identity B fragments: element j of step s is 1 for column n's (h, s, j)
-  bf16x8 eye[2];
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const bool one = h == (n >> 4) && s == ((n >> 3) & 1) && j == (n & 7);
-      eye[s][j] = static_cast<__bf16>(one ? 1.0f : 0.0f);
-    }
-  }
+  // transposed reads of the wave's X image (ds_read_b64_tr_b8, the map of F5)
+  const int gr = lane >> 4, qq = (lane & 15) >> 1, pp = lane & 1;
+  const uint32_t xt_base =
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>(&s_xb[wave][0])) +
+      16u * static_cast<uint32_t>((gr & 1) * 64 + ((8 * (gr >> 1) + qq) ^ (8 * (gr & 1)))) +
+      8u * static_cast<uint32_t>(pp);
   f32x16 acc[4] = {};
-  float tacc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  f32x2 tacc[4] = {};
   // the next tile's X fragment and G inputs are loaded while this tile computes
   const int grow = threadIdx.x >> 3, gpart = threadIdx.x & 7;  // G producer (threads < 256)
   // loads are issued unconditionally (a clamped row, the value zeroed past
@@ -320,46 +319,39 @@ __global__ __launch_bounds__(kBwdThreads) void k_fm_bwd(const uint8_t* __restric
   auto tile = [&](int64_t t0, uint4 (&xw)[4]) {
     put_g(cb ^ 1, gv_n, v_n);  // the next tile's G (its buffer was consumed last tile)
     load_g(t0 + 64, &gv_n, &v_n);
-    if (active) {
-      // G^T fragments: element j of step s = row 16 s + 8 (j >> 2) + 4 h + (j & 3)
-      // (8-byte LDS reads: elements j = 0..3 and 4..7 are 4 consecutive rows)
+    if (active) {  // wave-uniform (the transposed reads need every lane)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s_xb[wave][i * 64 + (lane ^ (8 * (i & 1)))] = xw[i];
+      wave_sync();
+      // A = G^T rows 16 s + 8 h + j (natural order), B = X rows along K
       bf16x8 ga[2];
-      const uint2* gt_row = reinterpret_cast<const uint2*>(&s_gt[cb][n][0]);
+      f32x2 g2[2][4];
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const uint2 lo = gt_row[4 * s + h], hi = gt_row[4 * s + 2 + h];
-        const uint4 q = make_uint4(lo.x, lo.y, hi.x, hi.y);
-        ga[s] = __builtin_bit_cast(bf16x8, q);
+        ga[s] = *reinterpret_cast<const bf16x8*>(&s_gt[cb][n][16 * s + 8 * h]);
+        const float4 ga4 = *reinterpret_cast<const float4*>(&s_g[cb][16 * s + 8 * h]);
+        const float4 gb4 = *reinterpret_cast<const float4*>(&s_g[cb][16 * s + 8 * h + 4]);
+        g2[s][0] = f32x2{ga4.x, ga4.y};
+        g2[s][1] = f32x2{ga4.z, ga4.w};
+        g2[s][2] = f32x2{gb4.x, gb4.y};
+        g2[s][3] = f32x2{gb4.z, gb4.w};
       }
-      float gr[16];
-#pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4) {
-        const float4 g4 = *reinterpret_cast<const float4*>(&s_g[cb][8 * r4 + 4 * h]);
-        gr[4 * r4 + 0] = g4.x;
-        gr[4 * r4 + 1] = g4.y;
-        gr[4 * r4 + 2] = g4.z;
-        gr[4 * r4 + 3] = g4.w;
-      }
+      typedef __attribute__((address_space(3))) v2i lds_v2i;
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
-        // T: this block's 32 x 32 X tile, features on lanes, rows in registers
-        f32x16 tt = {};
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          tt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              fp8x8_bf16(word(xw, 2 * (2 * b + s)), word(xw, 2 * (2 * b + s) + 1)), eye[s], tt,
-              0, 0, 0);
-        }
-        float ta = 0.0f;
+          const uint32_t a = xt_base + 2048u * (b & 1) + 512u * (b >> 1) + 256u * s;
+          const v2i raw = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(static_cast<uintptr_t>(a)));
+          const uint32_t lo = static_cast<uint32_t>(raw.x), hi = static_cast<uint32_t>(raw.y);
+          acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[s], fp8x8_bf16(lo, hi), acc[b], 0, 0, 0);
+          float f[8];
+          fp8x8(lo, hi, f);
 #pragma unroll
-        for (int reg = 0; reg < 16; ++reg) ta += tt[reg] * tt[reg] * gr[reg];
-        tacc[b] += ta;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          bf16x8 tb;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) tb[j] = static_cast<__bf16>(tt[8 * s + j]);
-          acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[s], tb, acc[b], 0, 0, 0);
+          for (int k = 0; k < 4; ++k) {
+            const f32x2 x2 = f32x2{f[2 * k], f[2 * k + 1]};
+            tacc[b] = __builtin_elementwise_fma(x2 * x2, g2[s][k], tacc[b]);
+          }
         }
       }
     }
@@ -376,14 +368,14 @@ __global__ __launch_bounds__(kBwdThreads) void k_fm_bwd(const uint8_t* __restric
   float* out = part + static_cast<size_t>(blockIdx.x) * (kFmCols + 1) * dim;
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
-    // column n of block b <-> feature 64 (n >> 4) + 16 b + 8 ((n >> 3) & 1) + (n & 7)
-    const int feat = fbase + 64 * (n >> 4) + 16 * b + 8 * ((n >> 3) & 1) + (n & 7);
+    const int feat = fbase + 32 * b + n;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
       const int c = (reg & 3) + 8 * (reg >> 2) + 4 * h;
       if (c < kFmCols) out[static_cast<size_t>(c) * dim + feat] = acc[b][reg];
     }
-    const float tt = tacc[b] + __shfl_xor(tacc[b], 32, kWave);
+    const float t1 = tacc[b][0] + tacc[b][1];
+    const float tt = t1 + __shfl_xor(t1, 32, kWave);
     if (h == 0) out[static_cast<size_t>(kFmCols) * dim + feat] = tt;
   }
 }
