@@ -639,20 +639,36 @@ __device__ __noinline__ QidResult qid_token(const uint8_t* __restrict__ text, si
  */
 __device__ __forceinline__ QidResult qid_lds(const uint4* lds, uint32_t a) {
   QidResult r{0, false};
-  const uint4 g0 = tok::ext16(lds, a), g1 = tok::ext16(lds, a + 16);
-  if (g0.x != 0x3A646971u) return r;  // "qid:"
-  uint32_t i = 4;
-  const uint32_t c0 = tok::win_byte(g0, g1, 4);
+  const uint3 g = tok::ext12(lds, a);
+  if (g.x != 0x3A646971u) return r;  // "qid:"
+  const uint32_t c0 = g.y & 0xFFu;
   const bool neg = c0 == '-';
-  if (neg || c0 == '+') i = 5;
-  uint64_t v = 0;
-  for (int k = 0; k < 20; ++k, ++i) {
-    const uint32_t c = tok::win_byte(g0, g1, i);
-    if (c - '0' > 9u) break;
-    v = v * 10 + (c - '0');
+  const uint32_t s = (neg || c0 == '+') ? 1u : 0u;
+  // the digits 8 at a time (digit_run8); 16 or more: the byte loop below
+  const uint3 d1 = tok::ext12(lds, a + 4u + s);
+  const tok::Run8 r1 = tok::digit_run8(d1.x, d1.y, d1.z & 0xFFu);
+  uint64_t v = r1.val;
+  uint32_t term = r1.term;
+  if (r1.k == 8u) {
+    const uint3 d2 = tok::ext12(lds, a + 12u + s);
+    const tok::Run8 r2 = tok::digit_run8(d2.x, d2.y, d2.z & 0xFFu);
+    if (r2.k == 8u) {
+      // 16+ digits (StrToInt over up to 20, wrapping): byte by byte
+      const uint4 g0 = tok::ext16(lds, a), g1 = tok::ext16(lds, a + 16);
+      uint32_t i = 4u + s;
+      v = 0;
+      for (int k = 0; k < 20; ++k, ++i) {
+        const uint32_t c = tok::win_byte(g0, g1, i);
+        if (c - '0' > 9u) break;
+        v = v * 10 + (c - '0');
+      }
+      term = tok::win_byte(g0, g1, i);
+    } else {
+      v = v * tok::pow10_u(r2.k) + r2.val;
+      term = r2.term;
+    }
   }
-  const uint32_t c = tok::win_byte(g0, g1, i);
-  if (c != ' ' && c != '\t' && c != '\n' && c != '\r' && c != 0) return r;  // junk after the digits
+  if (term != ' ' && term != '\t' && term != '\n' && term != '\r' && term != 0) return r;
   r.value = neg ? 0 - v : v;
   r.ok = true;
   return r;

@@ -206,6 +206,12 @@ __device__ __forceinline__ Num parse_num_g(uint4 g, uint32_t a);
  *  unconditionally: branch-free), each decoded by digit_run8.  The same
  *  values and flags as parse_num_g on every number whose fraction fits its
  *  16-byte window; a longer fraction (<= 7 digits) is taken here as well.
+ *  Two extensions run only when some lane of the wave needs them (wave-
+ *  uniform branches: free on plain `0.dddddd` data), with parse_num_ext's
+ *  arithmetic, so the values are the same bits: fractions of 8 to 15 digits
+ *  (a second digit run, the reference's double quotient) and exponents of up
+ *  to 3 digits with |e| <= 10 (10^e exact in float, one IEEE multiply or
+ *  divide).  Other exponents stay not-ok (the queued extended decoder).
  */
 __device__ __forceinline__ Num parse_num(const uint4* lds, uint32_t a) {
 #if defined(__clang__)
@@ -225,7 +231,7 @@ __device__ __forceinline__ Num parse_num(const uint4* lds, uint32_t a) {
   const uint32_t fa = a + s + k + 1u;
   const uint3 f = ext12(lds, fa);
   const Run8 fr = digit_run8(f.x, f.y, f.z & 0xFFu);
-  const uint32_t nf = fr.k;
+  uint32_t nf = fr.k;
   o.ok_float = (k <= 7) & (dot ? ((nf <= 7) & ((k | nf) != 0)) : k != 0);
   o.ok_uint = (s == 0) & !dot & (k != 0) & !((k == 8) & (ir.term - '0' < 10u));
   o.term = dot ? fr.term : ir.term;
@@ -237,9 +243,47 @@ __device__ __forceinline__ Num parse_num(const uint4* lds, uint32_t a) {
   const float ff = static_cast<float>(fr.val);
   const float q0 = ff * inv;
   const float rem = __builtin_fmaf(-q0, p, ff);
-  const float frac = __builtin_fmaf(rem, inv, q0);
+  float frac = __builtin_fmaf(rem, inv, q0);
   float v = static_cast<float>(ir.val);
-  v = dot ? v + frac : v;
+  const bool longf = dot & (nf == 8u);
+  // one wave-uniform test for both extensions: plain numbers pay only this
+  if (__any(longf | (o.term == 'e') | (o.term == 'E'))) {
+    if (__any(longf)) {
+      // 8 fraction digits read: up to 8 more from the window after them
+      const uint3 f2 = ext12(lds, fa + 8u);
+      const Run8 r2 = digit_run8(f2.x, f2.y, f2.z & 0xFFu);
+      if (longf) {
+        nf = 8u + r2.k;
+        const uint64_t fv = static_cast<uint64_t>(fr.val) * pow10_u(r2.k) + r2.val;
+        frac = static_cast<float>(static_cast<double>(fv) /
+                                  (1e8 * static_cast<double>(pow10_u(r2.k))));
+        o.ok_float = (k <= 7) & (nf < 16u);
+        o.term = r2.term;
+        o.end = fa + nf;
+      }
+    }
+    v = dot ? v + frac : v;
+    const bool has_e = (o.term == 'e') | (o.term == 'E');
+    if (__any(has_e & o.ok_float)) {
+      const uint3 e = ext12(lds, o.end + 1u);
+      const uint32_t cs = e.x & 0xFFu;
+      const bool eneg = cs == '-';
+      const uint32_t es = (cs == '-' || cs == '+') ? 1u : 0u;
+      const Run8 er = digit_run8(__builtin_amdgcn_alignbyte(e.y, e.x, es),
+                                 __builtin_amdgcn_alignbyte(e.z, e.y, es), 0u);
+      const uint32_t ex = er.val;
+      if (has_e) {
+        const float scale = ex <= 7u ? static_cast<float>(pow10_u(ex))
+                                     : (ex == 8u ? 1e8f : (ex == 9u ? 1e9f : 1e10f));
+        o.ok_float = o.ok_float & (er.k < 4u) & (ex <= 10u);
+        o.end = o.end + 1u + es + er.k;
+        o.term = er.term;
+        v = eneg ? (v / scale) : (v * scale);
+      }
+    }
+  } else {
+    v = dot ? v + frac : v;
+  }
   o.fval = neg ? -v : v;
   return o;
 }
