@@ -244,45 +244,40 @@ __device__ __forceinline__ Num parse_num(const uint4* lds, uint32_t a) {
   const float q0 = ff * inv;
   const float rem = __builtin_fmaf(-q0, p, ff);
   float frac = __builtin_fmaf(rem, inv, q0);
-  float v = static_cast<float>(ir.val);
   const bool longf = dot & (nf == 8u);
-  // one wave-uniform test for both extensions: plain numbers pay only this
-  if (__any(longf | (o.term == 'e') | (o.term == 'E'))) {
-    if (__any(longf)) {
-      // 8 fraction digits read: up to 8 more from the window after them
-      const uint3 f2 = ext12(lds, fa + 8u);
-      const Run8 r2 = digit_run8(f2.x, f2.y, f2.z & 0xFFu);
-      if (longf) {
-        nf = 8u + r2.k;
-        const uint64_t fv = static_cast<uint64_t>(fr.val) * pow10_u(r2.k) + r2.val;
-        frac = static_cast<float>(static_cast<double>(fv) /
-                                  (1e8 * static_cast<double>(pow10_u(r2.k))));
-        o.ok_float = (k <= 7) & (nf < 16u);
-        o.term = r2.term;
-        o.end = fa + nf;
-      }
+  if (__any(longf)) {
+    // 8 fraction digits read: up to 8 more from the window after them
+    const uint3 f2 = ext12(lds, fa + 8u);
+    const Run8 r2 = digit_run8(f2.x, f2.y, f2.z & 0xFFu);
+    if (longf) {
+      nf = 8u + r2.k;
+      const uint64_t fv = static_cast<uint64_t>(fr.val) * pow10_u(r2.k) + r2.val;
+      frac = static_cast<float>(static_cast<double>(fv) /
+                                (1e8 * static_cast<double>(pow10_u(r2.k))));
+      o.ok_float = (k <= 7) & (nf < 16u);
+      o.term = r2.term;
+      o.end = fa + nf;
     }
-    v = dot ? v + frac : v;
-    const bool has_e = (o.term == 'e') | (o.term == 'E');
-    if (__any(has_e & o.ok_float)) {
-      const uint3 e = ext12(lds, o.end + 1u);
-      const uint32_t cs = e.x & 0xFFu;
-      const bool eneg = cs == '-';
-      const uint32_t es = (cs == '-' || cs == '+') ? 1u : 0u;
-      const Run8 er = digit_run8(__builtin_amdgcn_alignbyte(e.y, e.x, es),
-                                 __builtin_amdgcn_alignbyte(e.z, e.y, es), 0u);
-      const uint32_t ex = er.val;
-      if (has_e) {
-        const float scale = ex <= 7u ? static_cast<float>(pow10_u(ex))
-                                     : (ex == 8u ? 1e8f : (ex == 9u ? 1e9f : 1e10f));
-        o.ok_float = o.ok_float & (er.k < 4u) & (ex <= 10u);
-        o.end = o.end + 1u + es + er.k;
-        o.term = er.term;
-        v = eneg ? (v / scale) : (v * scale);
-      }
+  }
+  float v = static_cast<float>(ir.val);
+  v = dot ? v + frac : v;
+  const bool has_e = (o.term == 'e') | (o.term == 'E');
+  if (__any(has_e & o.ok_float)) {
+    const uint3 e = ext12(lds, o.end + 1u);
+    const uint32_t cs = e.x & 0xFFu;
+    const bool eneg = cs == '-';
+    const uint32_t es = (cs == '-' || cs == '+') ? 1u : 0u;
+    const Run8 er = digit_run8(__builtin_amdgcn_alignbyte(e.y, e.x, es),
+                               __builtin_amdgcn_alignbyte(e.z, e.y, es), 0u);
+    const uint32_t ex = er.val;
+    if (has_e) {
+      const float scale = ex <= 7u ? static_cast<float>(pow10_u(ex))
+                                   : (ex == 8u ? 1e8f : (ex == 9u ? 1e9f : 1e10f));
+      o.ok_float = o.ok_float & (er.k < 4u) & (ex <= 10u);
+      o.end = o.end + 1u + es + er.k;
+      o.term = er.term;
+      v = eneg ? (v / scale) : (v * scale);
     }
-  } else {
-    v = dot ? v + frac : v;
   }
   o.fval = neg ? -v : v;
   return o;
