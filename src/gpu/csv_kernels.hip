@@ -37,6 +37,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <type_traits>
 
 #include "../data/strtonum.h"
 #include "./device_common.h"
@@ -87,6 +88,17 @@ __device__ __forceinline__ uint32_t mask16(uint32_t h0, uint32_t h1, uint32_t h2
     return (m | (m >> 14)) & 0xFu;            // b2 -> bit 2, b3 -> bit 3
   };
   return m4(h0) | (m4(h1) << 4) | (m4(h2) << 8) | (m4(h3) << 12);
+}
+
+/*! \brief mask16 by byte dot products: v_dot4_u32_u8 of each word's flag
+ *  bytes (0x80 or 0) with the bit weights, two words per accumulator -- six
+ *  VALU where the shift-or gather takes about twenty */
+__device__ __forceinline__ uint32_t mask16_dot(uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3) {
+  const uint32_t a0 = __builtin_amdgcn_udot4(h0, 0x08040201u, 0u, false);
+  const uint32_t a = __builtin_amdgcn_udot4(h1, 0x80402010u, a0, false);
+  const uint32_t b0 = __builtin_amdgcn_udot4(h2, 0x08040201u, 0u, false);
+  const uint32_t b = __builtin_amdgcn_udot4(h3, 0x80402010u, b0, false);
+  return (a >> 7) | (b << 1);  // b = 128 x (bits 8..15): << 1 puts them at 8
 }
 
 /*! \brief the byte classes of a 16-byte slice the CSV walk needs: eol (\\n,
@@ -148,6 +160,9 @@ __device__ __forceinline__ bool excluded(uint32_t col, const CsvCfg& cfg) {
 constexpr int kExclNone = 0;  // no label / weight column
 constexpr int kExclRows = 1;  // label / weight only in column 0: counted per row
 constexpr int kExclCols = 2;  // columns needed (per-field column numbers)
+// the fill's walk when only column 0 can be excluded: the column scan for the
+// listing, the excluded fields counted per row start (no per-field loop)
+constexpr int kExclRowsCols = 3;
 
 __device__ __forceinline__ void col_scan(const CsvCfg& cfg, bool count, int lane, Walk* w,
                                          Slice* o, uint32_t* nx);
@@ -230,7 +245,10 @@ __device__ __forceinline__ Slice step_slice(uint4 g, uint32_t s, uint32_t nrem, 
     nx = static_cast<uint32_t>(__popc(lm)) * static_cast<uint32_t>(cfg.zero_excl);
     o.col0 = 0;
   } else {
-    col_scan(cfg, true, lane, w, &o, &nx);
+    col_scan(cfg, excl_mode == kExclCols, lane, w, &o, &nx);
+    if (excl_mode == kExclRowsCols) {
+      nx = static_cast<uint32_t>(__popc(lm)) * static_cast<uint32_t>(cfg.zero_excl);
+    }
   }
   // fields / rows (<= 1024 each per step: 16-bit halves) and excluded
   // columns: two DPP scans, repacked to the 21-bit layout of f21
@@ -353,40 +371,50 @@ __global__ __launch_bounds__(kThreads) void k_csv_tile_count_pos(const uint8_t* 
   const uint32_t delim4 = cfg.delim * 0x01010101u;
   uint32_t rows = 0, fields = 0, ctl_any = 0;
   const bool full = tile0 + kTileBytes <= n;  // (else the bytes past n are no text)
+  // full tiles (every tile but a chunk's last): no NUL-past-the-end test (a NUL
+  // inside the text is a control byte: the chunk goes to the exact kernels)
+  auto walk = [&](auto fullc) {
 #pragma unroll
-  for (int j = 0; j < kLoads; ++j) {
-    const uint32_t w4[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
-    uint32_t he[4], hd[4], hc[4];
+    for (int j = 0; j < kLoads; ++j) {
+      const uint32_t w4[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+      uint32_t he[4], hd[4], hc[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      // line ends, and the zeros past the chunk (no field starts there)
-      const uint32_t nl = hb_eq(w4[k], 0x0A0A0A0Au), cr = hb_eq(w4[k], 0x0D0D0D0Du);
-      he[k] = nl | cr | hb_eq(w4[k], 0u);
-      hd[k] = hb_eq(w4[k], delim4);
-      // control bytes other than \t \n \r (NUL included): text to the
-      // reference, so the chunk goes to the exact kernels (the fill's check,
-      // made here once for the whole tile)
-      hc[k] = hb_lt20(w4[k]) & ~(hb_eq(w4[k], 0x09090909u) | nl | cr);
+      for (int k = 0; k < 4; ++k) {
+        // line ends, and the zeros past the chunk (no field starts there)
+        const uint32_t nl = hb_eq(w4[k], 0x0A0A0A0Au), cr = hb_eq(w4[k], 0x0D0D0D0Du);
+        he[k] = decltype(fullc)::value ? (nl | cr) : (nl | cr | hb_eq(w4[k], 0u));
+        hd[k] = hb_eq(w4[k], delim4);
+        // control bytes other than \t \n \r (NUL included): text to the
+        // reference, so the chunk goes to the exact kernels (the fill's check,
+        // made here once for the whole tile)
+        hc[k] = hb_lt20(w4[k]) & ~(hb_eq(w4[k], 0x09090909u) | nl | cr);
+      }
+      const uint32_t e = mask16_dot(he[0], he[1], he[2], he[3]);
+      const uint32_t d = mask16_dot(hd[0], hd[1], hd[2], hd[3]);
+      uint32_t c = hc[0] | hc[1] | hc[2] | hc[3];
+      if (!decltype(fullc)::value) {  // only the chunk's last tile
+        const size_t p = tile0 + j * 1024 + 16u * lane;
+        c = p >= n ? 0u
+                   : (n - p >= 16 ? c : mask16_dot(hc[0], hc[1], hc[2], hc[3]) & ((1u << (n - p)) - 1u));
+      }
+      ctl_any |= c;
+      masks[(tile * kLoads + j) * kWave + lane] = e | (d << 16);
+      const uint32_t last_e = (e >> 15) & 1u, last_d = (d >> 15) & 1u;
+      // the byte before each lane's 16: lane - 1's last, lane 0 the previous load's lane 63
+      const uint32_t up_e = lane_shr1(last_e), up_d = lane_shr1(last_d);
+      const uint32_t le = lane == 0 ? pe : up_e, ld = lane == 0 ? pd : up_d;
+      pe = lane63(last_e);
+      pd = lane63(last_d);
+      const uint32_t lm = ~e & ((e << 1) | le) & 0xFFFFu;
+      const uint32_t fm = lm | (((d << 1) | ld) & ~e & 0xFFFFu);
+      rows += static_cast<uint32_t>(__popc(lm));
+      fields += static_cast<uint32_t>(__popc(fm));
     }
-    const uint32_t e = mask16(he[0], he[1], he[2], he[3]);
-    const uint32_t d = mask16(hd[0], hd[1], hd[2], hd[3]);
-    uint32_t c = hc[0] | hc[1] | hc[2] | hc[3];
-    if (!full) {  // wave-uniform: only the chunk's last tile
-      const size_t p = tile0 + j * 1024 + 16u * lane;
-      c = p >= n ? 0u : (n - p >= 16 ? c : mask16(hc[0], hc[1], hc[2], hc[3]) & ((1u << (n - p)) - 1u));
-    }
-    ctl_any |= c;
-    masks[(tile * kLoads + j) * kWave + lane] = e | (d << 16);
-    const uint32_t last_e = (e >> 15) & 1u, last_d = (d >> 15) & 1u;
-    // the byte before each lane's 16: lane - 1's last, lane 0 the previous load's lane 63
-    const uint32_t up_e = lane_shr1(last_e), up_d = lane_shr1(last_d);
-    const uint32_t le = lane == 0 ? pe : up_e, ld = lane == 0 ? pd : up_d;
-    pe = lane63(last_e);
-    pd = lane63(last_d);
-    const uint32_t lm = ~e & ((e << 1) | le) & 0xFFFFu;
-    const uint32_t fm = lm | (((d << 1) | ld) & ~e & 0xFFFFu);
-    rows += static_cast<uint32_t>(__popc(lm));
-    fields += static_cast<uint32_t>(__popc(fm));
+  };
+  if (full) {
+    walk(std::true_type{});
+  } else {
+    walk(std::false_type{});
   }
   const uint64_t c = wave_sum_2x32((static_cast<uint64_t>(rows) << 32) | fields);
   const bool any_ctl = __any(ctl_any != 0);
@@ -460,6 +488,7 @@ __attribute__((amdgpu_waves_per_eu(6))) void k_csv_tile_fill(const uint8_t* __re
     w.carry_delim = c == cfg.delim ? 1u : 0u;
   }
   const uint32_t delim = cfg.delim;
+  const int fill_excl = (cfg.label_col > 0 || cfg.weight_col > 0) ? kExclCols : kExclRowsCols;
   uint64_t mx = 0;
   bool irregular = false, any_value = false;
   // slot 0 <- step 0 (+ mirror of its head past slot 1).  Step s + 1 is staged
@@ -509,7 +538,7 @@ __attribute__((amdgpu_waves_per_eu(6))) void k_csv_tile_fill(const uint8_t* __re
       mk = __builtin_amdgcn_raw_buffer_load_b32(mrs, static_cast<uint32_t>(lane) * 4,
                                                 (s + 1) * kWave * 4, 0);
     }
-    const Slice sl = step_slice(ring[slot + lane], s, nrem, cfg, kExclCols, &w, lane,
+    const Slice sl = step_slice(ring[slot + lane], s, nrem, cfg, fill_excl, &w, lane,
                                 pub ? &mk_s : nullptr);
     // list the lane's fields: x = ring byte | row in tile << 16, y = column | entry in tile << 16
     {
