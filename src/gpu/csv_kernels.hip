@@ -239,7 +239,7 @@ __device__ __forceinline__ Slice step_slice(uint4 g, uint32_t s, uint32_t nrem, 
   o.fm = fm;
   o.lm = lm;
   uint32_t nx = 0;  // excluded columns among the lane's fields
-  if (excl_mode != kExclCols) {
+  if (excl_mode == kExclNone || excl_mode == kExclRows) {
     // label / weight only in column 0 (or none): one excluded field per row,
     // no columns needed (the count pass of the common `label_column=0`)
     nx = static_cast<uint32_t>(__popc(lm)) * static_cast<uint32_t>(cfg.zero_excl);
@@ -489,7 +489,10 @@ __attribute__((amdgpu_waves_per_eu(6))) void k_csv_tile_fill(const uint8_t* __re
   }
   const uint32_t delim = cfg.delim;
   const int fill_excl = (cfg.label_col > 0 || cfg.weight_col > 0) ? kExclCols : kExclRowsCols;
-  uint64_t mx = 0;
+  uint32_t mx = 0;  // the largest column index (< 2^16)
+  // a field's "last in its row" matters only for short rows with a label /
+  // weight column after it (wave-uniform: skipped for label_column <= 0)
+  const bool need_last = cfg.label_col > 0 || cfg.has_weight;
   bool irregular = false, any_value = false;
   // slot 0 <- step 0 (+ mirror of its head past slot 1).  Step s + 1 is staged
   // during step s from `pv`, which was loaded during step s - 1 (the load
@@ -591,12 +594,12 @@ __attribute__((amdgpu_waves_per_eu(6))) void k_csv_tile_fill(const uint8_t* __re
           last = eol_c(rb[off + 8]);
         } else if (c0 == delim || eol_c(c0)) {
           v = 0.0f;  // empty field
-          last = c0 != delim || eol_c(rb[off + 1]);
+          last = need_last && (c0 != delim || eol_c(rb[off + 1]));
         } else {
           // the 8-digit run decoder of the LibSVM fill (token_decode.h)
           const tok::Num x = tok::parse_num(ring, off);
           const bool t_eol = eol_c(x.term);
-          const bool last_fast = t_eol || eol_c(rb[x.end + 1]);
+          const bool last_fast = need_last && (t_eol || eol_c(rb[x.end + 1]));
           if (x.ok_float && (x.term == delim || t_eol)) {
             v = x.fval;
             last = last_fast;
