@@ -57,9 +57,11 @@ constexpr unsigned kOffBits = 13;                            // tile offset < 81
 constexpr unsigned kMaxTileTokens = static_cast<unsigned>(kTileBytes / 2);
 static_assert(kTileBytes == 8192, "entry packing assumes 8 KiB tiles");
 
-/*! \brief the high bit of each byte of z (z & 0x80808080) as a 4-bit mask */
+/*! \brief the high bit of each byte of z (z & 0x80808080) as a 4-bit mask:
+ *  one byte dot product (v_dot4_u32_u8, full rate), not the quarter-rate
+ *  v_mul_lo_u32 of the multiply-gather */
 __device__ __forceinline__ uint32_t gather_hi(uint32_t z) {
-  return (((z >> 7) & 0x01010101u) * 0x01020408u) >> 24;
+  return __builtin_amdgcn_udot4(z, 0x08040201u, 0u, false) >> 7;
 }
 
 /*!
