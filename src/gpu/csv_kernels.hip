@@ -444,8 +444,12 @@ __device__ __noinline__ GenericField generic_field(const char* q, const char* en
   return r;
 }
 
-// 6 waves per SIMD (the LDS allows 6 workgroups per CU): <= 84 VGPRs
-template <typename IndexType>
+// 6 waves per SIMD (the LDS allows 6 workgroups per CU): <= 84 VGPRs.
+// kCol0: the common configuration compiled on its own -- positional counts
+// (label column 0 or none), no weight column, no pricing experiments: the
+// round loop loses the weight / short-row / experiment branches and the
+// scalar registers they held (the general kernel sits at the SGPR limit)
+template <typename IndexType, bool kCol0>
 __global__ __launch_bounds__(kThreads)
 __attribute__((amdgpu_waves_per_eu(6))) void k_csv_tile_fill(const uint8_t* __restrict__ text,
                                                             size_t n, size_t ntiles, CsvCfg cfg,
@@ -453,7 +457,8 @@ __attribute__((amdgpu_waves_per_eu(6))) void k_csv_tile_fill(const uint8_t* __re
                                                             const uint32_t* __restrict__ masks,
                                                             FillTarget<IndexType> out,
                                                             MetaPartial* __restrict__ partials,
-                                                            uint32_t exp) {
+                                                            uint32_t exp_arg) {
+  const uint32_t exp = kCol0 ? 0u : exp_arg;
   __shared__ uint4 s_ring[kWaves][kRingVecs];
   __shared__ uint2 s_list[kWaves][kListCap];
   const int lane = lane_id();
@@ -488,11 +493,15 @@ __attribute__((amdgpu_waves_per_eu(6))) void k_csv_tile_fill(const uint8_t* __re
     w.carry_delim = c == cfg.delim ? 1u : 0u;
   }
   const uint32_t delim = cfg.delim;
-  const int fill_excl = (cfg.label_col > 0 || cfg.weight_col > 0) ? kExclCols : kExclRowsCols;
+  const int fill_excl =
+      (!kCol0 && (cfg.label_col > 0 || cfg.weight_col > 0)) ? kExclCols : kExclRowsCols;
+  // kCol0: only a label in column 0 is excluded
+  const bool zl = cfg.label_col == 0;
+  auto excl_col = [&](uint32_t col) { return kCol0 ? (zl && col == 0) : excluded(col, cfg); };
   uint32_t mx = 0;  // the largest column index (< 2^16)
   // a field's "last in its row" matters only for short rows with a label /
   // weight column after it (wave-uniform: skipped for label_column <= 0)
-  const bool need_last = cfg.label_col > 0 || cfg.has_weight;
+  const bool need_last = !kCol0 && (cfg.label_col > 0 || cfg.has_weight);
   bool irregular = false, any_value = false;
   // slot 0 <- step 0 (+ mirror of its head past slot 1).  Step s + 1 is staged
   // during step s from `pv`, which was loaded during step s - 1 (the load
@@ -508,7 +517,7 @@ __attribute__((amdgpu_waves_per_eu(6))) void k_csv_tile_fill(const uint8_t* __re
   // S1p published the line-end / delimiter masks of every 16 bytes: the walk
   // takes them instead of classifying the bytes again (buffer loads: steps
   // past the chunk's last tile read zeros)
-  const bool pub = cfg.pos != 0;
+  const bool pub = kCol0 || cfg.pos != 0;
   __amdgpu_buffer_rsrc_t mrs;
   uint32_t mk = 0;
   if (pub) {
@@ -560,7 +569,7 @@ __attribute__((amdgpu_waves_per_eu(6))) void k_csv_tile_fill(const uint8_t* __re
                                 col | (ent << 16));
         }
         ++at;
-        ent += excluded(col, cfg) ? 0u : 1u;
+        ent += excl_col(col) ? 0u : 1u;
         ++col;
       }
     }
@@ -614,7 +623,7 @@ __attribute__((amdgpu_waves_per_eu(6))) void k_csv_tile_fill(const uint8_t* __re
         }
         // S1p: the prefix counts entries by position; the tile's own start
         // after the rest of the previous tile's last row (e: entry in the tile)
-        const uint32_t e = ent + (cfg.pos ? w.pre : 0u);
+        const uint32_t e = ent + (pub ? w.pre : 0u);
         if (exp & 2u) {  // pricing: no stores (a value sink the compiler keeps)
           mx = __float_as_uint(v) == 0x7FC00001u ? mx + 1 : mx;
         } else if (static_cast<int32_t>(row_t) >= row_room) {
@@ -622,12 +631,16 @@ __attribute__((amdgpu_waves_per_eu(6))) void k_csv_tile_fill(const uint8_t* __re
         } else {
           if (static_cast<int>(col) == cfg.label_col) {
             lab_at[row_t] = v;
-          } else if (static_cast<int>(col) == cfg.weight_col) {
+          } else if (!kCol0 && static_cast<int>(col) == cfg.weight_col) {
             wgt_at[row_t] = v;
           } else if (static_cast<int32_t>(e) < nnz_room) {
             uint32_t idx = col;
-            idx -= (cfg.label_col >= 0 && col > static_cast<uint32_t>(cfg.label_col)) ? 1u : 0u;
-            idx -= (cfg.weight_col >= 0 && col > static_cast<uint32_t>(cfg.weight_col)) ? 1u : 0u;
+            if (kCol0) {
+              idx -= zl ? 1u : 0u;  // col > 0 here when the label takes column 0
+            } else {
+              idx -= (cfg.label_col >= 0 && col > static_cast<uint32_t>(cfg.label_col)) ? 1u : 0u;
+              idx -= (cfg.weight_col >= 0 && col > static_cast<uint32_t>(cfg.weight_col)) ? 1u : 0u;
+            }
             idx_at[e] = static_cast<IndexType>(idx);
             val_at[e] = v;
             mx = idx > mx ? idx : mx;
@@ -639,7 +652,7 @@ __attribute__((amdgpu_waves_per_eu(6))) void k_csv_tile_fill(const uint8_t* __re
             off_at[row_t] = C + e;
             if (cfg.label_col < 0) lab_at[row_t] = 0.0f;
           }
-          if (last) {
+          if (!kCol0 && last) {
             // a short row: no label / weight field
             if (cfg.label_col >= 0 && col < static_cast<uint32_t>(cfg.label_col)) lab_at[row_t] = 0.0f;
             if (cfg.has_weight && (cfg.weight_col < 0 || col < static_cast<uint32_t>(cfg.weight_col))) {
@@ -658,7 +671,7 @@ __attribute__((amdgpu_waves_per_eu(6))) void k_csv_tile_fill(const uint8_t* __re
   unsigned fl = 0;
   if (irregular || w.bad) fl |= kFlagIrregular;
   if (any_value) fl |= kFlagValue;
-  if (cfg.has_weight) fl |= kFlagWeight;
+  if (!kCol0 && cfg.has_weight) fl |= kFlagWeight;
   const unsigned long long m = wave_max(static_cast<unsigned long long>(mx));
   fl = wave_or(fl);
   if (lane == 0) {
@@ -721,10 +734,16 @@ void LaunchCsvTileFill(const char* text, size_t nbytes, int label_column, int we
     const char* v = std::getenv("DMLC_CSV_EXP");
     return v != nullptr ? static_cast<uint32_t>(std::atoi(v)) : 0u;
   }();
-  hipLaunchKernelGGL((k_csv_tile_fill<IndexType>), dim3((ntiles + kWaves - 1) / kWaves),
-                     dim3(kThreads), 0, stream, reinterpret_cast<const uint8_t*>(text), nbytes,
-                     ntiles, MakeCfg(label_column, weight_column, delimiter), tile_prefix,
-                     tile_masks, out, partials, exp);
+  const CsvCfg cfg = MakeCfg(label_column, weight_column, delimiter);
+  const dim3 grid((ntiles + kWaves - 1) / kWaves);
+  const uint8_t* t = reinterpret_cast<const uint8_t*>(text);
+  if (cfg.pos && !cfg.has_weight && exp == 0) {
+    hipLaunchKernelGGL((k_csv_tile_fill<IndexType, true>), grid, dim3(kThreads), 0, stream, t, nbytes,
+                       ntiles, cfg, tile_prefix, tile_masks, out, partials, 0u);
+  } else {
+    hipLaunchKernelGGL((k_csv_tile_fill<IndexType, false>), grid, dim3(kThreads), 0, stream, t,
+                       nbytes, ntiles, cfg, tile_prefix, tile_masks, out, partials, exp);
+  }
 }
 
 template void LaunchCsvTileFill<uint32_t>(const char*, size_t, int, int, char, const uint64_t*,
