@@ -918,7 +918,11 @@ __device__ __forceinline__ uint32_t fill_exp(const FillPass& op) {
 #endif
 }
 
-template <TextFormat F, typename IndexType, bool kOnePass>
+// kLean: a target without qid / weight columns (the common case) compiled on
+// its own -- no qid pass, no weight stores, one flag for "weights seen": the
+// scalar registers those held are what the kernel spilled to VGPR lanes (it
+// sits at the SGPR limit)
+template <TextFormat F, typename IndexType, bool kOnePass, bool kLean = false>
 __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
     const uint8_t* __restrict__ text, size_t n, size_t ntiles, const uint64_t* __restrict__ prefix,
     FillTarget<IndexType> out, MetaPartial* __restrict__ partials, FillPass op) {
@@ -1042,11 +1046,11 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
   IndexType* const fld_at = out.field != nullptr ? out.field + C : nullptr;
   float* const lab_at = out.label + R - 1;
   uint64_t* const off_at = out.offset + R - 1;
-  float* const wgt_at = out.weight != nullptr ? out.weight + R - 1 : nullptr;
-  uint64_t* const qid_at = out.qid != nullptr ? out.qid + R - 1 : nullptr;
+  float* const wgt_at = !kLean && out.weight != nullptr ? out.weight + R - 1 : nullptr;
+  uint64_t* const qid_at = !kLean && out.qid != nullptr ? out.qid + R - 1 : nullptr;
   // the count pass saw 'q' token starts in this chunk (the host then enables
   // the qid column): only such chunks look for `qid:` tokens
-  const bool qid_chunk = F == TextFormat::kLibSVM && out.qid != nullptr;
+  const bool qid_chunk = !kLean && F == TextFormat::kLibSVM && out.qid != nullptr;
 
   uint32_t tok0 = 0;   // tile token ordinal of list position 0
   uint32_t lcnt = 0;   // line starts of this tile so far
@@ -1206,7 +1210,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
         if (wgt_at != nullptr) wgt_at[lc] = t.r == 2 ? t.f1 : 1.0f;
         // (qid: zero-filled by the host, the qid token's lane writes it)
       }
-      need_w |= active & is_label & (wgt_at == nullptr) & (t.r == 2);
+      if constexpr (!kLean) need_w |= active & is_label & (wgt_at == nullptr) & (t.r == 2);
       any_weight |= active & is_label & (t.r == 2);
       const bool feat = active & !is_label & nnz_ok & field_ok;
       const uint64_t u0 = (static_cast<uint64_t>(t.u0_hi) << 32) | t.u0;
@@ -1351,7 +1355,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_fill(
   if (any_weight) fl |= kFlagWeight;
   if (irregular) fl |= kFlagIrregular;
   if (neg) fl |= kFlagNegIndex;
-  if (need_w) fl |= kFlagNeedWeight;
+  if (kLean ? any_weight : need_w) fl |= kFlagNeedWeight;  // (lean: no weight column)
   if (over) fl |= kFlagOverflow;
   if (F == TextFormat::kLibFM) fl |= kFlagField;
   const unsigned long long mi = dev::wave_max(static_cast<unsigned long long>(mx_index));
@@ -2004,19 +2008,25 @@ size_t LaunchTileFill(const char* text, size_t nbytes, TextFormat format,
   }
   if (ntiles != 0) {
     const dim3 grid(static_cast<unsigned>(groups));
-#define DMLC_TILE_FILL(FMT, ONE)                                                                \
-  hipLaunchKernelGGL((k_tile_fill<FMT, IndexType, ONE>), grid, dim3(kThreads), 0, stream, t, nbytes, \
-                     ntiles, tile_prefix, out, partials, op)
+#define DMLC_TILE_FILL(FMT, ONE, LEAN)                                                       \
+  hipLaunchKernelGGL((k_tile_fill<FMT, IndexType, ONE, LEAN>), grid, dim3(kThreads), 0, stream, t, \
+                     nbytes, ntiles, tile_prefix, out, partials, op)
+    // counted path without qid / weight columns: the lean instantiation
+    const bool lean = one_pass == nullptr && out.qid == nullptr && out.weight == nullptr;
     if (format == TextFormat::kLibFM) {
       if (one_pass != nullptr) {
-        DMLC_TILE_FILL(TextFormat::kLibFM, true);
+        DMLC_TILE_FILL(TextFormat::kLibFM, true, false);
+      } else if (lean) {
+        DMLC_TILE_FILL(TextFormat::kLibFM, false, true);
       } else {
-        DMLC_TILE_FILL(TextFormat::kLibFM, false);
+        DMLC_TILE_FILL(TextFormat::kLibFM, false, false);
       }
     } else if (one_pass != nullptr) {
-      DMLC_TILE_FILL(TextFormat::kLibSVM, true);
+      DMLC_TILE_FILL(TextFormat::kLibSVM, true, false);
+    } else if (lean) {
+      DMLC_TILE_FILL(TextFormat::kLibSVM, false, true);
     } else {
-      DMLC_TILE_FILL(TextFormat::kLibSVM, false);
+      DMLC_TILE_FILL(TextFormat::kLibSVM, false, false);
     }
 #undef DMLC_TILE_FILL
   }
