@@ -1519,6 +1519,7 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
   bool irregular = false, neg = false, over = false;
   if (own != 0) {
     const uint64_t R = out.row_base + line_base;  // global row of tile line ordinal 1
+    float* const lab_at = out.label + R - 1;      // labels by tile line ordinal
     const bool pow2 = (dim & (dim - 1)) == 0;
     const uint32_t dmask = static_cast<uint32_t>(dim - 1);
     for (int c = lane * 4; c < dim; c += dev::kWave * 4) {
@@ -1730,7 +1731,8 @@ __global__ __launch_bounds__(kThreads, DMLC_FILL_WAVES) void k_tile_hash(
             bad = gr.bad;
             irregular |= !num_start(text[gpos]);  // qid:, comments, junk: the exact kernels
           }
-          if (active & is_label && R + lc - 1 < row_cap) out.label[R + lc - 1] = t.f0;
+          // (counted path: C2 sized the target, no row check)
+          if (active & is_label && (!kOnePass || R + lc - 1 < row_cap)) lab_at[lc] = t.f0;
           bool feat = active & !is_label;
           uint64_t key;
           float val;
