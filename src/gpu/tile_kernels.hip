@@ -160,8 +160,9 @@ __device__ __forceinline__ uint32_t prev_byte(const uint8_t* __restrict__ text, 
 
 /*!
  * \brief C1 lane step: line / token starts of 16 bytes as per-byte high-bit
- *  masks (bit 7 of byte j), popcounted without gathering, plus the irregular
- *  checks of lane_masks<true>.  pc: the byte before the 16.
+ *  masks (bit 7 of byte j), gathered into 16-bit masks by byte dot products
+ *  and popcounted once per 16 bytes, plus the irregular checks of
+ *  lane_masks<true>.  pc: the byte before the 16.
  */
 template <bool kFull>
 __device__ __forceinline__ bool count16(uint4 v, uint32_t pc, size_t pos, size_t n,
@@ -179,6 +180,7 @@ __device__ __forceinline__ bool count16(uint4 v, uint32_t pc, size_t pos, size_t
   uint32_t prev_sep = (pc <= 0x20u) ? 0x80u : 0u;  // sep bit of the byte before, at bit 7
   uint32_t prev_eol = (pc == '\n' || pc == '\r') ? 0x80u : 0u;
   bool bad = false;
+  uint32_t blank = 0;  // line starts that are no token starts (a line starting with a blank)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const uint32_t x = w[i];
@@ -199,13 +201,14 @@ __device__ __forceinline__ bool count16(uint4 v, uint32_t pc, size_t pos, size_t
     // have it clear) are no entries of the CSR: LibSVM `qid:` tokens, which
     // the fill decodes beside its list, or junk that sends the chunk to the
     // exact kernels.  Bit 6 of each byte, moved to bit 7: x << 1.
-    *toks += __popc(tm);
     *qtoks += __popc(tm & (x << 1));
-    *lines += __popc(lm);
+    // the starts gathered into the 16-bit masks by byte dot products (0x80 =
+    // 128 x the weight, two words per accumulator); the token / line counts
+    // are their popcounts, once per 16 bytes
     const uint32_t wgt = (i & 1) ? 0x80402010u : 0x08040201u;
     acc_t[i >> 1] = __builtin_amdgcn_udot4(tm, wgt, acc_t[i >> 1], false);
     acc_l[i >> 1] = __builtin_amdgcn_udot4(lm, wgt, acc_l[i >> 1], false);
-    bad |= (lm & ~tm) != 0;  // a line that starts with a blank
+    blank |= lm & ~tm;
     // (token starts outside [0-9+-.] are flagged by the fill / hash kernels:
     // such a token never passes the register-window decoder, so the check
     // costs nothing on the fast path -- here it was ~40% of the count's VALU)
@@ -220,9 +223,12 @@ __device__ __forceinline__ bool count16(uint4 v, uint32_t pc, size_t pos, size_t
     prev_sep = (sep >> 24) & 0x80u;
     prev_eol = (eol >> 24) & 0x80u;
   }
-  if (packed != nullptr) {
-    *packed = (acc_t[0] >> 7) | (acc_t[1] << 1) | (acc_l[0] << 9) | (acc_l[1] << 17);
-  }
+  const uint32_t pt = (acc_t[0] >> 7) | (acc_t[1] << 1);  // token starts, bit j = byte j
+  const uint32_t pl = (acc_l[0] >> 7) | (acc_l[1] << 1);  // line starts
+  *toks += __popc(pt);
+  *lines += __popc(pl);
+  bad |= blank != 0;
+  if (packed != nullptr) *packed = pt | (pl << 16);
   return bad;
 }
 
