@@ -90,6 +90,22 @@ def test_k9_and_fused_match_independent_hash(dataset, dim, seed):
     assert same.mean() > 0.999
 
 
+@pytest.mark.parametrize("dim", [200, 1024])
+@pytest.mark.parametrize("scale", [0.3, 0.5, 1.0])
+def test_fused_fp8_scales_match_k9(dataset, dim, scale):
+    """the fused kernel's fp8 rows equal K9's for any scale: a power of two
+    is applied per token, any other scale per column at the row flush"""
+    fmt, p, host = dataset
+    _, share = ref_dense(host, dim, 2, fmt == "libfm")
+    csr = data.csr_to_torch(data.GPUParser(p, format=fmt, chunk_bytes=128 * 1024).parse_all())
+    k9 = ops.hashed_dense(csr, dim, seed=2, fp8=True, scale=scale).cpu().view(torch.uint8)
+    f8 = data.GPUParser(p, format=fmt, chunk_bytes=128 * 1024).parse_all_hashed(
+        dim, seed=2, fp8=True, scale=scale, strategy="fused")["x"].cpu().view(torch.uint8)
+    same = (f8 == k9).numpy()
+    assert same[share <= 2].all()  # one or two terms: the f32 sums are exact
+    assert same.mean() > 0.999
+
+
 def test_hashed_fm_on_fused_fp8_batch(dataset):
     fmt, p, _ = dataset
     scale = 0.25
