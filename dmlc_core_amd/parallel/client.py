@@ -170,6 +170,15 @@ class TrackerClient:
         finally:
             ch.close()
 
+    def attempt(self) -> int:
+        """This launch's attempt number for the task id ``jobid`` (0 the
+        first time the tracker hears it, then 1, 2, ...)."""
+        ch = self._connect("attempt")
+        try:
+            return ch.recv_int()
+        finally:
+            ch.close()
+
     def barrier(self, key: str = "default", count: Optional[int] = None) -> None:
         ch = self._connect("barrier")
         try:

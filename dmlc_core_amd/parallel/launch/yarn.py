@@ -6,14 +6,16 @@ The reference submits through its own Java ApplicationMaster
 backend needs no JVM and no jar: the ResourceManager's YARN Services REST API
 (``$YARN_RM_ADDRESS``, Hadoop >= 3.1) runs the containers and the AM's
 per-task policy runs here, in `YarnServiceJob.wait`.  One component per
-  role, one container per task; with ``--gpus-per-node`` every worker container asks for one
-  ``amd.com/gpu`` (one process per GPU) and binds local rank 0.  Each
-  container exports its own ``DMLC_TASK_ID`` / ``DMLC_WORKER_ID`` (or
-  ``DMLC_SERVER_ID``) from the service's ``${COMPONENT_ID}`` and
-  ``DMLC_NODE_HOST``.  `YarnServiceJob.wait` applies the dmlc
-  ApplicationMaster's policy to the containers the service reports
-  (simulated end to end in `tests/yarn_am_sim.py`): a memory-limit kill aborts the job, other failures are
-  retried by YARN up to DMLC_MAX_ATTEMPT, and more than that aborts.
+  role, one container per task; with ``--gpus-per-node`` every worker
+  container asks for one ``amd.com/gpu`` (one process per GPU) and binds
+  local rank 0.  Each container exports its own ``DMLC_TASK_ID`` /
+  ``DMLC_WORKER_ID`` (or ``DMLC_SERVER_ID``) from the service's
+  ``${COMPONENT_ID}``, ``DMLC_NODE_HOST``, and ``DMLC_NUM_ATTEMPT`` (the
+  tracker's launch count of that task id, `dmlc_core_amd.parallel.attempt`).
+  `YarnServiceJob.wait` applies the dmlc ApplicationMaster's policy to the
+  containers the service reports (simulated end to end in
+  `tests/yarn_am_sim.py`): a memory-limit kill aborts the job, other failures
+  are retried by YARN up to DMLC_MAX_ATTEMPT, and more than that aborts.
   The node of every failed container is blacklisted (the service AM is asked
   to with ``yarn.service.node-blacklist.threshold`` = 1, and a task re-placed
   on such a node counts as a failed attempt).
@@ -130,8 +132,13 @@ def service_spec(args, envs: Dict[str, object], name: str,
         # ${COMPONENT_ID} to the instance index (0..n-1) in the launch command;
         # servers follow the workers in task-id space, like the tracker's ranks
         base = 0 if role == "worker" else int(args.num_workers)
+        # a relaunched container (restart_policy ON_FAILURE) keeps its
+        # instance: its attempt number comes from the tracker's launch count
+        # of that task id (dmlc_core_amd.parallel.attempt; 0 without one)
         ident = (f"export DMLC_TASK_ID=$(( ${{COMPONENT_ID}} + {base} )) "
                  f"DMLC_{role.upper()}_ID=${{COMPONENT_ID}} DMLC_NODE_HOST=$(hostname -f); "
+                 "export DMLC_NUM_ATTEMPT=$(python3 -m dmlc_core_amd.parallel.attempt "
+                 "2>/dev/null || echo 0); "
                  + ("export DMLC_LOCAL_RANK=0 LOCAL_RANK=0 LOCAL_WORLD_SIZE=1; " if gpu else ""))
         comps.append({
             "name": role, "number_of_containers": int(n), "launch_command": ident + cmd,

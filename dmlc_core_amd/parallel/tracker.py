@@ -255,6 +255,9 @@ class _JobState:
         self.failed_at = 0.0
         self.dead: Dict[int, bool] = {}
         self.fatal: Optional[BaseException] = None
+        # launches seen per task id (``attempt``): a relaunched container
+        # learns its DMLC_NUM_ATTEMPT here when its launcher cannot say
+        self.attempts: Dict[str, int] = {}
 
 
 class RabitTracker:
@@ -430,6 +433,16 @@ class RabitTracker:
                     st.rccl_waiters.setdefault(key, []).append(w)
                     return
             w.ch.send_bytes(blob)
+            w.ch.close()
+            return
+        if w.cmd == "attempt":
+            # the n-th launch of a task id (0 first): what the reference
+            # ApplicationMaster exports as DMLC_NUM_ATTEMPT per container
+            # (ApplicationMaster.java:446); the YARN services launcher asks here
+            with self._mu:
+                n = st.attempts.get(w.jobid, 0)
+                st.attempts[w.jobid] = n + 1
+            w.ch.send_int(n)
             w.ch.close()
             return
         if w.cmd == "barrier":

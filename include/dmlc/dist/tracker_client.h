@@ -84,6 +84,12 @@ class TrackerClient {
   /*! \brief block until `count` workers (default world size) reached `key` */
   void Barrier(const std::string& key = "default", int count = -1);
   /*!
+   * \brief this launch's attempt number for the task id `jobid`: 0 the first
+   *  time the tracker hears it, then 1, 2, ... (DMLC_NUM_ATTEMPT for
+   *  launchers that relaunch containers on their own)
+   */
+  int Attempt();
+  /*!
    * \brief rank 0 creates the id with make_id() and uploads it; every rank
    *  (rank 0 included) returns the same bytes
    */

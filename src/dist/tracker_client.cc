@@ -275,5 +275,10 @@ void TrackerClient::Barrier(const std::string& key, int count) {
   c->RecvInt();
 }
 
+int TrackerClient::Attempt() {
+  auto c = Connect("attempt");
+  return c->RecvInt();
+}
+
 }  // namespace dist
 }  // namespace dmlc

@@ -1031,6 +1031,7 @@ PYBIND11_MODULE(_dmlc, m) {
              }
              return py::bytes(b);
            })
+      .def("attempt", &TrackerClient::Attempt, py::call_guard<py::gil_scoped_release>())
       .def("barrier", &TrackerClient::Barrier, py::arg("key") = "default",
            py::arg("count") = -1, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("rank", &TrackerClient::rank)

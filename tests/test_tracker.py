@@ -139,6 +139,22 @@ def test_recover_keeps_rank_by_jobid():
     assert out["re"] == out[1]
 
 
+def test_attempt_counts_launches_per_task_id():
+    """``attempt``: the n-th launch of a task id learns n (0 first), per id,
+    and the job's rendezvous is untouched by it"""
+    from dmlc_core_amd import _dmlc
+    t = _start_tracker(1, timeout=60)
+    seen = [TrackerClient("127.0.0.1", t.port, jobid="attempt:worker:3").attempt() for _ in range(2)]
+    # the C++ client's twin of the command
+    seen.append(_dmlc.TrackerClient("127.0.0.1", t.port, "attempt:worker:3", -1, -1, 30.0).attempt())
+    other = TrackerClient("127.0.0.1", t.port, jobid="attempt:worker:4").attempt()
+    c = TrackerClient("127.0.0.1", t.port, jobid="w0")
+    assert c.start().rank == 0
+    c.shutdown()
+    t.join(30)
+    assert seen == [0, 1, 2] and other == 0
+
+
 def test_heartbeat_timeout_fails_the_job():
     t = _start_tracker(2, heartbeat_timeout=1.0, timeout=60)
     c0 = TrackerClient("127.0.0.1", t.port)

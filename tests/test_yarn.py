@@ -167,6 +167,31 @@ def test_service_containers_get_their_own_identity(instance, role):
     assert host
 
 
+def test_service_containers_count_their_attempts(tmp_path):
+    """A relaunched container (same instance) exports DMLC_NUM_ATTEMPT 1, 2,
+    ... from the tracker's launch count of its task id, as the reference AM
+    does per launch; without a tracker the first attempt, 0"""
+    import subprocess
+    from dmlc_core_amd.parallel import tracker as trk
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = yarn.service_spec(_args(), {}, "job")
+    comp = {c["name"]: c for c in spec["components"]}["worker"]
+    cmd = comp["launch_command"].replace("${COMPONENT_ID}", "2")
+    cmd = cmd[:cmd.rindex("python train.py")] + 'echo "$DMLC_TASK_ID $DMLC_NUM_ATTEMPT"'
+    env = dict(os.environ, PYTHONPATH=repo, DMLC_ROLE="worker")
+    env.pop("DMLC_TRACKER_URI", None)
+    run = lambda e: subprocess.run(["bash", "-c", cmd], capture_output=True, text=True,  # noqa: E731
+                                   check=True, env=e, cwd=str(tmp_path)).stdout.split()
+    assert run(env) == ["2", "0"]
+    t = trk.RabitTracker("127.0.0.1", 1, port=19500, port_end=19999, timeout=60)
+    t.start(1)
+    try:
+        env.update(DMLC_TRACKER_URI="127.0.0.1", DMLC_TRACKER_PORT=str(t.port))
+        assert [run(env) for _ in range(3)] == [["2", "0"], ["2", "1"], ["2", "2"]]
+    finally:
+        t.stop()
+
+
 def test_service_job_success_and_memory_abort(rm):
     job = yarn.YarnServiceJob(rm, "j1")
     job.submit(yarn.service_spec(_args(), {}, "j1"))
