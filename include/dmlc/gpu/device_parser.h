@@ -60,6 +60,15 @@ struct DeviceParserConfig {
    *  kernel is hidden behind the previous fill (profiles/r05_one_pass).
    */
   bool one_pass{false};
+  /*!
+   * \brief ParseAllHashed into a reused batch over HBM-resident text: one
+   *  k_tile_hash launch per merged chunk with look-back line counts
+   *  (`?hash_one_pass=1`) instead of C1 + C2 + the counted k_tile_hash with
+   *  the next chunk's count beside it.  Off by default: the look-back kernel
+   *  measured 6,011 VALU per tile against 1,042 + 4,185 counted, 2.17 vs
+   *  1.98 ms per 2 M x 1024 pass (profiles/r06_fill/hash_counted)
+   */
+  bool hash_one_pass{false};
   /*! \brief counted HBM replay: queue the next chunk's count + scan on a
    *  second stream beside the current fill (`?prelaunch=0`: in line, for
    *  pricing each kernel alone) */

@@ -30,6 +30,9 @@ def main():
                     help="first merged replay chunk (0: no ramp; default: the parser's)")
     ap.add_argument("--replay-chunk-mb", type=float, default=None,
                     help="merged replay chunk cap (default: the parser's)")
+    ap.add_argument("--hash-one-pass", type=int, default=None,
+                    help="reused batch: 1 one look-back launch per chunk, 0 C1 + C2 + the "
+                         "counted kernel (default: the parser's)")
     args = ap.parse_args()
     import torch
 
@@ -47,7 +50,8 @@ def main():
     if args.replay_chunk_mb is not None:
         cfg["replay_chunk_mb"] = args.replay_chunk_mb
     two = data.GPUParser(args.data, format="libfm", hbm_cache=1, **cfg)
-    fused = data.GPUParser(args.data, format="libfm", hbm_cache=1, **cfg)
+    fcfg = dict(cfg) if args.hash_one_pass is None else dict(cfg, hash_one_pass=args.hash_one_pass)
+    fused = data.GPUParser(args.data, format="libfm", hbm_cache=1, **fcfg)
 
     def step_two():
         two.before_first()
@@ -117,7 +121,7 @@ def main():
     res["hashed_fm_step_ms"] = res["hashed_fm_fused_step_ms"]
     res["hashed_fm_step_event_ms"] = res["hashed_fm_fused_step_event_ms"]
     res["hashed_fm_gemm"] = res["hashed_fm_fused_gemm"]
-    res["replay"] = cfg
+    res["replay"] = fcfg
     res.update({"rows": int(batch["x"].shape[0]), "dim": args.dim, "text_bytes": nbytes,
                 "speedup_fused_vs_csr_k9": round(res["csr_then_k9"]["ms"] / res["fused"]["ms"], 3)})
     sweep = {}

@@ -15,7 +15,7 @@ for d in sorted(glob.glob(f"{out}/pmc_{tag}_*/")):
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
-            m = re.search(r"(k_\w+)(<[^(]*>)?", row["Kernel_Name"])
+            m = re.search(r"(k_\w+)(<.*?>)?(?=\()", row["Kernel_Name"])  # (template args kept)
             k = (m.group(1) + (m.group(2) or "")) if m else row["Kernel_Name"][:40]
             agg[k][row["Counter_Name"]] += float(row["Counter_Value"])
     per = {}

@@ -76,6 +76,8 @@ void DeviceParserConfig::Update(const std::map<std::string, std::string>& args) 
       fast_path = v != "0" && v != "false";
     } else if (k == "one_pass") {
       one_pass = v != "0" && v != "false";
+    } else if (k == "hash_one_pass") {
+      hash_one_pass = v != "0" && v != "false";
     } else if (k == "prelaunch") {
       prelaunch = v != "0" && v != "false";
     } else if (k == "replay_chunk_mb") {
@@ -1126,7 +1128,8 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     // small first chunk -- merge up to 2 x replay_chunk_bytes from the start
     // (below 2 GiB: an irregular chunk falls back to the exact kernels' 32-bit
     // offsets, as DeviceParserConfig::Update checks for replay_chunk_bytes)
-    const bool one_pass = cfg_.fast_path && dim % 16 == 0 && replay_ && out->row_cap != 0;
+    const bool one_pass =
+        cfg_.hash_one_pass && cfg_.fast_path && dim % 16 == 0 && replay_ && out->row_cap != 0;
     if (one_pass) {
       merge_limit_ = std::min(2 * cfg_.replay_chunk_bytes, (size_t(1) << 31) - (size_t(64) << 20));
       if (merge_cap_ == 0) merge_cap_ = merge_limit_;

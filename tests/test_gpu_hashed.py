@@ -402,13 +402,14 @@ def test_fm_fused_step_trains():
 
 @pytest.mark.parametrize("fmt", ["libsvm", "libfm"])
 def test_one_pass_hashed_matches_counted(tmp_path, fmt):
-    """A replayed pass into a reused batch runs one kernel per chunk (line
-    counts by decoupled look-back, no count kernel): the same fp8 bytes and
+    """With ``hash_one_pass=1`` a replayed pass into a reused batch runs one
+    kernel per chunk (line counts by decoupled look-back, no count kernel;
+    the default is the counted kernel, measured faster): the same fp8 bytes and
     labels as the counted first pass; a batch too small for the partition
     overflows, grows and the chunk is written again."""
     p = str(tmp_path / f"big.{fmt}")
     data.write_synthetic(p, 0, 30000, format=fmt, seed=11)
-    g = data.GPUParser(p, format=fmt, chunk_bytes=1 << 20, hbm_cache=1)
+    g = data.GPUParser(p, format=fmt, chunk_bytes=1 << 20, hbm_cache=1, hash_one_pass=1)
     a = g.parse_all_hashed(512, seed=6)  # first pass: caching, C1 + C2 + hash
     want_x = a["x"].view(torch.uint8).clone()
     want_l = a["label"].clone()
@@ -441,7 +442,7 @@ def test_one_pass_hashed_irregular_falls_back(tmp_path, bad):
     data.write_synthetic(str(tmp_path / "t"), 8000, 16000, format="libsvm", seed=5)
     with open(p, "a") as f:
         f.write(open(str(tmp_path / "t")).read())
-    g = data.GPUParser(p, format="libsvm", chunk_bytes=1 << 20, hbm_cache=1)
+    g = data.GPUParser(p, format="libsvm", chunk_bytes=1 << 20, hbm_cache=1, hash_one_pass=1)
     a = g.parse_all_hashed(256, seed=3, fp8=False)
     want_x, want_l = a["x"].clone(), a["label"].clone()
     e0 = g.stats()["exact_chunks"]
