@@ -1124,13 +1124,15 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
       }
     } unmerge{&merge_replay_, &merge_limit_};
     // resident text and a batch that already has rows (a reused one): one pass
-    // per chunk (k_tile_hash look-back, no C1 / C2), so nothing is gained by a
-    // small first chunk -- merge up to 2 x replay_chunk_bytes from the start
-    // (below 2 GiB: an irregular chunk falls back to the exact kernels' 32-bit
-    // offsets, as DeviceParserConfig::Update checks for replay_chunk_bytes)
+    // per chunk (k_tile_hash look-back, no C1 / C2) with hash_one_pass, else
+    // the counted kernel; either way a merged chunk costs one host turnaround,
+    // so merge up to 2 x replay_chunk_bytes from the start (measured: 1.97 ->
+    // 1.91 ms per 1.49 GB pass with the whole pass in one chunk; below 2 GiB:
+    // an irregular chunk falls back to the exact kernels' 32-bit offsets, as
+    // DeviceParserConfig::Update checks for replay_chunk_bytes)
     const bool one_pass =
         cfg_.hash_one_pass && cfg_.fast_path && dim % 16 == 0 && replay_ && out->row_cap != 0;
-    if (one_pass) {
+    if (replay_ && out->row_cap != 0 && cfg_.fast_path && dim % 16 == 0) {
       merge_limit_ = std::min(2 * cfg_.replay_chunk_bytes, (size_t(1) << 31) - (size_t(64) << 20));
       if (merge_cap_ == 0) merge_cap_ = merge_limit_;
     }
