@@ -282,7 +282,9 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
 
   void Seek(size_t cursor) override {
     CHECK_LE(cursor, PartitionBytes()) << "DeviceParser::Seek: cursor beyond the partition";
-    DrainInflight();
+    // a replay restarting at 0 keeps the next epoch's first count, prelaunched
+    // beside the last fill (PrelaunchNextEpoch; dropped if the chunk differs)
+    DrainInflight(/*keep_prelaunch=*/cursor == 0 && cache_complete_ && cfg_.shuffle_parts <= 1);
     replay_ = false;
     caching_ = false;
     if (cfg_.hbm_cache) {
@@ -617,10 +619,10 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
     caching_ = true;
   }
 
-  void DrainInflight() {
+  void DrainInflight(bool keep_prelaunch = false) {
     copy_->Synchronize();
     compute_->Synchronize();
-    DropPrelaunch();
+    if (!keep_prelaunch) DropPrelaunch();
     while (!inflight_.empty()) {
       if (inflight_.front().slot != nullptr) iter_.Recycle(&inflight_.front().slot);
       inflight_.pop_front();
@@ -888,25 +890,59 @@ class DeviceParserImpl : public DeviceParser<IndexType> {
    *  adopts the set when its chunk is the one prelaunched.
    */
   void PrelaunchCount() {
-    if (!(replay_ && merge_replay_) || pre_.valid || inflight_.empty() || !cfg_.prelaunch) {
+    if (!(replay_ && merge_replay_) || pre_.valid || !cfg_.prelaunch) return;
+    if (inflight_.empty()) {
+      // the epoch's last chunk is being parsed: count the next epoch's first
+      // one beside it (a ParseAll over the cache replays the same merge)
+      if (reader_done_ && cfg_.shuffle_parts <= 1) PrelaunchNextEpoch();
       return;
     }
     const Inflight& nx = inflight_.front();
     if (nx.d >= 0) return;  // not resident (its copy would have to be waited for)
-    const size_t tiles = TileCount(nx.size);
+    PrelaunchFor(nx.text, nx.size);
+  }
+
+  /*!
+   * \brief the next epoch's first merged chunk (replay_list_ from the start,
+   *  the first merge cap FillPipeline will use), counted now on count_stream_
+   *  so the next pass's first fill does not wait for its count.  A next pass
+   *  that starts otherwise drops it unused (CountScanCurrent matches text and
+   *  size).
+   */
+  void PrelaunchNextEpoch() {
+    if (replay_list_.empty()) return;
+    const CachedChunk& c = cached_[replay_list_[0]];
+    const size_t limit = merge_limit_ != 0 ? merge_limit_ : cfg_.replay_chunk_bytes;
+    const size_t first = merge_limit_ != 0 ? merge_limit_
+                         : (cfg_.replay_first_bytes != 0 ? cfg_.replay_first_bytes
+                                                         : cfg_.replay_chunk_bytes);
+    const size_t cap = std::min(first, limit);
+    size_t size = c.size;
+    for (size_t i = 1; i < replay_list_.size() && cached_[replay_list_[i - 1]].eol_end &&
+                       cached_[replay_list_[i]].off == c.off + size &&
+                       size + cached_[replay_list_[i]].size <= cap;
+         ++i) {
+      size += cached_[replay_list_[i]].size;
+    }
+    if (size == 0) return;
+    PrelaunchFor(arena_->get<char>() + c.off, size);
+  }
+
+  void PrelaunchFor(const char* text, size_t nbytes) {
+    const size_t tiles = TileCount(nbytes);
     tcounts_next_.Reserve(TileScratchWords(tiles) * sizeof(uint64_t));
     tflags_next_.Reserve(TileScratchWords(tiles) * sizeof(uint32_t));
     tmasks_next_.Reserve(TileMaskWords(tiles) * sizeof(uint32_t));
     // its own stream: count + scan (HBM- and VALU-light next to the fill)
     // overlap the current fill instead of queueing behind it.  The set it
     // writes was last used by the chunk before the current one, which is done.
-    LaunchCountScan(nx.text, nx.size, tcounts_next_.get<uint64_t>(), tflags_next_.get<uint32_t>(),
+    LaunchCountScan(text, nbytes, tcounts_next_.get<uint64_t>(), tflags_next_.get<uint32_t>(),
                     tmasks_next_.get<uint32_t>(), meta_next_.get<ChunkMeta>(),
                     hmap_next_.get<ChunkMeta>(), count_stream_->get());
     pre_done_->Record(count_stream_->get());
     pre_.valid = true;
-    pre_.text = nx.text;
-    pre_.nbytes = nx.size;
+    pre_.text = text;
+    pre_.nbytes = nbytes;
   }
 
   /*! \brief retire a prelaunched count nobody will adopt (its flag re-armed) */
